@@ -1,0 +1,244 @@
+"""Benchmark of the binned-statistics hot path on MI355X (BASELINE.json configs[1] at N=1).
+
+One step = one query pass over resident synthetic columns:
+``count(binby=[x, y], limits=[[-4, 4], [-4, 4]], shape=1024)`` + ``sum(w)`` on the same
+binners (one merged pass, as ExecutorLocal merges them), 1e9 float64 rows per GPU
+(weak scaling), through the superagg surface -> libvaexhip C-ABI -> HIP kernels; with
+N > 1 GPUs the rows are sharded by rank and the dense grids are all-reduced over RCCL.
+Fresh aggregator grids are created in every step (as a query does); the grid read-back to
+the host is not in the timed region.
+
+Prints ONE JSON line (rank 0) with the roofline of the binning pipeline (HIP events on the
+library stream) and the CPU baseline (the oracle's C restatement with the reference
+threading model, on a bounded sample, rank 0 at N=1 only).
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_METRIC = "rows/sec 2D count grid 1e9×f64 + groupby-sum 1e6 keys; HBM GB/s %peak"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+TILE_KERNELS = ["tile_sample", "tile_scatter", "tile_prefix", "tile_reduce"]
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--rows", type=float, default=1e9, help="rows per GPU")
+    p.add_argument("--bins", type=int, default=1024)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
+    p.add_argument("--no-groupby", action="store_true")
+    p.add_argument("--groupby-rows", type=float, default=1e9)
+    p.add_argument("--check", action="store_true", help="verify size-independent properties")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    import vaex_amd
+    from vaex_amd import _lib, superagg
+    from vaex_amd.device import DeviceArray
+    from vaex_amd import distributed as vdist
+
+    _lib.call("vh_set_device", local_rank)
+    n = int(args.rows)
+    bins = args.bins
+    # resident synthetic columns (each rank its own shard: seeds offset by rank)
+    x = DeviceArray.random(n, "normal", seed=2 + 1000 * rank)
+    y = DeviceArray.random(n, "normal", seed=3 + 1000 * rank)
+    w = DeviceArray.random(n, "uniform", seed=4 + 1000 * rank)
+
+    def step():
+        bx = superagg.BinnerScalar_float64("x", -4.0, 4.0, bins)
+        by = superagg.BinnerScalar_float64("y", -4.0, 4.0, bins)
+        bx.set_data(x)
+        by.set_data(y)
+        grid = superagg.Grid([bx, by])
+        count = superagg.AggCount_int64(grid)
+        total = superagg.AggSum_float64(grid)
+        total.set_data(w, 0)
+        grid.bin([count, total])
+        if dist is not None:
+            vdist.allreduce_aggs([count, total])
+        return count, total
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        _lib.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    _lib.timing_reset()
+    _lib.timing_enable(True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    barrier()
+    t1 = time.perf_counter()
+    _lib.timing_enable(False)
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    total_rows = n * world * args.steps
+    value = total_rows / elapsed
+
+    # roofline of the binning pipeline: algorithmic bytes = 24 B/row (x, y, w read once)
+    kernel_ms = {}
+    for k in TILE_KERNELS + ["bin_fused_global", "bin_fused_lds"]:
+        cnt, ms = _lib.timing_read(k)
+        if cnt:
+            kernel_ms[k] = (cnt, ms)
+    launches = max([c for c, _ in kernel_ms.values()] or [1])
+    pipeline_ms = sum(ms for _, ms in kernel_ms.values()) / max(launches, 1)
+    algo_bytes = 24 * n
+    achieved = algo_bytes / (pipeline_ms * 1e-3) / 1e9 if pipeline_ms else None
+    scatter = kernel_ms.get("tile_scatter")
+    roofline = {
+        "bound": "hbm",
+        "kernel": "+".join(k for k in kernel_ms),
+        "achieved": round(achieved, 1) if achieved else None,
+        "peak": HBM_PEAK_GBPS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
+        "traffic": None,
+        "algorithmic_bytes_per_launch": algo_bytes,
+        "launch_ms": round(pipeline_ms, 4),
+        "per_kernel_ms": {k: round(ms / c, 4) for k, (c, ms) in kernel_ms.items()},
+    }
+    if scatter:
+        roofline["tile_scatter_GBps"] = round(algo_bytes / (scatter[1] / scatter[0] * 1e-3) / 1e9, 1)
+
+    check = None
+    if args.check and rank == 0:
+        count, total = res
+        c = np.asarray(count)
+        check = {"count_total": int(c.sum()), "rows": n * world, "count_equal": int(c.sum()) == n * world}
+
+    extra = {}
+    if rank == 0 and world == 1 and not args.no_groupby:
+        extra["groupby"] = bench_groupby(int(args.groupby_rows), args)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(x, y, w, n, bins, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": BASELINE_METRIC,
+            "value": value,
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: x,y ~ N(0,1), w ~ U[0,1) float64 generated in HBM (counter-based splitmix64)",
+            "config": {
+                "workload": "C2 (BASELINE configs[1]): count(binby=[x,y], limits=[[-4,4],[-4,4]], shape=1024)"
+                            " + sum(w), one merged pass",
+                "rows_per_gpu": n,
+                "grid": [bins + 3, bins + 3],
+                "parallelism": f"row-shard x{world}" + (" + RCCL grid all-reduce" if world > 1 else ""),
+            },
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        if check:
+            line["check"] = check
+        line.update(extra)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_groupby(n, args):
+    """C3: groupby(int32 key, 1e6 distinct).agg({v: [sum, count]}) on resident columns."""
+    from vaex_amd import _lib
+    from vaex_amd.device import DeviceArray
+    import vaex_amd
+    keys = DeviceArray.random(n, "randint", seed=5, a=5, b=5 + 1_000_000, dtype="int32")
+    v = DeviceArray.random(n, "normal", seed=6)
+    df = vaex_amd.from_arrays(key=keys, v=v)
+    df.groupby("key", agg={"v": ["sum", "count"]})  # warm-up
+    _lib.synchronize()
+    times = []
+    for _ in range(max(1, min(3, args.steps))):
+        t0 = time.perf_counter()
+        dfg = df.groupby("key", agg={"v": ["sum", "count"]})
+        _lib.synchronize()
+        times.append(time.perf_counter() - t0)
+    t = min(times)
+    ngroups = len(dfg["key"].to_numpy())
+    del keys, v, df
+    return {"rows": n, "groups": ngroups, "seconds": t, "rows_per_s": n / t,
+            "algorithmic_GBps": 12 * n / t / 1e9,
+            "note": "end to end incl. set build pass, set seal, aggregation pass and result read-back"}
+
+
+def cpu_baseline(x, y, w, n, bins, target_seconds):
+    """oracle/superagg_oracle.c or_bench_grid2d: reference threading model (1 Mi-row chunks,
+    max(2, T//8) private grids for a >=1e7-byte part, serial reduce) on a bounded sample."""
+    from oracle import oracle
+    L = oracle.lib()
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    nparts = max(2, threads // 8)  # cpu.py:487-499 for a 16.9 MB count+sum part
+    cells = (bins + 3) ** 2
+    cnt = np.zeros(cells, np.int64)
+    sm = np.zeros(cells, np.float64)
+
+    def run(m):
+        hx, hy, hw = x[:m].to_numpy(), y[:m].to_numpy(), w[:m].to_numpy()
+        t0 = time.perf_counter()
+        used = L.or_bench_grid2d(hx.ctypes.data, hy.ctypes.data, hw.ctypes.data, m, -4.0, 4.0, -4.0, 4.0, bins,
+                                 nparts, threads, 1 << 20, cnt.ctypes.data, sm.ctypes.data)
+        return time.perf_counter() - t0, used
+
+    probe = min(n, 1 << 24)
+    t, _ = run(probe)
+    m = int(min(n, 1 << 28, max(probe, probe * target_seconds / max(t, 1e-6))))
+    t, used = run(m)
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": m / t, "unit": "rows/s", "cores": used, "kind": "port",
+            "sample": f"first {m} rows of the same x,y,w columns, count+sum 1027x1027 grid, {t:.2f} s",
+            "threads_available": threads, "nparts_rule": "max(2, T//8) (cpu.py:487-499)",
+            "cpu_model": cpu_model, "host": platform.node()}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,167 @@
+/*
+ * vaexhip.h -- C-ABI of libvaexhip.so, the MI355X (gfx950) implementation of
+ * vaex-core's binned-statistics and groupby-aggregation hot path.
+ *
+ * The boundary is plain C: opaque handles, raw pointers + sizes, int status
+ * codes and a thread-local last-error string.  No torch / pybind11 types.
+ * Every entry point names the reference interface it replaces
+ * (paths relative to the reference root, packages/vaex-core/src unless noted).
+ *
+ * Pointer arguments tagged `loc` may point to host memory (VH_LOC_HOST: staged
+ * to HBM by the library, pipelined per chunk) or to HBM (VH_LOC_DEVICE: read in
+ * place); VH_LOC_AUTO asks the HIP runtime.  Like the reference (which stores
+ * raw pointers from py::buffer without incref, superagg_binners.cpp:63-73),
+ * the caller keeps column buffers alive until vh_grid_bin returns.
+ */
+#ifndef VAEXHIP_H
+#define VAEXHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VH_ABI_VERSION 1
+
+/* status codes; VH_ERR_RUNTIME mirrors the std::runtime_error the reference
+ * throws ("Expected a 1d array", "Itemsize of data and binner are not equal",
+ * "data not set", "data2 not set", "no binners set and no length given"). */
+enum vh_status {
+    VH_OK = 0,
+    VH_ERR_RUNTIME = 1,
+    VH_ERR_HIP = 2,
+    VH_ERR_NOMEM = 3,
+    VH_ERR_ARG = 4
+};
+
+/* dtype codes, same order as the reference's per-dtype bindings
+ * (superagg_binners.cpp:279-303, superagg.cpp:614-624) */
+enum vh_dtype {
+    VH_F64 = 0, VH_F32 = 1, VH_I64 = 2, VH_I32 = 3, VH_I16 = 4, VH_I8 = 5,
+    VH_U64 = 6, VH_U32 = 7, VH_U16 = 8, VH_U8 = 9, VH_BOOL = 10
+};
+
+enum vh_loc { VH_LOC_AUTO = 0, VH_LOC_HOST = 1, VH_LOC_DEVICE = 2 };
+
+/* aggregator kinds (superagg.cpp:547-555) */
+enum vh_agg_kind {
+    VH_AGG_COUNT = 0,      /* AggCount_<t>      superagg.cpp:155-192 */
+    VH_AGG_SUM = 1,        /* AggSum_<t>        superagg.cpp:349-389 */
+    VH_AGG_MIN = 2,        /* AggMin_<t>        superagg.cpp:241-287 */
+    VH_AGG_MAX = 3,        /* AggMax_<t>        superagg.cpp:194-239 */
+    VH_AGG_FIRST = 4,      /* AggFirst_<t>      superagg.cpp:436-511 */
+    VH_AGG_SUM_MOMENT = 5  /* AggSumMoment_<t>  superagg.cpp:391-434 */
+};
+
+typedef struct vh_binner vh_binner;
+typedef struct vh_grid vh_grid;
+typedef struct vh_agg vh_agg;
+typedef struct vh_set vh_set;
+
+/* ---- library / device plumbing ---------------------------------------- */
+const char *vh_last_error(void);
+int vh_abi_version(void);
+int vh_device_count(int *count);
+int vh_set_device(int device);
+int vh_get_device(int *device);
+int vh_synchronize(void);
+int vh_malloc(void **dptr, uint64_t bytes);
+int vh_free(void *dptr);
+int vh_memcpy_htod(void *dst, const void *src, uint64_t bytes);
+int vh_memcpy_dtoh(void *dst, const void *src, uint64_t bytes);
+int vh_memcpy_dtod(void *dst, const void *src, uint64_t bytes);
+int vh_memset(void *dptr, int value, uint64_t bytes);
+/* synthetic columns generated in HBM (bench/test data; counter-based
+ * splitmix64, so any sub-range can be regenerated on the host):
+ * dist 0 = uniform [a, b) f64, 1 = normal(mean a, sd b) f64,
+ *      2 = uniform integer [a, b) stored as `dtype` (I32/I64). */
+int vh_fill_random(void *dptr, uint64_t n, int dtype, int dist, uint64_t seed, double a, double b);
+/* kernel timing with hipEvents on the library stream (bench roofline) */
+int vh_timing_enable(int on);
+int vh_timing_reset(void);
+int vh_timing_read(const char *kernel, uint64_t *launches, double *total_ms);
+int vh_stream(void **stream);
+
+/* ---- Binners: superagg_binners.cpp ------------------------------------- */
+/* BinnerScalar_<dtype>[_non_native](expression, vmin, vmax, bins)
+ * superagg_binners.cpp:5-93 (ctor :9, to_bins :14-56) */
+int vh_binner_scalar_create(const char *expression, int dtype, int flip_endian, double vmin,
+                            double vmax, uint64_t bins, vh_binner **out);
+/* BinnerOrdinal_<dtype>[_non_native](expression, ordinal_count, min_value)
+ * superagg_binners.cpp:95-184; both arguments already converted to uint64_t
+ * the way the C++ ctor converts its T arguments (:99). */
+int vh_binner_ordinal_create(const char *expression, int dtype, int flip_endian,
+                             uint64_t ordinal_count, uint64_t min_value, vh_binner **out);
+/* BinnerOrdinal over _ordinal_values(key, set) (functions.py:2441-2448 +
+ * hash_primitives.hpp:556-583) fused into one binner: reads the raw key
+ * column and probes the GPU set inside the bin kernel. */
+int vh_binner_set_ordinal_create(const char *expression, vh_set *set, uint64_t ordinal_count,
+                                 vh_binner **out);
+int vh_binner_copy(const vh_binner *binner, vh_binner **out);   /* .copy() */
+int vh_binner_destroy(vh_binner *binner);
+/* set_data(buf): ndim must be 1 ("Expected a 1d array"), itemsize must match
+ * ("Itemsize of data and binner are not equal"), superagg_binners.cpp:63-73 */
+int vh_binner_set_data(vh_binner *binner, const void *ptr, uint64_t length, int itemsize, int ndim,
+                       int loc);
+int vh_binner_set_data_mask(vh_binner *binner, const uint8_t *mask, uint64_t length, int ndim,
+                            int loc);                           /* :78-85, 1 = masked */
+int vh_binner_clear_data_mask(vh_binner *binner);             /* :74-77 */
+int vh_binner_shape(const vh_binner *binner, uint64_t *shape); /* bins+3 / count+3 */
+int vh_binner_size(const vh_binner *binner, uint64_t *size);
+
+/* ---- Grid: agg.hpp:50-143 ----------------------------------------------- */
+int vh_grid_create(vh_binner *const *binners, int nbinners, vh_grid **out);
+int vh_grid_destroy(vh_grid *grid);
+/* shapes/strides must hold >= dims entries (agg.hpp:54-69: strides[0] = 1) */
+int vh_grid_info(const vh_grid *grid, int *dims, uint64_t *shapes, uint64_t *strides,
+                 uint64_t *length1d);
+/* Grid.bin(aggs[, length]) agg.hpp:76-105; has_length = 0 takes the first
+ * binner's size and fails with "no binners set and no length given". */
+int vh_grid_bin(vh_grid *grid, vh_agg *const *aggs, int naggs, uint64_t length, int has_length);
+
+/* ---- Aggregators: superagg.cpp ----------------------------------------- */
+/* Agg<Kind>_<dtype>[_non_native](grid[, moment]) -- `arg` is the moment of
+ * AggSumMoment, ignored otherwise.  The grid lives in HBM. */
+int vh_agg_create(vh_grid *grid, int kind, int dtype, int flip_endian, uint32_t arg, vh_agg **out);
+int vh_agg_destroy(vh_agg *agg);
+/* set_data(buf, index): index 1 = the order column of AggFirst (:449-461) */
+int vh_agg_set_data(vh_agg *agg, const void *ptr, uint64_t length, int itemsize, int ndim, int index,
+                    int loc);
+int vh_agg_set_data_mask(vh_agg *agg, const uint8_t *mask, uint64_t length, int ndim, int loc); /* 1 = keep */
+int vh_agg_clear_data_mask(vh_agg *agg);
+/* __sizeof__ (grid bytes, agg.hpp:162-164), grid dtype and itemsize */
+int vh_agg_info(const vh_agg *agg, uint64_t *bytes, int *grid_dtype, uint64_t *itemsize);
+/* buffer protocol (agg.hpp:166-179): the grid is copied to/from a host image */
+int vh_agg_download(vh_agg *agg, void *host, uint64_t bytes);
+int vh_agg_upload(vh_agg *agg, const void *host, uint64_t bytes);
+int vh_agg_download_order(vh_agg *agg, void *host, uint64_t bytes); /* AggFirst order grid */
+int vh_agg_device_ptr(vh_agg *agg, void **grid_dptr, void **grid2_dptr);
+/* Aggregator.reduce(list) superagg.cpp:160-167, 205-212, 252-259, 354-361, 470-480 */
+int vh_agg_reduce(vh_agg *agg, vh_agg *const *others, int nothers);
+
+/* ---- ordered_set_<dtype>: hash_primitives.hpp:417-621 ------------------- */
+int vh_set_create(int dtype, vh_set **out);
+int vh_set_destroy(vh_set *set);
+/* update(keys[, mask]) hash_primitives.hpp:96-281 (mask: 1 = null) */
+int vh_set_update(vh_set *set, const void *keys, const uint8_t *mask, uint64_t n, int loc);
+/* assigns ordinals (first-appearance order); called implicitly by the readers */
+int vh_set_seal(vh_set *set);
+/* len(set), nan_count, null_count, nan_value, null_value (ordinals; 0x7fffffff if absent) */
+int vh_set_info(vh_set *set, int64_t *length, int64_t *nan_count, int64_t *null_count,
+                int64_t *nan_value, int64_t *null_value);
+/* key_array() hash_primitives.hpp:289-312 -- out has `length` items of the key dtype */
+int vh_set_key_array(vh_set *set, void *out_host);
+/* map_ordinal(keys) hash_primitives.hpp:543-583: out_itemsize 1/2/4/8; -1 = unknown key */
+int vh_set_map_ordinal(vh_set *set, const void *keys, uint64_t n, int loc, void *out, int out_itemsize,
+                       int out_loc);
+
+/* ---- limits pre-pass: vaexfast.cpp:1043-1055 (op_min_max) --------------- */
+int vh_minmax(const void *data, uint64_t n, int dtype, int flip_endian, const uint8_t *mask, int loc,
+              double *out_min, double *out_max);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VAEXHIP_H */

@@ -94,12 +94,23 @@ def _dtype_info(ar):
     return name, int(flip)
 
 
-def as_u64_bits(value):
-    """Conversion of a binner ctor argument of type T to uint64_t (superagg_binners.cpp:99):
-    integers wrap modulo 2**64, floats truncate toward zero (x86-64 cvttsd2si)."""
-    if isinstance(value, (float, np.floating)):
-        return int(math.trunc(value)) & (2 ** 64 - 1)
-    return int(value) & (2 ** 64 - 1)
+def as_u64_bits(value, dtype=None):
+    """A BinnerOrdinal_<T> ctor argument: pybind11 casts the Python value to T
+    (py::init<std::string, T, T>, superagg_binners.cpp:191; bool via truthiness), then the
+    C++ ctor converts T to uint64_t (:99): integers sign-extend / wrap modulo 2**64, floats
+    truncate toward zero (x86-64 cvttsd2si)."""
+    dt = np.dtype(dtype) if dtype is not None else None
+    if dt is not None and dt.kind == "b":
+        return int(bool(value))
+    if isinstance(value, (float, np.floating)) or (dt is not None and dt.kind == "f"):
+        return int(math.trunc(float(value))) & (2 ** 64 - 1)
+    v = int(value)
+    if dt is not None and dt.kind in "iu":
+        bits = dt.itemsize * 8
+        v &= (1 << bits) - 1
+        if dt.kind == "i" and v >= 1 << (bits - 1):
+            v -= 1 << bits
+    return v & (2 ** 64 - 1)
 
 
 class Binner:
@@ -114,7 +125,9 @@ class Binner:
         self.ordinal_count, self.min_value = ordinal_count, min_value
 
     def shape(self):
-        return (self.bins if self.kind == "scalar" else self.ordinal_count) + 3
+        if self.kind == "scalar":
+            return self.bins + 3
+        return as_u64_bits(self.ordinal_count, _dtype_info(self.data)[0]) + 3
 
 
 def grid_shape(binners):
@@ -142,7 +155,7 @@ def bin_indices(binners, n):
                                     float(b.vmax), int(b.bins), stride, _ptr(out))
         else:
             rc = L.or_binner_ordinal(code, flip, _ptr(b.data), _ptr(b.mask), n,
-                                     as_u64_bits(b.ordinal_count), as_u64_bits(b.min_value),
+                                     as_u64_bits(b.ordinal_count, name), as_u64_bits(b.min_value, name),
                                      stride, _ptr(out))
         assert rc == 0
     return out

@@ -1,0 +1,182 @@
+"""DataFrame-level parity (count/sum/mean/min/max/first/minmax, groupby, binby) on the GPU,
+against the reference's own test expectations (tests/golden/kats.json) and the oracle."""
+import numpy as np
+import pytest
+
+from conftest import load_kats
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+KATS = load_kats()
+API = {k["name"]: k for k in KATS["api"]}
+
+
+def vx():
+    import vaex_amd
+    return vaex_amd
+
+
+def _df(name):
+    k = API[name]
+    return vx().from_arrays(**{c: np.array(v, dtype="f8" if any(isinstance(e, float) for e in v) else "i8")
+                                for c, v in k["columns"].items()})
+
+
+def _run(df, call):
+    op = call["op"]
+    kw = {}
+    for key in ("binby", "limits", "shape"):
+        if key in call:
+            kw[key] = call[key]
+    if "selection" in call:
+        df.select(call["selection"])
+        kw["selection"] = True
+    if op == "first":
+        order = call["order"]
+        if order.startswith("-"):
+            df.add_virtual_column("neg_" + order[1:], "-" + order[1:])
+            order = "neg_" + order[1:]
+        return df.first(call["expression"], order, **kw)
+    f = getattr(df, op)
+    return f(call.get("expression"), **kw) if op == "count" else f(call["expression"], **kw)
+
+
+@pytest.mark.parametrize("name", ["mean_basics", "count_basics_1d", "first"])
+def test_api_kats(name):
+    for call in API[name]["calls"]:
+        df = _df(name)
+        got = _run(df, call)
+        assert np.asarray(got).tolist() == call["expected"], call
+
+
+def test_count_1d_edges():
+    """tests/agg_test.py:150-158 through df._agg with edges=True."""
+    df = vx().from_arrays(x=np.array([-1, -2, 0.5, 1.5, 4.5, 5], dtype="f8"))
+    binner = df._binner_scalar("x", [0, 5], 5)
+    grid = df._agg(vx().agg.count(edges=True), (binner,))
+    assert grid.tolist() == [0, 2, 1, 1, 0, 0, 1, 1]
+
+
+def test_count_1d_ordinal_delay():
+    """tests/agg_test.py:171-181: add_tasks + df.execute()."""
+    df = vx().from_arrays(x=np.array([-1, -2, 0, 1, 4, 5], dtype="i8"))
+    binner = df._binner_ordinal("x", 5)
+    agg = vx().agg.count(edges=True)
+    tasks, result = agg.add_tasks(df, (binner,))
+    df.execute()
+    assert result.get().tolist() == [0, 2, 1, 1, 0, 0, 1, 1]
+
+
+def test_big_endian_and_strides():
+    """tests/agg_test.py:257-281."""
+    x = np.arange(10, dtype=">f8")
+    y = np.zeros(10, dtype=">f8")
+    df = vx().from_arrays(x=x, y=y)
+    counts = df.count(binby=[df.x, df.y], limits=[[-0.5, 9.5], [-0.5, 0.5]], shape=[10, 1])
+    assert counts.ravel().tolist() == np.ones(10).tolist()
+    ar = np.zeros((10, 2)).reshape(20)
+    x = ar[::2]
+    x[:] = np.arange(10)
+    df = vx().from_arrays(x=x)
+    assert df.count(binby=df.x, limits=[-0.5, 9.5], shape=10).tolist() == np.ones(10).tolist()
+
+
+def test_count_vs_numpy_minmax_limits():
+    """tests/count_test.py:23-38: limits='minmax' runs the GPU min/max pre-pass; counts equal
+    np.histogram except the last bin (the max lands in the overflow cell)."""
+    rng = np.random.default_rng(3)
+    x = rng.normal(size=100000)
+    df = vx().from_arrays(x=x)
+    counts = df.count(binby="x", shape=4, limits="minmax")
+    lo, hi = df.minmax("x")
+    assert (lo, hi) == oracle.minmax_f64(x)
+    ref, _ = np.histogram(x, bins=4, range=(lo, hi))
+    assert counts[:-1].tolist() == ref[:-1].tolist()
+
+
+def test_delay_merges_into_one_pass():
+    rng = np.random.default_rng(4)
+    x, w = rng.normal(size=50000), rng.random(50000)
+    df = vx().from_arrays(x=x, w=w)
+    before = df.executor.passes
+    c = df.count(binby="x", limits=[-3, 3], shape=64, delay=True)
+    s = df.sum("w", binby="x", limits=[-3, 3], shape=64, delay=True)
+    m = df.mean("w", binby="x", limits=[-3, 3], shape=64, delay=True)
+    df.execute()
+    assert df.executor.passes == before + 1
+    spec = oracle.Binner("scalar", x, vmin=-3, vmax=3, bins=64)
+    ec = oracle.extract_central_part(oracle.compute_grid([spec], "count"))
+    es = oracle.extract_central_part(oracle.compute_grid([spec], "sum", data=w))
+    assert c.get().tolist() == ec.tolist()
+    np.testing.assert_allclose(s.get(), es, rtol=1e-6)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        np.testing.assert_allclose(m.get(), es / ec, rtol=1e-6)
+
+
+def test_masked_column_and_selection():
+    rng = np.random.default_rng(8)
+    n = 40000
+    x = rng.normal(size=n)
+    w = np.ma.array(rng.normal(size=n), mask=rng.random(n) < 0.2)
+    df = vx().from_arrays(x=x, w=w)
+    df.select("x > 0")
+    got = df.sum("w", binby="x", limits=[-3, 3], shape=10, selection=True)
+    keep = ((x > 0) & ~np.ma.getmaskarray(w)).astype(np.uint8)
+    spec = oracle.Binner("scalar", x, vmin=-3, vmax=3, bins=10)
+    exp = oracle.extract_central_part(oracle.compute_grid([spec], "sum", data=w.data, mask=keep))
+    np.testing.assert_allclose(got, exp, rtol=1e-6, atol=1e-12)
+    cnt = df.count("w", binby="x", limits=[-3, 3], shape=10)
+    keep2 = (~np.ma.getmaskarray(w)).astype(np.uint8)
+    exp2 = oracle.extract_central_part(oracle.compute_grid([spec], "count", data=w.data, mask=keep2))
+    assert cnt.tolist() == exp2.tolist()
+
+
+def test_small_chunks_multi_chunk_path(monkeypatch):
+    """small_buffer (tests/common.py:45-56): chunk_size=3 exercises many chunks + reduce."""
+    monkeypatch.setenv("VAEX_CHUNK_SIZE", "3")
+    x = np.arange(10, dtype="f8")
+    y = x ** 2
+    df = vx().from_arrays(x=x, y=y)
+    assert df.first("y", "x", binby="x", limits=[0, 10], shape=2).tolist() == [0, 25]
+    assert df.sum("y", binby="x", limits=[0, 10], shape=10).tolist() == y.tolist()
+    assert df.count().item() == 10
+
+
+@pytest.mark.parametrize("name", ["groupby_1d", "groupby_1d_nan", "groupby_2d"])
+def test_groupby_kats(name):
+    call = API[name]["calls"][0]
+    df = _df(name)
+    by = call["by"]
+    dfg = df.groupby(by=by, agg={"count": vx().agg.count()}, sort=call["sort"])
+    if name == "groupby_1d_nan":
+        dfg = dfg.sort("g")
+    keys = call["expected_keys"]
+    if isinstance(by, list):
+        for k, col in zip(keys, by):
+            assert dfg[col].tolist() == k
+    else:
+        got = dfg[by].tolist()
+        if keys[-1] == "nan":
+            assert got[:-1] == keys[:-1] and np.isnan(got[-1])
+        else:
+            assert got == keys
+    assert dfg["count"].tolist() == call["expected_count"]
+
+
+def test_binby_2d_kat():
+    call = API["binby_2d"]["calls"][0]
+    df = _df("binby_2d")
+    ar = df.binby(by=call["by"], agg=vx().agg.count(), sort=True)
+    assert ar.data.tolist() == call["expected"]
+    assert ar.dims == ("g", "h")
+
+
+def test_categorical_groupby():
+    """tests/groupby_test.py:127-141: categorized ints bin by BinnerOrdinal(min, N) directly."""
+    g = np.array([0, 0, 0, 0, 1, 1, 1, 1, 2, 2])
+    df = vx().from_arrays(g=g)
+    df.categorize("g", labels=["cat", "dog", "snake"], inplace=True)
+    dfg = df.groupby(by="g", agg="count")
+    assert dfg.g.tolist() == ["cat", "dog", "snake"]
+    assert dfg["count"].tolist() == [4, 4, 2]

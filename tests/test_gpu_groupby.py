@@ -1,0 +1,132 @@
+"""GPU ordered_set (hash_primitives.hpp) and groupby parity against the oracle.
+
+The GPU set assigns ordinals in first-appearance order, which is exactly what the
+reference's ordered_set produces for a single-threaded update with nmaps=1; the oracle's
+OrderedSet(1) is that restatement, so ordinals and key_array are compared bit-exactly.
+groupby results are compared as key -> (sum, count) maps."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def su():
+    import vaex_amd.superutils as m
+    return m
+
+
+@pytest.mark.parametrize("dtype", ["int64", "int32", "int16", "int8", "uint64", "uint32", "uint8", "float64", "float32"])
+def test_set_matches_single_thread_reference(dtype):
+    rng = np.random.default_rng(1)
+    dt = np.dtype(dtype)
+    if dt.kind == "f":
+        keys = rng.integers(-50, 50, 20000).astype(dt)
+        keys[::97] = np.nan
+    else:
+        info = np.iinfo(dt)
+        keys = rng.integers(max(info.min, -100), min(info.max, 100), 20000).astype(dt)
+    s = getattr(su(), "ordered_set_" + dtype)(7)
+    s.update(keys[:12000])
+    s.update(keys[12000:])
+    ref = oracle.OrderedSet(1)
+    ref.update(keys[:12000])
+    ref.update(keys[12000:])
+    ka, rka = s.key_array(), ref.key_array(dtype)
+    assert len(s) == len(ref)
+    np.testing.assert_array_equal(ka, rka)
+    np.testing.assert_array_equal(s.map_ordinal(keys), ref.map_ordinal(keys))
+    assert s.map_ordinal(keys).dtype == ref.map_ordinal(keys).dtype
+
+
+@pytest.mark.parametrize("nan", [False, True])
+@pytest.mark.parametrize("missing", [False, True])
+def test_set_float_kat(nan, missing):
+    """tests/internal/hash_test.py:54-126."""
+    ar = np.arange(4, dtype="f8")[::-1].copy()
+    expected = list(ar)
+    mask = None
+    if missing:
+        mask = np.array([0, 0, 1, 0], dtype=bool)
+        expected[2] = None
+    if nan:
+        ar[1] = np.nan
+        expected[1] = "nan"
+    oset = su().ordered_set_float64(3)
+    ordinals, map_index = oset.update(ar, mask, return_values=True)
+    keys = oset.key_array().tolist()
+    if missing:
+        keys[oset.null_value] = None
+    norm = lambda v: "nan" if isinstance(v, float) and v != v else v
+    assert [norm(keys[o]) for o in ordinals] == [norm(e) for e in expected]
+    assert oset.map_ordinal(np.array([0.0])).dtype.name == "int8"
+    ka = oset.key_array()
+    ords = oset.map_ordinal(ka).tolist()
+    if missing:
+        ords[oset.null_value] = oset.null_value
+    assert ords == list(range(4))
+    # the create() constructor round trip
+    copy = su().ordered_set_float64(ka, oset.null_value, oset.nan_count, oset.null_count, "")
+    ords = copy.map_ordinal(copy.key_array()).tolist()
+    if missing:
+        ords[copy.null_value] = copy.null_value
+    assert ords == list(range(4))
+
+
+def test_set_special_keys_and_growth():
+    """int64 -1 (the EMPTY bit pattern) and >1e5 distinct keys (table growth)."""
+    rng = np.random.default_rng(2)
+    keys = rng.integers(-1, 300000, 1_000_000).astype(np.int64)
+    keys[5] = -1
+    s = su().ordered_set_int64()
+    s.update(keys)
+    ref = oracle.OrderedSet(1)
+    uniq, first = np.unique(keys, return_index=True)
+    order = uniq[np.argsort(first)]
+    np.testing.assert_array_equal(s.key_array(), order)
+    mo = s.map_ordinal(keys)
+    np.testing.assert_array_equal(s.key_array()[mo], keys)
+    assert (s.map_ordinal(np.array([10 ** 12], np.int64)) == -1).all()
+
+
+@pytest.mark.parametrize("sort", [False, True])
+def test_groupby_sum_count_matches_reference(sort):
+    import vaex_amd
+    rng = np.random.default_rng(3)
+    n = 2_000_000
+    keys = (5 + rng.integers(0, 100000, n)).astype(np.int32)
+    v = rng.normal(size=n)
+    v[::101] = np.nan
+    df = vaex_amd.from_arrays(key=keys, v=v)
+    dfg = df.groupby("key", agg={"v_sum": vaex_amd.agg.sum("v"), "v_count": vaex_amd.agg.count("v"),
+                                 "n": "count"}, sort=sort)
+    uk, s, c = oracle.groupby_reference(keys, v)
+    # the 'count' string is count(*) (groupby.py:390-391): NaN values still count
+    np.testing.assert_array_equal(np.sort(dfg["n"].to_numpy()), np.sort(np.bincount(keys)[uk]))
+    gk = dfg["key"].to_numpy()
+    order = np.argsort(gk)
+    assert gk[order].tolist() == uk.tolist()
+    if sort:
+        assert (np.diff(gk) > 0).all()
+    np.testing.assert_array_equal(dfg["v_count"].to_numpy()[order], c)
+    np.testing.assert_allclose(dfg["v_sum"].to_numpy()[order], s, rtol=1e-6, atol=1e-9)
+
+
+def test_groupby_device_resident_keys():
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    n = 3_000_000
+    dk = DeviceArray.random(n, "randint", seed=5, a=5, b=5 + 50000, dtype="int32")
+    dv = DeviceArray.random(n, "normal", seed=6)
+    df = vaex_amd.from_arrays(key=dk, v=dv)
+    dfg = df.groupby("key", agg={"v": ["sum", "count"]})
+    # {'v': ['sum', 'count']} -> columns v_sum and v (= count(*)), groupby.py:386-398
+    dfg["v_count"] = dfg["v"].to_numpy()
+    keys, v = dk.to_numpy(), dv.to_numpy()
+    uk, s, c = oracle.groupby_reference(keys, v)
+    gk = dfg["key"].to_numpy()
+    order = np.argsort(gk)
+    assert gk[order].tolist() == uk.tolist()
+    np.testing.assert_array_equal(dfg["v_count"].to_numpy()[order], c)
+    np.testing.assert_allclose(dfg["v_sum"].to_numpy()[order], s, rtol=1e-6, atol=1e-9)

@@ -1,0 +1,314 @@
+"""Parity of the HIP superagg surface (libvaexhip through the C-ABI) with the CPU oracle.
+
+Integer counts and bin indices must be bit-exact; float64 sums within 1e-6 relative
+(north_star); min/max/first are exact."""
+import zlib
+
+import numpy as np
+import pytest
+
+from conftest import kat_array, load_kats
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+KATS = load_kats()
+DTYPES = ["float64", "float32", "int64", "int32", "int16", "int8", "uint64", "uint32", "uint16", "uint8", "bool"]
+
+
+def sa():
+    import vaex_amd.superagg as m
+    return m
+
+
+def _binner_cls(kind, ar):
+    from vaex_amd.utils import find_type_from_dtype
+    return find_type_from_dtype(sa(), "BinnerScalar_" if kind == "scalar" else "BinnerOrdinal_", ar.dtype)
+
+
+def _agg_cls(kind, dtype):
+    from vaex_amd.utils import find_type_from_dtype
+    name = {"count": "AggCount_", "sum": "AggSum_", "min": "AggMin_", "max": "AggMax_", "first": "AggFirst_",
+            "sum_moment": "AggSumMoment_"}[kind]
+    return find_type_from_dtype(sa(), name, dtype)
+
+
+@pytest.mark.parametrize("kat", KATS["superagg"], ids=[k["name"] for k in KATS["superagg"]])
+def test_superagg_kat(kat):
+    binners = []
+    for s in kat["binners"]:
+        ar = kat_array(s)
+        ar = np.ascontiguousarray(ar)
+        if s["kind"] == "scalar":
+            b = _binner_cls("scalar", ar)("x", s["vmin"], s["vmax"], s["bins"])
+        else:
+            b = _binner_cls("ordinal", ar)("x", s["ordinal_count"], s["min_value"])
+        b.set_data(ar)
+        binners.append(b)
+    grid = sa().Grid(binners)
+    a = kat["agg"]
+    if "data" in a:
+        data = np.array(a["data"], dtype=a["dtype"])
+        agg = _agg_cls(a["kind"], data.dtype)(grid)
+        agg.set_data(data, 0)
+    else:
+        agg = _agg_cls(a["kind"], np.dtype("float64"))(grid)
+    view = np.asarray(agg)
+    grid.bin([agg])
+    if "expected" in kat:
+        assert view.tolist() == kat["expected"]
+    if "expected_diagonal" in kat:
+        assert [view[k, k] for k in range(view.shape[0])] == kat["expected_diagonal"]
+    if "expected_central" in kat:
+        assert view[(slice(2, -1),) * view.ndim].tolist() == kat["expected_central"]
+    if "expected_central_diagonal" in kat:
+        assert np.diagonal(view[2:-1, 2:-1]).tolist() == kat["expected_central_diagonal"]
+
+
+def test_live_view_mutation_before_bin():
+    """tests/internal/superagg_tests.py:86-106 pattern: the array view is live and writable."""
+    x = np.array([-1, -1, 0, 0, 4, 6, 10], dtype="i8")
+    y = np.array([-1, 2, 4, 1, 9, 6, 10], dtype="i8")
+    b = sa().BinnerOrdinal_int64("x", 5, 0)
+    b.set_data(x)
+    grid = sa().Grid([b])
+    agg = sa().AggMax_int64(grid)
+    view = np.asarray(agg)
+    view[:] = -100
+    agg.set_data(y, 0)
+    grid.bin([agg])
+    assert view.tolist() == [-100, 2, 4, -100, -100, -100, 9, 10]
+    agg = sa().AggMin_int64(grid)
+    view = np.asarray(agg)
+    view[:] = 100
+    agg.set_data(y, 0)
+    grid.bin([agg])
+    assert view.tolist() == [100, -1, 1, 100, 100, 100, 9, 6]
+
+
+def test_errors():
+    b = sa().BinnerScalar_float64("x", 0, 1, 4)
+    with pytest.raises(RuntimeError, match="Expected a 1d array"):
+        b.set_data(np.zeros((2, 2)))
+    with pytest.raises(RuntimeError, match="Itemsize of data and binner are not equal"):
+        b.set_data(np.zeros(4, dtype="f4"))
+    grid = sa().Grid([])
+    with pytest.raises(RuntimeError, match="no binners set and no length given"):
+        grid.bin([sa().AggCount_int64(grid)])
+    b.set_data(np.zeros(4))
+    grid = sa().Grid([b])
+    with pytest.raises(RuntimeError, match="data not set"):
+        grid.bin([sa().AggSum_float64(grid)])
+    agg = sa().AggFirst_float64(grid)
+    agg.set_data(np.zeros(4), 0)
+    with pytest.raises(RuntimeError, match="data2 not set"):
+        grid.bin([agg])
+
+
+def _random_column(rng, dtype, n, with_nan=True):
+    dt = np.dtype(dtype)
+    if dt.kind == "f":
+        a = rng.normal(0, 3, n).astype(dt)
+        if with_nan:
+            a[rng.random(n) < 0.05] = np.nan
+    elif dt.kind == "b":
+        a = rng.random(n) < 0.5
+    else:
+        info = np.iinfo(dt)
+        lo, hi = max(info.min, -20), min(info.max, 40)
+        a = rng.integers(lo, hi, n).astype(dt)
+    return a
+
+
+def _oracle_grid(binner_specs, kind, data=None, data2=None, mask=None, moment=2):
+    return oracle.compute_grid(binner_specs, kind, data=data, data2=data2, mask=mask, moment=moment)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("flip", [False, True])
+def test_binners_random_parity(dtype, flip):
+    """Both binner kinds, every dtype, native and byte-swapped, with a binner mask."""
+    rng = np.random.default_rng(zlib.crc32(f"{dtype}{flip}".encode()))
+    n = 5000
+    a = _random_column(rng, dtype, n)
+    b2 = _random_column(rng, "float64", n)
+    if flip:
+        a = a.astype(a.dtype.newbyteorder(">"))
+    mask = (rng.random(n) < 0.1).astype(np.uint8)
+    for kind in ("scalar", "ordinal"):
+        if kind == "scalar":
+            spec = oracle.Binner("scalar", a, vmin=-7.5, vmax=25.0, bins=13, mask=mask)
+            gb = _binner_cls("scalar", a)("a", -7.5, 25.0, 13)
+        else:
+            spec = oracle.Binner("ordinal", a, ordinal_count=17, min_value=-3 if np.dtype(dtype).kind == "i" else 2,
+                                 mask=mask)
+            gb = _binner_cls("ordinal", a)("a", 17, spec.min_value)
+        gb.set_data(a)
+        gb.set_data_mask(mask)
+        spec2 = oracle.Binner("scalar", b2, vmin=-4, vmax=4, bins=5)
+        gb2 = sa().BinnerScalar_float64("b", -4, 4, 5)
+        gb2.set_data(b2)
+        grid = sa().Grid([gb, gb2])
+        agg = sa().AggCount_int64(grid)
+        grid.bin([agg])
+        expected = _oracle_grid([spec, spec2], "count")
+        assert np.asarray(agg).tolist() == expected.tolist(), kind
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("kind", ["count", "sum", "min", "max", "first", "sum_moment"])
+def test_aggregators_random_parity(dtype, kind):
+    rng = np.random.default_rng(zlib.crc32(f"{dtype}{kind}".encode()))
+    n = 20000
+    x = rng.normal(0, 1, n)
+    data = _random_column(rng, dtype, n)
+    data2 = _random_column(rng, dtype, n)
+    keep = (rng.random(n) < 0.8).astype(np.uint8)
+    spec = oracle.Binner("scalar", x, vmin=-3, vmax=3, bins=32)
+    gb = sa().BinnerScalar_float64("x", -3, 3, 32)
+    gb.set_data(x)
+    grid = sa().Grid([gb])
+    agg = _agg_cls(kind, data.dtype)(grid, *([2] if kind == "sum_moment" else []))
+    agg.set_data(data, 0)
+    if kind == "first":
+        agg.set_data(data2, 1)
+        expected = _oracle_grid([spec], "first", data=data, data2=data2)
+    else:
+        agg.set_data_mask(keep)
+        expected = _oracle_grid([spec], kind, data=data, mask=keep, moment=2)
+    grid.bin([agg])
+    got = np.asarray(agg)
+    if kind in ("sum", "sum_moment") and got.dtype.kind == "f":
+        np.testing.assert_allclose(got, expected, rtol=1e-6, atol=1e-9)
+    else:
+        np.testing.assert_array_equal(got, expected)
+
+
+def test_count_with_data_skips_nan_and_mask():
+    rng = np.random.default_rng(5)
+    n = 10000
+    x = rng.normal(size=n)
+    w = rng.normal(size=n)
+    w[::7] = np.nan
+    keep = (rng.random(n) < 0.7).astype(np.uint8)
+    spec = oracle.Binner("scalar", x, vmin=-2, vmax=2, bins=20)
+    gb = sa().BinnerScalar_float64("x", -2, 2, 20)
+    gb.set_data(x)
+    grid = sa().Grid([gb])
+    c = sa().AggCount_float64(grid)
+    c.set_data(w, 0)
+    c.set_data_mask(keep)
+    s = sa().AggSum_float64(grid)
+    s.set_data(w, 0)
+    s.set_data_mask(keep)
+    grid.bin([c, s])
+    np.testing.assert_array_equal(np.asarray(c), _oracle_grid([spec], "count", data=w, mask=keep))
+    np.testing.assert_allclose(np.asarray(s), _oracle_grid([spec], "sum", data=w, mask=keep), rtol=1e-6, atol=1e-12)
+
+
+def test_scalar_grid_no_binners():
+    """Grid([]) with an explicit length: everything lands in cell 0 (df.count() without binby)."""
+    grid = sa().Grid([])
+    c = sa().AggCount_int64(grid)
+    s = sa().AggSum_float64(grid)
+    w = np.arange(100, dtype="f8")
+    s.set_data(w, 0)
+    grid.bin([c, s], 100)
+    assert np.asarray(c).item() == 100
+    assert np.asarray(s).item() == w.sum()
+
+
+@pytest.mark.parametrize("kind", ["count", "sum", "min", "max", "first"])
+def test_reduce_parts(kind):
+    rng = np.random.default_rng(7)
+    n = 30000
+    x = rng.normal(size=n)
+    w = rng.normal(size=n)
+    o = rng.permutation(n).astype("f8")
+    spec = oracle.Binner("scalar", x, vmin=-3, vmax=3, bins=16)
+    expected = _oracle_grid([spec], kind, data=w, data2=o) if kind != "count" else _oracle_grid([spec], "count")
+    parts = []
+    for p in range(3):
+        sl = slice(p * n // 3, (p + 1) * n // 3)
+        gb = sa().BinnerScalar_float64("x", -3, 3, 16)
+        gb.set_data(x[sl])
+        grid = sa().Grid([gb])
+        agg = _agg_cls(kind, np.dtype("f8"))(grid)
+        if kind != "count":
+            agg.set_data(w[sl], 0)
+        if kind == "first":
+            agg.set_data(o[sl], 1)
+        grid.bin([agg])
+        parts.append(agg)
+    parts[0].reduce(parts[1:])
+    got = np.asarray(parts[0])
+    if kind == "sum":
+        np.testing.assert_allclose(got, expected, rtol=1e-6, atol=1e-9)
+    else:
+        np.testing.assert_array_equal(got, expected)
+
+
+def test_device_resident_columns_match_host():
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(11)
+    n = 200000
+    x, y, w = rng.normal(size=n), rng.normal(size=n), rng.random(n)
+    bx = oracle.Binner("scalar", x, vmin=-4, vmax=4, bins=100)
+    by = oracle.Binner("scalar", y, vmin=-4, vmax=4, bins=100)
+    exp_c = _oracle_grid([bx, by], "count")
+    exp_s = _oracle_grid([bx, by], "sum", data=w)
+    dx, dy, dw = DeviceArray.from_numpy(x), DeviceArray.from_numpy(y), DeviceArray.from_numpy(w)
+    gx, gy = sa().BinnerScalar_float64("x", -4, 4, 100), sa().BinnerScalar_float64("y", -4, 4, 100)
+    gx.set_data(dx)
+    gy.set_data(dy)
+    grid = sa().Grid([gx, gy])
+    c, s = sa().AggCount_int64(grid), sa().AggSum_float64(grid)
+    s.set_data(dw, 0)
+    grid.bin([c, s])
+    np.testing.assert_array_equal(np.asarray(c), exp_c)
+    np.testing.assert_allclose(np.asarray(s), exp_s, rtol=1e-6, atol=1e-12)
+
+
+@pytest.mark.parametrize("dist", ["normal", "uniform"])
+@pytest.mark.parametrize("with_sum", [False, True])
+def test_tiled_path_large_grid(dist, with_sum):
+    """1027x1027 grid (the C2 shape) over 4M rows takes the tile-partitioned LDS path."""
+    from vaex_amd.device import DeviceArray
+    n = 4_000_000
+    rng = np.random.default_rng(13)
+    if dist == "normal":
+        x, y = rng.normal(size=n), rng.normal(size=n)
+    else:
+        x, y = rng.uniform(-4.5, 4.5, n), rng.uniform(-4.5, 4.5, n)
+    x[::1001] = np.nan
+    w = rng.random(n)
+    bx = oracle.Binner("scalar", x, vmin=-4, vmax=4, bins=1024)
+    by = oracle.Binner("scalar", y, vmin=-4, vmax=4, bins=1024)
+    exp_c = _oracle_grid([bx, by], "count")
+    gx, gy = sa().BinnerScalar_float64("x", -4, 4, 1024), sa().BinnerScalar_float64("y", -4, 4, 1024)
+    gx.set_data(DeviceArray.from_numpy(x))
+    gy.set_data(DeviceArray.from_numpy(y))
+    grid = sa().Grid([gx, gy])
+    aggs = [sa().AggCount_int64(grid)]
+    if with_sum:
+        s = sa().AggSum_float64(grid)
+        s.set_data(DeviceArray.from_numpy(w), 0)
+        aggs.append(s)
+    grid.bin(aggs)
+    np.testing.assert_array_equal(np.asarray(aggs[0]), exp_c)
+    if with_sum:
+        np.testing.assert_allclose(np.asarray(aggs[1]), _oracle_grid([bx, by], "sum", data=w), rtol=1e-6, atol=1e-12)
+
+
+def test_host_staging_multiple_chunks():
+    """Host columns longer than one staging chunk (16 Mi rows)."""
+    n = (1 << 24) + 12345
+    rng = np.random.default_rng(17)
+    x = rng.normal(size=n)
+    spec = oracle.Binner("scalar", x, vmin=-5, vmax=5, bins=256)
+    gb = sa().BinnerScalar_float64("x", -5, 5, 256)
+    gb.set_data(x)
+    grid = sa().Grid([gb])
+    c = sa().AggCount_int64(grid)
+    grid.bin([c])
+    np.testing.assert_array_equal(np.asarray(c), _oracle_grid([spec], "count"))

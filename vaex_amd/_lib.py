@@ -1,0 +1,147 @@
+"""ctypes binding of ``libvaexhip.so`` (C-ABI declared in ``include/vaexhip.h``).
+
+The product path has no fallback: if the HIP library is missing this module raises
+``ImportError`` and every GPU entry point fails loudly.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("VAEX_AMD_LIB", os.path.join(HERE, "libvaexhip.so"))
+
+DTYPES = ["float64", "float32", "int64", "int32", "int16", "int8",
+          "uint64", "uint32", "uint16", "uint8", "bool"]
+DTYPE_CODE = {name: i for i, name in enumerate(DTYPES)}
+AGG_KIND = {"AggCount": 0, "AggSum": 1, "AggMin": 2, "AggMax": 3, "AggFirst": 4, "AggSumMoment": 5}
+LOC_AUTO, LOC_HOST, LOC_DEVICE = 0, 1, 2
+
+# every symbol the header declares, with (restype, argtypes)
+_vp, _u64, _i32, _i64, _dbl = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int64, ctypes.c_double
+_p = ctypes.POINTER
+SIGNATURES = {
+    "vh_last_error": (ctypes.c_char_p, []),
+    "vh_abi_version": (_i32, []),
+    "vh_device_count": (_i32, [_p(_i32)]),
+    "vh_set_device": (_i32, [_i32]),
+    "vh_get_device": (_i32, [_p(_i32)]),
+    "vh_synchronize": (_i32, []),
+    "vh_malloc": (_i32, [_p(_vp), _u64]),
+    "vh_free": (_i32, [_vp]),
+    "vh_memcpy_htod": (_i32, [_vp, _vp, _u64]),
+    "vh_memcpy_dtoh": (_i32, [_vp, _vp, _u64]),
+    "vh_memcpy_dtod": (_i32, [_vp, _vp, _u64]),
+    "vh_memset": (_i32, [_vp, _i32, _u64]),
+    "vh_fill_random": (_i32, [_vp, _u64, _i32, _i32, _u64, _dbl, _dbl]),
+    "vh_timing_enable": (_i32, [_i32]),
+    "vh_timing_reset": (_i32, []),
+    "vh_timing_read": (_i32, [ctypes.c_char_p, _p(_u64), _p(_dbl)]),
+    "vh_stream": (_i32, [_p(_vp)]),
+    "vh_binner_scalar_create": (_i32, [ctypes.c_char_p, _i32, _i32, _dbl, _dbl, _u64, _p(_vp)]),
+    "vh_binner_ordinal_create": (_i32, [ctypes.c_char_p, _i32, _i32, _u64, _u64, _p(_vp)]),
+    "vh_binner_set_ordinal_create": (_i32, [ctypes.c_char_p, _vp, _u64, _p(_vp)]),
+    "vh_binner_copy": (_i32, [_vp, _p(_vp)]),
+    "vh_binner_destroy": (_i32, [_vp]),
+    "vh_binner_set_data": (_i32, [_vp, _vp, _u64, _i32, _i32, _i32]),
+    "vh_binner_set_data_mask": (_i32, [_vp, _vp, _u64, _i32, _i32]),
+    "vh_binner_clear_data_mask": (_i32, [_vp]),
+    "vh_binner_shape": (_i32, [_vp, _p(_u64)]),
+    "vh_binner_size": (_i32, [_vp, _p(_u64)]),
+    "vh_grid_create": (_i32, [_p(_vp), _i32, _p(_vp)]),
+    "vh_grid_destroy": (_i32, [_vp]),
+    "vh_grid_info": (_i32, [_vp, _p(_i32), _p(_u64), _p(_u64), _p(_u64)]),
+    "vh_grid_bin": (_i32, [_vp, _p(_vp), _i32, _u64, _i32]),
+    "vh_agg_create": (_i32, [_vp, _i32, _i32, _i32, ctypes.c_uint32, _p(_vp)]),
+    "vh_agg_destroy": (_i32, [_vp]),
+    "vh_agg_set_data": (_i32, [_vp, _vp, _u64, _i32, _i32, _i32, _i32]),
+    "vh_agg_set_data_mask": (_i32, [_vp, _vp, _u64, _i32, _i32]),
+    "vh_agg_clear_data_mask": (_i32, [_vp]),
+    "vh_agg_info": (_i32, [_vp, _p(_u64), _p(_i32), _p(_u64)]),
+    "vh_agg_download": (_i32, [_vp, _vp, _u64]),
+    "vh_agg_upload": (_i32, [_vp, _vp, _u64]),
+    "vh_agg_download_order": (_i32, [_vp, _vp, _u64]),
+    "vh_agg_device_ptr": (_i32, [_vp, _p(_vp), _p(_vp)]),
+    "vh_agg_reduce": (_i32, [_vp, _p(_vp), _i32]),
+    "vh_set_create": (_i32, [_i32, _p(_vp)]),
+    "vh_set_destroy": (_i32, [_vp]),
+    "vh_set_update": (_i32, [_vp, _vp, _vp, _u64, _i32]),
+    "vh_set_seal": (_i32, [_vp]),
+    "vh_set_info": (_i32, [_vp, _p(_i64), _p(_i64), _p(_i64), _p(_i64), _p(_i64)]),
+    "vh_set_key_array": (_i32, [_vp, _vp]),
+    "vh_set_map_ordinal": (_i32, [_vp, _vp, _u64, _i32, _vp, _i32, _i32]),
+    "vh_minmax": (_i32, [_vp, _u64, _i32, _i32, _vp, _i32, _p(_dbl), _p(_dbl)]),
+}
+
+_lib = None
+
+
+class HipError(RuntimeError):
+    """A failed libvaexhip call (the reference raises RuntimeError from its C++ too)."""
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: the HIP library must be built "
+                "(python -c 'import __graft_entry__ as g; g.build()' or make -C vaex_amd/csrc)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        if L.vh_abi_version() != 1:
+            raise ImportError("libvaexhip ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().vh_last_error().decode(errors="replace")
+        raise HipError(msg)
+
+
+def call(name, *args):
+    check(getattr(lib(), name)(*args))
+
+
+def dtype_code(dtype):
+    """(code, flip_endian) of a numpy dtype (find_type_from_dtype, utils.py:879-903:
+    datetime/timedelta bin as int64, non-native byte order -> *_non_native)."""
+    dt = np.dtype(dtype)
+    flip = dt.byteorder not in ("<", "=", "|")
+    native = dt.newbyteorder("=") if flip else dt
+    if native.kind in "mM":
+        name = "int64"
+    else:
+        name = native.name
+    if name not in DTYPE_CODE:
+        raise ValueError(f"dtype {dt} is not supported")
+    return DTYPE_CODE[name], int(flip)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(lib().vh_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def synchronize():
+    call("vh_synchronize")
+
+
+def timing_enable(on=True):
+    call("vh_timing_enable", int(bool(on)))
+
+
+def timing_reset():
+    call("vh_timing_reset")
+
+
+def timing_read(kernel):
+    n, ms = ctypes.c_uint64(), ctypes.c_double()
+    call("vh_timing_read", kernel.encode(), ctypes.byref(n), ctypes.byref(ms))
+    return n.value, ms.value

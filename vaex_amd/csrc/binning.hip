@@ -1,0 +1,907 @@
+// Grid / Binner / Aggregator engine of libvaexhip.so -- the MI355X (gfx950)
+// realisation of vaex-core's superagg module:
+//   Grid<>::bin / bin_            packages/vaex-core/src/agg.hpp:76-136
+//   BinnerScalar / BinnerOrdinal  packages/vaex-core/src/superagg_binners.cpp:5-184
+//   AggCount/Sum/Min/Max/First/SumMoment  packages/vaex-core/src/superagg.cpp:155-511
+//
+// Execution:
+//  * fused path -- binner index math in registers, no indices1d round trip;
+//    count/sum aggregators accumulate into LDS-privatised per-workgroup grids
+//    when the grid fits (small grids), otherwise into tile-partitioned LDS
+//    sub-grids (tiled.hip) or global atomics;
+//  * generic path -- any binner/aggregator/dtype mix: an index kernel writes
+//    indices1d for a chunk of rows, then one kernel per aggregator.
+// Host (numpy) columns are staged to HBM chunk by chunk; HBM columns are read
+// in place.
+#include <limits>
+#include <memory>
+
+#include "common.hpp"
+#include "engine.hpp"
+#include "binner_dev.hpp"
+#include "hashset.hpp"
+
+using namespace vh;
+
+// ============================================================================
+// host objects
+// ============================================================================
+struct vh_binner {
+    int kind = 0;  // 0 scalar, 1 ordinal, 2 set-ordinal
+    std::string expression;
+    int dtype = VH_F64;
+    int flip = 0;
+    double vmin = 0, vmax = 0;
+    uint64_t bins = 0;
+    uint64_t ordinal_count = 0, min_value = 0;
+    vh_set *set = nullptr;
+    ColumnRef data, mask;
+    uint64_t shape() const { return (kind == 0 ? bins : ordinal_count) + 3; }
+};
+
+struct vh_grid {
+    std::vector<vh_binner *> binners;
+    std::vector<uint64_t> shapes, strides;
+    uint64_t length1d = 1;
+    Workspace ws;
+};
+
+struct vh_agg {
+    vh_grid *grid = nullptr;
+    int kind = 0, dtype = VH_F64, flip = 0;
+    uint32_t moment = 0;
+    int grid_dtype = VH_I64;
+    int grid_isz = 8;
+    DevBuf g, g2;          // grid, AggFirst order grid
+    DevBuf s_key, s_row;   // AggFirst per-chunk scratch
+    ColumnRef data, data2, mask;
+};
+
+namespace vh {
+
+// ============================================================================
+// device: binner index math
+// ============================================================================
+// ============================================================================
+// device: generic path
+// ============================================================================
+__global__ __launch_bounds__(256) void k_indices(BinPlan p, uint64_t n, uint64_t *idx) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        idx[i] = plan_index(p, i);
+}
+
+template <typename T> __device__ inline void atomic_add_grid(T *addr, T v);
+template <> __device__ inline void atomic_add_grid<double>(double *a, double v) { atomicAdd(a, v); }
+template <> __device__ inline void atomic_add_grid<int64_t>(int64_t *a, int64_t v) {
+    atomicAdd((unsigned long long *)a, (unsigned long long)v);
+}
+template <> __device__ inline void atomic_add_grid<uint64_t>(uint64_t *a, uint64_t v) {
+    atomicAdd((unsigned long long *)a, (unsigned long long)v);
+}
+
+// exact std::min/std::max(value, grid) semantics (superagg.cpp:226,274) with CAS
+template <typename T> __device__ inline T minmax_apply(T g, T value, bool is_max) {
+    return is_max ? ((value < g) ? g : value) : ((g < value) ? g : value);
+}
+
+template <typename T> __device__ inline void atomic_minmax(T *addr, T value, bool is_max) {
+    if constexpr (sizeof(T) == 8 || sizeof(T) == 4) {
+        using W = typename std::conditional<sizeof(T) == 8, unsigned long long, unsigned int>::type;
+        W *a = reinterpret_cast<W *>(addr);
+        W old = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (;;) {
+            T g;
+            __builtin_memcpy(&g, &old, sizeof(T));
+            T nv = minmax_apply(g, value, is_max);
+            W nb;
+            __builtin_memcpy(&nb, &nv, sizeof(T));
+            if (nb == old) return;
+            W prev = atomicCAS(a, old, nb);
+            if (prev == old) return;
+            old = prev;
+        }
+    } else {
+        uintptr_t addr_u = reinterpret_cast<uintptr_t>(addr);
+        unsigned int *word = reinterpret_cast<unsigned int *>(addr_u & ~(uintptr_t)3);
+        const unsigned shift = (unsigned)(addr_u & 3) * 8;
+        const unsigned mask = (sizeof(T) == 2 ? 0xffffu : 0xffu) << shift;
+        unsigned int old = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (;;) {
+            unsigned cur_bits = (old & mask) >> shift;
+            T g;
+            if constexpr (sizeof(T) == 2) {
+                uint16_t cb = (uint16_t)cur_bits;
+                __builtin_memcpy(&g, &cb, 2);
+            } else {
+                uint8_t cb = (uint8_t)cur_bits;
+                __builtin_memcpy(&g, &cb, 1);
+            }
+            T nv = minmax_apply(g, value, is_max);
+            unsigned nbits;
+            if constexpr (sizeof(T) == 2) {
+                uint16_t t;
+                __builtin_memcpy(&t, &nv, 2);
+                nbits = t;
+            } else {
+                uint8_t t;
+                __builtin_memcpy(&t, &nv, 1);
+                nbits = t;
+            }
+            if (nbits == cur_bits) return;
+            unsigned int nw = (old & ~mask) | (nbits << shift);
+            unsigned int prev = atomicCAS(word, old, nw);
+            if (prev == old) return;
+            old = prev;
+        }
+    }
+}
+
+template <typename T> struct Upcast { using type = int64_t; };
+template <> struct Upcast<double> { using type = double; };
+template <> struct Upcast<float> { using type = double; };
+template <> struct Upcast<uint64_t> { using type = uint64_t; };
+template <> struct Upcast<uint32_t> { using type = uint64_t; };
+template <> struct Upcast<uint16_t> { using type = uint64_t; };
+template <> struct Upcast<uint8_t> { using type = uint64_t; };
+
+template <typename T> __device__ inline typename Upcast<T>::type upcast_v(T v) {
+    return (typename Upcast<T>::type)v;
+}
+template <> __device__ inline int64_t upcast_v<vbool>(vbool v) { return v.v ? 1 : 0; }
+
+// AggCount (superagg.cpp:168-191), AggSum (:362-388), AggMin/AggMax (:213-286),
+// AggSumMoment (:406-432) over one chunk of precomputed indices
+template <int KIND, typename T>
+__global__ __launch_bounds__(256) void k_agg(AggDev a, const uint64_t *idx, uint64_t n) {
+    using G = typename Upcast<T>::type;
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n;
+         j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = idx[j];
+        if constexpr (KIND == VH_AGG_COUNT) {
+            if (a.mask && a.mask[j] != 1) continue;
+            if (a.data) {
+                T v = load_v<T>(a.data, j, a.flip);
+                if (is_nan_v(v)) continue;
+            }
+            atomicAdd((unsigned long long *)a.grid + c, 1ULL);
+        } else if constexpr (KIND == VH_AGG_SUM) {
+            if (a.mask && a.mask[j] != 1) continue;
+            T v = load_v<T>(a.data, j, a.flip);
+            if (is_nan_v(v)) continue;
+            atomic_add_grid<G>(reinterpret_cast<G *>(a.grid) + c, upcast_v(v));
+        } else if constexpr (KIND == VH_AGG_MIN || KIND == VH_AGG_MAX) {
+            if (a.mask && a.mask[j] != 1) continue;
+            T v = load_v<T>(a.data, j, a.flip);
+            if (is_nan_v(v)) continue;
+            atomic_minmax<T>(reinterpret_cast<T *>(a.grid) + c, v, KIND == VH_AGG_MAX);
+        } else if constexpr (KIND == VH_AGG_SUM_MOMENT) {
+            if (a.mask && a.mask[j] != 1) continue;
+            // the reference converts to the upcast type first, then byte swaps (superagg.cpp:415-417)
+            G value = upcast_v(reinterpret_cast<const T *>(a.data)[j]);
+            if (a.flip) value = bswap_v(value);
+            if (is_nan_v(value)) continue;
+            double p;
+            if (a.moment == 0) p = 1.0;
+            else if (a.moment == 1) p = (double)value;
+            else if (a.moment == 2) p = (double)value * (double)value;
+            else p = pow((double)value, (double)a.moment);
+            atomic_add_grid<G>(reinterpret_cast<G *>(a.grid) + c, (G)p);
+        }
+    }
+}
+
+// AggFirst (superagg.cpp:481-505).  Per chunk: (A) min order key per cell,
+// (B) lowest row holding that key, (C) per cell: take it if strictly smaller
+// than the grid's order -- ties go to the earliest row, as a serial pass does.
+template <typename T> __device__ inline uint64_t order_key(T v) {
+    if constexpr (is_float_t<T>::value) {
+        double d = (double)v;
+        if (d == 0.0) d = 0.0;
+        uint64_t u;
+        __builtin_memcpy(&u, &d, 8);
+        return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
+    } else if constexpr (is_signed_int_t<T>::value) {
+        return (uint64_t)(int64_t)v ^ 0x8000000000000000ULL;
+    } else if constexpr (std::is_same<T, vbool>::value) {
+        return v.v;
+    } else {
+        return (uint64_t)v;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_first_a(AggDev a, const uint64_t *idx, uint64_t n) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n;
+         j += (uint64_t)gridDim.x * blockDim.x) {
+        T v = load_v<T>(a.data, j, a.flip), o = load_v<T>(a.data2, j, a.flip);
+        if (is_nan_v(v) || is_nan_v(o)) continue;
+        atomicMin((unsigned long long *)a.s_key + idx[j], (unsigned long long)order_key(o));
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_first_b(AggDev a, const uint64_t *idx, uint64_t n, uint64_t row0) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n;
+         j += (uint64_t)gridDim.x * blockDim.x) {
+        T v = load_v<T>(a.data, j, a.flip), o = load_v<T>(a.data2, j, a.flip);
+        if (is_nan_v(v) || is_nan_v(o)) continue;
+        const uint64_t c = idx[j];
+        if (order_key(o) == reinterpret_cast<const uint64_t *>(a.s_key)[c])
+            atomicMin((unsigned long long *)a.s_row + c, (unsigned long long)(row0 + j));
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_first_c(AggDev a, uint64_t cells, uint64_t row0) {
+    uint64_t *sk = reinterpret_cast<uint64_t *>(a.s_key);
+    uint64_t *sr = reinterpret_cast<uint64_t *>(a.s_row);
+    for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < cells;
+         c += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t r = sr[c];
+        if (r == ~0ULL) continue;
+        uint64_t j = r - row0;
+        T o = load_v<T>(a.data2, j, a.flip);
+        T v = load_v<T>(a.data, j, a.flip);
+        T *g = reinterpret_cast<T *>(a.grid);
+        T *g2 = reinterpret_cast<T *>(a.grid2);
+        if (o < g2[c]) {
+            g[c] = v;
+            g2[c] = o;
+        }
+        sk[c] = ~0ULL;
+        sr[c] = ~0ULL;
+    }
+}
+
+// ============================================================================
+// device: grid fill / reduce (Aggregator::reduce)
+// ============================================================================
+template <typename T> __global__ void k_fill(T *p, uint64_t n, T value) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        p[i] = value;
+}
+
+template <typename G> __global__ void k_reduce_add(G *dst, const G *src, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        dst[i] = dst[i] + src[i];
+}
+
+// std::max(this, other) / std::min(this, other) (superagg.cpp:209,256)
+template <typename T> __global__ void k_reduce_minmax(T *dst, const T *src, uint64_t n, int is_max) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        T a = dst[i], b = src[i];
+        dst[i] = is_max ? ((a < b) ? b : a) : ((b < a) ? b : a);
+    }
+}
+
+template <typename T>
+__global__ void k_reduce_first(T *dst, T *dst2, const T *src, const T *src2, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        if (src2[i] < dst2[i]) {
+            dst[i] = src[i];
+            dst2[i] = src2[i];
+        }
+    }
+}
+
+// ============================================================================
+// device: fused count/sum path (global atomics or LDS-privatised grid)
+// ============================================================================
+template <bool USE_LDS, int ND>
+__global__ __launch_bounds__(256) void k_fused(BinPlan p, FusedAggs fa, uint64_t n, uint64_t cells) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    if constexpr (USE_LDS) {
+        // zero the per-workgroup sub-grids
+        uint32_t *w = reinterpret_cast<uint32_t *>(lds_raw);
+        for (uint32_t i = threadIdx.x; i < fa.lds_words; i += blockDim.x) w[i] = 0;
+        __syncthreads();
+    }
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t c;
+        if constexpr (ND == 0) {
+            c = plan_index(p, i);
+        } else {
+            c = 0;
+#pragma unroll
+            for (int d = 0; d < ND; d++) c += scalar_index<double>(p.b[d], i) * p.b[d].stride;
+        }
+        for (int k = 0; k < fa.na; k++) {
+            const FusedAgg &a = fa.a[k];
+            if (a.mask && a.mask[i] != 1) continue;
+            if (a.kind == VH_AGG_COUNT) {
+                if (a.data && is_nan_v(a.data[i])) continue;
+                if constexpr (USE_LDS)
+                    atomicAdd(reinterpret_cast<uint32_t *>(lds_raw + a.lds_off) + c, 1u);
+                else
+                    atomicAdd((unsigned long long *)a.grid + c, 1ULL);
+            } else {
+                double v = a.data[i];
+                if (v != v) continue;
+                if constexpr (USE_LDS)
+                    atomicAdd(reinterpret_cast<double *>(lds_raw + a.lds_off) + c, v);
+                else
+                    atomicAdd(reinterpret_cast<double *>(a.grid) + c, v);
+            }
+        }
+    }
+    if constexpr (USE_LDS) {
+        __syncthreads();
+        for (int k = 0; k < fa.na; k++) {
+            const FusedAgg &a = fa.a[k];
+            for (uint64_t c = threadIdx.x; c < cells; c += blockDim.x) {
+                if (a.kind == VH_AGG_COUNT) {
+                    uint32_t v = reinterpret_cast<const uint32_t *>(lds_raw + a.lds_off)[c];
+                    if (v) atomicAdd((unsigned long long *)a.grid + c, (unsigned long long)v);
+                } else {
+                    double v = reinterpret_cast<const double *>(lds_raw + a.lds_off)[c];
+                    if (v != 0.0) atomicAdd(reinterpret_cast<double *>(a.grid) + c, v);
+                }
+            }
+        }
+    }
+}
+
+}  // namespace vh
+
+// ============================================================================
+// host helpers
+// ============================================================================
+namespace {
+
+void check_column(const ColumnRef &c, uint64_t length, const char *what) {
+    if (!c.set) fail(VH_ERR_RUNTIME, std::string(what) + " not set");
+    if (c.size < length)
+        fail(VH_ERR_RUNTIME, std::string(what) + " has " + std::to_string(c.size) + " rows, bin() asked for " +
+                                 std::to_string(length));
+}
+
+ColumnRef make_col(const void *ptr, uint64_t length, int itemsize, int loc) {
+    ColumnRef c;
+    c.ptr = ptr;
+    c.size = length;
+    c.itemsize = itemsize;
+    c.loc = resolve_loc(ptr, loc);
+    c.set = true;
+    return c;
+}
+
+template <typename T> void fill_grid(void *p, uint64_t n, T v) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_fill<T>, dim3(blocks_for(n, 256)), dim3(256), 0, stream(), (T *)p, n, v);
+    VH_HIP(hipGetLastError());
+}
+
+template <typename T> T minmax_fill(bool mx) {
+    if constexpr (std::is_same<T, vbool>::value) {
+        T v;
+        v.v = mx ? 0 : 1;
+        return v;
+    } else if constexpr (is_float_t<T>::value) {
+        return mx ? -std::numeric_limits<T>::infinity() : std::numeric_limits<T>::infinity();
+    } else {
+        return mx ? std::numeric_limits<T>::min() : std::numeric_limits<T>::max();
+    }
+}
+
+template <typename T> T max_fill() {
+    if constexpr (std::is_same<T, vbool>::value) {
+        T v;
+        v.v = 1;
+        return v;
+    } else {
+        return std::numeric_limits<T>::max();
+    }
+}
+
+void init_agg_grid(vh_agg *a) {
+    const uint64_t L = a->grid->length1d;
+    VH_HIP(hipMemsetAsync(a->g.ptr, 0, L * a->grid_isz, stream()));
+    if (a->kind == VH_AGG_MIN || a->kind == VH_AGG_MAX) {
+        // numeric_limits fill (superagg.cpp:199-204, 246-251)
+        const bool mx = a->kind == VH_AGG_MAX;
+        VH_DISPATCH_DTYPE(a->dtype, T, fill_grid<T>(a->g.ptr, L, minmax_fill<T>(mx)));
+    } else if (a->kind == VH_AGG_FIRST) {
+        // order grid = numeric_limits<T>::max() (superagg.cpp:441-445), data grid 0
+        VH_DISPATCH_DTYPE(a->dtype, T, fill_grid<T>(a->g2.ptr, L, max_fill<T>()));
+        VH_HIP(hipMemsetAsync(a->s_key.ptr, 0xff, L * 8, stream()));
+        VH_HIP(hipMemsetAsync(a->s_row.ptr, 0xff, L * 8, stream()));
+    }
+    VH_HIP(hipStreamSynchronize(stream()));
+}
+
+// chunk-relative device pointer of a column, staging host columns into the workspace
+struct Stager {
+    Workspace &ws;
+    uint64_t row0 = 0, len = 0;
+    int slot = 0;
+    const void *get(const ColumnRef &c) {
+        if (!c.set) return nullptr;
+        const char *base = reinterpret_cast<const char *>(c.ptr) + row0 * c.itemsize;
+        if (c.loc == VH_LOC_DEVICE) return base;
+        DevBuf &b = ws.stage_buf(slot++, len * c.itemsize);
+        VH_HIP(hipMemcpyAsync(b.ptr, base, len * c.itemsize, hipMemcpyHostToDevice, stream()));
+        return b.ptr;
+    }
+};
+
+}  // namespace
+
+namespace vh {
+Workspace::~Workspace() = default;
+
+DevBuf &Workspace::stage_buf(int slot, uint64_t bytes) {
+    while ((int)stage.size() <= slot) stage.emplace_back(new DevBuf());
+    stage[slot]->ensure(bytes);
+    return *stage[slot];
+}
+}  // namespace vh
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int vh_binner_scalar_create(const char *expression, int dtype, int flip, double vmin, double vmax,
+                            uint64_t bins, vh_binner **out) {
+    VH_API_BEGIN
+    dtype_itemsize(dtype);
+    auto *b = new vh_binner();
+    b->kind = 0;
+    b->expression = expression ? expression : "";
+    b->dtype = dtype;
+    b->flip = flip ? 1 : 0;
+    b->vmin = vmin;
+    b->vmax = vmax;
+    b->bins = bins;
+    *out = b;
+    VH_API_END
+}
+
+int vh_binner_ordinal_create(const char *expression, int dtype, int flip, uint64_t ordinal_count,
+                             uint64_t min_value, vh_binner **out) {
+    VH_API_BEGIN
+    dtype_itemsize(dtype);
+    auto *b = new vh_binner();
+    b->kind = 1;
+    b->expression = expression ? expression : "";
+    b->dtype = dtype;
+    b->flip = flip ? 1 : 0;
+    b->ordinal_count = ordinal_count;
+    b->min_value = min_value;
+    *out = b;
+    VH_API_END
+}
+
+int vh_binner_set_ordinal_create(const char *expression, vh_set *set, uint64_t ordinal_count,
+                                 vh_binner **out) {
+    VH_API_BEGIN
+    if (!set) fail(VH_ERR_ARG, "set is NULL");
+    auto *b = new vh_binner();
+    b->kind = 2;
+    b->expression = expression ? expression : "";
+    b->dtype = set_dtype(set);
+    b->set = set;
+    b->ordinal_count = ordinal_count;
+    *out = b;
+    VH_API_END
+}
+
+int vh_binner_copy(const vh_binner *binner, vh_binner **out) {
+    VH_API_BEGIN
+    *out = new vh_binner(*binner);
+    VH_API_END
+}
+
+int vh_binner_destroy(vh_binner *binner) {
+    VH_API_BEGIN
+    delete binner;
+    VH_API_END
+}
+
+int vh_binner_set_data(vh_binner *b, const void *ptr, uint64_t length, int itemsize, int ndim, int loc) {
+    VH_API_BEGIN
+    if (ndim != 1) fail(VH_ERR_RUNTIME, "Expected a 1d array");
+    if (itemsize != dtype_itemsize(b->dtype)) fail(VH_ERR_RUNTIME, "Itemsize of data and binner are not equal");
+    b->data = make_col(ptr, length, itemsize, loc);
+    VH_API_END
+}
+
+int vh_binner_set_data_mask(vh_binner *b, const uint8_t *mask, uint64_t length, int ndim, int loc) {
+    VH_API_BEGIN
+    if (ndim != 1) fail(VH_ERR_RUNTIME, "Expected a 1d array");
+    b->mask = make_col(mask, length, 1, loc);
+    VH_API_END
+}
+
+int vh_binner_clear_data_mask(vh_binner *b) {
+    VH_API_BEGIN
+    b->mask = ColumnRef();
+    VH_API_END
+}
+
+int vh_binner_shape(const vh_binner *b, uint64_t *shape) {
+    VH_API_BEGIN
+    *shape = b->shape();
+    VH_API_END
+}
+
+int vh_binner_size(const vh_binner *b, uint64_t *size) {
+    VH_API_BEGIN
+    *size = b->data.set ? b->data.size : 0;
+    VH_API_END
+}
+
+int vh_grid_create(vh_binner *const *binners, int nbinners, vh_grid **out) {
+    VH_API_BEGIN
+    if (nbinners < 0 || nbinners > MAX_DIM) fail(VH_ERR_ARG, "at most 16 binners (agg.hpp:25)");
+    auto *g = new vh_grid();
+    g->length1d = 1;
+    for (int i = 0; i < nbinners; i++) {
+        g->binners.push_back(binners[i]);
+        g->shapes.push_back(binners[i]->shape());
+        g->length1d *= binners[i]->shape();
+    }
+    g->strides.resize(nbinners);
+    if (nbinners > 0) {
+        g->strides[0] = 1;  // agg.hpp:64-69, first binner varies fastest
+        for (int i = 1; i < nbinners; i++) g->strides[i] = g->strides[i - 1] * g->shapes[i - 1];
+    }
+    *out = g;
+    VH_API_END
+}
+
+int vh_grid_destroy(vh_grid *g) {
+    VH_API_BEGIN
+    if (g) (void)hipStreamSynchronize(stream());
+    delete g;
+    VH_API_END
+}
+
+int vh_grid_info(const vh_grid *g, int *dims, uint64_t *shapes, uint64_t *strides, uint64_t *length1d) {
+    VH_API_BEGIN
+    if (dims) *dims = (int)g->binners.size();
+    for (size_t i = 0; i < g->binners.size(); i++) {
+        if (shapes) shapes[i] = g->shapes[i];
+        if (strides) strides[i] = g->strides[i];
+    }
+    if (length1d) *length1d = g->length1d;
+    VH_API_END
+}
+
+int vh_agg_create(vh_grid *grid, int kind, int dtype, int flip, uint32_t arg, vh_agg **out) {
+    VH_API_BEGIN
+    if (kind < VH_AGG_COUNT || kind > VH_AGG_SUM_MOMENT) fail(VH_ERR_ARG, "unknown aggregator kind");
+    dtype_itemsize(dtype);
+    std::unique_ptr<vh_agg> a(new vh_agg());
+    a->grid = grid;
+    a->kind = kind;
+    a->dtype = dtype;
+    a->flip = flip ? 1 : 0;
+    a->moment = arg;
+    switch (kind) {
+    case VH_AGG_COUNT: a->grid_dtype = VH_I64; break;
+    case VH_AGG_SUM: case VH_AGG_SUM_MOMENT: a->grid_dtype = upcast_dtype(dtype); break;
+    default: a->grid_dtype = dtype;
+    }
+    a->grid_isz = dtype_itemsize(a->grid_dtype);
+    const uint64_t L = grid->length1d;
+    a->g.ensure(L * a->grid_isz);
+    if (kind == VH_AGG_FIRST) {
+        a->g2.ensure(L * a->grid_isz);
+        a->s_key.ensure(L * 8);
+        a->s_row.ensure(L * 8);
+    }
+    init_agg_grid(a.get());
+    *out = a.release();
+    VH_API_END
+}
+
+int vh_agg_destroy(vh_agg *a) {
+    VH_API_BEGIN
+    if (a) (void)hipStreamSynchronize(stream());
+    delete a;
+    VH_API_END
+}
+
+int vh_agg_set_data(vh_agg *a, const void *ptr, uint64_t length, int itemsize, int ndim, int index, int loc) {
+    VH_API_BEGIN
+    if (ndim != 1) fail(VH_ERR_RUNTIME, "Expected a 1d array");
+    if (itemsize != dtype_itemsize(a->dtype))
+        fail(VH_ERR_RUNTIME, "Itemsize of data and aggregator are not equal");
+    if (a->kind == VH_AGG_FIRST && index == 1) a->data2 = make_col(ptr, length, itemsize, loc);
+    else a->data = make_col(ptr, length, itemsize, loc);
+    VH_API_END
+}
+
+int vh_agg_set_data_mask(vh_agg *a, const uint8_t *mask, uint64_t length, int ndim, int loc) {
+    VH_API_BEGIN
+    if (ndim != 1) fail(VH_ERR_RUNTIME, "Expected a 1d array");
+    a->mask = make_col(mask, length, 1, loc);
+    VH_API_END
+}
+
+int vh_agg_clear_data_mask(vh_agg *a) {
+    VH_API_BEGIN
+    a->mask = ColumnRef();
+    VH_API_END
+}
+
+int vh_agg_info(const vh_agg *a, uint64_t *bytes, int *grid_dtype, uint64_t *itemsize) {
+    VH_API_BEGIN
+    if (bytes) *bytes = a->grid->length1d * a->grid_isz;
+    if (grid_dtype) *grid_dtype = a->grid_dtype;
+    if (itemsize) *itemsize = a->grid_isz;
+    VH_API_END
+}
+
+int vh_agg_download(vh_agg *a, void *host, uint64_t bytes) {
+    VH_API_BEGIN
+    if (bytes != a->grid->length1d * a->grid_isz) fail(VH_ERR_ARG, "download size mismatch");
+    VH_HIP(hipMemcpyAsync(host, a->g.ptr, bytes, hipMemcpyDeviceToHost, stream()));
+    VH_HIP(hipStreamSynchronize(stream()));
+    VH_API_END
+}
+
+int vh_agg_download_order(vh_agg *a, void *host, uint64_t bytes) {
+    VH_API_BEGIN
+    if (a->kind != VH_AGG_FIRST) fail(VH_ERR_ARG, "not an AggFirst");
+    if (bytes != a->grid->length1d * a->grid_isz) fail(VH_ERR_ARG, "download size mismatch");
+    VH_HIP(hipMemcpyAsync(host, a->g2.ptr, bytes, hipMemcpyDeviceToHost, stream()));
+    VH_HIP(hipStreamSynchronize(stream()));
+    VH_API_END
+}
+
+int vh_agg_upload(vh_agg *a, const void *host, uint64_t bytes) {
+    VH_API_BEGIN
+    if (bytes != a->grid->length1d * a->grid_isz) fail(VH_ERR_ARG, "upload size mismatch");
+    VH_HIP(hipMemcpyAsync(a->g.ptr, host, bytes, hipMemcpyHostToDevice, stream()));
+    VH_HIP(hipStreamSynchronize(stream()));
+    VH_API_END
+}
+
+int vh_agg_device_ptr(vh_agg *a, void **grid_dptr, void **grid2_dptr) {
+    VH_API_BEGIN
+    if (grid_dptr) *grid_dptr = a->g.ptr;
+    if (grid2_dptr) *grid2_dptr = a->g2.ptr;
+    VH_API_END
+}
+
+int vh_agg_reduce(vh_agg *a, vh_agg *const *others, int nothers) {
+    VH_API_BEGIN
+    const uint64_t L = a->grid->length1d;
+    for (int k = 0; k < nothers; k++) {
+        vh_agg *o = others[k];
+        if (o->kind != a->kind || o->dtype != a->dtype || o->grid->length1d != L)
+            fail(VH_ERR_RUNTIME, "cannot reduce aggregators of different type or grid");
+        if (!L) continue;
+        dim3 grd(blocks_for(L, 256)), blk(256);
+        switch (a->kind) {
+        case VH_AGG_COUNT:
+            hipLaunchKernelGGL(k_reduce_add<int64_t>, grd, blk, 0, stream(), a->g.as<int64_t>(), o->g.as<int64_t>(), L);
+            break;
+        case VH_AGG_SUM: case VH_AGG_SUM_MOMENT:
+            if (a->grid_dtype == VH_F64)
+                hipLaunchKernelGGL(k_reduce_add<double>, grd, blk, 0, stream(), a->g.as<double>(), o->g.as<double>(), L);
+            else if (a->grid_dtype == VH_I64)
+                hipLaunchKernelGGL(k_reduce_add<int64_t>, grd, blk, 0, stream(), a->g.as<int64_t>(), o->g.as<int64_t>(), L);
+            else
+                hipLaunchKernelGGL(k_reduce_add<uint64_t>, grd, blk, 0, stream(), a->g.as<uint64_t>(), o->g.as<uint64_t>(), L);
+            break;
+        case VH_AGG_MIN: case VH_AGG_MAX:
+            VH_DISPATCH_DTYPE(a->dtype, T,
+                              hipLaunchKernelGGL(k_reduce_minmax<T>, grd, blk, 0, stream(), a->g.as<T>(),
+                                                 o->g.as<T>(), L, (int)(a->kind == VH_AGG_MAX)));
+            break;
+        case VH_AGG_FIRST:
+            VH_DISPATCH_DTYPE(a->dtype, T,
+                              hipLaunchKernelGGL(k_reduce_first<T>, grd, blk, 0, stream(), a->g.as<T>(),
+                                                 a->g2.as<T>(), o->g.as<T>(), o->g2.as<T>(), L));
+            break;
+        }
+        VH_HIP(hipGetLastError());
+    }
+    VH_HIP(hipStreamSynchronize(stream()));
+    VH_API_END
+}
+
+int vh_grid_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length, int has_length) {
+    VH_API_BEGIN
+    if (!has_length) {
+        if (g->binners.empty()) fail(VH_ERR_RUNTIME, "no binners set and no length given");
+        if (!g->binners[0]->data.set) fail(VH_ERR_RUNTIME, "data not set");
+        length = g->binners[0]->data.size;
+    }
+    for (auto *b : g->binners) {
+        check_column(b->data, length, "binner data");
+        if (b->mask.set) check_column(b->mask, length, "binner mask");
+    }
+    for (int k = 0; k < naggs; k++) {
+        vh_agg *a = aggs[k];
+        if (a->grid != g) fail(VH_ERR_RUNTIME, "aggregator belongs to another grid");
+        const bool needs_data = a->kind != VH_AGG_COUNT;
+        if (needs_data && !a->data.set) fail(VH_ERR_RUNTIME, "data not set");
+        if (a->kind == VH_AGG_FIRST && !a->data2.set) fail(VH_ERR_RUNTIME, "data2 not set");
+        if (a->data.set) check_column(a->data, length, "aggregator data");
+        if (a->data2.set) check_column(a->data2, length, "aggregator data2");
+        if (a->mask.set) check_column(a->mask, length, "aggregator mask");
+    }
+    if (length == 0 || naggs == 0) return VH_OK;
+    run_bin(g, aggs, naggs, length);
+    VH_API_END
+}
+
+}  // extern "C"
+
+// ============================================================================
+// the bin driver
+// ============================================================================
+namespace vh {
+
+static BinnerDev binner_dev(vh_binner *b, uint64_t stride, Stager &st) {
+    BinnerDev d{};
+    d.kind = b->kind;
+    d.dtype = b->dtype;
+    d.flip = b->flip;
+    d.data = st.get(b->data);
+    d.mask = reinterpret_cast<const uint8_t *>(st.get(b->mask));
+    d.vmin = b->vmin;
+    d.scale = 1. / (b->vmax - b->vmin);  // scale_v, superagg_binners.cpp:15
+    d.bins = b->bins;
+    d.ordinal_count = b->ordinal_count;
+    d.min_value = b->min_value;
+    d.stride = stride;
+    if (b->kind == 2) d.set = set_device_view(b->set);
+    return d;
+}
+
+static AggDev agg_dev(vh_agg *a, Stager &st) {
+    AggDev d{};
+    d.kind = a->kind;
+    d.dtype = a->dtype;
+    d.flip = a->flip;
+    d.moment = a->moment;
+    d.data = st.get(a->data);
+    d.data2 = st.get(a->data2);
+    d.mask = reinterpret_cast<const uint8_t *>(st.get(a->mask));
+    d.grid = a->g.ptr;
+    d.grid2 = a->g2.ptr;
+    d.s_key = a->s_key.ptr;
+    d.s_row = a->s_row.ptr;
+    return d;
+}
+
+// count (any data dtype=f64 or none) / sum(float64), native byte order
+static bool fusable(vh_agg *a) {
+    if (a->kind == VH_AGG_COUNT) return !a->data.set || (a->dtype == VH_F64 && !a->flip);
+    if (a->kind == VH_AGG_SUM) return a->dtype == VH_F64 && !a->flip;
+    return false;
+}
+
+static int scalar_f64_dims(vh_grid *g) {
+    for (auto *b : g->binners)
+        if (!(b->kind == 0 && b->dtype == VH_F64 && !b->flip)) return 0;
+    return (int)g->binners.size();
+}
+
+void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
+    bool all_fusable = naggs <= MAX_FUSED_AGGS;
+    for (int k = 0; k < naggs && all_fusable; k++) all_fusable = fusable(aggs[k]);
+    bool any_host = false;
+    auto note = [&](const ColumnRef &c) { any_host |= c.set && c.loc == VH_LOC_HOST; };
+    for (auto *b : g->binners) {
+        note(b->data);
+        note(b->mask);
+    }
+    for (int k = 0; k < naggs; k++) {
+        note(aggs[k]->data);
+        note(aggs[k]->data2);
+        note(aggs[k]->mask);
+    }
+    const uint64_t L = g->length1d;
+    const uint64_t chunk_max = any_host ? (uint64_t(1) << 24) : (all_fusable ? length : (uint64_t(1) << 26));
+    for (uint64_t row0 = 0; row0 < length; row0 += chunk_max) {
+        const uint64_t len = std::min(chunk_max, length - row0);
+        Stager st{g->ws, row0, len, 0};
+        BinPlan plan{};
+        plan.nb = (int)g->binners.size();
+        for (int d = 0; d < plan.nb; d++) plan.b[d] = binner_dev(g->binners[d], g->strides[d], st);
+        if (all_fusable) {
+            FusedAggs fa{};
+            fa.na = naggs;
+            for (int k = 0; k < naggs; k++) {
+                AggDev ad = agg_dev(aggs[k], st);
+                fa.a[k].kind = ad.kind;
+                fa.a[k].data = reinterpret_cast<const double *>(ad.data);
+                fa.a[k].mask = ad.mask;
+                fa.a[k].grid = ad.grid;
+            }
+            launch_fused(plan, fa, len, L, scalar_f64_dims(g), g->ws);
+        } else {
+            std::vector<AggDev> ads;
+            for (int k = 0; k < naggs; k++) ads.push_back(agg_dev(aggs[k], st));
+            g->ws.idx.ensure(len * 8);
+            uint64_t *idx = g->ws.idx.as<uint64_t>();
+            {
+                TimedScope ts("bin_indices");
+                hipLaunchKernelGGL(k_indices, dim3(blocks_for(len, 256)), dim3(256), 0, stream(), plan, len, idx);
+                VH_HIP(hipGetLastError());
+            }
+            for (int k = 0; k < naggs; k++) {
+                AggDev &ad = ads[k];
+                dim3 grd(blocks_for(len, 256)), blk(256);
+                TimedScope ts("bin_aggregate");
+                switch (ad.kind) {
+                case VH_AGG_COUNT:
+                    VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg<VH_AGG_COUNT, T>), grd, blk, 0, stream(), ad, idx, len));
+                    break;
+                case VH_AGG_SUM:
+                    VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg<VH_AGG_SUM, T>), grd, blk, 0, stream(), ad, idx, len));
+                    break;
+                case VH_AGG_MIN:
+                    VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg<VH_AGG_MIN, T>), grd, blk, 0, stream(), ad, idx, len));
+                    break;
+                case VH_AGG_MAX:
+                    VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg<VH_AGG_MAX, T>), grd, blk, 0, stream(), ad, idx, len));
+                    break;
+                case VH_AGG_SUM_MOMENT:
+                    VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg<VH_AGG_SUM_MOMENT, T>), grd, blk, 0, stream(), ad, idx, len));
+                    break;
+                case VH_AGG_FIRST:
+                    VH_DISPATCH_DTYPE(ad.dtype, T, {
+                        hipLaunchKernelGGL(k_first_a<T>, grd, blk, 0, stream(), ad, idx, len);
+                        hipLaunchKernelGGL(k_first_b<T>, grd, blk, 0, stream(), ad, idx, len, row0);
+                        hipLaunchKernelGGL(k_first_c<T>, dim3(blocks_for(L, 256)), blk, 0, stream(), ad, L, row0);
+                    });
+                    break;
+                }
+                VH_HIP(hipGetLastError());
+            }
+        }
+        if (any_host) VH_HIP(hipStreamSynchronize(stream()));  // staging buffers are reused
+    }
+    VH_HIP(hipStreamSynchronize(stream()));
+}
+
+void launch_fused(const BinPlan &plan, FusedAggs &fa, uint64_t n, uint64_t cells, int nd_f64, Workspace &ws) {
+    // LDS-privatised sub-grids when every aggregator's grid fits (u32 counts, f64 sums)
+    uint64_t off = 0;
+    for (int k = 0; k < fa.na; k++) {
+        off = (off + 7) & ~uint64_t(7);
+        fa.a[k].lds_off = (uint32_t)off;
+        off += cells * (fa.a[k].kind == VH_AGG_COUNT ? 4 : 8);
+    }
+    const uint64_t lds_bytes = (off + 15) & ~uint64_t(15);
+    const bool use_lds = lds_bytes <= LDS_FUSED_MAX && cells > 0;
+    fa.lds_words = (uint32_t)(lds_bytes / 4);
+    if (!use_lds && try_tiled(plan, fa, n, cells, nd_f64, ws)) return;
+    const int per_cu = use_lds ? (int)std::max<uint64_t>(1, std::min<uint64_t>(8, (64 * 1024) / std::max<uint64_t>(lds_bytes, 1))) : 8;
+    dim3 grd(blocks_for(n, 256, per_cu)), blk(256);
+    const size_t shm = use_lds ? lds_bytes : 0;
+    TimedScope ts(use_lds ? "bin_fused_lds" : "bin_fused_global");
+#define VH_LAUNCH_FUSED(LDS, ND) hipLaunchKernelGGL((k_fused<LDS, ND>), grd, blk, shm, stream(), plan, fa, n, cells)
+    if (use_lds) {
+        switch (nd_f64) {
+        case 1: VH_LAUNCH_FUSED(true, 1); break;
+        case 2: VH_LAUNCH_FUSED(true, 2); break;
+        case 3: VH_LAUNCH_FUSED(true, 3); break;
+        default: VH_LAUNCH_FUSED(true, 0);
+        }
+    } else {
+        switch (nd_f64) {
+        case 1: VH_LAUNCH_FUSED(false, 1); break;
+        case 2: VH_LAUNCH_FUSED(false, 2); break;
+        case 3: VH_LAUNCH_FUSED(false, 3); break;
+        default: VH_LAUNCH_FUSED(false, 0);
+        }
+    }
+#undef VH_LAUNCH_FUSED
+    VH_HIP(hipGetLastError());
+}
+
+}  // namespace vh

@@ -1,0 +1,200 @@
+// Shared plumbing for libvaexhip.so: error state, dtype traits, the library
+// stream, kernel timing, launch helpers.  gfx950 only (wave64, 256 CUs).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/vaexhip.h"
+
+namespace vh {
+
+// ---- errors --------------------------------------------------------------
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+void set_error(const char *fmt, ...);
+void set_error_str(const std::string &s);
+
+[[noreturn]] inline void fail(int code, const std::string &msg) { throw Error(code, msg); }
+
+#define VH_HIP(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            ::vh::fail(VH_ERR_HIP, std::string("HIP error '") + hipGetErrorString(e_) +     \
+                                       "' in " #expr " at " __FILE__ ":" +                  \
+                                       std::to_string(__LINE__));                           \
+    } while (0)
+
+// every C entry point: translate exceptions into status codes + last error
+#define VH_API_BEGIN try {
+#define VH_API_END                                                                          \
+    return VH_OK;                                                                           \
+    }                                                                                       \
+    catch (const ::vh::Error &e) {                                                          \
+        ::vh::set_error_str(e.what());                                                      \
+        return e.code;                                                                      \
+    }                                                                                       \
+    catch (const std::bad_alloc &) {                                                        \
+        ::vh::set_error_str("out of host memory");                                          \
+        return VH_ERR_NOMEM;                                                                \
+    }                                                                                       \
+    catch (const std::exception &e) {                                                       \
+        ::vh::set_error_str(e.what());                                                      \
+        return VH_ERR_RUNTIME;                                                              \
+    }
+
+// ---- dtypes ---------------------------------------------------------------
+// numpy bool is one byte holding 0 or 1
+struct vbool {
+    uint8_t v;
+};
+
+inline int dtype_itemsize(int dtype) {
+    switch (dtype) {
+    case VH_F64: case VH_I64: case VH_U64: return 8;
+    case VH_F32: case VH_I32: case VH_U32: return 4;
+    case VH_I16: case VH_U16: return 2;
+    case VH_I8: case VH_U8: case VH_BOOL: return 1;
+    }
+    fail(VH_ERR_ARG, "unknown dtype code " + std::to_string(dtype));
+}
+
+// upcast<T> (superagg.cpp:289-346) as dtype codes
+inline int upcast_dtype(int dtype) {
+    switch (dtype) {
+    case VH_F64: case VH_F32: return VH_F64;
+    case VH_I64: case VH_I32: case VH_I16: case VH_I8: case VH_BOOL: return VH_I64;
+    default: return VH_U64;
+    }
+}
+
+#define VH_DISPATCH_DTYPE(code, T, ...)                                                     \
+    switch (code) {                                                                         \
+    case VH_F64: { using T = double; __VA_ARGS__; break; }                                  \
+    case VH_F32: { using T = float; __VA_ARGS__; break; }                                   \
+    case VH_I64: { using T = int64_t; __VA_ARGS__; break; }                                 \
+    case VH_I32: { using T = int32_t; __VA_ARGS__; break; }                                 \
+    case VH_I16: { using T = int16_t; __VA_ARGS__; break; }                                 \
+    case VH_I8: { using T = int8_t; __VA_ARGS__; break; }                                   \
+    case VH_U64: { using T = uint64_t; __VA_ARGS__; break; }                                \
+    case VH_U32: { using T = uint32_t; __VA_ARGS__; break; }                                \
+    case VH_U16: { using T = uint16_t; __VA_ARGS__; break; }                                \
+    case VH_U8: { using T = uint8_t; __VA_ARGS__; break; }                                  \
+    case VH_BOOL: { using T = ::vh::vbool; __VA_ARGS__; break; }                            \
+    default: ::vh::fail(VH_ERR_ARG, "unknown dtype code");                                  \
+    }
+
+// ---- device-side helpers ---------------------------------------------------
+template <typename T> struct is_float_t { static constexpr bool value = false; };
+template <> struct is_float_t<double> { static constexpr bool value = true; };
+template <> struct is_float_t<float> { static constexpr bool value = true; };
+
+template <typename T> struct is_signed_int_t { static constexpr bool value = false; };
+template <> struct is_signed_int_t<int64_t> { static constexpr bool value = true; };
+template <> struct is_signed_int_t<int32_t> { static constexpr bool value = true; };
+template <> struct is_signed_int_t<int16_t> { static constexpr bool value = true; };
+template <> struct is_signed_int_t<int8_t> { static constexpr bool value = true; };
+
+// _to_native<T> (agg.hpp:13-21)
+__host__ __device__ inline double bswap_v(double v) {
+    uint64_t u;
+    __builtin_memcpy(&u, &v, 8);
+    u = __builtin_bswap64(u);
+    __builtin_memcpy(&v, &u, 8);
+    return v;
+}
+__host__ __device__ inline float bswap_v(float v) {
+    uint32_t u;
+    __builtin_memcpy(&u, &v, 4);
+    u = __builtin_bswap32(u);
+    __builtin_memcpy(&v, &u, 4);
+    return v;
+}
+__host__ __device__ inline int64_t bswap_v(int64_t v) { return (int64_t)__builtin_bswap64((uint64_t)v); }
+__host__ __device__ inline uint64_t bswap_v(uint64_t v) { return __builtin_bswap64(v); }
+__host__ __device__ inline int32_t bswap_v(int32_t v) { return (int32_t)__builtin_bswap32((uint32_t)v); }
+__host__ __device__ inline uint32_t bswap_v(uint32_t v) { return __builtin_bswap32(v); }
+__host__ __device__ inline int16_t bswap_v(int16_t v) { return (int16_t)__builtin_bswap16((uint16_t)v); }
+__host__ __device__ inline uint16_t bswap_v(uint16_t v) { return __builtin_bswap16(v); }
+__host__ __device__ inline int8_t bswap_v(int8_t v) { return v; }
+__host__ __device__ inline uint8_t bswap_v(uint8_t v) { return v; }
+__host__ __device__ inline vbool bswap_v(vbool v) { return v; }
+
+template <typename T> __device__ inline T load_v(const void *p, uint64_t i, int flip) {
+    T v = reinterpret_cast<const T *>(p)[i];
+    return flip ? bswap_v(v) : v;
+}
+
+template <typename T> __device__ inline double to_double(T v) { return (double)v; }
+template <> __device__ inline double to_double<vbool>(vbool v) { return v.v ? 1.0 : 0.0; }
+
+template <typename T> __device__ inline bool is_nan_v(T v) {
+    if constexpr (is_float_t<T>::value) return v != v;
+    else return false;
+}
+
+// ---- runtime ---------------------------------------------------------------
+hipStream_t stream();
+int current_device();
+int cu_count();
+
+// grid size for a grid-stride kernel over n items
+inline unsigned blocks_for(uint64_t n, unsigned threads, unsigned per_cu = 8) {
+    uint64_t b = (n + threads - 1) / threads;
+    uint64_t cap = (uint64_t)cu_count() * per_cu;
+    if (b > cap) b = cap;
+    if (b == 0) b = 1;
+    return (unsigned)b;
+}
+
+// kernel timing (hipEvents around named launches on the library stream)
+struct TimedScope {
+    const char *name;
+    hipEvent_t start = nullptr, stop = nullptr;
+    bool on;
+    explicit TimedScope(const char *n);
+    ~TimedScope();
+};
+
+// device memory owned by the library (RAII)
+struct DevBuf {
+    void *ptr = nullptr;
+    uint64_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    void ensure(uint64_t b) {
+        if (b <= bytes) return;
+        release();
+        if (b == 0) return;
+        hipError_t e = hipMalloc(&ptr, b);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            ptr = nullptr;
+            fail(VH_ERR_NOMEM, "hipMalloc of " + std::to_string(b) + " bytes failed: " + hipGetErrorString(e));
+        }
+        bytes = b;
+    }
+    template <typename T> T *as() const { return reinterpret_cast<T *>(ptr); }
+};
+
+// resolve VH_LOC_AUTO
+int resolve_loc(const void *ptr, int loc);
+
+}  // namespace vh

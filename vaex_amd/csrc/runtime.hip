@@ -1,0 +1,349 @@
+// Device/runtime plumbing of libvaexhip.so: last-error state, the per-device
+// library stream, device memory entry points, synthetic data generation in
+// HBM, kernel timing and the NaN-ignoring min/max limits pre-pass
+// (the reference's vaexfast statisticNd<op_min_max>, vaexfast.cpp:1043-1055).
+#include <map>
+#include <mutex>
+
+#include "common.hpp"
+
+namespace vh {
+
+static thread_local std::string g_last_error;
+
+void set_error_str(const std::string &s) { g_last_error = s; }
+void set_error(const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+}
+
+static std::mutex g_mu;
+static std::map<int, hipStream_t> g_streams;
+static std::map<int, int> g_cus;
+
+int current_device() {
+    int d = 0;
+    VH_HIP(hipGetDevice(&d));
+    return d;
+}
+
+hipStream_t stream() {
+    int d = current_device();
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_streams.find(d);
+    if (it != g_streams.end()) return it->second;
+    hipStream_t s;
+    VH_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    g_streams[d] = s;
+    return s;
+}
+
+int cu_count() {
+    int d = current_device();
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = g_cus.find(d);
+        if (it != g_cus.end()) return it->second;
+    }
+    int n = 0;
+    VH_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d));
+    if (n <= 0) n = 256;
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_cus[d] = n;
+    return n;
+}
+
+int resolve_loc(const void *ptr, int loc) {
+    if (loc == VH_LOC_HOST || loc == VH_LOC_DEVICE) return loc;
+    if (ptr == nullptr) return VH_LOC_HOST;
+    hipPointerAttribute_t attr;
+    hipError_t e = hipPointerGetAttributes(&attr, ptr);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return VH_LOC_HOST;
+    }
+    return attr.type == hipMemoryTypeDevice ? VH_LOC_DEVICE : VH_LOC_HOST;
+}
+
+// ---- kernel timing -----------------------------------------------------------
+static bool g_timing = false;
+struct TimingRec {
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+};
+static std::map<std::string, TimingRec> g_timing_recs;
+
+TimedScope::TimedScope(const char *n) : name(n), on(g_timing) {
+    if (!on) return;
+    VH_HIP(hipEventCreate(&start));
+    VH_HIP(hipEventCreate(&stop));
+    VH_HIP(hipEventRecord(start, vh::stream()));
+}
+
+TimedScope::~TimedScope() {
+    if (!on) return;
+    if (hipEventRecord(stop, vh::stream()) != hipSuccess) return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_timing_recs[name].ev.emplace_back(start, stop);
+}
+
+// ---- synthetic data (counter-based, reproducible for any row range) ------
+__host__ __device__ inline uint64_t splitmix64(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ULL;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+    return x ^ (x >> 31);
+}
+
+__device__ inline double u01(uint64_t bits) { return (double)(bits >> 11) * 0x1.0p-53; }
+
+__global__ void k_fill_random(void *dst, uint64_t n, int dtype, int dist, uint64_t seed, double a,
+                              double b) {
+    const uint64_t s = splitmix64(seed * 0x632be59bd9b4e019ULL + 0x1234567ULL);
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t r1 = splitmix64(s ^ (2 * i));
+        if (dist == 0) {
+            reinterpret_cast<double *>(dst)[i] = a + (b - a) * u01(r1);
+        } else if (dist == 1) {
+            uint64_t r2 = splitmix64(s ^ (2 * i + 1));
+            double u1 = 1.0 - u01(r1);  // (0, 1]
+            double u2 = u01(r2);
+            double z = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+            reinterpret_cast<double *>(dst)[i] = a + b * z;
+        } else {
+            uint64_t span = (uint64_t)(int64_t)(b - a);
+            int64_t v = (int64_t)a + (int64_t)(span ? r1 % span : 0);
+            if (dtype == VH_I32) reinterpret_cast<int32_t *>(dst)[i] = (int32_t)v;
+            else reinterpret_cast<int64_t *>(dst)[i] = v;
+        }
+    }
+}
+
+// ---- min/max limits pre-pass --------------------------------------------------
+// order-preserving map double -> uint64 (non-NaN input)
+__device__ inline uint64_t f64_key(double d) {
+    if (d == 0.0) d = 0.0;  // -0 == +0
+    uint64_t u;
+    __builtin_memcpy(&u, &d, 8);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
+}
+__host__ inline double f64_from_key(uint64_t k) {
+    uint64_t u = (k >> 63) ? (k & 0x7fffffffffffffffULL) : ~k;
+    double d;
+    memcpy(&d, &u, 8);
+    return d;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_minmax(const void *data, uint64_t n, int flip,
+                                                const uint8_t *mask, uint64_t *keys) {
+    uint64_t lo = ~0ULL, hi = 0ULL;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        if (mask && mask[i]) continue;
+        T v = load_v<T>(data, i, flip);
+        double d = to_double(v);
+        if (d != d) continue;
+        uint64_t k = f64_key(d);
+        lo = k < lo ? k : lo;
+        hi = k > hi ? k : hi;
+    }
+    // wave64 reduction, then one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) {
+        uint64_t l2 = __shfl_down(lo, off, 64);
+        uint64_t h2 = __shfl_down(hi, off, 64);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (lo != ~0ULL) atomicMin((unsigned long long *)&keys[0], (unsigned long long)lo);
+        if (hi != 0ULL) atomicMax((unsigned long long *)&keys[1], (unsigned long long)hi);
+    }
+}
+
+}  // namespace vh
+
+using namespace vh;
+
+extern "C" {
+
+const char *vh_last_error(void) { return g_last_error.c_str(); }
+int vh_abi_version(void) { return VH_ABI_VERSION; }
+
+int vh_device_count(int *count) {
+    VH_API_BEGIN
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        n = 0;
+    }
+    *count = n;
+    VH_API_END
+}
+
+int vh_set_device(int device) {
+    VH_API_BEGIN
+    VH_HIP(hipSetDevice(device));
+    VH_API_END
+}
+
+int vh_get_device(int *device) {
+    VH_API_BEGIN
+    *device = current_device();
+    VH_API_END
+}
+
+int vh_synchronize(void) {
+    VH_API_BEGIN
+    VH_HIP(hipStreamSynchronize(stream()));
+    VH_API_END
+}
+
+int vh_malloc(void **dptr, uint64_t bytes) {
+    VH_API_BEGIN
+    hipError_t e = hipMalloc(dptr, bytes ? bytes : 1);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        fail(VH_ERR_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
+    }
+    VH_API_END
+}
+
+int vh_free(void *dptr) {
+    VH_API_BEGIN
+    VH_HIP(hipStreamSynchronize(stream()));
+    VH_HIP(hipFree(dptr));
+    VH_API_END
+}
+
+int vh_memcpy_htod(void *dst, const void *src, uint64_t bytes) {
+    VH_API_BEGIN
+    VH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream()));
+    VH_HIP(hipStreamSynchronize(stream()));
+    VH_API_END
+}
+
+int vh_memcpy_dtoh(void *dst, const void *src, uint64_t bytes) {
+    VH_API_BEGIN
+    VH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream()));
+    VH_HIP(hipStreamSynchronize(stream()));
+    VH_API_END
+}
+
+int vh_memcpy_dtod(void *dst, const void *src, uint64_t bytes) {
+    VH_API_BEGIN
+    VH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream()));
+    VH_HIP(hipStreamSynchronize(stream()));
+    VH_API_END
+}
+
+int vh_memset(void *dptr, int value, uint64_t bytes) {
+    VH_API_BEGIN
+    VH_HIP(hipMemsetAsync(dptr, value, bytes, stream()));
+    VH_HIP(hipStreamSynchronize(stream()));
+    VH_API_END
+}
+
+int vh_fill_random(void *dptr, uint64_t n, int dtype, int dist, uint64_t seed, double a, double b) {
+    VH_API_BEGIN
+    if (dist < 0 || dist > 2) fail(VH_ERR_ARG, "unknown distribution");
+    if (dist < 2 && dtype != VH_F64) fail(VH_ERR_ARG, "uniform/normal fill needs float64");
+    if (dist == 2 && dtype != VH_I32 && dtype != VH_I64) fail(VH_ERR_ARG, "integer fill needs int32/int64");
+    if (n) {
+        hipLaunchKernelGGL(k_fill_random, dim3(blocks_for(n, 256)), dim3(256), 0, stream(), dptr, n, dtype,
+                           dist, seed, a, b);
+        VH_HIP(hipGetLastError());
+    }
+    VH_HIP(hipStreamSynchronize(stream()));
+    VH_API_END
+}
+
+int vh_timing_enable(int on) {
+    VH_API_BEGIN
+    g_timing = on != 0;
+    VH_API_END
+}
+
+int vh_timing_reset(void) {
+    VH_API_BEGIN
+    VH_HIP(hipStreamSynchronize(stream()));
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (auto &kv : g_timing_recs)
+        for (auto &p : kv.second.ev) {
+            (void)hipEventDestroy(p.first);
+            (void)hipEventDestroy(p.second);
+        }
+    g_timing_recs.clear();
+    VH_API_END
+}
+
+int vh_timing_read(const char *kernel, uint64_t *launches, double *total_ms) {
+    VH_API_BEGIN
+    VH_HIP(hipStreamSynchronize(stream()));
+    std::lock_guard<std::mutex> lk(g_mu);
+    *launches = 0;
+    *total_ms = 0;
+    auto it = g_timing_recs.find(kernel);
+    if (it == g_timing_recs.end()) return VH_OK;
+    for (auto &p : it->second.ev) {
+        float ms = 0;
+        VH_HIP(hipEventElapsedTime(&ms, p.first, p.second));
+        *total_ms += ms;
+        *launches += 1;
+    }
+    VH_API_END
+}
+
+int vh_stream(void **s) {
+    VH_API_BEGIN
+    *s = (void *)stream();
+    VH_API_END
+}
+
+int vh_minmax(const void *data, uint64_t n, int dtype, int flip, const uint8_t *mask, int loc,
+              double *out_min, double *out_max) {
+    VH_API_BEGIN
+    loc = resolve_loc(data, loc);
+    int isz = dtype_itemsize(dtype);
+    DevBuf stage, mstage, keys;
+    const void *d = data;
+    const uint8_t *m = mask;
+    if (loc == VH_LOC_HOST && n) {
+        stage.ensure(n * isz);
+        VH_HIP(hipMemcpyAsync(stage.ptr, data, n * isz, hipMemcpyHostToDevice, stream()));
+        d = stage.ptr;
+        if (mask) {
+            mstage.ensure(n);
+            VH_HIP(hipMemcpyAsync(mstage.ptr, mask, n, hipMemcpyHostToDevice, stream()));
+            m = mstage.as<uint8_t>();
+        }
+    }
+    keys.ensure(16);
+    uint64_t init[2] = {~0ULL, 0ULL};
+    VH_HIP(hipMemcpyAsync(keys.ptr, init, 16, hipMemcpyHostToDevice, stream()));
+    if (n) {
+        TimedScope ts("minmax");
+        VH_DISPATCH_DTYPE(dtype, T,
+                          hipLaunchKernelGGL(k_minmax<T>, dim3(blocks_for(n, 256, 4)), dim3(256), 0, stream(),
+                                             d, n, flip, m, keys.as<uint64_t>()));
+        VH_HIP(hipGetLastError());
+    }
+    uint64_t res[2];
+    VH_HIP(hipMemcpyAsync(res, keys.ptr, 16, hipMemcpyDeviceToHost, stream()));
+    VH_HIP(hipStreamSynchronize(stream()));
+    if (res[0] == ~0ULL) {  // no non-NaN value (nanmin of all-NaN -> nan)
+        *out_min = __builtin_nan("");
+        *out_max = __builtin_nan("");
+    } else {
+        *out_min = f64_from_key(res[0]);
+        *out_max = f64_from_key(res[1]);
+    }
+    VH_API_END
+}
+
+}  // extern "C"

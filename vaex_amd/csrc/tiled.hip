@@ -1,0 +1,471 @@
+// Tile-partitioned LDS aggregation for grids larger than one workgroup's LDS
+// (the 1027x1027 grid of df.count(binby=[x, y], shape=1024), the 1e6-cell
+// groupby grid).  Global atomics on a scattered 8 MB grid cost ~one 64-B
+// atomic request per row (MI355X_MICROARCH.md §Global float atomics: "64 lanes
+// in 64 different rows ~17x slower"); instead the rows are partitioned by grid
+// tile and every tile is aggregated in LDS:
+//
+//   sample  -- per-tile row fractions p_t from ~1M evenly spaced rows (LDS
+//              histogram per workgroup); they size the partition regions.
+//   pass A  -- workgroup w owns a contiguous row range and, per tile t, a
+//              private region of cap_t entries.  Per batch of 2048 rows it reads
+//              the binby/value columns coalesced, computes the cell in
+//              registers, ranks the rows per tile in an LDS histogram, counting-
+//              sorts (entry, value) by tile into LDS and streams the sorted runs
+//              to its regions (consecutive lanes -> consecutive addresses).  No
+//              global atomics; a row beyond its region's capacity (an unlikely
+//              sampling miss) is applied directly with global atomics.
+//   pass B  -- work units (tile, range of pass-A workgroups) sized from p_t:
+//              stream the regions' entries, aggregate into an LDS copy of the
+//              tile (u32 counts, f64 sums), flush with coalesced global atomics.
+//
+// Entry formats: u16 local cell (counts unconditional or keyed on a carried
+// value's NaN-ness) or u32 local cell | keep flags << 16.  Results equal
+// AggCount/AggSum (superagg.cpp:168-191,362-388): counts exact, float sums in a
+// different association order (within 1e-6 relative, north_star).
+#include <algorithm>
+#include <cmath>
+
+#include "binner_dev.hpp"
+#include "common.hpp"
+#include "engine.hpp"
+
+namespace vh {
+
+constexpr int TA_THREADS = 256;
+constexpr int TA_RPT = 8;
+constexpr int TA_BATCH = TA_THREADS * TA_RPT;
+constexpr int TB_THREADS = 256;
+constexpr uint64_t TILE_LDS_BUDGET = 64 * 1024;
+constexpr uint32_t TILE_MAX_TILES = 4096;
+constexpr int TA_WG_PER_CU = 4;
+constexpr int SAMPLE_BLOCKS = 512;
+
+enum : int32_t { CNT_ALWAYS = -2, CNT_FLAG = -1 };
+
+struct TileParams {
+    uint32_t s_log2, ntiles, flags_mode, nvals;
+    uint64_t cells;
+    uint32_t W;                // pass-A workgroups
+    uint32_t pad;
+    uint64_t rows_per_wg;
+    uint64_t wg_stride;        // entries of one workgroup's regions
+    const uint32_t *cap;       // [T]
+    const uint64_t *toff;      // [T] region offset inside a workgroup's block
+    uint32_t *fills;           // [T][W] entries produced (may exceed cap)
+    void *entries;             // u16 / u32, W * wg_stride
+    double *values[2];         // per value slot, W * wg_stride
+    int32_t val_slot[MAX_FUSED_AGGS];  // sum agg k -> value slot
+    int32_t cnt_slot[MAX_FUSED_AGGS];  // count agg k -> CNT_ALWAYS / CNT_FLAG / value slot
+};
+
+struct WorkUnit {
+    uint32_t tile, w_begin, w_end, pad;
+};
+
+template <int ND> __device__ inline uint64_t cell_of(const BinPlan &p, uint64_t i) {
+    if constexpr (ND == 0) {
+        return plan_index(p, i);
+    } else {
+        uint64_t c = 0;
+#pragma unroll
+        for (int d = 0; d < ND; d++) c += scalar_index<double>(p.b[d], i) * p.b[d].stride;
+        return c;
+    }
+}
+
+// keep flags of a row (bit k: aggregator k takes the row) and the carried values
+template <int NV>
+__device__ inline uint32_t row_contrib(const FusedAggs &fa, const TileParams &tp, uint64_t i, double *vals) {
+    uint32_t f = 0;
+    for (int k = 0; k < fa.na; k++) {
+        const FusedAgg &a = fa.a[k];
+        bool keep = !a.mask || a.mask[i] == 1;
+        double v = 0.0;
+        if (a.data) {
+            v = a.data[i];
+            keep = keep && (v == v);
+        }
+        if (keep) f |= 1u << k;
+        if constexpr (NV > 0) {
+            const int s = tp.val_slot[k];
+            if (s >= 0 && s < NV) vals[s] = keep ? v : __builtin_nan("");
+        }
+    }
+    return f;
+}
+
+// ---- sample: per-tile histogram of SAMPLE_BLOCKS evenly spaced row blocks ----
+template <int ND>
+__global__ __launch_bounds__(TA_THREADS) void k_tile_sample(BinPlan p, uint64_t n, uint32_t s_log2, uint32_t ntiles,
+                                                            uint64_t block_stride, uint64_t *hist) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    uint32_t *h = reinterpret_cast<uint32_t *>(lds_raw);
+    for (uint32_t t = threadIdx.x; t < ntiles; t += TA_THREADS) h[t] = 0;
+    __syncthreads();
+    const uint64_t row0 = blockIdx.x * block_stride;
+    for (uint64_t r = threadIdx.x; r < TA_BATCH; r += TA_THREADS) {
+        const uint64_t i = row0 + r;
+        if (i >= n) break;
+        atomicAdd(&h[cell_of<ND>(p, i) >> s_log2], 1u);
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < ntiles; t += TA_THREADS)
+        if (h[t]) atomicAdd((unsigned long long *)&hist[t], (unsigned long long)h[t]);
+}
+
+// exclusive scan of in[0..T) into out[0..T), returns the total (all threads)
+__device__ inline uint32_t block_exclusive_scan(const uint32_t *in, uint32_t *out, uint32_t T, uint32_t *wave_sums) {
+    const uint32_t per = (T + TA_THREADS - 1) / TA_THREADS;
+    const uint32_t t0 = threadIdx.x * per;
+    uint32_t s = 0;
+    for (uint32_t t = t0; t < t0 + per && t < T; t++) s += in[t];
+    // inclusive scan of s across the workgroup (wave64 shuffles + 4 wave partials)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t inc = s;
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t y = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += y;
+    }
+    if (lane == 63) wave_sums[wave] = inc;
+    __syncthreads();
+    uint32_t wave_base = 0, total = 0;
+    for (int k = 0; k < TA_THREADS / 64; k++) {
+        if (k < wave) wave_base += wave_sums[k];
+        total += wave_sums[k];
+    }
+    uint32_t acc = wave_base + inc - s;
+    for (uint32_t t = t0; t < t0 + per && t < T; t++) {
+        out[t] = acc;
+        acc += in[t];
+    }
+    return total;
+}
+
+template <int ND, int NV>
+__global__ __launch_bounds__(TA_THREADS) void k_tile_scatter(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const uint32_t T = tp.ntiles;
+    // LDS: staged values | staged entries | staged tiles | hist | cursor | boff | wave sums
+    double *sv = reinterpret_cast<double *>(lds_raw);
+    uint32_t *se = reinterpret_cast<uint32_t *>(lds_raw + (size_t)8 * NV * TA_BATCH);
+    uint16_t *st = reinterpret_cast<uint16_t *>(se + TA_BATCH);
+    uint32_t *hist = reinterpret_cast<uint32_t *>(st + TA_BATCH);
+    uint32_t *cursor = hist + T;
+    uint32_t *boff = cursor + T;
+    uint32_t *wave_sums = boff + T;
+    __shared__ uint32_t s_total;
+
+    for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) {
+        hist[t] = 0;
+        cursor[t] = 0;
+    }
+    __syncthreads();
+    const uint32_t w = blockIdx.x;
+    const uint64_t row_begin = (uint64_t)w * tp.rows_per_wg;
+    const uint64_t row_end = min(n, row_begin + tp.rows_per_wg);
+    const uint32_t smask = (1u << tp.s_log2) - 1;
+    const uint64_t region0 = (uint64_t)w * tp.wg_stride;
+
+    for (uint64_t b0 = row_begin; b0 < row_end; b0 += TA_BATCH) {
+        uint32_t tile[TA_RPT], ent[TA_RPT];
+        int32_t rank[TA_RPT];
+        double vals[TA_RPT][NV > 0 ? NV : 1];
+#pragma unroll
+        for (int r = 0; r < TA_RPT; r++) {
+            const uint64_t i = b0 + (uint64_t)r * TA_THREADS + threadIdx.x;
+            rank[r] = -1;
+            if (i < row_end) {
+                const uint64_t c = cell_of<ND>(p, i);
+                const uint32_t f = row_contrib<NV>(fa, tp, i, vals[r]);
+                tile[r] = (uint32_t)(c >> tp.s_log2);
+                ent[r] = ((uint32_t)c & smask) | (f << 16);
+                if (f) rank[r] = (int32_t)atomicAdd(&hist[tile[r]], 1u);
+            }
+        }
+        __syncthreads();
+        const uint32_t total = block_exclusive_scan(hist, boff, T, wave_sums);
+        if (threadIdx.x == 0) s_total = total;
+        __syncthreads();
+        // counting sort of the batch by tile into LDS
+#pragma unroll
+        for (int r = 0; r < TA_RPT; r++) {
+            if (rank[r] < 0) continue;
+            const uint32_t pos = boff[tile[r]] + (uint32_t)rank[r];
+            se[pos] = ent[r];
+            st[pos] = (uint16_t)tile[r];
+#pragma unroll
+            for (int s = 0; s < NV; s++) sv[s * TA_BATCH + pos] = vals[r][s];
+        }
+        __syncthreads();
+        // stream the sorted runs into the workgroup's tile regions
+        const uint32_t tot = s_total;
+        for (uint32_t k = threadIdx.x; k < tot; k += TA_THREADS) {
+            const uint32_t t = st[k];
+            const uint32_t j = cursor[t] + (k - boff[t]);
+            const uint32_t e32 = se[k];
+            if (j < tp.cap[t]) {
+                const uint64_t e = region0 + tp.toff[t] + j;
+                if (tp.flags_mode) reinterpret_cast<uint32_t *>(tp.entries)[e] = e32;
+                else reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)(e32 & 0xffffu);
+#pragma unroll
+                for (int s = 0; s < NV; s++) tp.values[s][e] = sv[s * TA_BATCH + k];
+            } else {
+                // region overflow (a sampling miss): apply the staged row with global atomics
+                const uint64_t c = ((uint64_t)t << tp.s_log2) | (e32 & 0xffffu);
+                const uint32_t f = e32 >> 16;
+                for (int a = 0; a < fa.na; a++) {
+                    if (!((f >> a) & 1)) continue;
+                    if (fa.a[a].kind == VH_AGG_COUNT) {
+                        atomicAdd((unsigned long long *)fa.a[a].grid + c, 1ULL);
+                    } else if constexpr (NV > 0) {
+                        atomicAdd(reinterpret_cast<double *>(fa.a[a].grid) + c, sv[tp.val_slot[a] * TA_BATCH + k]);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) {
+            cursor[t] += hist[t];
+            hist[t] = 0;
+        }
+        __syncthreads();
+    }
+    for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = cursor[t];
+}
+
+template <int NV>
+__global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TileParams tp, const WorkUnit *units) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const WorkUnit u = units[blockIdx.x];
+    const uint32_t t = u.tile;
+    const uint32_t cap = tp.cap[t];
+    // skip empty units without touching LDS
+    bool any = false;
+    for (uint32_t w = u.w_begin + threadIdx.x; w < u.w_end && !any; w += TB_THREADS)
+        any = tp.fills[(uint64_t)t * tp.W + w] != 0;
+    if (!__syncthreads_or(any)) return;
+    uint32_t *lw = reinterpret_cast<uint32_t *>(lds_raw);
+    for (uint32_t i = threadIdx.x; i < fa.lds_words; i += TB_THREADS) lw[i] = 0;
+    __syncthreads();
+    for (uint32_t w = u.w_begin; w < u.w_end; w++) {
+        const uint32_t cnt = min(tp.fills[(uint64_t)t * tp.W + w], cap);
+        const uint64_t base = (uint64_t)w * tp.wg_stride + tp.toff[t];
+        for (uint32_t q = threadIdx.x; q < cnt; q += TB_THREADS) {
+            const uint64_t e = base + q;
+            uint32_t local, fl;
+            if (tp.flags_mode) {
+                const uint32_t v = reinterpret_cast<const uint32_t *>(tp.entries)[e];
+                local = v & 0xffffu;
+                fl = v >> 16;
+            } else {
+                local = reinterpret_cast<const uint16_t *>(tp.entries)[e];
+                fl = 0xfu;
+            }
+            double v[NV > 0 ? NV : 1];
+#pragma unroll
+            for (int s = 0; s < NV; s++) v[s] = tp.values[s][e];
+            for (int k = 0; k < fa.na; k++) {
+                if (fa.a[k].kind == VH_AGG_COUNT) {
+                    const int cs = tp.cnt_slot[k];
+                    bool take;
+                    if (cs == CNT_ALWAYS) take = true;
+                    else if (cs == CNT_FLAG) take = (fl >> k) & 1;
+                    else {
+                        take = false;
+#pragma unroll
+                        for (int s = 0; s < NV; s++)
+                            if (s == cs) take = v[s] == v[s];
+                    }
+                    if (take) atomicAdd(reinterpret_cast<uint32_t *>(lds_raw + fa.a[k].lds_off) + local, 1u);
+                } else {
+#pragma unroll
+                    for (int s = 0; s < NV; s++) {
+                        if (s == tp.val_slot[k] && v[s] == v[s])
+                            atomicAdd(reinterpret_cast<double *>(lds_raw + fa.a[k].lds_off) + local, v[s]);
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t c0 = (uint64_t)t << tp.s_log2;
+    const uint32_t ncell = (uint32_t)min((uint64_t)1 << tp.s_log2, tp.cells - c0);
+    for (int k = 0; k < fa.na; k++) {
+        for (uint32_t i = threadIdx.x; i < ncell; i += TB_THREADS) {
+            if (fa.a[k].kind == VH_AGG_COUNT) {
+                const uint32_t v = reinterpret_cast<const uint32_t *>(lds_raw + fa.a[k].lds_off)[i];
+                if (v) atomicAdd((unsigned long long *)fa.a[k].grid + c0 + i, (unsigned long long)v);
+            } else {
+                const double v = reinterpret_cast<const double *>(lds_raw + fa.a[k].lds_off)[i];
+                if (v != 0.0) atomicAdd(reinterpret_cast<double *>(fa.a[k].grid) + c0 + i, v);
+            }
+        }
+    }
+}
+
+template <int ND, int NV>
+static void launch_scatter(unsigned grid, size_t lds, const BinPlan &plan, const FusedAggs &fa, const TileParams &tp,
+                           uint64_t n) {
+    hipLaunchKernelGGL((k_tile_scatter<ND, NV>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
+}
+
+template <int NV>
+static void launch_scatter_nd(int nd, unsigned grid, size_t lds, const BinPlan &plan, const FusedAggs &fa,
+                              const TileParams &tp, uint64_t n) {
+    switch (nd) {
+    case 1: launch_scatter<1, NV>(grid, lds, plan, fa, tp, n); break;
+    case 2: launch_scatter<2, NV>(grid, lds, plan, fa, tp, n); break;
+    case 3: launch_scatter<3, NV>(grid, lds, plan, fa, tp, n); break;
+    default: launch_scatter<0, NV>(grid, lds, plan, fa, tp, n);
+    }
+}
+
+bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64, Workspace &ws) {
+    if (n < (1u << 20) || cells >= (1ull << 40)) return false;
+    TileParams tp{};
+    // carried values: one slot per sum aggregator; counts keyed on a matching sum's value
+    int nv = 0;
+    for (int k = 0; k < fa_in.na; k++) {
+        tp.val_slot[k] = -1;
+        tp.cnt_slot[k] = CNT_ALWAYS;
+        if (fa_in.a[k].kind != VH_AGG_COUNT) tp.val_slot[k] = nv++;
+    }
+    if (nv > 2) return false;
+    bool flags_mode = false;
+    for (int k = 0; k < fa_in.na; k++) {
+        const FusedAgg &a = fa_in.a[k];
+        if (a.kind != VH_AGG_COUNT || (!a.data && !a.mask)) continue;
+        tp.cnt_slot[k] = CNT_FLAG;
+        for (int j = 0; j < fa_in.na; j++)
+            if (fa_in.a[j].kind != VH_AGG_COUNT && fa_in.a[j].data == a.data && fa_in.a[j].mask == a.mask && a.data)
+                tp.cnt_slot[k] = tp.val_slot[j];
+        if (tp.cnt_slot[k] == CNT_FLAG) flags_mode = true;
+    }
+    if (flags_mode)
+        for (int k = 0; k < fa_in.na; k++)
+            if (fa_in.a[k].kind == VH_AGG_COUNT) tp.cnt_slot[k] = CNT_FLAG;
+    uint64_t per_cell = 0;
+    for (int k = 0; k < fa_in.na; k++) per_cell += fa_in.a[k].kind == VH_AGG_COUNT ? 4 : 8;
+    uint32_t s_log2 = 0;
+    while (s_log2 < 16 && ((uint64_t)2 << s_log2) * per_cell <= TILE_LDS_BUDGET) s_log2++;
+    const uint64_t S = 1ull << s_log2;
+    const uint64_t T64 = (cells + S - 1) / S;
+    if (T64 > TILE_MAX_TILES || T64 < 2) return false;
+    const uint32_t T = (uint32_t)T64;
+
+    FusedAggs fa = fa_in;
+    uint64_t off = 0;
+    for (int k = 0; k < fa.na; k++) {
+        off = (off + 7) & ~uint64_t(7);
+        fa.a[k].lds_off = (uint32_t)off;
+        off += S * (fa.a[k].kind == VH_AGG_COUNT ? 4 : 8);
+    }
+    const uint64_t lds_b = (off + 15) & ~uint64_t(15);
+    fa.lds_words = (uint32_t)(lds_b / 4);
+    hipStream_t st = stream();
+
+    // ---- sample
+    const uint32_t W = (uint32_t)cu_count() * TA_WG_PER_CU;
+    DevBuf &meta = ws.tile_meta;
+    const uint64_t meta_bytes = 8 * (uint64_t)T /*hist*/ + 4 * (uint64_t)T /*cap*/ + 8 * (uint64_t)T /*toff*/ +
+                                4 * (uint64_t)T * W /*fills*/ + 16 * (uint64_t)(T + 2 * W + 16) /*units*/ + 256;
+    meta.ensure(meta_bytes);
+    unsigned char *mb = meta.as<unsigned char>();
+    uint64_t *d_hist = reinterpret_cast<uint64_t *>(mb);
+    uint64_t *d_toff = d_hist + T;
+    uint32_t *d_cap = reinterpret_cast<uint32_t *>(d_toff + T);
+    uint32_t *d_fills = d_cap + ((T + 3) & ~3u);
+    WorkUnit *d_units = reinterpret_cast<WorkUnit *>(d_fills + (uint64_t)T * W + 4 - ((uint64_t)T * W) % 4);
+    const uint64_t nb = (n + TA_BATCH - 1) / TA_BATCH;
+    const uint64_t sblocks = std::min<uint64_t>(nb, SAMPLE_BLOCKS);
+    const uint64_t bstride = std::max<uint64_t>(TA_BATCH, (n / sblocks));
+    VH_HIP(hipMemsetAsync(d_hist, 0, 8 * (uint64_t)T, st));
+    {
+        TimedScope ts("tile_sample");
+        const size_t lds = 4 * (size_t)T;
+        switch (nd_f64) {
+        case 1: hipLaunchKernelGGL(k_tile_sample<1>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist); break;
+        case 2: hipLaunchKernelGGL(k_tile_sample<2>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist); break;
+        case 3: hipLaunchKernelGGL(k_tile_sample<3>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist); break;
+        default: hipLaunchKernelGGL(k_tile_sample<0>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist);
+        }
+        VH_HIP(hipGetLastError());
+    }
+    std::vector<uint64_t> hist(T);
+    VH_HIP(hipMemcpyAsync(hist.data(), d_hist, 8 * (uint64_t)T, hipMemcpyDeviceToHost, st));
+    VH_HIP(hipStreamSynchronize(st));
+    uint64_t sampled = 0;
+    for (auto h : hist) sampled += h;
+    if (!sampled) return false;
+
+    // ---- region capacities per workgroup
+    const uint64_t rows_per_wg = (n + W - 1) / W;
+    std::vector<uint32_t> cap(T);
+    std::vector<uint64_t> toff(T);
+    uint64_t stride = 0;
+    for (uint32_t t = 0; t < T; t++) {
+        const double e = (double)rows_per_wg * (double)hist[t] / (double)sampled;
+        uint64_t c = (uint64_t)(e * 1.04 + 6.0 * std::sqrt(e + 1.0)) + 32;
+        c = std::min<uint64_t>((c + 7) & ~uint64_t(7), rows_per_wg + 8);
+        cap[t] = (uint32_t)c;
+        toff[t] = stride;
+        stride += c;
+    }
+    const uint64_t total = stride * W;
+    const int ebytes = flags_mode ? 4 : 2;
+    ws.tile_entries.ensure(total * ebytes);
+    if (nv) ws.tile_values.ensure(total * 8 * nv);
+    tp.s_log2 = s_log2;
+    tp.ntiles = T;
+    tp.flags_mode = flags_mode ? 1 : 0;
+    tp.nvals = nv;
+    tp.cells = cells;
+    tp.W = W;
+    tp.rows_per_wg = rows_per_wg;
+    tp.wg_stride = stride;
+    tp.cap = d_cap;
+    tp.toff = d_toff;
+    tp.fills = d_fills;
+    tp.entries = ws.tile_entries.ptr;
+    for (int s = 0; s < nv; s++) tp.values[s] = ws.tile_values.as<double>() + (uint64_t)s * total;
+    VH_HIP(hipMemcpyAsync(d_cap, cap.data(), 4 * (uint64_t)T, hipMemcpyHostToDevice, st));
+    VH_HIP(hipMemcpyAsync(d_toff, toff.data(), 8 * (uint64_t)T, hipMemcpyHostToDevice, st));
+
+    // ---- pass B work units: tiles split over ranges of pass-A workgroups by expected size
+    std::vector<WorkUnit> units;
+    const double target = std::max(1.0, (double)n / ((double)cu_count() * 4));
+    for (uint32_t t = 0; t < T; t++) {
+        const double e = (double)n * (double)hist[t] / (double)sampled;
+        uint32_t g = (uint32_t)std::min<double>(W, std::max(1.0, std::ceil(e / target)));
+        for (uint32_t k = 0; k < g; k++) units.push_back({t, (uint32_t)((uint64_t)W * k / g), (uint32_t)((uint64_t)W * (k + 1) / g), 0});
+    }
+    if (units.size() > (size_t)T + 2 * W + 16) units.resize(T + 2 * W + 16);  // cannot happen: g sums to <= T + 4 cu
+    VH_HIP(hipMemcpyAsync(d_units, units.data(), sizeof(WorkUnit) * units.size(), hipMemcpyHostToDevice, st));
+
+    // ---- pass A
+    {
+        TimedScope ts("tile_scatter");
+        const size_t lds = (size_t)8 * nv * TA_BATCH + (size_t)6 * TA_BATCH + 12 * (size_t)T + 64;
+        switch (nv) {
+        case 0: launch_scatter_nd<0>(nd_f64, W, lds, plan, fa, tp, n); break;
+        case 1: launch_scatter_nd<1>(nd_f64, W, lds, plan, fa, tp, n); break;
+        default: launch_scatter_nd<2>(nd_f64, W, lds, plan, fa, tp, n);
+        }
+        VH_HIP(hipGetLastError());
+    }
+    // ---- pass B
+    {
+        TimedScope ts("tile_reduce");
+        const unsigned g = (unsigned)units.size();
+        switch (nv) {
+        case 0: hipLaunchKernelGGL(k_tile_reduce<0>, dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units); break;
+        case 1: hipLaunchKernelGGL(k_tile_reduce<1>, dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units); break;
+        default: hipLaunchKernelGGL(k_tile_reduce<2>, dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
+        }
+        VH_HIP(hipGetLastError());
+    }
+    return true;
+}
+
+}  // namespace vh

@@ -1,0 +1,144 @@
+"""``ExecutorLocal`` for the GPU (the role of ``packages/vaex-core/vaex/execution.py:132-377``).
+
+Same contract -- tasks are scheduled, aggregation tasks sharing binners are merged into
+one ``TaskAggregations`` (one pass, ``execution.py:47-73``), the DataFrame's rows are
+walked in chunks, every task part processes each chunk, parts are reduced and results
+fulfilled -- but the chunk loop feeds the HIP library instead of a CPU thread pool:
+
+* HBM-resident columns (:class:`DeviceArray`) are handed over whole (one chunk): the
+  library reads them in place;
+* numpy columns are handed over in host chunks (default 16 Mi rows, ``VAEX_CHUNK_SIZE``
+  overrides, as ``execution.py:20-24``); the library stages each to HBM.
+
+One task part per task: the per-thread private grids of ``ideal_splits`` exist on the CPU
+to avoid write races, which device atomics already resolve.
+"""
+import os
+import threading
+
+import numpy as np
+
+from .device import DeviceArray
+from .tasks import TaskAggregation, TaskAggregations, TaskMinMax, TaskSetCreate
+from .taskparts import TaskPartAggregation, TaskPartMinMax, TaskPartSetCreate
+
+CHUNK_SIZE_HOST = int(os.environ.get("VAEX_AMD_CHUNK_SIZE", 16 * 1024 * 1024))
+
+
+def _env_chunk_size():
+    v = os.environ.get("VAEX_CHUNK_SIZE")
+    return int(v) if v not in (None, "None", "") else None
+
+
+def _merge(tasks, df):
+    """execution.py:47-73: aggregation tasks with equal binners -> one TaskAggregations."""
+    non_mergable = [t for t in tasks if not isinstance(t, TaskAggregation)]
+    per_grid = {}
+    for t in tasks:
+        if isinstance(t, TaskAggregation):
+            per_grid.setdefault(t.binners, []).append(t)
+    merged = []
+    for binners, subtasks in per_grid.items():
+        tm = TaskAggregations(df, binners)
+        tm.original_tasks = subtasks
+        for i, sub in enumerate(subtasks):
+            tm.add_aggregation_operation(sub.aggregation_description)
+
+            def assign(value, i=i, sub=sub):
+                sub.fulfill(value[i])
+
+            def fail(error, sub=sub):
+                sub.reject(error)
+
+            tm.then(assign, fail)
+        merged.append(tm)
+    return non_mergable + merged
+
+
+class ExecutorLocal:
+    def __init__(self, chunk_size=None):
+        self.tasks = []
+        self.chunk_size = chunk_size
+        self.passes = 0
+        self.local = threading.local()
+        self.lock = threading.Lock()
+
+    def schedule(self, task):
+        with self.lock:
+            self.tasks.append(task)
+        return task
+
+    def _pop_tasks(self):
+        with self.lock:
+            tasks, self.tasks = self.tasks, []
+        return tasks
+
+    def chunk_size_for(self, df):
+        cs = self.chunk_size or _env_chunk_size()
+        if cs is not None:
+            return int(cs)
+        if df.is_device_resident():
+            return max(1, df.length_unfiltered())
+        return CHUNK_SIZE_HOST
+
+    def _create_part(self, task, df):
+        if isinstance(task, TaskAggregations):
+            return TaskPartAggregation(df, task.binners, task.aggregation_descriptions)
+        if isinstance(task, TaskSetCreate):
+            return TaskPartSetCreate(df, task.expression, df.data_type(task.expression), task.unique_limit,
+                                     task.selection)
+        if isinstance(task, TaskMinMax):
+            return TaskPartMinMax(df, task.expression, task.selection)
+        raise TypeError(f"unknown task {task!r}")
+
+    def execute(self):
+        if getattr(self.local, "executing", False):
+            raise RuntimeError("nested execute call")
+        self.local.executing = True
+        try:
+            while True:
+                tasks = self._pop_tasks()
+                if not tasks:
+                    break
+                per_df = {}
+                for t in tasks:
+                    per_df.setdefault(id(t.df), (t.df, []))[1].append(t)
+                for df, df_tasks in per_df.values():
+                    self._run(df, _merge(df_tasks, df))
+        finally:
+            self.local.executing = False
+
+    def _run(self, df, tasks):
+        self.passes += 1
+        parts = []
+        try:
+            for t in tasks:
+                parts.append(self._create_part(t, df))
+        except Exception as e:
+            for t in tasks:
+                t.reject(e)
+            raise
+        expressions = []
+        for p in parts:
+            for e in p.expressions:
+                if e not in expressions:
+                    expressions.append(e)
+        n = df.length_unfiltered()
+        chunk_size = self.chunk_size_for(df)
+        try:
+            for i1 in range(0, n, chunk_size):
+                i2 = min(n, i1 + chunk_size)
+                filter_mask = df.evaluate_filter_mask(i1, i2) if df.filtered else None
+                blocks = {e: df.evaluate_chunk(e, i1, i2, filter_mask) for e in expressions}
+                for p in parts:
+                    p.process(0, i1, i2, filter_mask, blocks)
+            for t, p in zip(tasks, parts):
+                p.reduce([])
+                t.fulfill(p.get_result())
+        except Exception as e:
+            for t in tasks:
+                t.reject(e)
+            raise
+
+
+default_executor = ExecutorLocal()

@@ -1,0 +1,216 @@
+"""groupby / binby on the GPU path (``packages/vaex-core/vaex/groupby.py``).
+
+``Grouper`` (groupby.py:97-168): pass 1 builds the GPU ordered set of the key
+(``df._set``), its ``key_array`` becomes the group labels (ints down-cast with
+``required_dtype_for_max``), ``sort=True`` rebuilds a sorted set (``ordered_set.create``);
+pass 2 bins ``_ordinal_values(key, set)`` with a ``BinnerOrdinal`` -- which the task part
+turns into the fused set-ordinal binner (hash probe inside the bin kernel, no ordinal
+column materialised).  ``GrouperCategory`` (groupby.py:216-245) bins categorical columns
+directly.  ``GroupBy.agg`` (groupby.py:484-533) strips the edges; with >1 key the
+cartesian grid is filtered by count > 0.
+"""
+import numpy as np
+
+from . import agg as vagg
+from .dataframe import DataFrame, Expression, RowLimitException
+from .utils import extract_central_part, required_dtype_for_max
+
+
+class BinnerBase:
+    pass
+
+
+class Grouper(BinnerBase):
+    def __init__(self, expression, df=None, sort=False, pre_sort=True, row_limit=None, df_original=None):
+        self.df = df if df is not None else expression.df
+        df_original = df_original if df_original is not None else self.df
+        self.sort = sort
+        self.expression = str(expression)
+        self.label = self.expression
+        oset = df_original._set(self.expression, unique_limit=row_limit)
+        self.bin_values = oset.key_array()
+        if self.bin_values.dtype.kind in "iu" and len(self.bin_values):
+            self.bin_values = self.bin_values.astype(required_dtype_for_max(int(self.bin_values.max())))
+        self.has_null = oset.has_null
+        self.null_value = oset.null_value
+        self.sort_indices = None
+        if sort:
+            values = self.bin_values
+            nulls = np.zeros(len(values), bool)
+            if oset.has_null:
+                nulls[oset.null_value] = True
+            # arrow-style sort: nulls last, NaN after numbers (groupby.py:137-156)
+            order = sorted(range(len(values)), key=lambda i: (bool(nulls[i]), _nan_key(values[i])))
+            order = np.asarray(order, dtype=np.int64)
+            sorted_values = values[order]
+            null_value = int(np.nonzero(nulls[order])[0][0]) if oset.has_null else -1
+            oset = type(oset)(sorted_values.astype(oset._dtype), null_value, oset.nan_count, oset.null_count,
+                              oset.fingerprint + "-sorted")
+            self.bin_values = sorted_values
+            self.null_value = null_value
+        self.set = oset
+        basename = "set_%s" % "".join(c if c.isalnum() else "_" for c in self.expression)
+        self.setname = self.df.add_variable(basename, self.set, unique=True)
+        self.binby_expression = "_ordinal_values(%s, %s)" % (self.expression, self.setname)
+        self.N = len(self.bin_values)
+        self.binner = self.df._binner_ordinal(self.binby_expression, self.N)
+
+    def labels(self):
+        vals = self.bin_values.tolist()
+        if self.has_null:
+            vals[self.null_value] = None
+        return vals
+
+
+def _nan_key(v):
+    try:
+        return (1, 0) if v != v else (0, v)
+    except TypeError:
+        return (0, v)
+
+
+class GrouperCategory(BinnerBase):
+    """groupby.py:216-245: categorical column -> BinnerOrdinal(min_value, N)."""
+
+    def __init__(self, expression, df=None, sort=False, row_limit=None):
+        self.df = df if df is not None else expression.df
+        self.expression = str(expression)
+        self.label = self.expression
+        cat = self.df._categories[self.expression]
+        self.bin_values = np.asarray(cat["labels"], dtype=object)
+        self.N = cat["N"]
+        self.min_value = cat["min_value"]
+        self.sort_indices = None
+        self.binner = self.df._binner_ordinal(self.expression, self.N, self.min_value)
+        if row_limit is not None and self.N > row_limit:
+            raise RowLimitException(f"Resulting grouper has {self.N:,} unique combinations, which is larger "
+                                    f"than the allowed row limit of {row_limit:,}")
+
+    def labels(self):
+        return list(self.bin_values)
+
+
+class GroupByBase:
+    def __init__(self, df, by, sort=False, row_limit=None):
+        df_original = df
+        df = df.copy()
+        self.df = df
+        self.sort = sort
+        if not isinstance(by, (list, tuple)):
+            by = [by]
+        self.by = []
+        for by_value in by:
+            if isinstance(by_value, BinnerBase):
+                self.by.append(by_value)
+            elif df.is_category(by_value):
+                self.by.append(GrouperCategory(df[str(by_value)], df=df, sort=sort, row_limit=row_limit))
+            else:
+                self.by.append(Grouper(df[str(by_value)], df=df, sort=sort, row_limit=row_limit,
+                                       df_original=df_original))
+        self.groupby_expression = [str(b.expression) for b in self.by]
+        self.binners = tuple(b.binner for b in self.by)
+        self.shape = [b.N for b in self.by]
+        self.dims = self.groupby_expression[:]
+
+    def _agg(self, actions):
+        """groupby.py:345-402: every aggregate gets edges=True on the grouper binners."""
+        df = self.df
+        if isinstance(actions, dict):
+            actions = list(actions.items())
+        elif not isinstance(actions, (list, tuple)) or isinstance(actions, str):
+            actions = [actions]
+        grids = {}
+        self.counts = None
+
+        def add(aggregate, column_name=None, override_name=None):
+            if column_name is None or override_name is not None:
+                column_name = aggregate.pretty_name(override_name, df)
+            aggregate.edges = True
+            values = df._agg(aggregate, self.binners, delay=True)
+            grids[column_name] = values
+            if isinstance(aggregate, vagg.AggregatorDescriptorBasic) and aggregate.name == "AggCount" \
+                    and aggregate.expression == "*" and aggregate.selection in (None, False):
+                self.counts = values
+
+        for item in actions:
+            override_name = None
+            if isinstance(item, tuple):
+                name, aggregates = item
+            else:
+                aggregates, name = item, None
+            if not isinstance(aggregates, (list, tuple)) or isinstance(aggregates, str):
+                aggregates = [aggregates]
+            elif name is not None:
+                override_name = name
+            for aggregate in aggregates:
+                if isinstance(aggregate, str) and aggregate == "count":
+                    add(vagg.count(), "count" if name is None else name)
+                else:
+                    if isinstance(aggregate, str):
+                        aggregate = vagg.aggregates[aggregate]
+                    if callable(aggregate):
+                        if name is None:
+                            for column_name in df.get_column_names():
+                                if column_name not in self.groupby_expression:
+                                    add(aggregate(column_name), override_name=override_name)
+                        else:
+                            add(aggregate(name), name, override_name=override_name)
+                    else:
+                        add(aggregate, name, override_name=override_name)
+        return grids
+
+
+class GroupBy(GroupByBase):
+    def agg(self, actions):
+        """groupby.py:484-533."""
+        arrays = self._agg(actions)
+        has_non_existing_pairs = len(self.by) > 1
+        counts = self.counts
+        if has_non_existing_pairs and counts is None:
+            counts = self.df._agg(vagg.count(edges=True), self.binners, delay=True)
+        self.df.execute()
+        arrays = {k: extract_central_part(np.asarray(v.get())) for k, v in arrays.items()}
+        columns = {}
+        if has_non_existing_pairs:
+            counts = extract_central_part(np.asarray(counts.get()))
+            mask = counts > 0
+            coords = [c[mask] for c in np.meshgrid(*[np.asarray(b.bin_values) for b in self.by], indexing="ij")]
+            for b, coord in zip(self.by, coords):
+                columns[b.label] = coord
+            for k, v in arrays.items():
+                columns[k] = v[mask]
+        else:
+            columns[self.by[0].label] = np.asarray(self.by[0].bin_values)
+            for k, v in arrays.items():
+                assert v.ndim == 1
+                columns[k] = v
+        return DataFrame(columns)
+
+
+class _Coord:
+    def __init__(self, values):
+        self.values = np.asarray(values)
+
+
+class BinByResult:
+    """The xarray.DataArray the reference returns, reduced to data / dims / coords."""
+
+    def __init__(self, data, dims, coords):
+        self.data = data
+        self.dims = tuple(dims)
+        self.coords = {k: _Coord(v) for k, v in coords.items()}
+
+
+class BinBy(GroupByBase):
+    def agg(self, actions):
+        arrays = self._agg(actions)
+        self.df.execute()
+        arrays = {k: extract_central_part(np.asarray(v.get())) for k, v in arrays.items()}
+        keys = list(arrays)
+        coords = {b.label: list(b.bin_values) for b in self.by}
+        if len(arrays) == 1 and not isinstance(actions, dict):
+            return BinByResult(arrays[keys[0]], self.dims, coords)
+        final = np.stack([arrays[k] for k in keys])
+        coords = dict(coords)
+        coords["statistic"] = keys
+        return BinByResult(final, ["statistic"] + self.dims, coords)
