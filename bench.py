@@ -26,7 +26,7 @@ sys.path.insert(0, ROOT)
 
 BASELINE_METRIC = "rows/sec 2D count grid 1e9×f64 + groupby-sum 1e6 keys; HBM GB/s %peak"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-TILE_KERNELS = ["tile_sample", "tile_scatter", "tile_prefix", "tile_reduce"]
+TILE_KERNELS = ["tile_sample", "tile_scatter", "tile_scatter_f64", "tile_reduce"]
 
 
 def parse():

@@ -311,7 +311,9 @@ __global__ __launch_bounds__(256) void k_fused(BinPlan p, FusedAggs fa, uint64_t
 #pragma unroll
             for (int d = 0; d < ND; d++) c += scalar_index<double>(p.b[d], i) * p.b[d].stride;
         }
-        for (int k = 0; k < fa.na; k++) {
+        #pragma unroll
+        for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+            if (k >= fa.na) break;
             const FusedAgg &a = fa.a[k];
             if (a.mask && a.mask[i] != 1) continue;
             if (a.kind == VH_AGG_COUNT) {
@@ -332,7 +334,9 @@ __global__ __launch_bounds__(256) void k_fused(BinPlan p, FusedAggs fa, uint64_t
     }
     if constexpr (USE_LDS) {
         __syncthreads();
-        for (int k = 0; k < fa.na; k++) {
+        #pragma unroll
+        for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+            if (k >= fa.na) break;
             const FusedAgg &a = fa.a[k];
             for (uint64_t c = threadIdx.x; c < cells; c += blockDim.x) {
                 if (a.kind == VH_AGG_COUNT) {

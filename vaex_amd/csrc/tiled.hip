@@ -35,7 +35,7 @@ namespace vh {
 constexpr int TA_THREADS = 256;
 constexpr int TA_RPT = 8;
 constexpr int TA_BATCH = TA_THREADS * TA_RPT;
-constexpr int TB_THREADS = 256;
+constexpr int TB_THREADS = 512;
 constexpr uint64_t TILE_LDS_BUDGET = 64 * 1024;
 constexpr uint32_t TILE_MAX_TILES = 4096;
 constexpr int TA_WG_PER_CU = 4;
@@ -57,6 +57,7 @@ struct TileParams {
     double *values[2];         // per value slot, W * wg_stride
     int32_t val_slot[MAX_FUSED_AGGS];  // sum agg k -> value slot
     int32_t cnt_slot[MAX_FUSED_AGGS];  // count agg k -> CNT_ALWAYS / CNT_FLAG / value slot
+    const double *vdata[2];    // value slot -> source column (fast kernel)
 };
 
 struct WorkUnit {
@@ -78,7 +79,9 @@ template <int ND> __device__ inline uint64_t cell_of(const BinPlan &p, uint64_t 
 template <int NV>
 __device__ inline uint32_t row_contrib(const FusedAggs &fa, const TileParams &tp, uint64_t i, double *vals) {
     uint32_t f = 0;
-    for (int k = 0; k < fa.na; k++) {
+    #pragma unroll
+    for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+        if (k >= fa.na) break;
         const FusedAgg &a = fa.a[k];
         bool keep = !a.mask || a.mask[i] == 1;
         double v = 0.0;
@@ -114,6 +117,16 @@ __global__ __launch_bounds__(TA_THREADS) void k_tile_sample(BinPlan p, uint64_t 
         if (h[t]) atomicAdd((unsigned long long *)&hist[t], (unsigned long long)h[t]);
 }
 
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup fence +
+// s_barrier, which waits vmcnt(0): it would drain the prefetched loads of the next batch
+// and every outstanding region store at each of the batch's barriers
+// (cdna_hip_programming.md "Pipelining across barriers").  Only LDS traffic is ordered here.
+__device__ inline void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // exclusive scan of in[0..T) into out[0..T), returns the total (all threads)
 __device__ inline uint32_t block_exclusive_scan(const uint32_t *in, uint32_t *out, uint32_t T, uint32_t *wave_sums) {
     const uint32_t per = (T + TA_THREADS - 1) / TA_THREADS;
@@ -128,7 +141,7 @@ __device__ inline uint32_t block_exclusive_scan(const uint32_t *in, uint32_t *ou
         if (lane >= off) inc += y;
     }
     if (lane == 63) wave_sums[wave] = inc;
-    __syncthreads();
+    lds_barrier();
     uint32_t wave_base = 0, total = 0;
     for (int k = 0; k < TA_THREADS / 64; k++) {
         if (k < wave) wave_base += wave_sums[k];
@@ -142,23 +155,91 @@ __device__ inline uint32_t block_exclusive_scan(const uint32_t *in, uint32_t *ou
     return total;
 }
 
+// LDS layout of pass A: staged values | staged entries | staged tiles | hist | cursor | boff | wave sums
+struct ScatterLds {
+    double *sv;
+    uint32_t *se;
+    uint16_t *st;
+    uint32_t *hist, *cursor, *boff, *wave_sums;
+};
+
+template <int NV> __device__ inline ScatterLds scatter_lds(unsigned char *raw, uint32_t T) {
+    ScatterLds l;
+    l.sv = reinterpret_cast<double *>(raw);
+    l.se = reinterpret_cast<uint32_t *>(raw + (size_t)8 * NV * TA_BATCH);
+    l.st = reinterpret_cast<uint16_t *>(l.se + TA_BATCH);
+    l.hist = reinterpret_cast<uint32_t *>(l.st + TA_BATCH);
+    l.cursor = l.hist + T;
+    l.boff = l.cursor + T;
+    l.wave_sums = l.boff + T;
+    return l;
+}
+
+// phases 2-5 of a batch, after every row has its tile, entry, rank (-1 = drop) and
+// carried values: exclusive scan of the tile histogram, counting sort into LDS, stream
+// the sorted runs to the workgroup's tile regions, advance the region cursors.
+template <int NV>
+__device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, const TileParams &tp, uint32_t T,
+                                    uint64_t region0, const uint32_t *tile, const uint32_t *ent, const int32_t *rank,
+                                    const double (*vals)[NV > 0 ? NV : 1], uint32_t *s_total) {
+    lds_barrier();
+    const uint32_t total = block_exclusive_scan(l.hist, l.boff, T, l.wave_sums);
+    if (threadIdx.x == 0) *s_total = total;
+    lds_barrier();
+#pragma unroll
+    for (int r = 0; r < TA_RPT; r++) {
+        if (rank[r] < 0) continue;
+        const uint32_t pos = l.boff[tile[r]] + (uint32_t)rank[r];
+        l.se[pos] = ent[r];
+        l.st[pos] = (uint16_t)tile[r];
+#pragma unroll
+        for (int s = 0; s < NV; s++) l.sv[s * TA_BATCH + pos] = vals[r][s];
+    }
+    lds_barrier();
+    const uint32_t tot = *s_total;
+    for (uint32_t k = threadIdx.x; k < tot; k += TA_THREADS) {
+        const uint32_t t = l.st[k];
+        const uint32_t j = l.cursor[t] + (k - l.boff[t]);
+        const uint32_t e32 = l.se[k];
+        if (j < tp.cap[t]) {
+            const uint64_t e = region0 + tp.toff[t] + j;
+            if (tp.flags_mode) reinterpret_cast<uint32_t *>(tp.entries)[e] = e32;
+            else reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)(e32 & 0xffffu);
+#pragma unroll
+            for (int s = 0; s < NV; s++) tp.values[s][e] = l.sv[s * TA_BATCH + k];
+        } else {
+            // region overflow (a sampling miss): apply the staged row with global atomics
+            const uint64_t c = ((uint64_t)t << tp.s_log2) | (e32 & 0xffffu);
+            const uint32_t f = e32 >> 16;
+            #pragma unroll
+            for (int a = 0; a < MAX_FUSED_AGGS; a++) {
+                if (a >= fa.na) break;
+                if (!((f >> a) & 1)) continue;
+                if (fa.a[a].kind == VH_AGG_COUNT) {
+                    atomicAdd((unsigned long long *)fa.a[a].grid + c, 1ULL);
+                } else if constexpr (NV > 0) {
+                    atomicAdd(reinterpret_cast<double *>(fa.a[a].grid) + c, l.sv[tp.val_slot[a] * TA_BATCH + k]);
+                }
+            }
+        }
+    }
+    lds_barrier();
+    for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) {
+        l.cursor[t] += l.hist[t];
+        l.hist[t] = 0;
+    }
+}
+
+// generic pass A: any binner kinds/dtypes, masks and keep flags
 template <int ND, int NV>
 __global__ __launch_bounds__(TA_THREADS) void k_tile_scatter(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const uint32_t T = tp.ntiles;
-    // LDS: staged values | staged entries | staged tiles | hist | cursor | boff | wave sums
-    double *sv = reinterpret_cast<double *>(lds_raw);
-    uint32_t *se = reinterpret_cast<uint32_t *>(lds_raw + (size_t)8 * NV * TA_BATCH);
-    uint16_t *st = reinterpret_cast<uint16_t *>(se + TA_BATCH);
-    uint32_t *hist = reinterpret_cast<uint32_t *>(st + TA_BATCH);
-    uint32_t *cursor = hist + T;
-    uint32_t *boff = cursor + T;
-    uint32_t *wave_sums = boff + T;
+    const ScatterLds l = scatter_lds<NV>(lds_raw, T);
     __shared__ uint32_t s_total;
-
     for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) {
-        hist[t] = 0;
-        cursor[t] = 0;
+        l.hist[t] = 0;
+        l.cursor[t] = 0;
     }
     __syncthreads();
     const uint32_t w = blockIdx.x;
@@ -166,7 +247,6 @@ __global__ __launch_bounds__(TA_THREADS) void k_tile_scatter(BinPlan p, FusedAgg
     const uint64_t row_end = min(n, row_begin + tp.rows_per_wg);
     const uint32_t smask = (1u << tp.s_log2) - 1;
     const uint64_t region0 = (uint64_t)w * tp.wg_stride;
-
     for (uint64_t b0 = row_begin; b0 < row_end; b0 += TA_BATCH) {
         uint32_t tile[TA_RPT], ent[TA_RPT];
         int32_t rank[TA_RPT];
@@ -180,118 +260,196 @@ __global__ __launch_bounds__(TA_THREADS) void k_tile_scatter(BinPlan p, FusedAgg
                 const uint32_t f = row_contrib<NV>(fa, tp, i, vals[r]);
                 tile[r] = (uint32_t)(c >> tp.s_log2);
                 ent[r] = ((uint32_t)c & smask) | (f << 16);
-                if (f) rank[r] = (int32_t)atomicAdd(&hist[tile[r]], 1u);
+                if (f) rank[r] = (int32_t)atomicAdd(&l.hist[tile[r]], 1u);
             }
         }
-        __syncthreads();
-        const uint32_t total = block_exclusive_scan(hist, boff, T, wave_sums);
-        if (threadIdx.x == 0) s_total = total;
-        __syncthreads();
-        // counting sort of the batch by tile into LDS
+        batch_commit<NV>(l, fa, tp, T, region0, tile, ent, rank, vals, &s_total);
+        lds_barrier();
+    }
+    for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.cursor[t];
+}
+
+// BinnerScalar<double> index from a loaded value (superagg_binners.cpp:42-53)
+__device__ inline uint64_t scalar_f64_index(double v, double vmin, double scale, uint64_t bins) {
+    const double scaled = (v - vmin) * scale;
+    if (scaled != scaled) return 0;
+    if (scaled < 0) return 1;
+    if (scaled >= 1) return bins + 2;
+    return (uint64_t)(int64_t)((int)(scaled * (double)bins) + 2);
+}
+
+// fast pass A: ND native float64 scalar binners without masks, NV float64 sums without
+// masks, counts unconditional or keyed on a carried value (mean).  Rows are read as
+// 16-byte pairs and the next batch is prefetched into registers while the current one
+// is ranked, sorted and written.
+template <int ND, int NV>
+__global__ __launch_bounds__(TA_THREADS) void k_tile_scatter_f64(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
+    constexpr int NC = ND + NV;
+    constexpr int PAIRS = TA_RPT / 2;
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const uint32_t T = tp.ntiles;
+    const ScatterLds l = scatter_lds<NV>(lds_raw, T);
+    __shared__ uint32_t s_total;
+    for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) {
+        l.hist[t] = 0;
+        l.cursor[t] = 0;
+    }
+    __syncthreads();
+    const double *col[NC];
+#pragma unroll
+    for (int d = 0; d < ND; d++) col[d] = reinterpret_cast<const double *>(p.b[d].data);
+#pragma unroll
+    for (int s = 0; s < NV; s++) col[ND + s] = tp.vdata[s];
+    uint32_t count_mask = 0, keyed_slot_of[MAX_FUSED_AGGS];
+    #pragma unroll
+    for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+        if (k >= fa.na) break;
+        keyed_slot_of[k] = fa.a[k].kind == VH_AGG_COUNT ? (uint32_t)tp.cnt_slot[k] : (uint32_t)tp.val_slot[k];
+        if (fa.a[k].kind == VH_AGG_COUNT && tp.cnt_slot[k] == CNT_ALWAYS) count_mask |= 1u << k;
+    }
+    const uint32_t w = blockIdx.x;
+    const uint64_t row_begin = (uint64_t)w * tp.rows_per_wg;
+    const uint64_t row_end = min(n, row_begin + tp.rows_per_wg);
+    const uint32_t smask = (1u << tp.s_log2) - 1;
+    const uint64_t region0 = (uint64_t)w * tp.wg_stride;
+    const double qnan = __builtin_nan("");
+
+    auto load = [&](uint64_t b0, double2 (&dst)[PAIRS][NC]) {
+#pragma unroll
+        for (int q = 0; q < PAIRS; q++) {
+            const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + threadIdx.x);
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                if (i + 1 < row_end) dst[q][c] = *reinterpret_cast<const double2 *>(col[c] + i);
+                else dst[q][c] = make_double2(i < row_end ? col[c][i] : qnan, qnan);
+            }
+        }
+    };
+    double2 cur[PAIRS][NC], nxt[PAIRS][NC];
+    if (row_begin < row_end) load(row_begin, cur);
+    for (uint64_t b0 = row_begin; b0 < row_end; b0 += TA_BATCH) {
+        if (b0 + TA_BATCH < row_end) load(b0 + TA_BATCH, nxt);
+        uint32_t tile[TA_RPT], ent[TA_RPT];
+        int32_t rank[TA_RPT];
+        double vals[TA_RPT][NV > 0 ? NV : 1];
 #pragma unroll
         for (int r = 0; r < TA_RPT; r++) {
-            if (rank[r] < 0) continue;
-            const uint32_t pos = boff[tile[r]] + (uint32_t)rank[r];
-            se[pos] = ent[r];
-            st[pos] = (uint16_t)tile[r];
+            const int q = r >> 1, h = r & 1;
+            const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + threadIdx.x) + h;
+            rank[r] = -1;
+            if (i < row_end) {
+                uint64_t c = 0;
 #pragma unroll
-            for (int s = 0; s < NV; s++) sv[s * TA_BATCH + pos] = vals[r][s];
-        }
-        __syncthreads();
-        // stream the sorted runs into the workgroup's tile regions
-        const uint32_t tot = s_total;
-        for (uint32_t k = threadIdx.x; k < tot; k += TA_THREADS) {
-            const uint32_t t = st[k];
-            const uint32_t j = cursor[t] + (k - boff[t]);
-            const uint32_t e32 = se[k];
-            if (j < tp.cap[t]) {
-                const uint64_t e = region0 + tp.toff[t] + j;
-                if (tp.flags_mode) reinterpret_cast<uint32_t *>(tp.entries)[e] = e32;
-                else reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)(e32 & 0xffffu);
+                for (int d = 0; d < ND; d++) {
+                    const double v = h ? cur[q][d].y : cur[q][d].x;
+                    c += scalar_f64_index(v, p.b[d].vmin, p.b[d].scale, p.b[d].bins) * p.b[d].stride;
+                }
+                uint32_t f = count_mask;
 #pragma unroll
-                for (int s = 0; s < NV; s++) tp.values[s][e] = sv[s * TA_BATCH + k];
-            } else {
-                // region overflow (a sampling miss): apply the staged row with global atomics
-                const uint64_t c = ((uint64_t)t << tp.s_log2) | (e32 & 0xffffu);
-                const uint32_t f = e32 >> 16;
-                for (int a = 0; a < fa.na; a++) {
-                    if (!((f >> a) & 1)) continue;
-                    if (fa.a[a].kind == VH_AGG_COUNT) {
-                        atomicAdd((unsigned long long *)fa.a[a].grid + c, 1ULL);
-                    } else if constexpr (NV > 0) {
-                        atomicAdd(reinterpret_cast<double *>(fa.a[a].grid) + c, sv[tp.val_slot[a] * TA_BATCH + k]);
+                for (int s = 0; s < NV; s++) vals[r][s] = h ? cur[q][ND + s].y : cur[q][ND + s].x;
+                #pragma unroll
+                for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+                    if (k >= fa.na) break;
+                    const uint32_t sl = keyed_slot_of[k];
+                    if (!((count_mask >> k) & 1)) {
+#pragma unroll
+                        for (int s = 0; s < NV; s++)
+                            if (s == (int)sl && vals[r][s] == vals[r][s]) f |= 1u << k;
                     }
                 }
+                tile[r] = (uint32_t)(c >> tp.s_log2);
+                ent[r] = ((uint32_t)c & smask) | (f << 16);
+                if (f) rank[r] = (int32_t)atomicAdd(&l.hist[tile[r]], 1u);
             }
         }
-        __syncthreads();
-        for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) {
-            cursor[t] += hist[t];
-            hist[t] = 0;
-        }
-        __syncthreads();
+        batch_commit<NV>(l, fa, tp, T, region0, tile, ent, rank, vals, &s_total);
+#pragma unroll
+        for (int q = 0; q < PAIRS; q++)
+#pragma unroll
+            for (int c = 0; c < NC; c++) cur[q][c] = nxt[q][c];
+        lds_barrier();
     }
-    for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = cursor[t];
+    for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.cursor[t];
 }
+
+template <int NV>
+__device__ inline void reduce_entry(const FusedAggs &fa, const TileParams &tp, unsigned char *lds, uint32_t local,
+                                    uint32_t fl, const double *v) {
+    #pragma unroll
+    for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+        if (k >= fa.na) break;
+        if (fa.a[k].kind == VH_AGG_COUNT) {
+            const int cs = tp.cnt_slot[k];
+            bool take;
+            if (cs == CNT_ALWAYS) take = true;
+            else if (cs == CNT_FLAG) take = (fl >> k) & 1;
+            else {
+                take = false;
+#pragma unroll
+                for (int s = 0; s < NV; s++)
+                    if (s == cs) take = v[s] == v[s];
+            }
+            if (take) atomicAdd(reinterpret_cast<uint32_t *>(lds + fa.a[k].lds_off) + local, 1u);
+        } else {
+#pragma unroll
+            for (int s = 0; s < NV; s++) {
+                if (s == tp.val_slot[k] && v[s] == v[s])
+                    atomicAdd(reinterpret_cast<double *>(lds + fa.a[k].lds_off) + local, v[s]);
+            }
+        }
+    }
+}
+
+constexpr int TB_UNROLL = 8;
 
 template <int NV>
 __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TileParams tp, const WorkUnit *units) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
+    __shared__ uint32_t s_fill[1024];
     const WorkUnit u = units[blockIdx.x];
     const uint32_t t = u.tile;
     const uint32_t cap = tp.cap[t];
-    // skip empty units without touching LDS
+    const uint32_t nw = u.w_end - u.w_begin;  // <= W <= 1024 (host checks)
     bool any = false;
-    for (uint32_t w = u.w_begin + threadIdx.x; w < u.w_end && !any; w += TB_THREADS)
-        any = tp.fills[(uint64_t)t * tp.W + w] != 0;
+    for (uint32_t k = threadIdx.x; k < nw; k += TB_THREADS) {
+        const uint32_t f = min(tp.fills[(uint64_t)t * tp.W + u.w_begin + k], cap);
+        s_fill[k] = f;
+        any |= f != 0;
+    }
     if (!__syncthreads_or(any)) return;
     uint32_t *lw = reinterpret_cast<uint32_t *>(lds_raw);
     for (uint32_t i = threadIdx.x; i < fa.lds_words; i += TB_THREADS) lw[i] = 0;
     __syncthreads();
-    for (uint32_t w = u.w_begin; w < u.w_end; w++) {
-        const uint32_t cnt = min(tp.fills[(uint64_t)t * tp.W + w], cap);
-        const uint64_t base = (uint64_t)w * tp.wg_stride + tp.toff[t];
-        for (uint32_t q = threadIdx.x; q < cnt; q += TB_THREADS) {
-            const uint64_t e = base + q;
-            uint32_t local, fl;
-            if (tp.flags_mode) {
-                const uint32_t v = reinterpret_cast<const uint32_t *>(tp.entries)[e];
-                local = v & 0xffffu;
-                fl = v >> 16;
-            } else {
-                local = reinterpret_cast<const uint16_t *>(tp.entries)[e];
-                fl = 0xfu;
-            }
-            double v[NV > 0 ? NV : 1];
+    for (uint32_t k = 0; k < nw; k++) {
+        const uint32_t cnt = s_fill[k];
+        const uint64_t base = (uint64_t)(u.w_begin + k) * tp.wg_stride + tp.toff[t];
+        for (uint32_t q0 = 0; q0 < cnt; q0 += TB_THREADS * TB_UNROLL) {
+            uint32_t ent[TB_UNROLL];
+            double v[TB_UNROLL][NV > 0 ? NV : 1];
 #pragma unroll
-            for (int s = 0; s < NV; s++) v[s] = tp.values[s][e];
-            for (int k = 0; k < fa.na; k++) {
-                if (fa.a[k].kind == VH_AGG_COUNT) {
-                    const int cs = tp.cnt_slot[k];
-                    bool take;
-                    if (cs == CNT_ALWAYS) take = true;
-                    else if (cs == CNT_FLAG) take = (fl >> k) & 1;
-                    else {
-                        take = false;
+            for (int j = 0; j < TB_UNROLL; j++) {
+                const uint32_t q = q0 + j * TB_THREADS + threadIdx.x;
+                if (q < cnt) {
+                    const uint64_t e = base + q;
+                    ent[j] = tp.flags_mode ? reinterpret_cast<const uint32_t *>(tp.entries)[e]
+                                           : (0xf0000u | reinterpret_cast<const uint16_t *>(tp.entries)[e]);
 #pragma unroll
-                        for (int s = 0; s < NV; s++)
-                            if (s == cs) take = v[s] == v[s];
-                    }
-                    if (take) atomicAdd(reinterpret_cast<uint32_t *>(lds_raw + fa.a[k].lds_off) + local, 1u);
-                } else {
-#pragma unroll
-                    for (int s = 0; s < NV; s++) {
-                        if (s == tp.val_slot[k] && v[s] == v[s])
-                            atomicAdd(reinterpret_cast<double *>(lds_raw + fa.a[k].lds_off) + local, v[s]);
-                    }
+                    for (int s = 0; s < NV; s++) v[j][s] = tp.values[s][e];
                 }
+            }
+#pragma unroll
+            for (int j = 0; j < TB_UNROLL; j++) {
+                const uint32_t q = q0 + j * TB_THREADS + threadIdx.x;
+                if (q < cnt) reduce_entry<NV>(fa, tp, lds_raw, ent[j] & 0xffffu, ent[j] >> 16, v[j]);
             }
         }
     }
     __syncthreads();
     const uint64_t c0 = (uint64_t)t << tp.s_log2;
     const uint32_t ncell = (uint32_t)min((uint64_t)1 << tp.s_log2, tp.cells - c0);
-    for (int k = 0; k < fa.na; k++) {
+    #pragma unroll
+    for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+        if (k >= fa.na) break;
         for (uint32_t i = threadIdx.x; i < ncell; i += TB_THREADS) {
             if (fa.a[k].kind == VH_AGG_COUNT) {
                 const uint32_t v = reinterpret_cast<const uint32_t *>(lds_raw + fa.a[k].lds_off)[i];
@@ -305,19 +463,48 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
 }
 
 template <int ND, int NV>
-static void launch_scatter(unsigned grid, size_t lds, const BinPlan &plan, const FusedAggs &fa, const TileParams &tp,
-                           uint64_t n) {
+static void launch_scatter(bool fast, unsigned grid, size_t lds, const BinPlan &plan, const FusedAggs &fa,
+                           const TileParams &tp, uint64_t n) {
+    if constexpr (ND > 0) {
+        if (fast) {
+            hipLaunchKernelGGL((k_tile_scatter_f64<ND, NV>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
+            return;
+        }
+    }
     hipLaunchKernelGGL((k_tile_scatter<ND, NV>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
 }
 
 template <int NV>
-static void launch_scatter_nd(int nd, unsigned grid, size_t lds, const BinPlan &plan, const FusedAggs &fa,
+static void launch_scatter_nd(int nd, bool fast, unsigned grid, size_t lds, const BinPlan &plan, const FusedAggs &fa,
                               const TileParams &tp, uint64_t n) {
     switch (nd) {
-    case 1: launch_scatter<1, NV>(grid, lds, plan, fa, tp, n); break;
-    case 2: launch_scatter<2, NV>(grid, lds, plan, fa, tp, n); break;
-    case 3: launch_scatter<3, NV>(grid, lds, plan, fa, tp, n); break;
-    default: launch_scatter<0, NV>(grid, lds, plan, fa, tp, n);
+    case 1: launch_scatter<1, NV>(fast, grid, lds, plan, fa, tp, n); break;
+    case 2: launch_scatter<2, NV>(fast, grid, lds, plan, fa, tp, n); break;
+    case 3: launch_scatter<3, NV>(fast, grid, lds, plan, fa, tp, n); break;
+    default: launch_scatter<0, NV>(false, grid, lds, plan, fa, tp, n);
+    }
+}
+
+static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+template <int ND, int NV> static int scatter_blocks_per_cu(bool fast, size_t lds) {
+    int nb = 0;
+    if constexpr (ND > 0) {
+        if (fast) {
+            VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter_f64<ND, NV>, TA_THREADS, lds));
+            return nb;
+        }
+    }
+    VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter<ND, NV>, TA_THREADS, lds));
+    return nb;
+}
+
+template <int NV> static int scatter_blocks_per_cu_nd(int nd, bool fast, size_t lds) {
+    switch (nd) {
+    case 1: return scatter_blocks_per_cu<1, NV>(fast, lds);
+    case 2: return scatter_blocks_per_cu<2, NV>(fast, lds);
+    case 3: return scatter_blocks_per_cu<3, NV>(fast, lds);
+    default: return scatter_blocks_per_cu<0, NV>(false, lds);
     }
 }
 
@@ -366,7 +553,22 @@ bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t
     hipStream_t st = stream();
 
     // ---- sample
-    const uint32_t W = (uint32_t)cu_count() * TA_WG_PER_CU;
+    // the fast pass A: native f64 binners and sums, no masks, 16-byte aligned columns
+    bool fast = nd_f64 > 0 && !flags_mode;
+    for (int d = 0; d < plan.nb && fast; d++) fast = !plan.b[d].mask && aligned16(plan.b[d].data);
+    for (int k = 0; k < fa.na; k++) {
+        if (fa.a[k].mask) fast = false;
+        if (fa.a[k].kind != VH_AGG_COUNT) {
+            tp.vdata[tp.val_slot[k]] = fa.a[k].data;
+            fast = fast && fa.a[k].data && aligned16(fa.a[k].data);
+        }
+    }
+    const size_t lds_a = (size_t)8 * nv * TA_BATCH + (size_t)6 * TA_BATCH + 12 * (size_t)T + 64;
+    int bpc = nv == 0 ? scatter_blocks_per_cu_nd<0>(nd_f64, fast, lds_a)
+                      : nv == 1 ? scatter_blocks_per_cu_nd<1>(nd_f64, fast, lds_a)
+                                : scatter_blocks_per_cu_nd<2>(nd_f64, fast, lds_a);
+    bpc = std::max(1, std::min(bpc, TA_WG_PER_CU));
+    const uint32_t W = std::min<uint32_t>(1024, (uint32_t)cu_count() * bpc);
     DevBuf &meta = ws.tile_meta;
     const uint64_t meta_bytes = 8 * (uint64_t)T /*hist*/ + 4 * (uint64_t)T /*cap*/ + 8 * (uint64_t)T /*toff*/ +
                                 4 * (uint64_t)T * W /*fills*/ + 16 * (uint64_t)(T + 2 * W + 16) /*units*/ + 256;
@@ -400,7 +602,7 @@ bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t
     if (!sampled) return false;
 
     // ---- region capacities per workgroup
-    const uint64_t rows_per_wg = (n + W - 1) / W;
+    const uint64_t rows_per_wg = ((n + W - 1) / W + TA_BATCH - 1) / TA_BATCH * TA_BATCH;
     std::vector<uint32_t> cap(T);
     std::vector<uint64_t> toff(T);
     uint64_t stride = 0;
@@ -445,12 +647,12 @@ bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t
 
     // ---- pass A
     {
-        TimedScope ts("tile_scatter");
-        const size_t lds = (size_t)8 * nv * TA_BATCH + (size_t)6 * TA_BATCH + 12 * (size_t)T + 64;
+        TimedScope ts(fast ? "tile_scatter_f64" : "tile_scatter");
+        const size_t lds = lds_a;
         switch (nv) {
-        case 0: launch_scatter_nd<0>(nd_f64, W, lds, plan, fa, tp, n); break;
-        case 1: launch_scatter_nd<1>(nd_f64, W, lds, plan, fa, tp, n); break;
-        default: launch_scatter_nd<2>(nd_f64, W, lds, plan, fa, tp, n);
+        case 0: launch_scatter_nd<0>(nd_f64, fast, W, lds, plan, fa, tp, n); break;
+        case 1: launch_scatter_nd<1>(nd_f64, fast, W, lds, plan, fa, tp, n); break;
+        default: launch_scatter_nd<2>(nd_f64, fast, W, lds, plan, fa, tp, n);
         }
         VH_HIP(hipGetLastError());
     }

@@ -69,7 +69,8 @@ def allreduce_aggs(aggs, group=None):
             t = t.view(torch.int64)
         order = None
         if agg._kind == "AggFirst":
-            raise NotImplementedError("AggFirst across GPUs: gather order grids via combine_grids")
+            odev = DeviceArray(length, agg._grid_dtype, _ptr=agg.device_order_ptr(), _owner=agg)
+            order = torch.as_tensor(odev, device="cuda")
         combine_grids(agg._kind, t, order, group=group)
         torch.cuda.synchronize()
         agg._after_device_write()

@@ -309,6 +309,12 @@ class Aggregator:
         _lib.call("vh_agg_device_ptr", self._handle, ctypes.byref(p), ctypes.byref(p2))
         return p.value
 
+    def device_order_ptr(self):
+        """HBM address of AggFirst's order grid."""
+        p, p2 = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.call("vh_agg_device_ptr", self._handle, ctypes.byref(p), ctypes.byref(p2))
+        return p2.value
+
     def order_grid(self):
         """AggFirst's order grid (host copy, same layout as the value grid)."""
         out = np.empty(self._grid.length1d, self._grid_dtype)
