@@ -41,6 +41,7 @@ def parse():
     p.add_argument("--no-groupby", action="store_true")
     p.add_argument("--groupby-rows", type=float, default=1e9)
     p.add_argument("--check", action="store_true", help="verify size-independent properties")
+    p.add_argument("--breakdown", action="store_true", help="print host-side timing of one step")
     return p.parse_args()
 
 
@@ -89,6 +90,27 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if args.breakdown and rank == 0:
+        _lib.synchronize()
+        t = [time.perf_counter()]
+        bx = superagg.BinnerScalar_float64("x", -4.0, 4.0, bins)
+        by = superagg.BinnerScalar_float64("y", -4.0, 4.0, bins)
+        bx.set_data(x)
+        by.set_data(y)
+        grid = superagg.Grid([bx, by])
+        t.append(time.perf_counter())
+        count = superagg.AggCount_int64(grid)
+        total = superagg.AggSum_float64(grid)
+        total.set_data(w, 0)
+        t.append(time.perf_counter())
+        grid.bin([count, total])
+        t.append(time.perf_counter())
+        grid.bin([count, total])
+        t.append(time.perf_counter())
+        del count, total, grid
+        t.append(time.perf_counter())
+        print("breakdown_ms", {k: round((b - a) * 1e3, 3) for k, a, b in
+                               zip(["grid", "aggs", "bin1", "bin2_same_grid", "free"], t, t[1:])}, flush=True)
     _lib.timing_reset()
     _lib.timing_enable(True)
     barrier()
@@ -180,27 +202,31 @@ def main():
 
 
 def bench_groupby(n, args):
-    """C3: groupby(int32 key, 1e6 distinct).agg({v: [sum, count]}) on resident columns."""
+    """C3: groupby(int32 key, 1e6 distinct).agg({v: [sum, count]}) on resident columns, end to
+    end (key pass, aggregation pass, result read-back): 'auto' takes the dense-key grouper
+    (min/max pass + BinnerOrdinal), 'hash' forces the GPU ordered_set path (set build pass +
+    fused hash-probe binner)."""
     from vaex_amd import _lib
     from vaex_amd.device import DeviceArray
     import vaex_amd
     keys = DeviceArray.random(n, "randint", seed=5, a=5, b=5 + 1_000_000, dtype="int32")
     v = DeviceArray.random(n, "normal", seed=6)
     df = vaex_amd.from_arrays(key=keys, v=v)
-    df.groupby("key", agg={"v": ["sum", "count"]})  # warm-up
-    _lib.synchronize()
-    times = []
-    for _ in range(max(1, min(3, args.steps))):
-        t0 = time.perf_counter()
-        dfg = df.groupby("key", agg={"v": ["sum", "count"]})
+    out = {"rows": n, "algorithmic_bytes_per_row": 12}
+    for mode, sparse in (("auto", "auto"), ("hash", True)):
+        df.groupby("key", agg={"v": ["sum", "count"]}, assume_sparse=sparse)  # warm-up
         _lib.synchronize()
-        times.append(time.perf_counter() - t0)
-    t = min(times)
-    ngroups = len(dfg["key"].to_numpy())
+        times = []
+        for _ in range(max(1, min(3, args.steps))):
+            t0 = time.perf_counter()
+            dfg = df.groupby("key", agg={"v": ["sum", "count"]}, assume_sparse=sparse)
+            _lib.synchronize()
+            times.append(time.perf_counter() - t0)
+        t = min(times)
+        out[mode] = {"groups": len(dfg["key"].to_numpy()), "seconds": t, "rows_per_s": n / t,
+                     "algorithmic_GBps": 12 * n / t / 1e9}
     del keys, v, df
-    return {"rows": n, "groups": ngroups, "seconds": t, "rows_per_s": n / t,
-            "algorithmic_GBps": 12 * n / t / 1e9,
-            "note": "end to end incl. set build pass, set seal, aggregation pass and result read-back"}
+    return out
 
 
 def cpu_baseline(x, y, w, n, bins, target_seconds):

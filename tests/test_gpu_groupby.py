@@ -130,3 +130,26 @@ def test_groupby_device_resident_keys():
     assert gk[order].tolist() == uk.tolist()
     np.testing.assert_array_equal(dfg["v_count"].to_numpy()[order], c)
     np.testing.assert_allclose(dfg["v_sum"].to_numpy()[order], s, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("dense", [True, False])
+def test_dense_and_hash_groupers_agree(dense):
+    """Dense integer keys bin like a categorical (GrouperDense); assume_sparse=True forces the
+    hash set path (Grouper); both must give the oracle's key -> (sum, count) map."""
+    import vaex_amd
+    from vaex_amd import groupby as vg
+    rng = np.random.default_rng(9)
+    n = 1_500_000
+    keys = rng.integers(-300, 4000, n).astype(np.int64)
+    keys[keys % 7 == 0] = 10 ** 6  # a gap: most of the range is empty
+    v = rng.normal(size=n)
+    df = vaex_amd.from_arrays(key=keys, v=v)
+    g = vg.GroupBy(df, "key", dense=dense)
+    assert isinstance(g.by[0], vg.GrouperDense if dense else vg.Grouper)
+    dfg = g.agg({"v_sum": vaex_amd.agg.sum("v"), "n": vaex_amd.agg.count()})
+    uk, s, c = oracle.groupby_reference(keys, v)
+    gk = dfg["key"].to_numpy()
+    order = np.argsort(gk)
+    assert gk[order].tolist() == uk.tolist()
+    np.testing.assert_array_equal(dfg["n"].to_numpy()[order], c)
+    np.testing.assert_allclose(dfg["v_sum"].to_numpy()[order], s, rtol=1e-6, atol=1e-9)

@@ -269,12 +269,12 @@ def test_device_resident_columns_match_host():
     np.testing.assert_allclose(np.asarray(s), exp_s, rtol=1e-6, atol=1e-12)
 
 
-@pytest.mark.parametrize("dist", ["normal", "uniform"])
+@pytest.mark.parametrize("dist,n", [("normal", 4_000_000), ("uniform", 4_000_000), ("normal", 1_048_577)])
 @pytest.mark.parametrize("with_sum", [False, True])
-def test_tiled_path_large_grid(dist, with_sum):
-    """1027x1027 grid (the C2 shape) over 4M rows takes the tile-partitioned LDS path."""
+def test_tiled_path_large_grid(dist, n, with_sum):
+    """1027x1027 grid (the C2 shape) over >1M rows takes the tile-partitioned LDS path
+    (odd n: the last row goes through the global-atomic path)."""
     from vaex_amd.device import DeviceArray
-    n = 4_000_000
     rng = np.random.default_rng(13)
     if dist == "normal":
         x, y = rng.normal(size=n), rng.normal(size=n)

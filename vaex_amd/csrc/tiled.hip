@@ -25,6 +25,9 @@
 // different association order (within 1e-6 relative, north_star).
 #include <algorithm>
 #include <cmath>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 #include "binner_dev.hpp"
 #include "common.hpp"
@@ -32,10 +35,22 @@
 
 namespace vh {
 
-constexpr int TA_THREADS = 256;
-constexpr int TA_RPT = 8;
+#ifndef VH_TA_THREADS
+#define VH_TA_THREADS 512
+#endif
+#ifndef VH_TA_WAVES
+#define VH_TA_WAVES 0  // amdgpu_waves_per_eu floor for pass A (0 = compiler's choice)
+#endif
+constexpr int TA_THREADS = VH_TA_THREADS;
+#ifndef VH_TA_RPT
+#define VH_TA_RPT 8
+#endif
+#ifndef VH_TB_THREADS
+#define VH_TB_THREADS 512
+#endif
+constexpr int TA_RPT = VH_TA_RPT;
 constexpr int TA_BATCH = TA_THREADS * TA_RPT;
-constexpr int TB_THREADS = 512;
+constexpr int TB_THREADS = VH_TB_THREADS;
 constexpr uint64_t TILE_LDS_BUDGET = 64 * 1024;
 constexpr uint32_t TILE_MAX_TILES = 4096;
 constexpr int TA_WG_PER_CU = 4;
@@ -58,6 +73,7 @@ struct TileParams {
     int32_t val_slot[MAX_FUSED_AGGS];  // sum agg k -> value slot
     int32_t cnt_slot[MAX_FUSED_AGGS];  // count agg k -> CNT_ALWAYS / CNT_FLAG / value slot
     const double *vdata[2];    // value slot -> source column (fast kernel)
+    uint32_t debug;            // experiment switches (VH_TILE_DEBUG), 0 in production
 };
 
 struct WorkUnit {
@@ -121,6 +137,12 @@ __global__ __launch_bounds__(TA_THREADS) void k_tile_sample(BinPlan p, uint64_t 
 // s_barrier, which waits vmcnt(0): it would drain the prefetched loads of the next batch
 // and every outstanding region store at each of the batch's barriers
 // (cdna_hip_programming.md "Pipelining across barriers").  Only LDS traffic is ordered here.
+#if VH_TA_WAVES > 0
+#define TA_ATTR __attribute__((amdgpu_waves_per_eu(VH_TA_WAVES)))
+#else
+#define TA_ATTR
+#endif
+
 __device__ inline void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -158,21 +180,39 @@ __device__ inline uint32_t block_exclusive_scan(const uint32_t *in, uint32_t *ou
 // LDS layout of pass A: staged values | staged entries | staged tiles | hist | cursor | boff | wave sums
 struct ScatterLds {
     double *sv;
+    uint64_t *toff;
     uint32_t *se;
     uint16_t *st;
-    uint32_t *hist, *cursor, *boff, *wave_sums;
+    uint32_t *hist, *cursor, *boff, *cap, *wave_sums;
 };
+
+// LDS bytes of pass A (must match scatter_lds)
+__host__ __device__ inline size_t scatter_lds_bytes(int nv, uint32_t T) {
+    return (size_t)8 * nv * TA_BATCH + 8 * (size_t)T + (size_t)6 * TA_BATCH + 16 * (size_t)T + 64;
+}
 
 template <int NV> __device__ inline ScatterLds scatter_lds(unsigned char *raw, uint32_t T) {
     ScatterLds l;
     l.sv = reinterpret_cast<double *>(raw);
-    l.se = reinterpret_cast<uint32_t *>(raw + (size_t)8 * NV * TA_BATCH);
+    l.toff = reinterpret_cast<uint64_t *>(raw + (size_t)8 * NV * TA_BATCH);
+    l.se = reinterpret_cast<uint32_t *>(l.toff + T);
     l.st = reinterpret_cast<uint16_t *>(l.se + TA_BATCH);
     l.hist = reinterpret_cast<uint32_t *>(l.st + TA_BATCH);
     l.cursor = l.hist + T;
     l.boff = l.cursor + T;
-    l.wave_sums = l.boff + T;
+    l.cap = l.boff + T;
+    l.wave_sums = l.cap + T;
     return l;
+}
+
+// per-workgroup init: zero the histogram and cursors, stage the region table in LDS
+__device__ inline void scatter_lds_init(const ScatterLds &l, const TileParams &tp, uint32_t T) {
+    for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) {
+        l.hist[t] = 0;
+        l.cursor[t] = 0;
+        l.cap[t] = tp.cap[t];
+        l.toff[t] = tp.toff[t];
+    }
 }
 
 // phases 2-5 of a batch, after every row has its tile, entry, rank (-1 = drop) and
@@ -201,8 +241,10 @@ __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, co
         const uint32_t t = l.st[k];
         const uint32_t j = l.cursor[t] + (k - l.boff[t]);
         const uint32_t e32 = l.se[k];
-        if (j < tp.cap[t]) {
-            const uint64_t e = region0 + tp.toff[t] + j;
+        if (tp.debug & 1) {
+            asm volatile("" :: "v"(e32), "v"(j));
+        } else if (j < l.cap[t]) {
+            const uint64_t e = region0 + l.toff[t] + j;
             if (tp.flags_mode) reinterpret_cast<uint32_t *>(tp.entries)[e] = e32;
             else reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)(e32 & 0xffffu);
 #pragma unroll
@@ -232,15 +274,12 @@ __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, co
 
 // generic pass A: any binner kinds/dtypes, masks and keep flags
 template <int ND, int NV>
-__global__ __launch_bounds__(TA_THREADS) void k_tile_scatter(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
+__global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const uint32_t T = tp.ntiles;
     const ScatterLds l = scatter_lds<NV>(lds_raw, T);
     __shared__ uint32_t s_total;
-    for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) {
-        l.hist[t] = 0;
-        l.cursor[t] = 0;
-    }
+    scatter_lds_init(l, tp, T);
     __syncthreads();
     const uint32_t w = blockIdx.x;
     const uint64_t row_begin = (uint64_t)w * tp.rows_per_wg;
@@ -283,17 +322,14 @@ __device__ inline uint64_t scalar_f64_index(double v, double vmin, double scale,
 // 16-byte pairs and the next batch is prefetched into registers while the current one
 // is ranked, sorted and written.
 template <int ND, int NV>
-__global__ __launch_bounds__(TA_THREADS) void k_tile_scatter_f64(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
+__global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
     constexpr int NC = ND + NV;
     constexpr int PAIRS = TA_RPT / 2;
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const uint32_t T = tp.ntiles;
     const ScatterLds l = scatter_lds<NV>(lds_raw, T);
     __shared__ uint32_t s_total;
-    for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) {
-        l.hist[t] = 0;
-        l.cursor[t] = 0;
-    }
+    scatter_lds_init(l, tp, T);
     __syncthreads();
     const double *col[NC];
 #pragma unroll
@@ -312,23 +348,25 @@ __global__ __launch_bounds__(TA_THREADS) void k_tile_scatter_f64(BinPlan p, Fuse
     const uint64_t row_end = min(n, row_begin + tp.rows_per_wg);
     const uint32_t smask = (1u << tp.s_log2) - 1;
     const uint64_t region0 = (uint64_t)w * tp.wg_stride;
-    const double qnan = __builtin_nan("");
-
+    // Branch-free 16-byte loads: n is even on this path (the host bins an odd last row
+    // separately) and workgroup ranges are multiples of TA_BATCH, so a pair is either
+    // wholly inside [row_begin, row_end) or wholly past it; past-the-end pairs load the
+    // clamped last pair and are dropped by the i < row_end test.  With no load behind an
+    // exec branch the compiler counts vmcnt instead of draining to 0, so the prefetched
+    // batch stays in flight.
     auto load = [&](uint64_t b0, double2 (&dst)[PAIRS][NC]) {
 #pragma unroll
         for (int q = 0; q < PAIRS; q++) {
             const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + threadIdx.x);
+            const uint64_t is = i < n - 2 ? i : n - 2;
 #pragma unroll
-            for (int c = 0; c < NC; c++) {
-                if (i + 1 < row_end) dst[q][c] = *reinterpret_cast<const double2 *>(col[c] + i);
-                else dst[q][c] = make_double2(i < row_end ? col[c][i] : qnan, qnan);
-            }
+            for (int c = 0; c < NC; c++) dst[q][c] = *reinterpret_cast<const double2 *>(col[c] + is);
         }
     };
     double2 cur[PAIRS][NC], nxt[PAIRS][NC];
-    if (row_begin < row_end) load(row_begin, cur);
+    load(row_begin, cur);
     for (uint64_t b0 = row_begin; b0 < row_end; b0 += TA_BATCH) {
-        if (b0 + TA_BATCH < row_end) load(b0 + TA_BATCH, nxt);
+        load(b0 + TA_BATCH, nxt);
         uint32_t tile[TA_RPT], ent[TA_RPT];
         int32_t rank[TA_RPT];
         double vals[TA_RPT][NV > 0 ? NV : 1];
@@ -359,10 +397,11 @@ __global__ __launch_bounds__(TA_THREADS) void k_tile_scatter_f64(BinPlan p, Fuse
                 }
                 tile[r] = (uint32_t)(c >> tp.s_log2);
                 ent[r] = ((uint32_t)c & smask) | (f << 16);
-                if (f) rank[r] = (int32_t)atomicAdd(&l.hist[tile[r]], 1u);
+                if (f && !(tp.debug & 4)) rank[r] = (int32_t)atomicAdd(&l.hist[tile[r]], 1u);
+                if (tp.debug & 4) asm volatile("" :: "v"(ent[r]), "v"(tile[r]));
             }
         }
-        batch_commit<NV>(l, fa, tp, T, region0, tile, ent, rank, vals, &s_total);
+        if (!(tp.debug & 2)) batch_commit<NV>(l, fa, tp, T, region0, tile, ent, rank, vals, &s_total);
 #pragma unroll
         for (int q = 0; q < PAIRS; q++)
 #pragma unroll
@@ -401,6 +440,10 @@ __device__ inline void reduce_entry(const FusedAggs &fa, const TileParams &tp, u
 }
 
 constexpr int TB_UNROLL = 8;
+#ifndef VH_TB_VU
+#define VH_TB_VU 2
+#endif
+constexpr int TB_VU = VH_TB_VU;
 
 template <int NV>
 __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TileParams tp, const WorkUnit *units) {
@@ -423,6 +466,43 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
     for (uint32_t k = 0; k < nw; k++) {
         const uint32_t cnt = s_fill[k];
         const uint64_t base = (uint64_t)(u.w_begin + k) * tp.wg_stride + tp.toff[t];
+        if (!tp.flags_mode) {
+            // 8 consecutive u16 entries (16 B) and their values (16-B loads) per lane.  Regions
+            // start at multiples of 8 entries and hold a multiple of 8, so a lane's 8 entries
+            // never leave the region; loads past `cnt` are clamped in-region and ignored.
+            const uint16_t *eb = reinterpret_cast<const uint16_t *>(tp.entries) + base;
+            const uint32_t qmax = cap - 8;
+            for (uint32_t q0 = 0; q0 < cnt; q0 += TB_THREADS * 8 * TB_VU) {
+                uint4 ev[TB_VU];
+                double2 vv[TB_VU][NV > 0 ? NV : 1][4];
+#pragma unroll
+                for (int j = 0; j < TB_VU; j++) {
+                    uint32_t q = q0 + (j * TB_THREADS + threadIdx.x) * 8;
+                    q = q < qmax ? q : qmax;
+                    ev[j] = *reinterpret_cast<const uint4 *>(eb + q);
+#pragma unroll
+                    for (int s = 0; s < NV; s++)
+#pragma unroll
+                        for (int h = 0; h < 4; h++)
+                            vv[j][s][h] = *reinterpret_cast<const double2 *>(tp.values[s] + base + q + 2 * h);
+                }
+#pragma unroll
+                for (int j = 0; j < TB_VU; j++) {
+                    const uint32_t q = q0 + (j * TB_THREADS + threadIdx.x) * 8;
+                    const uint32_t words[4] = {ev[j].x, ev[j].y, ev[j].z, ev[j].w};
+#pragma unroll
+                    for (int e = 0; e < 8; e++) {
+                        if (q + e >= cnt) break;
+                        double v[NV > 0 ? NV : 1];
+#pragma unroll
+                        for (int s = 0; s < NV; s++) v[s] = (e & 1) ? vv[j][s][e >> 1].y : vv[j][s][e >> 1].x;
+                        const uint32_t local = (words[e >> 1] >> (16 * (e & 1))) & 0xffffu;
+                        reduce_entry<NV>(fa, tp, lds_raw, local, 0xfu, v);
+                    }
+                }
+            }
+            continue;
+        }
         for (uint32_t q0 = 0; q0 < cnt; q0 += TB_THREADS * TB_UNROLL) {
             uint32_t ent[TB_UNROLL];
             double v[TB_UNROLL][NV > 0 ? NV : 1];
@@ -431,8 +511,7 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                 const uint32_t q = q0 + j * TB_THREADS + threadIdx.x;
                 if (q < cnt) {
                     const uint64_t e = base + q;
-                    ent[j] = tp.flags_mode ? reinterpret_cast<const uint32_t *>(tp.entries)[e]
-                                           : (0xf0000u | reinterpret_cast<const uint16_t *>(tp.entries)[e]);
+                    ent[j] = reinterpret_cast<const uint32_t *>(tp.entries)[e];
 #pragma unroll
                     for (int s = 0; s < NV; s++) v[j][s] = tp.values[s][e];
                 }
@@ -508,9 +587,35 @@ template <int NV> static int scatter_blocks_per_cu_nd(int nd, bool fast, size_t 
     }
 }
 
+static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64,
+                           Workspace &ws);
+
 bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64, Workspace &ws) {
     if (n < (1u << 20) || cells >= (1ull << 40)) return false;
+    if ((n & 1) && nd_f64 > 0) {
+        // the fast pass A reads row pairs: tile all rows but the last, which takes the
+        // global-atomic path (every binner and value column is float64 here)
+        if (!try_tiled_impl(plan, fa_in, n - 1, cells, nd_f64, ws)) return false;
+        BinPlan p1 = plan;
+        FusedAggs f1 = fa_in;
+        for (int d = 0; d < p1.nb; d++) {
+            p1.b[d].data = reinterpret_cast<const double *>(p1.b[d].data) + (n - 1);
+            if (p1.b[d].mask) p1.b[d].mask += n - 1;
+        }
+        for (int k = 0; k < f1.na; k++) {
+            if (f1.a[k].data) f1.a[k].data += n - 1;
+            if (f1.a[k].mask) f1.a[k].mask += n - 1;
+        }
+        launch_fused(p1, f1, 1, cells, nd_f64, ws);
+        return true;
+    }
+    return try_tiled_impl(plan, fa_in, n, cells, nd_f64, ws);
+}
+
+static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64,
+                           Workspace &ws) {
     TileParams tp{};
+    if (const char *dbg = getenv("VH_TILE_DEBUG")) tp.debug = (uint32_t)atoi(dbg);
     // carried values: one slot per sum aggregator; counts keyed on a matching sum's value
     int nv = 0;
     for (int k = 0; k < fa_in.na; k++) {
@@ -563,15 +668,29 @@ bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t
             fast = fast && fa.a[k].data && aligned16(fa.a[k].data);
         }
     }
-    const size_t lds_a = (size_t)8 * nv * TA_BATCH + (size_t)6 * TA_BATCH + 12 * (size_t)T + 64;
-    int bpc = nv == 0 ? scatter_blocks_per_cu_nd<0>(nd_f64, fast, lds_a)
-                      : nv == 1 ? scatter_blocks_per_cu_nd<1>(nd_f64, fast, lds_a)
-                                : scatter_blocks_per_cu_nd<2>(nd_f64, fast, lds_a);
+    const size_t lds_a = scatter_lds_bytes(nv, T);
+    int bpc;
+    {
+        static std::mutex mu;
+        static std::map<std::tuple<int, int, int, bool, size_t>, int> cache;
+        std::lock_guard<std::mutex> lk(mu);
+        const auto key = std::make_tuple(current_device(), nd_f64, nv, fast, lds_a);
+        auto it = cache.find(key);
+        if (it == cache.end()) {
+            const int v = nv == 0 ? scatter_blocks_per_cu_nd<0>(nd_f64, fast, lds_a)
+                                  : nv == 1 ? scatter_blocks_per_cu_nd<1>(nd_f64, fast, lds_a)
+                                            : scatter_blocks_per_cu_nd<2>(nd_f64, fast, lds_a);
+            it = cache.emplace(key, v).first;
+        }
+        bpc = it->second;
+    }
     bpc = std::max(1, std::min(bpc, TA_WG_PER_CU));
     const uint32_t W = std::min<uint32_t>(1024, (uint32_t)cu_count() * bpc);
+    // pass-B work units: sum over tiles of ceil(e_t / target) <= T + 4 cu (target = n / 4 cu)
+    const uint64_t max_units = (uint64_t)T + 4 * (uint64_t)cu_count() + 16;
     DevBuf &meta = ws.tile_meta;
     const uint64_t meta_bytes = 8 * (uint64_t)T /*hist*/ + 4 * (uint64_t)T /*cap*/ + 8 * (uint64_t)T /*toff*/ +
-                                4 * (uint64_t)T * W /*fills*/ + 16 * (uint64_t)(T + 2 * W + 16) /*units*/ + 256;
+                                4 * (uint64_t)T * W /*fills*/ + 16 * max_units /*units*/ + 256;
     meta.ensure(meta_bytes);
     unsigned char *mb = meta.as<unsigned char>();
     uint64_t *d_hist = reinterpret_cast<uint64_t *>(mb);
@@ -642,7 +761,7 @@ bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t
         uint32_t g = (uint32_t)std::min<double>(W, std::max(1.0, std::ceil(e / target)));
         for (uint32_t k = 0; k < g; k++) units.push_back({t, (uint32_t)((uint64_t)W * k / g), (uint32_t)((uint64_t)W * (k + 1) / g), 0});
     }
-    if (units.size() > (size_t)T + 2 * W + 16) units.resize(T + 2 * W + 16);  // cannot happen: g sums to <= T + 4 cu
+    if (units.size() > max_units) fail(VH_ERR_RUNTIME, "tiled binning: work-unit table overflow");
     VH_HIP(hipMemcpyAsync(d_units, units.data(), sizeof(WorkUnit) * units.size(), hipMemcpyHostToDevice, st));
 
     // ---- pass A

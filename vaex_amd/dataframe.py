@@ -484,7 +484,7 @@ class DataFrame:
                 progress=None, delay=False):
         """dataframe.py:6622-6683."""
         from .groupby import GroupBy
-        groupby = GroupBy(self, by=by, sort=sort, row_limit=row_limit)
+        groupby = GroupBy(self, by=by, sort=sort, row_limit=row_limit, dense=assume_sparse != True)  # noqa: E712
         if agg is None:
             return groupby
         return groupby.agg(agg)

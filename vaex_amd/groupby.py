@@ -69,6 +69,60 @@ def _nan_key(v):
         return (0, v)
 
 
+# integer keys whose value range is at most this many cells are binned densely
+DENSE_KEY_MAX = 1 << 24
+
+
+class GrouperDense(BinnerBase):
+    """Integer keys spanning a small value range: ``BinnerOrdinal(key, N = max - min + 1,
+    min_value = min)``, exactly how the reference bins categoricals (GrouperCategory,
+    groupby.py:216-245), after one GPU min/max pass.  This replaces the set-build pass and
+    the per-row hash probe of ``_ordinal_values`` (Grouper) for dense keys; groups that do not
+    occur are dropped with the count(*) grid.  Groups come out sorted by key, which is also
+    the ``sort=True`` order."""
+
+    dense = True
+
+    def __init__(self, expression, vmin, vmax, df=None, row_limit=None):
+        self.df = df if df is not None else expression.df
+        self.expression = str(expression)
+        self.label = self.expression
+        self.min_value = int(vmin)
+        self.N = int(vmax) - int(vmin) + 1
+        dtype = self.df.data_type(self.expression)
+        self.bin_values = np.arange(int(vmin), int(vmax) + 1, dtype=np.int64)
+        if len(self.bin_values):
+            lo, hi = int(self.bin_values[0]), int(self.bin_values[-1])
+            self.bin_values = self.bin_values.astype(required_dtype_for_max(max(abs(lo), abs(hi))))
+        self.sort_indices = None
+        self.binner = self.df._binner_ordinal(self.expression, self.N, self.min_value)
+        self.key_dtype = dtype
+
+    def labels(self):
+        return self.bin_values.tolist()
+
+
+def _dense_range(df, expression):
+    """(min, max) when an integer, unmasked key spans <= DENSE_KEY_MAX values, else None."""
+    expression = str(expression)
+    col = df.columns.get(expression)
+    if col is None or np.ma.isMaskedArray(col):
+        return None
+    dtype = np.dtype(col.dtype)
+    if dtype.kind not in "iu" or df.filtered:
+        return None
+    n = df.length_unfiltered()
+    if n == 0:
+        return None
+    vmin, vmax = df.minmax(expression)
+    if not (abs(int(vmin)) < 2 ** 53 and abs(int(vmax)) < 2 ** 53):
+        return None
+    span = int(vmax) - int(vmin) + 1
+    if span > DENSE_KEY_MAX or span > 4 * n + 1024:
+        return None
+    return int(vmin), int(vmax)
+
+
 class GrouperCategory(BinnerBase):
     """groupby.py:216-245: categorical column -> BinnerOrdinal(min_value, N)."""
 
@@ -91,7 +145,7 @@ class GrouperCategory(BinnerBase):
 
 
 class GroupByBase:
-    def __init__(self, df, by, sort=False, row_limit=None):
+    def __init__(self, df, by, sort=False, row_limit=None, dense=True):
         df_original = df
         df = df.copy()
         self.df = df
@@ -104,6 +158,8 @@ class GroupByBase:
                 self.by.append(by_value)
             elif df.is_category(by_value):
                 self.by.append(GrouperCategory(df[str(by_value)], df=df, sort=sort, row_limit=row_limit))
+            elif dense and (rng := _dense_range(df, by_value)) is not None:
+                self.by.append(GrouperDense(df[str(by_value)], rng[0], rng[1], df=df, row_limit=row_limit))
             else:
                 self.by.append(Grouper(df[str(by_value)], df=df, sort=sort, row_limit=row_limit,
                                        df_original=df_original))
@@ -164,7 +220,7 @@ class GroupBy(GroupByBase):
     def agg(self, actions):
         """groupby.py:484-533."""
         arrays = self._agg(actions)
-        has_non_existing_pairs = len(self.by) > 1
+        has_non_existing_pairs = len(self.by) > 1 or any(getattr(b, "dense", False) for b in self.by)
         counts = self.counts
         if has_non_existing_pairs and counts is None:
             counts = self.df._agg(vagg.count(edges=True), self.binners, delay=True)
