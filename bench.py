@@ -39,6 +39,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
     p.add_argument("--no-groupby", action="store_true")
+    p.add_argument("--host-rows", type=float, default=2e8,
+                   help="rows of the PCIe-inclusive measurement (host numpy columns); 0 = skip")
     p.add_argument("--groupby-rows", type=float, default=1e9)
     p.add_argument("--check", action="store_true", help="verify size-independent properties")
     p.add_argument("--breakdown", action="store_true", help="print host-side timing of one step")
@@ -130,31 +132,38 @@ def main():
     total_rows = n * world * args.steps
     value = total_rows / elapsed
 
-    # roofline of the binning pipeline: algorithmic bytes = 24 B/row (x, y, w read once)
+    # roofline of the dominant kernel (pass A of the tiled path): algorithmic bytes = 24 B/row
+    # (x, y, w read once) x rows per launch / its average HIP-event duration
     kernel_ms = {}
     for k in TILE_KERNELS + ["bin_fused_global", "bin_fused_lds"]:
         cnt, ms = _lib.timing_read(k)
         if cnt:
             kernel_ms[k] = (cnt, ms)
+    algo_bytes = 24 * n
+    dom = max(kernel_ms, key=lambda k: kernel_ms[k][1]) if kernel_ms else None
+    dom_ms = kernel_ms[dom][1] / kernel_ms[dom][0] if dom else None
+    achieved = algo_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms else None
     launches = max([c for c, _ in kernel_ms.values()] or [1])
     pipeline_ms = sum(ms for _, ms in kernel_ms.values()) / max(launches, 1)
-    algo_bytes = 24 * n
-    achieved = algo_bytes / (pipeline_ms * 1e-3) / 1e9 if pipeline_ms else None
-    scatter = kernel_ms.get("tile_scatter")
     roofline = {
         "bound": "hbm",
-        "kernel": "+".join(k for k in kernel_ms),
+        "kernel": dom,
         "achieved": round(achieved, 1) if achieved else None,
         "peak": HBM_PEAK_GBPS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
         "traffic": None,
         "algorithmic_bytes_per_launch": algo_bytes,
-        "launch_ms": round(pipeline_ms, 4),
+        "kernel_ms": round(dom_ms, 4) if dom_ms else None,
         "per_kernel_ms": {k: round(ms / c, 4) for k, (c, ms) in kernel_ms.items()},
+        # whole binning pipeline (sample + pass A + pass B) against the same 24 B/row
+        "pipeline_ms": round(pipeline_ms, 4),
+        "pipeline_achieved": round(algo_bytes / (pipeline_ms * 1e-3) / 1e9, 1) if pipeline_ms else None,
     }
-    if scatter:
-        roofline["tile_scatter_GBps"] = round(algo_bytes / (scatter[1] / scatter[0] * 1e-3) / 1e9, 1)
+    traffic = pmc_traffic(dom, n, bins)
+    if traffic:
+        roofline["traffic"] = traffic["bytes"]
+        roofline["traffic_source"] = traffic["source"]
 
     check = None
     if args.check and rank == 0:
@@ -165,6 +174,8 @@ def main():
     extra = {}
     if rank == 0 and world == 1 and not args.no_groupby:
         extra["groupby"] = bench_groupby(int(args.groupby_rows), args)
+    if rank == 0 and world == 1 and args.host_rows > 0:
+        extra["host_columns"] = bench_host_columns(x, y, w, int(min(args.host_rows, n)), bins)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(x, y, w, n, bins, args.cpu_seconds)
@@ -199,6 +210,62 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_c2.json")
+PMC_KERNEL = {"tile_scatter_f64": "k_tile_scatter_f64<2, 1>", "tile_scatter": "k_tile_scatter<2, 1>",
+              "tile_reduce": "k_tile_reduce<1>"}
+
+
+def pmc_traffic(timer, n, bins):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
+    (profiles/pmc_c2.json, written by scripts/prof_summary.py from separate FETCH_SIZE and
+    WRITE_SIZE passes of this same bench command): 2 x FETCH_SIZE (gfx950 reports half of
+    a wide streaming read, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, KiB -> bytes.  Only used
+    when the profiled workload is the one being run."""
+    try:
+        with open(PMC_FILE) as f:
+            pmc = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if pmc.get("rows") != n or pmc.get("bins") != bins or timer not in PMC_KERNEL:
+        return None
+    for name, k in pmc["kernels"].items():
+        if name.endswith(PMC_KERNEL[timer]) and k.get("fetch_bytes_x2") is not None and k.get("write_bytes") is not None:
+            return {"bytes": int(k["fetch_bytes_x2"] + k["write_bytes"]),
+                    "source": f"{os.path.relpath(PMC_FILE, ROOT)} ({pmc.get('source')}): 2*FETCH_SIZE + WRITE_SIZE"}
+    return None
+
+
+def bench_host_columns(x, y, w, m, bins):
+    """PCIe-inclusive rate: the same count+sum query on host (numpy) columns, which the
+    library streams through its double-buffered pinned H2D pipeline (16 Mi-row chunks)."""
+    from vaex_amd import _lib, superagg
+    hx, hy, hw = x[:m].to_numpy(), y[:m].to_numpy(), w[:m].to_numpy()
+
+    def run():
+        bx = superagg.BinnerScalar_float64("x", -4.0, 4.0, bins)
+        by = superagg.BinnerScalar_float64("y", -4.0, 4.0, bins)
+        bx.set_data(hx)
+        by.set_data(hy)
+        grid = superagg.Grid([bx, by])
+        count = superagg.AggCount_int64(grid)
+        total = superagg.AggSum_float64(grid)
+        total.set_data(hw, 0)
+        grid.bin([count, total])
+        return count
+
+    run()
+    _lib.synchronize()
+    times = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        c = run()
+        _lib.synchronize()
+        times.append(time.perf_counter() - t0)
+    t = min(times)
+    ok = int(np.asarray(c).sum()) == m
+    return {"rows": m, "seconds": t, "rows_per_s": m / t, "host_GBps": 24 * m / t / 1e9, "count_equal": ok}
 
 
 def bench_groupby(n, args):

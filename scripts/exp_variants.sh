@@ -1,4 +1,4 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
-for v in libvaexhip.so libvaexhip_r16.so libvaexhip_r4.so libvaexhip_t1024.so libvaexhip_tb256.so libvaexhip_tb1024.so; do echo "== $v"
-VAEX_AMD_LIB=$PWD/vaex_amd/$v timeout -k 10 300 python -m pytest tests/test_gpu_superagg.py -m gpu -q -p no:cacheprovider -k "tiled_path" 2>&1 | tail -1
-EXP_DEBUG=0 VAEX_AMD_LIB=$PWD/vaex_amd/$v timeout -k 10 300 python scripts/exp_tiles.py 1e9 || exit $?; done
+timeout -k 10 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 300 > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -le 1 ] || exit $rc
+EXP_DEBUG=${EXP_DEBUG:-0} timeout -k 10 300 python scripts/exp_tiles.py 1e9 || exit $?
+timeout -k 10 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench.log 2>&1; rc=$?; tail -c 3000 gpurun_out/bench.log; exit $rc

@@ -1,10 +1,12 @@
 """Summarise a rocprofv3 run (rocpd SQLite output) into a text table for profiles/.
 
-usage: python scripts/prof_summary.py gpurun_out/prof_<tag> > profiles/<tag>.txt
+usage: python scripts/prof_summary.py gpurun_out/prof_<tag> [profiles/<tag>_pmc.json ROWS] > profiles/<tag>.txt
 Per kernel: calls, average duration (us; rocpd top_kernels reports us), and the PMC counters collected in the separate
 --pmc passes (FETCH_SIZE / WRITE_SIZE, kB per dispatch as rocprofv3 reports them).  Per
 MI355X_MICROARCH.md §HBM, FETCH_SIZE on gfx950 reads half the bytes of a wide coalesced
-streaming read: the 'fetch_GB_x2' column doubles it.
+streaming read: the 'fetch_GB_x2' column doubles it.  Units: rocprofv3 reports both counters
+in KiB (bytes = value * 1024, cdna_hip_programming.md §7).  With a second argument the
+per-kernel numbers are also written as JSON (bench.py reads the HBM traffic from it).
 """
 import glob
 import os
@@ -28,7 +30,8 @@ def pmc(db):
     return {(short(n), c): v for n, c, v, _ in rows}
 
 
-def main(d):
+def main(d, json_path=None, rows=None):
+    out = {}
     trace = glob.glob(os.path.join(d, "trace", "*.db"))[0]
     ks = kernel_stats(trace)
     counters = {}
@@ -42,10 +45,16 @@ def main(d):
         f = counters.get((k, "FETCH_SIZE"))
         w = counters.get((k, "WRITE_SIZE"))
         fs = f"{f:12.0f}" if f is not None else f"{'-':>12s}"
-        f2 = f"{2 * f / 1e6:11.3f}" if f is not None else f"{'-':>11s}"
+        f2 = f"{2 * f * 1024 / 1e9:11.3f}" if f is not None else f"{'-':>11s}"
         ws = f"{w:12.0f}" if w is not None else f"{'-':>12s}"
         print(f"{k[:60]:60s} {c:6d} {avg:11.2f} {tot / 1e3:10.3f} {fs} {f2} {ws}")
+        out[k] = {"calls": c, "avg_us": avg, "fetch_bytes_x2": None if f is None else 2 * f * 1024,
+                  "write_bytes": None if w is None else w * 1024}
+    if json_path:
+        import json
+        with open(json_path, "w") as fh:
+            json.dump({"source": d, "rows": rows, "bins": 1024, "kernels": out}, fh, indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None, int(float(sys.argv[3])) if len(sys.argv) > 3 else None)

@@ -419,18 +419,19 @@ void init_agg_grid(vh_agg *a) {
     VH_HIP(hipStreamSynchronize(stream()));
 }
 
-// chunk-relative device pointer of a column, staging host columns into the workspace
+// chunk-relative device pointer of a column: HBM columns in place, host columns from the
+// pipeline buffer the chunk was staged into
 struct Stager {
     Workspace &ws;
     uint64_t row0 = 0, len = 0;
-    int slot = 0;
+    int buf = 0;
     const void *get(const ColumnRef &c) {
         if (!c.set) return nullptr;
         const char *base = reinterpret_cast<const char *>(c.ptr) + row0 * c.itemsize;
         if (c.loc == VH_LOC_DEVICE) return base;
-        DevBuf &b = ws.stage_buf(slot++, len * c.itemsize);
-        VH_HIP(hipMemcpyAsync(b.ptr, base, len * c.itemsize, hipMemcpyHostToDevice, stream()));
-        return b.ptr;
+        const int i = ws.pipe.find(c.ptr);
+        if (i < 0) fail(VH_ERR_RUNTIME, "internal: host column not staged");
+        return ws.pipe.dev[buf].as<char>() + ws.pipe.off[i];
     }
 };
 
@@ -439,10 +440,68 @@ struct Stager {
 namespace vh {
 Workspace::~Workspace() = default;
 
-DevBuf &Workspace::stage_buf(int slot, uint64_t bytes) {
-    while ((int)stage.size() <= slot) stage.emplace_back(new DevBuf());
-    stage[slot]->ensure(bytes);
-    return *stage[slot];
+HostPipe::~HostPipe() {
+    for (int b = 0; b < 2; b++) {
+        if (copied[b]) (void)hipEventDestroy(copied[b]);
+        if (consumed[b]) (void)hipEventDestroy(consumed[b]);
+    }
+}
+
+void HostPipe::add(const ColumnRef &c) {
+    if (!c.set || c.loc != VH_LOC_HOST || find(c.ptr) >= 0) return;
+    cols.push_back(c.ptr);
+    isz.push_back(c.itemsize);
+}
+
+int HostPipe::find(const void *ptr) const {
+    for (size_t i = 0; i < cols.size(); i++)
+        if (cols[i] == ptr) return (int)i;
+    return -1;
+}
+
+void HostPipe::plan(uint64_t chunk_rows) {
+    chunk = chunk_rows;
+    off.assign(cols.size(), 0);
+    uint64_t o = 0;
+    for (size_t i = 0; i < cols.size(); i++) {
+        off[i] = o;
+        o = (o + chunk_rows * isz[i] + 255) & ~uint64_t(255);
+    }
+    bytes = o;
+    for (int b = 0; b < 2; b++) {
+        // the previous bin() call's copies and kernels are done (run_bin syncs at its end)
+        pending_copy[b] = pending_use[b] = false;
+        pinned[b].ensure(bytes);
+        dev[b].ensure(bytes);
+        if (!copied[b]) VH_HIP(hipEventCreateWithFlags(&copied[b], hipEventDisableTiming));
+        if (!consumed[b]) VH_HIP(hipEventCreateWithFlags(&consumed[b], hipEventDisableTiming));
+    }
+}
+
+void HostPipe::issue(uint64_t ci, uint64_t row0, uint64_t len) {
+    static const int threads = [] {
+        const char *e = getenv("VH_COPY_THREADS");
+        return e ? std::max(1, atoi(e)) : 8;
+    }();
+    const int b = (int)(ci & 1);
+    hipStream_t cs = copy_stream();
+    if (pending_copy[b]) VH_HIP(hipEventSynchronize(copied[b]));  // bounce buffer b drained
+    for (size_t i = 0; i < cols.size(); i++)
+        parallel_memcpy(pinned[b].as<char>() + off[i], reinterpret_cast<const char *>(cols[i]) + row0 * isz[i],
+                        len * isz[i], threads);
+    if (pending_use[b]) VH_HIP(hipStreamWaitEvent(cs, consumed[b], 0));  // chunk ci-2 binned
+    for (size_t i = 0; i < cols.size(); i++)
+        VH_HIP(hipMemcpyAsync(dev[b].as<char>() + off[i], pinned[b].as<char>() + off[i], len * isz[i],
+                              hipMemcpyHostToDevice, cs));
+    VH_HIP(hipEventRecord(copied[b], cs));
+    pending_copy[b] = true;
+}
+
+void HostPipe::wait_copied(int b) { VH_HIP(hipStreamWaitEvent(stream(), copied[b], 0)); }
+
+void HostPipe::mark_consumed(int b) {
+    VH_HIP(hipEventRecord(consumed[b], stream()));
+    pending_use[b] = true;
 }
 }  // namespace vh
 
@@ -809,9 +868,31 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
     }
     const uint64_t L = g->length1d;
     const uint64_t chunk_max = any_host ? (uint64_t(1) << 24) : (all_fusable ? length : (uint64_t(1) << 26));
-    for (uint64_t row0 = 0; row0 < length; row0 += chunk_max) {
+    HostPipe &pipe = g->ws.pipe;
+    if (any_host) {
+        pipe.cols.clear();
+        pipe.isz.clear();
+        for (auto *b : g->binners) {
+            pipe.add(b->data);
+            pipe.add(b->mask);
+        }
+        for (int k = 0; k < naggs; k++) {
+            pipe.add(aggs[k]->data);
+            pipe.add(aggs[k]->data2);
+            pipe.add(aggs[k]->mask);
+        }
+        pipe.plan(std::min(chunk_max, std::max<uint64_t>(length, 1)));
+        if (length) pipe.issue(0, 0, std::min(chunk_max, length));
+    }
+    for (uint64_t row0 = 0, ci = 0; row0 < length; row0 += chunk_max, ci++) {
         const uint64_t len = std::min(chunk_max, length - row0);
-        Stager st{g->ws, row0, len, 0};
+        const int buf = (int)(ci & 1);
+        if (any_host) {
+            // stage the next chunk while this one is binned
+            if (row0 + len < length) pipe.issue(ci + 1, row0 + len, std::min(chunk_max, length - row0 - len));
+            pipe.wait_copied(buf);
+        }
+        Stager st{g->ws, row0, len, buf};
         BinPlan plan{};
         plan.nb = (int)g->binners.size();
         for (int d = 0; d < plan.nb; d++) plan.b[d] = binner_dev(g->binners[d], g->strides[d], st);
@@ -867,7 +948,7 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                 VH_HIP(hipGetLastError());
             }
         }
-        if (any_host) VH_HIP(hipStreamSynchronize(stream()));  // staging buffers are reused
+        if (any_host) pipe.mark_consumed(buf);
     }
     VH_HIP(hipStreamSynchronize(stream()));
 }

@@ -145,6 +145,8 @@ template <typename T> __device__ inline bool is_nan_v(T v) {
 
 // ---- runtime ---------------------------------------------------------------
 hipStream_t stream();
+hipStream_t copy_stream();  // H2D staging copies (overlap the compute stream)
+void parallel_memcpy(void *dst, const void *src, uint64_t bytes, int threads);
 int current_device();
 int cu_count();
 
@@ -188,6 +190,33 @@ struct DevBuf {
             (void)hipGetLastError();
             ptr = nullptr;
             fail(VH_ERR_NOMEM, "hipMalloc of " + std::to_string(b) + " bytes failed: " + hipGetErrorString(e));
+        }
+        bytes = b;
+    }
+    template <typename T> T *as() const { return reinterpret_cast<T *>(ptr); }
+};
+
+// page-locked host buffer (DMA source of the H2D staging pipeline)
+struct PinnedBuf {
+    void *ptr = nullptr;
+    uint64_t bytes = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf &) = delete;
+    PinnedBuf &operator=(const PinnedBuf &) = delete;
+    ~PinnedBuf() { release(); }
+    void release() {
+        if (ptr) (void)hipHostFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    void ensure(uint64_t b) {
+        if (b <= bytes) return;
+        release();
+        hipError_t e = hipHostMalloc(&ptr, b, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            ptr = nullptr;
+            fail(VH_ERR_NOMEM, "hipHostMalloc of " + std::to_string(b) + " bytes failed: " + hipGetErrorString(e));
         }
         bytes = b;
     }

@@ -68,13 +68,34 @@ struct FusedAggs {
     FusedAgg a[MAX_FUSED_AGGS];
 };
 
+// Double-buffered H2D pipeline for host (numpy) columns, replacing the ExecutorLocal
+// chunk loop's in-place reads (execution.py:299-377): chunk i+1 is memcpy'd by host
+// threads into a pinned bounce buffer and DMA'd on the copy stream while chunk i is binned
+// on the compute stream; events order buffer reuse in both directions.
+struct HostPipe {
+    std::vector<const void *> cols;  // distinct host columns of this bin() call
+    std::vector<int> isz;
+    std::vector<uint64_t> off;       // byte offset of each column inside a chunk buffer
+    uint64_t chunk = 0, bytes = 0;
+    PinnedBuf pinned[2];
+    DevBuf dev[2];
+    hipEvent_t copied[2] = {nullptr, nullptr}, consumed[2] = {nullptr, nullptr};
+    bool pending_copy[2] = {false, false}, pending_use[2] = {false, false};
+    ~HostPipe();
+    void add(const ColumnRef &c);
+    void plan(uint64_t chunk_rows);
+    void issue(uint64_t ci, uint64_t row0, uint64_t len);  // stage chunk ci into buffer ci & 1
+    void wait_copied(int b);                                // compute stream waits for buffer b
+    void mark_consumed(int b);                              // after the chunk's kernels
+    int find(const void *ptr) const;
+};
+
 // per-grid device scratch, reused across bin() calls
 struct Workspace {
     DevBuf idx;                                   // generic path indices1d
-    std::vector<std::unique_ptr<DevBuf>> stage;   // host-column staging
+    HostPipe pipe;                                // host-column staging
     DevBuf tile_entries, tile_values, tile_meta;  // tiled path
     ~Workspace();
-    DevBuf &stage_buf(int slot, uint64_t bytes);
 };
 
 void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length);

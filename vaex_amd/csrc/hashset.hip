@@ -4,16 +4,18 @@
 // hopscotch maps:
 //   update      -- every row inserts its key with a CAS on an EMPTY slot
 //                  (linear probing from _hash64(bits), hash.hpp:25-30) and
-//                  lowers the slot's first-seen row with atomicMin;
+//                  lowers the slot's first-seen row with atomicMin (only when
+//                  the row is older than the slot's current one);
 //   seal        -- occupied slots are compacted and ordinals assigned in
 //                  first-appearance order (the order a single-threaded
 //                  reference update assigns `ordinal = map.size()`,
 //                  hash_primitives.hpp:453-461, with nmaps = 1);
 //   map_ordinal -- one probe per row (hash_primitives.hpp:556-583).
 // NaN and null keys get their own ordinals (nan_value / null_value,
-// hash_primitives.hpp:436-450).  The table grows x4 when half full or when a
-// probe sequence exceeds SET_MAX_PROBE (the chunk is then re-run: inserts are
-// idempotent).
+// hash_primitives.hpp:436-450).  Rows are inserted in chunks that double while the
+// table does not need to grow; inside a chunk an insert that would push the table past
+// 3/4 full, or a probe sequence longer than SET_MAX_PROBE, is refused and flags overflow:
+// the table then grows x4 and the chunk is re-run (inserts are idempotent).
 #include <algorithm>
 #include <limits>
 #include <memory>
@@ -29,7 +31,7 @@ enum { C_DISTINCT = 0, C_OVERFLOW, C_NAN_FIRST, C_NULL_FIRST, C_SPECIAL_FIRST, C
 struct vh_set {
     int dtype = VH_I64;
     uint64_t cap = 0;
-    DevBuf keys, first, ords, ctr;
+    DevBuf tab, lut, ctr;
     DevBuf stage_keys, stage_mask;
     DevBuf c_slot, c_first, c_ord, c_bits;
     uint64_t rows_seen = 0;
@@ -48,7 +50,7 @@ namespace vh {
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_set_insert(const T *keys, const uint8_t *mask, uint64_t n, uint64_t row0,
-                                                    uint64_t *tk, uint64_t *tf, uint64_t cap_mask, uint64_t *ctr) {
+                                                    uint64_t *tab, uint64_t cap_mask, uint64_t limit, uint64_t *ctr) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t row = row0 + i;
@@ -70,11 +72,18 @@ __global__ __launch_bounds__(256) void k_set_insert(const T *keys, const uint8_t
         }
         uint64_t pos = hash64(kb) & cap_mask;
         int p = 0;
+        bool refused = false;
         for (; p <= SET_MAX_PROBE; p++) {
-            uint64_t k = __hip_atomic_load(&tk[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint64_t k = __hip_atomic_load(&tab[2 * pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (k == kb) break;
             if (k == SET_EMPTY) {
-                uint64_t old = atomicCAS((unsigned long long *)&tk[pos], (unsigned long long)SET_EMPTY,
+                // a new key: refuse it once the table holds `limit` keys (the host grows the
+                // table and re-runs the chunk)
+                if (__hip_atomic_load(&ctr[C_DISTINCT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= limit) {
+                    refused = true;
+                    break;
+                }
+                uint64_t old = atomicCAS((unsigned long long *)&tab[2 * pos], (unsigned long long)SET_EMPTY,
                                          (unsigned long long)kb);
                 if (old == SET_EMPTY) {
                     atomicAdd((unsigned long long *)&ctr[C_DISTINCT], 1ULL);
@@ -84,49 +93,163 @@ __global__ __launch_bounds__(256) void k_set_insert(const T *keys, const uint8_t
             }
             pos = (pos + 1) & cap_mask;
         }
-        if (p > SET_MAX_PROBE) {
+        if (refused || p > SET_MAX_PROBE) {
             ctr[C_OVERFLOW] = 1;
             continue;
         }
-        if (__hip_atomic_load(&tf[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > row)
-            atomicMin((unsigned long long *)&tf[pos], (unsigned long long)row);
+        if (__hip_atomic_load(&tab[2 * pos + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > row)
+            atomicMin((unsigned long long *)&tab[2 * pos + 1], (unsigned long long)row);
     }
 }
 
-__global__ void k_set_rehash(const uint64_t *ok, const uint64_t *of, uint64_t ocap, uint64_t *nk, uint64_t *nf,
-                             uint64_t ncap_mask) {
+__global__ void k_set_rehash(const uint64_t *otab, uint64_t ocap, uint64_t *ntab, uint64_t ncap_mask) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ocap;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t kb = ok[i];
+        const uint64_t kb = otab[2 * i];
         if (kb == SET_EMPTY) continue;
         uint64_t pos = hash64(kb) & ncap_mask;
         for (;;) {
-            uint64_t old = atomicCAS((unsigned long long *)&nk[pos], (unsigned long long)SET_EMPTY,
+            uint64_t old = atomicCAS((unsigned long long *)&ntab[2 * pos], (unsigned long long)SET_EMPTY,
                                      (unsigned long long)kb);
             if (old == SET_EMPTY) break;
             pos = (pos + 1) & ncap_mask;
         }
-        nf[pos] = of[i];
+        ntab[2 * pos + 1] = otab[2 * i + 1];
     }
 }
 
-__global__ void k_set_compact(const uint64_t *tk, const uint64_t *tf, uint64_t cap, uint64_t *slot, uint64_t *first,
-                              uint64_t *bits, uint64_t *ctr) {
+__global__ void k_set_compact(const uint64_t *tab, uint64_t cap, uint64_t *slot, uint64_t *first, uint64_t *bits,
+                              uint64_t *ctr) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t kb = tk[i];
+        const uint64_t kb = tab[2 * i];
         if (kb == SET_EMPTY) continue;
         const uint64_t j = atomicAdd((unsigned long long *)&ctr[C_CURSOR], 1ULL);
         slot[j] = i;
-        first[j] = tf[i];
+        first[j] = tab[2 * i + 1];
         bits[j] = kb;
     }
 }
 
-__global__ void k_set_scatter_ords(const uint64_t *slot, const int64_t *ord, uint64_t m, int64_t *ords) {
+// ---- first-appearance ranks without a sort: first rows are distinct, so the rank of key j
+// is the number of set bits below first[j] in a row bitmap (per-word popcounts + scan)
+__global__ void k_rank_mark(const uint64_t *first, uint64_t m, uint64_t *bitmap) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < m; j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t f = first[j];
+        atomicOr((unsigned long long *)&bitmap[f >> 6], 1ULL << (f & 63));
+    }
+}
+
+constexpr int SCAN_THREADS = 256, SCAN_PER_THREAD = 16, SCAN_TILE = SCAN_THREADS * SCAN_PER_THREAD;
+
+// inclusive block scan of one value per thread (wave64 shuffles + wave partials in LDS)
+__device__ inline uint32_t block_scan_inclusive(uint32_t v, uint32_t *wsum, uint32_t *total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(v, off, 64);
+        if (lane >= off) v += y;
+    }
+    if (lane == 63) wsum[wave] = v;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+    for (int k = 0; k < SCAN_THREADS / 64; k++) {
+        if (k < wave) base += wsum[k];
+        tot += wsum[k];
+    }
+    __syncthreads();
+    *total = tot;
+    return base + v;
+}
+
+// phase 1: per-tile sums of popcount(bitmap words)
+__global__ __launch_bounds__(SCAN_THREADS) void k_rank_tile_sums(const uint64_t *bitmap, uint64_t nw, uint32_t *tile_sum) {
+    __shared__ uint32_t wsum[SCAN_THREADS / 64];
+    const uint64_t w0 = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_PER_THREAD;
+    uint32_t c = 0;
+    for (int k = 0; k < SCAN_PER_THREAD; k++)
+        if (w0 + k < nw) c += __popcll(bitmap[w0 + k]);
+    uint32_t tot;
+    block_scan_inclusive(c, wsum, &tot);
+    if (threadIdx.x == 0) tile_sum[blockIdx.x] = tot;
+}
+
+// phase 2: exclusive scan of the tile sums in place (one workgroup)
+__global__ __launch_bounds__(SCAN_THREADS) void k_rank_scan_tiles(uint32_t *tile_sum, uint64_t ntiles) {
+    __shared__ uint32_t wsum[SCAN_THREADS / 64];
+    uint32_t carry = 0;
+    for (uint64_t b = 0; b < ntiles; b += SCAN_THREADS) {
+        const uint64_t i = b + threadIdx.x;
+        const uint32_t v = i < ntiles ? tile_sum[i] : 0;
+        uint32_t tot;
+        const uint32_t inc = block_scan_inclusive(v, wsum, &tot);
+        if (i < ntiles) tile_sum[i] = carry + inc - v;
+        carry += tot;
+    }
+}
+
+// phase 3: exclusive prefix of set bits per word
+__global__ __launch_bounds__(SCAN_THREADS) void k_rank_word_prefix(const uint64_t *bitmap, uint64_t nw,
+                                                                   const uint32_t *tile_base, uint32_t *word_prefix) {
+    __shared__ uint32_t wsum[SCAN_THREADS / 64];
+    const uint64_t w0 = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_PER_THREAD;
+    uint32_t c[SCAN_PER_THREAD], sum = 0;
+    for (int k = 0; k < SCAN_PER_THREAD; k++) {
+        c[k] = w0 + k < nw ? __popcll(bitmap[w0 + k]) : 0;
+        sum += c[k];
+    }
+    uint32_t tot;
+    uint32_t acc = tile_base[blockIdx.x] + block_scan_inclusive(sum, wsum, &tot) - sum;
+    for (int k = 0; k < SCAN_PER_THREAD; k++) {
+        if (w0 + k < nw) word_prefix[w0 + k] = acc;
+        acc += c[k];
+    }
+}
+
+__device__ inline uint64_t rank_of_row(const uint64_t *bitmap, const uint32_t *word_prefix, uint64_t r) {
+    const uint64_t w = r >> 6, b = r & 63;
+    return word_prefix[w] + __popcll(bitmap[w] & ((1ULL << b) - 1));
+}
+
+struct SpecialKeys {
+    uint64_t key[3];  // sort keys (2*row for the EMPTY-bits key, 2*end_of_call - 1 for NaN / null)
+    int n;
+};
+
+// ordinal of compacted key j = its rank among the regular keys + the special keys before it;
+// also records the key bits per ordinal
+__global__ void k_rank_assign(const uint64_t *first, const uint64_t *bits, uint64_t m, const uint64_t *bitmap,
+                              const uint32_t *word_prefix, SpecialKeys sk, int64_t *ord, uint64_t *bits_by_ord) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < m; j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t f = first[j];
+        uint64_t o = rank_of_row(bitmap, word_prefix, f);
+        for (int s = 0; s < sk.n; s++) o += 2 * f > sk.key[s];
+        ord[j] = (int64_t)o;
+        bits_by_ord[o] = bits[j];
+    }
+}
+
+// number of regular keys first seen before row r (r may be the end of the rows)
+__global__ void k_rank_rows(const uint64_t *bitmap, const uint32_t *word_prefix, uint64_t nrows, uint64_t m,
+                            SpecialKeys sk, uint64_t *out) {
+    const int s = threadIdx.x;
+    if (s >= sk.n) return;
+    const uint64_t r = (sk.key[s] + 1) / 2;  // regular keys with 2 * first < key
+    out[s] = r >= nrows ? m : rank_of_row(bitmap, word_prefix, r);
+}
+
+// lookup table slot j <- (key bits, ordinal) of compacted key j at its table position
+__global__ void k_set_build_lut(const uint64_t *slot, const uint64_t *bits, const int64_t *ord, uint64_t m, int wide,
+                                uint64_t *lut) {
     for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < m;
-         j += (uint64_t)gridDim.x * blockDim.x)
-        ords[slot[j]] = ord[j];
+         j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t pos = slot[j];
+        if (wide) {
+            lut[2 * pos] = bits[j];
+            lut[2 * pos + 1] = (uint64_t)ord[j];
+        } else {
+            lut[pos] = ((uint64_t)ord[j] << 32) | (bits[j] & 0xffffffffULL);
+        }
+    }
 }
 
 template <typename T, typename O>
@@ -140,21 +263,17 @@ __global__ __launch_bounds__(256) void k_set_map_ordinal(const T *keys, uint64_t
 }
 
 static void set_grow(vh_set *s, uint64_t new_cap) {
-    DevBuf nk, nf;
-    nk.ensure(new_cap * 8);
-    nf.ensure(new_cap * 8);
-    VH_HIP(hipMemsetAsync(nk.ptr, 0xff, new_cap * 8, stream()));
-    VH_HIP(hipMemsetAsync(nf.ptr, 0xff, new_cap * 8, stream()));
+    DevBuf nt;
+    nt.ensure(new_cap * 16);
+    VH_HIP(hipMemsetAsync(nt.ptr, 0xff, new_cap * 16, stream()));
     if (s->cap) {
-        hipLaunchKernelGGL(k_set_rehash, dim3(blocks_for(s->cap, 256)), dim3(256), 0, stream(), s->keys.as<uint64_t>(),
-                           s->first.as<uint64_t>(), s->cap, nk.as<uint64_t>(), nf.as<uint64_t>(), new_cap - 1);
+        hipLaunchKernelGGL(k_set_rehash, dim3(blocks_for(s->cap, 256)), dim3(256), 0, stream(), s->tab.as<uint64_t>(),
+                           s->cap, nt.as<uint64_t>(), new_cap - 1);
         VH_HIP(hipGetLastError());
     }
     VH_HIP(hipStreamSynchronize(stream()));
-    std::swap(s->keys.ptr, nk.ptr);
-    std::swap(s->keys.bytes, nk.bytes);
-    std::swap(s->first.ptr, nf.ptr);
-    std::swap(s->first.bytes, nf.bytes);
+    std::swap(s->tab.ptr, nt.ptr);
+    std::swap(s->tab.bytes, nt.bytes);
     s->cap = new_cap;
     s->sealed = false;
 }
@@ -176,62 +295,86 @@ static void set_seal(vh_set *s) {
     s->c_ord.ensure(cap * 8);
     uint64_t zero = 0;
     VH_HIP(hipMemcpyAsync(s->ctr.as<uint64_t>() + C_CURSOR, &zero, 8, hipMemcpyHostToDevice, stream()));
-    hipLaunchKernelGGL(k_set_compact, dim3(blocks_for(cap, 256)), dim3(256), 0, stream(), s->keys.as<uint64_t>(),
-                       s->first.as<uint64_t>(), cap, s->c_slot.as<uint64_t>(), s->c_first.as<uint64_t>(),
-                       s->c_bits.as<uint64_t>(), s->ctr.as<uint64_t>());
+    hipLaunchKernelGGL(k_set_compact, dim3(blocks_for(cap, 256)), dim3(256), 0, stream(), s->tab.as<uint64_t>(), cap,
+                       s->c_slot.as<uint64_t>(), s->c_first.as<uint64_t>(), s->c_bits.as<uint64_t>(),
+                       s->ctr.as<uint64_t>());
     VH_HIP(hipGetLastError());
     c = read_ctr(s);
     const uint64_t m = c[C_CURSOR];
-    std::vector<uint64_t> first(m), bits(m);
-    VH_HIP(hipMemcpyAsync(first.data(), s->c_first.ptr, m * 8, hipMemcpyDeviceToHost, stream()));
-    VH_HIP(hipMemcpyAsync(bits.data(), s->c_bits.ptr, m * 8, hipMemcpyDeviceToHost, stream()));
-    VH_HIP(hipStreamSynchronize(stream()));
-    // order: regular keys (index j < m), then the special, nan, null pseudo keys
-    struct Ent {
-        uint64_t first;
-        int tie;
-        int64_t j;
+    // special keys (at most 3), ordered by (sort key, tie) as the reference flushes them
+    struct Spec {
+        uint64_t key;
+        int tie;  // 0 EMPTY-bits key, 1 NaN, 2 null
     };
-    std::vector<Ent> ents(m);
-    // sort keys: 2*row for keys, 2*end_of_call - 1 for NaN/null (after that call's keys,
-    // before any key first seen by a later call)
-    for (uint64_t j = 0; j < m; j++) ents[j] = {2 * first[j], 0, (int64_t)j};
-    if (c[C_SPECIAL_FIRST] != ~0ULL) ents.push_back({2 * c[C_SPECIAL_FIRST], 0, -3});
-    if (c[C_NAN_FIRST] != ~0ULL) ents.push_back({2 * s->nan_pos - 1, 1, -1});
-    if (c[C_NULL_FIRST] != ~0ULL) ents.push_back({2 * s->null_pos - 1, 2, -2});
-    std::sort(ents.begin(), ents.end(), [](const Ent &a, const Ent &b) {
-        return a.first != b.first ? a.first < b.first : a.tie < b.tie;
+    std::vector<Spec> specs;
+    if (c[C_SPECIAL_FIRST] != ~0ULL) specs.push_back({2 * c[C_SPECIAL_FIRST], 0});
+    if (c[C_NAN_FIRST] != ~0ULL) specs.push_back({2 * s->nan_pos - 1, 1});
+    if (c[C_NULL_FIRST] != ~0ULL) specs.push_back({2 * s->null_pos - 1, 2});
+    std::sort(specs.begin(), specs.end(), [](const Spec &a, const Spec &b) {
+        return a.key != b.key ? a.key < b.key : a.tie < b.tie;
     });
-    std::vector<int64_t> ord_of(m);
-    s->key_bits.assign(ents.size(), 0);
-    s->key_kind.assign(ents.size(), 0);
+    SpecialKeys sk{};
+    sk.n = (int)specs.size();
+    for (int k = 0; k < sk.n; k++) sk.key[k] = specs[k].key;
+    const uint64_t total = m + specs.size();
+    const uint64_t nrows = std::max<uint64_t>(s->rows_seen, 1);
+    const uint64_t nw = (nrows + 63) / 64;
+    const uint64_t ntiles = (nw + SCAN_TILE - 1) / SCAN_TILE;
+    DevBuf bitmap, prefix, tiles, bits_by_ord, spec_rank;
+    bitmap.ensure(nw * 8);
+    prefix.ensure(nw * 4);
+    tiles.ensure(ntiles * 4);
+    bits_by_ord.ensure(std::max<uint64_t>(total, 1) * 8);
+    spec_rank.ensure(3 * 8);
+    VH_HIP(hipMemsetAsync(bitmap.ptr, 0, nw * 8, stream()));
+    VH_HIP(hipMemsetAsync(bits_by_ord.ptr, 0xff, std::max<uint64_t>(total, 1) * 8, stream()));
+    {
+        TimedScope ts("set_rank");
+        if (m) hipLaunchKernelGGL(k_rank_mark, dim3(blocks_for(m, 256)), dim3(256), 0, stream(), s->c_first.as<uint64_t>(), m,
+                                  bitmap.as<uint64_t>());
+        hipLaunchKernelGGL(k_rank_tile_sums, dim3(ntiles), dim3(SCAN_THREADS), 0, stream(), bitmap.as<uint64_t>(), nw,
+                           tiles.as<uint32_t>());
+        hipLaunchKernelGGL(k_rank_scan_tiles, dim3(1), dim3(SCAN_THREADS), 0, stream(), tiles.as<uint32_t>(), ntiles);
+        hipLaunchKernelGGL(k_rank_word_prefix, dim3(ntiles), dim3(SCAN_THREADS), 0, stream(), bitmap.as<uint64_t>(), nw,
+                           tiles.as<uint32_t>(), prefix.as<uint32_t>());
+        if (m) hipLaunchKernelGGL(k_rank_assign, dim3(blocks_for(m, 256)), dim3(256), 0, stream(), s->c_first.as<uint64_t>(),
+                                  s->c_bits.as<uint64_t>(), m, bitmap.as<uint64_t>(), prefix.as<uint32_t>(), sk,
+                                  s->c_ord.as<int64_t>(), bits_by_ord.as<uint64_t>());
+        if (sk.n) hipLaunchKernelGGL(k_rank_rows, dim3(1), dim3(64), 0, stream(), bitmap.as<uint64_t>(), prefix.as<uint32_t>(),
+                                     s->rows_seen, m, sk, spec_rank.as<uint64_t>());
+        VH_HIP(hipGetLastError());
+    }
+    std::vector<uint64_t> srank(3, 0);
+    s->key_bits.assign(total, 0);
+    s->key_kind.assign(total, 0);
+    if (total) VH_HIP(hipMemcpyAsync(s->key_bits.data(), bits_by_ord.ptr, total * 8, hipMemcpyDeviceToHost, stream()));
+    if (sk.n) VH_HIP(hipMemcpyAsync(srank.data(), spec_rank.ptr, 3 * 8, hipMemcpyDeviceToHost, stream()));
+    const int wide = dtype_itemsize(s->dtype) > 4;
+    s->lut.ensure(cap * (wide ? 16 : 8));
+    VH_HIP(hipMemsetAsync(s->lut.ptr, 0xff, cap * (wide ? 16 : 8), stream()));
+    if (m) {
+        hipLaunchKernelGGL(k_set_build_lut, dim3(blocks_for(m, 256)), dim3(256), 0, stream(), s->c_slot.as<uint64_t>(),
+                           s->c_bits.as<uint64_t>(), s->c_ord.as<int64_t>(), m, wide, s->lut.as<uint64_t>());
+        VH_HIP(hipGetLastError());
+    }
+    VH_HIP(hipStreamSynchronize(stream()));
     s->nan_ord = s->null_ord = s->special_ord = -1;
-    for (size_t o = 0; o < ents.size(); o++) {
-        const int64_t j = ents[o].j;
-        if (j >= 0) {
-            ord_of[j] = (int64_t)o;
-            s->key_bits[o] = bits[j];
-        } else if (j == -1) {
-            s->nan_ord = (int64_t)o;
+    for (int k = 0; k < sk.n; k++) {
+        const int64_t o = (int64_t)srank[k] + k;  // regular keys before it + earlier specials
+        if (specs[k].tie == 1) {
+            s->nan_ord = o;
             s->key_kind[o] = 1;
-        } else if (j == -2) {
-            s->null_ord = (int64_t)o;
+        } else if (specs[k].tie == 2) {
+            s->null_ord = o;
             s->key_kind[o] = 2;
         } else {
-            s->special_ord = (int64_t)o;
+            s->special_ord = o;
             s->key_kind[o] = 3;
             s->key_bits[o] = SET_EMPTY;
         }
     }
-    s->ords.ensure(cap * 8);
-    if (m) {
-        VH_HIP(hipMemcpyAsync(s->c_ord.ptr, ord_of.data(), m * 8, hipMemcpyHostToDevice, stream()));
-        hipLaunchKernelGGL(k_set_scatter_ords, dim3(blocks_for(m, 256)), dim3(256), 0, stream(), s->c_slot.as<uint64_t>(),
-                           s->c_ord.as<int64_t>(), m, s->ords.as<int64_t>());
-        VH_HIP(hipGetLastError());
-    }
     VH_HIP(hipStreamSynchronize(stream()));
-    s->length = (int64_t)ents.size();
+    s->length = (int64_t)total;
     s->nan_count = (int64_t)c[C_NAN_COUNT];
     s->null_count = (int64_t)c[C_NULL_COUNT];
     s->sealed = true;
@@ -240,8 +383,8 @@ static void set_seal(vh_set *s) {
 SetDev set_device_view(vh_set *s) {
     set_seal(s);
     SetDev d{};
-    d.keys = s->keys.as<uint64_t>();
-    d.ords = s->ords.as<int64_t>();
+    d.lut = s->lut.as<uint64_t>();
+    d.wide = dtype_itemsize(s->dtype) > 4;
     d.cap_mask = s->cap - 1;
     d.nan_ord = s->nan_ord;
     d.null_ord = s->null_ord;
@@ -297,13 +440,14 @@ int vh_set_update(vh_set *s, const void *keys, const uint8_t *mask, uint64_t n, 
     VH_API_BEGIN
     loc = resolve_loc(keys, loc);
     const int isz = dtype_itemsize(s->dtype);
-    // Rows are inserted in chunks no longer than the table capacity while the table may
-    // still need to grow (a chunk can add at most `len` keys), so a too-small table is
-    // detected after one cheap chunk instead of after probing every row to the limit.
+    // Chunks start at cap/4 rows and double after every chunk that did not need the table
+    // to grow, so a too-small table is found after a cheap chunk and a settled one is
+    // streamed in a few large launches.  Inside a launch, new keys past `limit` (3/4 of the
+    // capacity) are refused and flag overflow; the table then grows and the chunk re-runs.
     const uint64_t stage_max = loc == VH_LOC_HOST ? (uint64_t(1) << 24) : ~0ULL;
+    uint64_t want = std::max<uint64_t>(s->cap / 4, 1 << 16);
     for (uint64_t row0 = 0, len = 0; row0 < n; row0 += len) {
-        // at most cap/4 new keys per chunk on a table kept <= half full: load stays <= 3/4
-        len = std::min({s->cap / 4, stage_max, n - row0});
+        len = std::min({want, stage_max, n - row0});
         const void *dk = reinterpret_cast<const char *>(keys) + row0 * isz;
         const uint8_t *dm = mask ? mask + row0 : nullptr;
         if (loc == VH_LOC_HOST) {
@@ -316,13 +460,15 @@ int vh_set_update(vh_set *s, const void *keys, const uint8_t *mask, uint64_t n, 
                 dm = s->stage_mask.as<uint8_t>();
             }
         }
+        bool grew = false;
         for (int attempt = 0;; attempt++) {
             {
                 TimedScope ts("set_insert");
+                const uint64_t limit = s->cap / 4 * 3;
                 VH_DISPATCH_DTYPE(s->dtype, T,
-                                  hipLaunchKernelGGL(k_set_insert<T>, dim3(blocks_for(len, 256)), dim3(256), 0, stream(),
-                                                     reinterpret_cast<const T *>(dk), dm, len, s->rows_seen + row0,
-                                                     s->keys.as<uint64_t>(), s->first.as<uint64_t>(), s->cap - 1,
+                                  hipLaunchKernelGGL(k_set_insert<T>, dim3(std::min<uint64_t>(blocks_for(len, 256), 1 << 16)),
+                                                     dim3(256), 0, stream(), reinterpret_cast<const T *>(dk), dm, len,
+                                                     s->rows_seen + row0, s->tab.as<uint64_t>(), s->cap - 1, limit,
                                                      s->ctr.as<uint64_t>()));
                 VH_HIP(hipGetLastError());
             }
@@ -332,12 +478,14 @@ int vh_set_update(vh_set *s, const void *keys, const uint8_t *mask, uint64_t n, 
                 uint64_t nc = s->cap * 4;
                 while (c[C_DISTINCT] * 2 > nc) nc *= 2;
                 set_grow(s, nc);
+                grew = true;
                 uint64_t zero = 0;
                 VH_HIP(hipMemcpyAsync(s->ctr.as<uint64_t>() + C_OVERFLOW, &zero, 8, hipMemcpyHostToDevice, stream()));
             }
             if (!overflow) break;
-            if (attempt > 8) fail(VH_ERR_RUNTIME, "hash set could not grow enough");
+            if (attempt > 16) fail(VH_ERR_RUNTIME, "hash set could not grow enough");
         }
+        want = grew ? std::max<uint64_t>(want, s->cap / 4) : want * 2;
     }
     s->rows_seen += n;
     {

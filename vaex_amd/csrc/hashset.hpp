@@ -1,10 +1,11 @@
 // GPU open-address hash set shared by hashset.hip (ordered_set) and the
 // fused set-ordinal binner in binning.hip.
 //
-// Layout in HBM: `keys[cap]` (uint64, key bits zero-extended, EMPTY = ~0),
-// `first[cap]` (uint64, first row a key was seen at: the ordinal order),
-// `ords[cap]` (int64 ordinal per slot, valid once sealed).  Linear probing
-// from _hash64(bits) (the reference's splitmix64 finaliser, hash.hpp:25-30).
+// Layout in HBM: `tab[cap]` of 16-byte slots {key bits zero-extended (EMPTY = ~0),
+// first row the key was seen at (the ordinal order)}, so an insert probe and its
+// first-row update touch one cache line; after sealing, a lookup table (below).
+// Linear probing from _hash64(bits) (the reference's splitmix64 finaliser,
+// hash.hpp:25-30).
 // 64-bit integer keys whose bits equal EMPTY (int64 -1, uint64 max) live in a
 // side slot ("special").  NaN and null keys get their own ordinals like the
 // reference's nan_value/null_value (hash_primitives.hpp:436-450).
@@ -42,9 +43,12 @@ template <typename T> __device__ inline uint64_t key_bits(T v) {
     }
 }
 
+// Lookup table built when the set is sealed: one 8-byte slot (ordinal << 32 | key bits)
+// for keys of <= 4 bytes, one 16-byte slot {key bits, ordinal} for 8-byte keys, so a
+// probe touches one cache line; EMPTY slots are all ones.
 struct SetDev {
-    const uint64_t *keys;
-    const int64_t *ords;
+    const uint64_t *lut;
+    int wide;             // 0: packed 8-byte slots, 1: {key, ord} 16-byte slots
     uint64_t cap_mask;
     int64_t nan_ord;      // ordinal of NaN (0x7fffffff when absent, as the reference)
     int64_t null_ord;     // ordinal of null / masked keys (-1 when absent)
@@ -55,11 +59,20 @@ struct SetDev {
 __device__ inline int64_t set_lookup_bits(const SetDev &s, uint64_t kb) {
     if (kb == SET_EMPTY) return s.special_ord;
     uint64_t pos = hash64(kb) & s.cap_mask;
-    for (int p = 0; p <= SET_MAX_PROBE; p++) {
-        uint64_t k = s.keys[pos];
-        if (k == kb) return s.ords[pos];
-        if (k == SET_EMPTY) return -1;
-        pos = (pos + 1) & s.cap_mask;
+    if (!s.wide) {
+        for (int p = 0; p <= SET_MAX_PROBE; p++) {
+            const uint64_t e = s.lut[pos];
+            if (e == SET_EMPTY) return -1;
+            if ((uint32_t)e == (uint32_t)kb) return (int64_t)(e >> 32);
+            pos = (pos + 1) & s.cap_mask;
+        }
+    } else {
+        for (int p = 0; p <= SET_MAX_PROBE; p++) {
+            const ulonglong2 e = reinterpret_cast<const ulonglong2 *>(s.lut)[pos];
+            if (e.x == kb) return (int64_t)e.y;
+            if (e.x == SET_EMPTY) return -1;
+            pos = (pos + 1) & s.cap_mask;
+        }
     }
     return -1;
 }

@@ -4,6 +4,8 @@
 // (the reference's vaexfast statisticNd<op_min_max>, vaexfast.cpp:1043-1055).
 #include <map>
 #include <mutex>
+#include <thread>
+#include <cstring>
 
 #include "common.hpp"
 
@@ -40,6 +42,38 @@ hipStream_t stream() {
     VH_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     g_streams[d] = s;
     return s;
+}
+
+static std::map<int, hipStream_t> g_copy_streams;
+
+hipStream_t copy_stream() {
+    int d = current_device();
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_copy_streams.find(d);
+    if (it != g_copy_streams.end()) return it->second;
+    hipStream_t s;
+    VH_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    g_copy_streams[d] = s;
+    return s;
+}
+
+// memcpy split over up to `threads` host threads (pageable -> pinned bounce copies)
+void parallel_memcpy(void *dst, const void *src, uint64_t bytes, int threads) {
+    const uint64_t min_part = 8ull << 20;
+    int t = (int)std::min<uint64_t>((uint64_t)std::max(1, threads), std::max<uint64_t>(1, bytes / min_part));
+    if (t <= 1) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    std::vector<std::thread> pool;
+    const uint64_t part = (bytes / t + 63) & ~uint64_t(63);
+    for (int i = 0; i < t; i++) {
+        const uint64_t o = (uint64_t)i * part;
+        if (o >= bytes) break;
+        const uint64_t len = std::min(part, bytes - o);
+        pool.emplace_back([=] { memcpy((char *)dst + o, (const char *)src + o, len); });
+    }
+    for (auto &th : pool) th.join();
 }
 
 int cu_count() {

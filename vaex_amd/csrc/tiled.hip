@@ -46,12 +46,15 @@ constexpr int TA_THREADS = VH_TA_THREADS;
 #define VH_TA_RPT 8
 #endif
 #ifndef VH_TB_THREADS
-#define VH_TB_THREADS 512
+#define VH_TB_THREADS 1024
 #endif
 constexpr int TA_RPT = VH_TA_RPT;
 constexpr int TA_BATCH = TA_THREADS * TA_RPT;
 constexpr int TB_THREADS = VH_TB_THREADS;
-constexpr uint64_t TILE_LDS_BUDGET = 64 * 1024;
+#ifndef VH_TILE_LDS_KB
+#define VH_TILE_LDS_KB 96
+#endif
+constexpr uint64_t TILE_LDS_BUDGET = VH_TILE_LDS_KB * 1024;
 constexpr uint32_t TILE_MAX_TILES = 4096;
 constexpr int TA_WG_PER_CU = 4;
 constexpr int SAMPLE_BLOCKS = 512;
@@ -177,47 +180,48 @@ __device__ inline uint32_t block_exclusive_scan(const uint32_t *in, uint32_t *ou
     return total;
 }
 
-// LDS layout of pass A: staged values | staged entries | staged tiles | hist | cursor | boff | wave sums
+// LDS layout of pass A: staged values | staged (destination, entry) pairs | per-tile
+// hist | batch offsets | region write base | region limit | wave sums
 struct ScatterLds {
     double *sv;
-    uint64_t *toff;
-    uint32_t *se;
-    uint16_t *st;
-    uint32_t *hist, *cursor, *boff, *cap, *wave_sums;
+    uint64_t *sp;
+    uint32_t *hist, *boff, *base, *lim, *wave_sums;
 };
 
 // LDS bytes of pass A (must match scatter_lds)
 __host__ __device__ inline size_t scatter_lds_bytes(int nv, uint32_t T) {
-    return (size_t)8 * nv * TA_BATCH + 8 * (size_t)T + (size_t)6 * TA_BATCH + 16 * (size_t)T + 64;
+    return (size_t)8 * nv * TA_BATCH + (size_t)8 * TA_BATCH + 16 * (size_t)T + 64;
 }
 
 template <int NV> __device__ inline ScatterLds scatter_lds(unsigned char *raw, uint32_t T) {
     ScatterLds l;
     l.sv = reinterpret_cast<double *>(raw);
-    l.toff = reinterpret_cast<uint64_t *>(raw + (size_t)8 * NV * TA_BATCH);
-    l.se = reinterpret_cast<uint32_t *>(l.toff + T);
-    l.st = reinterpret_cast<uint16_t *>(l.se + TA_BATCH);
-    l.hist = reinterpret_cast<uint32_t *>(l.st + TA_BATCH);
-    l.cursor = l.hist + T;
-    l.boff = l.cursor + T;
-    l.cap = l.boff + T;
-    l.wave_sums = l.cap + T;
+    l.sp = reinterpret_cast<uint64_t *>(raw + (size_t)8 * NV * TA_BATCH);
+    l.hist = reinterpret_cast<uint32_t *>(l.sp + TA_BATCH);
+    l.boff = l.hist + T;
+    l.base = l.boff + T;
+    l.lim = l.base + T;
+    l.wave_sums = l.lim + T;
     return l;
 }
 
-// per-workgroup init: zero the histogram and cursors, stage the region table in LDS
+// per-workgroup init: zero the histogram; a tile's region of this workgroup is
+// [toff, toff + cap) inside the workgroup's block, written from base upwards
 __device__ inline void scatter_lds_init(const ScatterLds &l, const TileParams &tp, uint32_t T) {
     for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) {
         l.hist[t] = 0;
-        l.cursor[t] = 0;
-        l.cap[t] = tp.cap[t];
-        l.toff[t] = tp.toff[t];
+        l.base[t] = (uint32_t)tp.toff[t];
+        l.lim[t] = (uint32_t)tp.toff[t] + tp.cap[t];
     }
 }
 
+constexpr uint32_t DEST_OVERFLOW = 0x80000000u;  // | tile: region full, global atomics
+
 // phases 2-5 of a batch, after every row has its tile, entry, rank (-1 = drop) and
-// carried values: exclusive scan of the tile histogram, counting sort into LDS, stream
-// the sorted runs to the workgroup's tile regions, advance the region cursors.
+// carried values: exclusive scan of the tile histogram; every row computes its final
+// destination (region base + rank, or overflow) and is counting-sorted into LDS as one
+// (destination, entry) pair + its values; the sorted pairs are streamed out as runs;
+// the region bases advance.
 template <int NV>
 __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, const TileParams &tp, uint32_t T,
                                     uint64_t region0, const uint32_t *tile, const uint32_t *ent, const int32_t *rank,
@@ -229,28 +233,30 @@ __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, co
 #pragma unroll
     for (int r = 0; r < TA_RPT; r++) {
         if (rank[r] < 0) continue;
-        const uint32_t pos = l.boff[tile[r]] + (uint32_t)rank[r];
-        l.se[pos] = ent[r];
-        l.st[pos] = (uint16_t)tile[r];
+        const uint32_t t = tile[r];
+        const uint32_t pos = l.boff[t] + (uint32_t)rank[r];
+        const uint32_t d = l.base[t] + (uint32_t)rank[r];
+        const uint32_t dest = d < l.lim[t] ? d : (DEST_OVERFLOW | t);
+        l.sp[pos] = ((uint64_t)dest << 32) | ent[r];
 #pragma unroll
         for (int s = 0; s < NV; s++) l.sv[s * TA_BATCH + pos] = vals[r][s];
     }
     lds_barrier();
     const uint32_t tot = *s_total;
     for (uint32_t k = threadIdx.x; k < tot; k += TA_THREADS) {
-        const uint32_t t = l.st[k];
-        const uint32_t j = l.cursor[t] + (k - l.boff[t]);
-        const uint32_t e32 = l.se[k];
+        const uint64_t pk = l.sp[k];
+        const uint32_t dest = (uint32_t)(pk >> 32), e32 = (uint32_t)pk;
         if (tp.debug & 1) {
-            asm volatile("" :: "v"(e32), "v"(j));
-        } else if (j < l.cap[t]) {
-            const uint64_t e = region0 + l.toff[t] + j;
+            asm volatile("" :: "v"(e32), "v"(dest));
+        } else if (!(dest & DEST_OVERFLOW)) {
+            const uint64_t e = region0 + dest;
             if (tp.flags_mode) reinterpret_cast<uint32_t *>(tp.entries)[e] = e32;
             else reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)(e32 & 0xffffu);
 #pragma unroll
             for (int s = 0; s < NV; s++) tp.values[s][e] = l.sv[s * TA_BATCH + k];
         } else {
             // region overflow (a sampling miss): apply the staged row with global atomics
+            const uint32_t t = dest & ~DEST_OVERFLOW;
             const uint64_t c = ((uint64_t)t << tp.s_log2) | (e32 & 0xffffu);
             const uint32_t f = e32 >> 16;
             #pragma unroll
@@ -267,7 +273,7 @@ __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, co
     }
     lds_barrier();
     for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) {
-        l.cursor[t] += l.hist[t];
+        l.base[t] += l.hist[t];
         l.hist[t] = 0;
     }
 }
@@ -305,7 +311,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter(BinPlan p, 
         batch_commit<NV>(l, fa, tp, T, region0, tile, ent, rank, vals, &s_total);
         lds_barrier();
     }
-    for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.cursor[t];
+    for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.base[t] - (uint32_t)tp.toff[t];
 }
 
 // BinnerScalar<double> index from a loaded value (superagg_binners.cpp:42-53)
@@ -408,7 +414,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan
             for (int c = 0; c < NC; c++) cur[q][c] = nxt[q][c];
         lds_barrier();
     }
-    for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.cursor[t];
+    for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.base[t] - (uint32_t)tp.toff[t];
 }
 
 template <int NV>
@@ -441,14 +447,21 @@ __device__ inline void reduce_entry(const FusedAggs &fa, const TileParams &tp, u
 
 constexpr int TB_UNROLL = 8;
 #ifndef VH_TB_VU
-#define VH_TB_VU 2
+#define VH_TB_VU 0  // 8-entry chunks per lane per step (0 = by NV)
 #endif
-constexpr int TB_VU = VH_TB_VU;
+template <int NV> constexpr int tb_vu() { return VH_TB_VU ? VH_TB_VU : NV == 0 ? 8 : NV == 1 ? 3 : 2; }
 
+// Pass B: one work unit = one tile x a range of pass-A workgroups.  The unit's regions are
+// read as one flat stream of 8-entry chunks (prefix sums of the region fills in LDS), so
+// every step issues TB_THREADS * VU full 16-byte entry loads (+ their values) no matter how
+// short the regions are; a lane finds the region of its chunk by a forward scan (chunk
+// indices of a lane only grow).  Entries are reduced with LDS atomics, then the tile is
+// flushed with coalesced global atomics.
 template <int NV>
 __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TileParams tp, const WorkUnit *units) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
     __shared__ uint32_t s_fill[1024];
+    __shared__ uint32_t s_pre[1025];
     const WorkUnit u = units[blockIdx.x];
     const uint32_t t = u.tile;
     const uint32_t cap = tp.cap[t];
@@ -462,68 +475,92 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
     if (!__syncthreads_or(any)) return;
     uint32_t *lw = reinterpret_cast<uint32_t *>(lds_raw);
     for (uint32_t i = threadIdx.x; i < fa.lds_words; i += TB_THREADS) lw[i] = 0;
+    if (!tp.flags_mode && threadIdx.x < 64) {
+        // exclusive scan of the chunk counts by the first wave (16 regions per lane)
+        const uint32_t lane = threadIdx.x, k0 = lane * 16;
+        uint32_t sum = 0;
+        for (uint32_t k = k0; k < k0 + 16 && k < nw; k++) sum += (s_fill[k] + 7) >> 3;
+        uint32_t inc = sum;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(inc, off, 64);
+            if ((int)lane >= off) inc += y;
+        }
+        uint32_t acc = inc - sum;
+        for (uint32_t k = k0; k < k0 + 16 && k < nw; k++) {
+            s_pre[k] = acc;
+            acc += (s_fill[k] + 7) >> 3;
+        }
+        if (lane == 63) s_pre[nw] = inc;
+    }
     __syncthreads();
-    for (uint32_t k = 0; k < nw; k++) {
-        const uint32_t cnt = s_fill[k];
-        const uint64_t base = (uint64_t)(u.w_begin + k) * tp.wg_stride + tp.toff[t];
-        if (!tp.flags_mode) {
-            // 8 consecutive u16 entries (16 B) and their values (16-B loads) per lane.  Regions
-            // start at multiples of 8 entries and hold a multiple of 8, so a lane's 8 entries
-            // never leave the region; loads past `cnt` are clamped in-region and ignored.
-            const uint16_t *eb = reinterpret_cast<const uint16_t *>(tp.entries) + base;
-            const uint32_t qmax = cap - 8;
-            for (uint32_t q0 = 0; q0 < cnt; q0 += TB_THREADS * 8 * TB_VU) {
-                uint4 ev[TB_VU];
-                double2 vv[TB_VU][NV > 0 ? NV : 1][4];
+    if (!tp.flags_mode) {
+        constexpr int VU = tb_vu<NV>();
+        const uint32_t C = s_pre[nw];
+        const uint16_t *ent16 = reinterpret_cast<const uint16_t *>(tp.entries);
+        const uint64_t toff_t = tp.toff[t];
+        uint32_t kk = 0;  // region of this lane's current chunk
+        for (uint32_t c0 = 0; c0 < C; c0 += TB_THREADS * VU) {
+            uint4 ev[VU];
+            double2 vv[VU][NV > 0 ? NV : 1][4];
+            uint32_t rem[VU];
 #pragma unroll
-                for (int j = 0; j < TB_VU; j++) {
-                    uint32_t q = q0 + (j * TB_THREADS + threadIdx.x) * 8;
-                    q = q < qmax ? q : qmax;
-                    ev[j] = *reinterpret_cast<const uint4 *>(eb + q);
+            for (int j = 0; j < VU; j++) {
+                const uint32_t c = c0 + j * TB_THREADS + threadIdx.x;
+                const uint32_t cc = c < C ? c : C - 1;
+                while (s_pre[kk + 1] <= cc) kk++;
+                const uint32_t q = (cc - s_pre[kk]) * 8;
+                // regions start at multiples of 8 entries and hold a multiple of 8, so the
+                // chunk never leaves its region (entries past the fill are ignored)
+                const uint64_t e = (uint64_t)(u.w_begin + kk) * tp.wg_stride + toff_t + q;
+                rem[j] = c < C ? min(8u, s_fill[kk] - q) : 0u;
+                ev[j] = *reinterpret_cast<const uint4 *>(ent16 + e);
 #pragma unroll
-                    for (int s = 0; s < NV; s++)
+                for (int s = 0; s < NV; s++)
 #pragma unroll
-                        for (int h = 0; h < 4; h++)
-                            vv[j][s][h] = *reinterpret_cast<const double2 *>(tp.values[s] + base + q + 2 * h);
+                    for (int h = 0; h < 4; h++) vv[j][s][h] = *reinterpret_cast<const double2 *>(tp.values[s] + e + 2 * h);
+            }
+#pragma unroll
+            for (int j = 0; j < VU; j++) {
+                const uint32_t words[4] = {ev[j].x, ev[j].y, ev[j].z, ev[j].w};
+#pragma unroll
+                for (int x = 0; x < 8; x++) {
+                    if ((uint32_t)x >= rem[j]) break;
+                    double v[NV > 0 ? NV : 1];
+#pragma unroll
+                    for (int s = 0; s < NV; s++) v[s] = (x & 1) ? vv[j][s][x >> 1].y : vv[j][s][x >> 1].x;
+                    const uint32_t local = (words[x >> 1] >> (16 * (x & 1))) & 0xffffu;
+                    if (tp.debug & 8) asm volatile("" :: "v"(local));
+                    else reduce_entry<NV>(fa, tp, lds_raw, local, 0xfu, v);
                 }
+            }
+        }
+    } else {
+        for (uint32_t k = 0; k < nw; k++) {
+            const uint32_t cnt = s_fill[k];
+            const uint64_t base = (uint64_t)(u.w_begin + k) * tp.wg_stride + tp.toff[t];
+            for (uint32_t q0 = 0; q0 < cnt; q0 += TB_THREADS * TB_UNROLL) {
+                uint32_t ent[TB_UNROLL];
+                double v[TB_UNROLL][NV > 0 ? NV : 1];
 #pragma unroll
-                for (int j = 0; j < TB_VU; j++) {
-                    const uint32_t q = q0 + (j * TB_THREADS + threadIdx.x) * 8;
-                    const uint32_t words[4] = {ev[j].x, ev[j].y, ev[j].z, ev[j].w};
+                for (int j = 0; j < TB_UNROLL; j++) {
+                    const uint32_t q = q0 + j * TB_THREADS + threadIdx.x;
+                    if (q < cnt) {
+                        const uint64_t e = base + q;
+                        ent[j] = reinterpret_cast<const uint32_t *>(tp.entries)[e];
 #pragma unroll
-                    for (int e = 0; e < 8; e++) {
-                        if (q + e >= cnt) break;
-                        double v[NV > 0 ? NV : 1];
-#pragma unroll
-                        for (int s = 0; s < NV; s++) v[s] = (e & 1) ? vv[j][s][e >> 1].y : vv[j][s][e >> 1].x;
-                        const uint32_t local = (words[e >> 1] >> (16 * (e & 1))) & 0xffffu;
-                        reduce_entry<NV>(fa, tp, lds_raw, local, 0xfu, v);
+                        for (int s = 0; s < NV; s++) v[j][s] = tp.values[s][e];
                     }
                 }
-            }
-            continue;
-        }
-        for (uint32_t q0 = 0; q0 < cnt; q0 += TB_THREADS * TB_UNROLL) {
-            uint32_t ent[TB_UNROLL];
-            double v[TB_UNROLL][NV > 0 ? NV : 1];
 #pragma unroll
-            for (int j = 0; j < TB_UNROLL; j++) {
-                const uint32_t q = q0 + j * TB_THREADS + threadIdx.x;
-                if (q < cnt) {
-                    const uint64_t e = base + q;
-                    ent[j] = reinterpret_cast<const uint32_t *>(tp.entries)[e];
-#pragma unroll
-                    for (int s = 0; s < NV; s++) v[j][s] = tp.values[s][e];
+                for (int j = 0; j < TB_UNROLL; j++) {
+                    const uint32_t q = q0 + j * TB_THREADS + threadIdx.x;
+                    if (q < cnt) reduce_entry<NV>(fa, tp, lds_raw, ent[j] & 0xffffu, ent[j] >> 16, v[j]);
                 }
-            }
-#pragma unroll
-            for (int j = 0; j < TB_UNROLL; j++) {
-                const uint32_t q = q0 + j * TB_THREADS + threadIdx.x;
-                if (q < cnt) reduce_entry<NV>(fa, tp, lds_raw, ent[j] & 0xffffu, ent[j] >> 16, v[j]);
             }
         }
     }
     __syncthreads();
+    if (tp.debug & 16) return;
     const uint64_t c0 = (uint64_t)t << tp.s_log2;
     const uint32_t ncell = (uint32_t)min((uint64_t)1 << tp.s_log2, tp.cells - c0);
     #pragma unroll
@@ -733,6 +770,8 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         toff[t] = stride;
         stride += c;
     }
+    // pass A keeps region positions in u32 (destination | overflow bit)
+    if (stride + rows_per_wg >= (uint64_t)DEST_OVERFLOW) return false;
     const uint64_t total = stride * W;
     const int ebytes = flags_mode ? 4 : 2;
     ws.tile_entries.ensure(total * ebytes);
