@@ -39,6 +39,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
     p.add_argument("--no-groupby", action="store_true")
+    p.add_argument("--no-count-only", action="store_true")
     p.add_argument("--host-rows", type=float, default=2e8,
                    help="rows of the PCIe-inclusive measurement (host numpy columns); 0 = skip")
     p.add_argument("--groupby-rows", type=float, default=1e9)
@@ -174,6 +175,8 @@ def main():
     extra = {}
     if rank == 0 and world == 1 and not args.no_groupby:
         extra["groupby"] = bench_groupby(int(args.groupby_rows), args)
+    if rank == 0 and world == 1 and not args.no_count_only:
+        extra["count_only"] = bench_count_only(x, y, n, bins, args)
     if rank == 0 and world == 1 and args.host_rows > 0:
         extra["host_columns"] = bench_host_columns(x, y, w, int(min(args.host_rows, n)), bins)
     cpu = None
@@ -235,6 +238,47 @@ def pmc_traffic(timer, n, bins):
             return {"bytes": int(k["fetch_bytes_x2"] + k["write_bytes"]),
                     "source": f"{os.path.relpath(PMC_FILE, ROOT)} ({pmc.get('source')}): 2*FETCH_SIZE + WRITE_SIZE"}
     return None
+
+
+def bench_count_only(x, y, n, bins, args):
+    """C2 count-only variant (SURVEY.md §8d target: >= 60 % of HBM peak at 16 B/row):
+    count(binby=[x, y]) alone, same timing method as the headline line."""
+    from vaex_amd import _lib, superagg
+
+    def step():
+        bx = superagg.BinnerScalar_float64("x", -4.0, 4.0, bins)
+        by = superagg.BinnerScalar_float64("y", -4.0, 4.0, bins)
+        bx.set_data(x)
+        by.set_data(y)
+        grid = superagg.Grid([bx, by])
+        count = superagg.AggCount_int64(grid)
+        grid.bin([count])
+        return count
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    _lib.synchronize()
+    _lib.timing_reset()
+    _lib.timing_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    _lib.synchronize()
+    t = time.perf_counter() - t0
+    _lib.timing_enable(False)
+    per = {}
+    for k in TILE_KERNELS + ["bin_fused_global", "bin_fused_lds"]:
+        c, ms = _lib.timing_read(k)
+        if c:
+            per[k] = ms / c
+    dom = max(per, key=per.get) if per else None
+    pipe = sum(per.values())
+    return {"rows": n, "ms_per_step": t / args.steps * 1e3, "rows_per_s": n * args.steps / t,
+            "algorithmic_bytes_per_row": 16, "per_kernel_ms": {k: round(v, 4) for k, v in per.items()},
+            "kernel": dom, "kernel_GBps": round(16 * n / (per[dom] * 1e-3) / 1e9, 1) if dom else None,
+            "kernel_frac": round(16 * n / (per[dom] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if dom else None,
+            "pipeline_GBps": round(16 * n / (pipe * 1e-3) / 1e9, 1) if pipe else None,
+            "pipeline_frac": round(16 * n / (pipe * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if pipe else None}
 
 
 def bench_host_columns(x, y, w, m, bins):
@@ -307,12 +351,19 @@ def cpu_baseline(x, y, w, n, bins, target_seconds):
     cnt = np.zeros(cells, np.int64)
     sm = np.zeros(cells, np.float64)
 
-    def run(m):
-        hx, hy, hw = x[:m].to_numpy(), y[:m].to_numpy(), w[:m].to_numpy()
+    host = {}
+
+    def run_parts(m, parts):
+        if host.get("m") != m:
+            host.update(m=m, x=x[:m].to_numpy(), y=y[:m].to_numpy(), w=w[:m].to_numpy())
+        hx, hy, hw = host["x"], host["y"], host["w"]
         t0 = time.perf_counter()
         used = L.or_bench_grid2d(hx.ctypes.data, hy.ctypes.data, hw.ctypes.data, m, -4.0, 4.0, -4.0, 4.0, bins,
-                                 nparts, threads, 1 << 20, cnt.ctypes.data, sm.ctypes.data)
+                                 parts, threads, 1 << 20, cnt.ctypes.data, sm.ctypes.data)
         return time.perf_counter() - t0, used
+
+    def run(m):
+        return run_parts(m, nparts)
 
     probe = min(n, 1 << 24)
     t, _ = run(probe)
@@ -327,7 +378,10 @@ def cpu_baseline(x, y, w, n, bins, target_seconds):
                     break
     except OSError:
         pass
+    # the same sample without the ideal_splits cap (one private grid per thread)
+    t_unc, used_unc = run_parts(m, threads)
     return {"value": m / t, "unit": "rows/s", "cores": used, "kind": "port",
+            "uncapped": {"value": m / t_unc, "cores": used_unc, "nparts": threads},
             "sample": f"first {m} rows of the same x,y,w columns, count+sum 1027x1027 grid, {t:.2f} s",
             "threads_available": threads, "nparts_rule": "max(2, T//8) (cpu.py:487-499)",
             "cpu_model": cpu_model, "host": platform.node()}

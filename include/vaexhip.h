@@ -137,6 +137,7 @@ int vh_agg_info(const vh_agg *agg, uint64_t *bytes, int *grid_dtype, uint64_t *i
 int vh_agg_download(vh_agg *agg, void *host, uint64_t bytes);
 int vh_agg_upload(vh_agg *agg, const void *host, uint64_t bytes);
 int vh_agg_download_order(vh_agg *agg, void *host, uint64_t bytes); /* AggFirst order grid */
+int vh_agg_upload_order(vh_agg *agg, const void *host, uint64_t bytes);   /* (new) combine across ranks */
 int vh_agg_device_ptr(vh_agg *agg, void **grid_dptr, void **grid2_dptr);
 /* Aggregator.reduce(list) superagg.cpp:160-167, 205-212, 252-259, 354-361, 470-480 */
 int vh_agg_reduce(vh_agg *agg, vh_agg *const *others, int nothers);

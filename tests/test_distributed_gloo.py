@@ -92,3 +92,64 @@ def test_shard_range_covers_rows():
             ranges = [shard_range(n, r, world) for r in range(world)]
             assert ranges[0][0] == 0 and ranges[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+
+
+def _keys():
+    rng = np.random.default_rng(7)
+    keys = rng.integers(0, 500, 20001).astype("f8")
+    keys[rng.integers(0, len(keys), 40)] = np.nan
+    mask = np.zeros(len(keys), bool)
+    mask[rng.integers(0, len(keys), 30)] = True
+    return keys, mask
+
+
+def _set_worker(rank, world, path):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from oracle import oracle
+    from vaex_amd.distributed import combine_minmax, merge_key_arrays, shard_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    keys, mask = _keys()
+    i1, i2 = shard_range(len(keys), rank, world)
+    local = oracle.OrderedSet(1)
+    local.update(keys[i1:i2], mask[i1:i2])
+    gathered = [None] * world
+    ka = local.key_array(np.float64)
+    dist.all_gather_object(gathered, (ka, local.null_value if local.null_count else -1))
+    merged = merge_key_arrays(gathered, lambda: oracle.OrderedSet(1))
+    shard = keys[i1:i2]
+    lo, hi = combine_minmax(np.nanmin(shard), np.nanmax(shard))
+    empty_lo, empty_hi = combine_minmax(np.nan if rank == 0 else 3.0, np.nan if rank == 0 else 4.0)
+    if rank == 0:
+        np.savez(path, keys=merged.key_array(np.float64), null_value=merged.null_value, nan_value=merged.nan_value,
+                 minmax=np.array([lo, hi, empty_lo, empty_hi]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_set_merge_and_minmax():
+    """Global ordered set from two ranks' key arrays == one set updated shard by shard
+    (ordinals in first-appearance order; NaN / null at the end of the update call that
+    first saw them), and NaN-ignoring min/max across ranks."""
+    pytest.importorskip("torch")
+    import sys
+    import torch.multiprocessing as mp
+    sys.path.insert(0, ROOT)
+    from oracle import oracle
+    from vaex_amd.distributed import shard_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(30500 + os.getpid() % 1000)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "set.npz")
+        mp.spawn(_set_worker, args=(2, path), nprocs=2, join=True)
+        got = np.load(path)
+        keys, mask = _keys()
+        ref = oracle.OrderedSet(1)
+        for r in range(2):
+            i1, i2 = shard_range(len(keys), r, 2)
+            ref.update(keys[i1:i2], mask[i1:i2])
+        np.testing.assert_array_equal(got["keys"], ref.key_array(np.float64))
+        assert int(got["null_value"]) == ref.null_value and int(got["nan_value"]) == ref.nan_value
+        np.testing.assert_array_equal(got["minmax"], [np.nanmin(keys), np.nanmax(keys), 3.0, 4.0])

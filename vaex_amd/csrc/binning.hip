@@ -720,6 +720,15 @@ int vh_agg_download_order(vh_agg *a, void *host, uint64_t bytes) {
     VH_API_END
 }
 
+int vh_agg_upload_order(vh_agg *a, const void *host, uint64_t bytes) {
+    VH_API_BEGIN
+    if (a->kind != VH_AGG_FIRST) fail(VH_ERR_ARG, "not an AggFirst");
+    if (bytes != a->grid->length1d * a->grid_isz) fail(VH_ERR_ARG, "upload size mismatch");
+    VH_HIP(hipMemcpyAsync(a->g2.ptr, host, bytes, hipMemcpyHostToDevice, stream()));
+    VH_HIP(hipStreamSynchronize(stream()));
+    VH_API_END
+}
+
 int vh_agg_upload(vh_agg *a, const void *host, uint64_t bytes) {
     VH_API_BEGIN
     if (bytes != a->grid->length1d * a->grid_isz) fail(VH_ERR_ARG, "upload size mismatch");

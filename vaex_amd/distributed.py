@@ -14,7 +14,7 @@ same code runs on CPU with the gloo backend in the tests.
 """
 import numpy as np
 
-_NP_TO_TORCH = None
+from .execution import ExecutorLocal
 
 
 def shard_range(n, rank, world):
@@ -74,3 +74,149 @@ def allreduce_aggs(aggs, group=None):
         combine_grids(agg._kind, t, order, group=group)
         torch.cuda.synchronize()
         agg._after_device_write()
+
+
+# ---------------------------------------------------------------------------------------
+# Distributed execution: every task pass of a DataFrame runs on each rank's row shard and
+# the reduced task parts are combined across ranks before the results are fulfilled, so
+# df.count/sum/mean/minmax/groupby/binby work unchanged on top.
+# ---------------------------------------------------------------------------------------
+
+def _reduce_op_for(kind):
+    return {"AggCount": "sum", "AggSum": "sum", "AggSumMoment": "sum", "AggMin": "min", "AggMax": "max",
+            "AggFirst": "first"}[kind]
+
+
+def combine_minmax(vmin, vmax, group=None):
+    """NaN-ignoring global (min, max) of per-rank limits (tasks.py:173-185 across ranks)."""
+    import torch
+    import torch.distributed as dist
+    lo = torch.tensor([np.inf if np.isnan(vmin) else float(vmin)], dtype=torch.float64)
+    hi = torch.tensor([-np.inf if np.isnan(vmax) else float(vmax)], dtype=torch.float64)
+    if dist.get_backend(group) == "nccl":
+        lo, hi = lo.cuda(), hi.cuda()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    lo, hi = float(lo.item()), float(hi.item())
+    return (np.nan if np.isinf(lo) and lo > 0 else lo), (np.nan if np.isinf(hi) and hi < 0 else hi)
+
+
+def merge_key_arrays(gathered, make_set):
+    """Global ordered set from the ranks' key arrays: rank r's keys are inserted after
+    those of ranks < r, each rank's in its own ordinal order, so with contiguous row shards
+    the ordinals are first-appearance order over the whole column (what one update pass
+    over all rows gives, ``ordered_set::merge`` semantics, hash_primitives.hpp:96-281).
+    ``gathered``: per rank (keys, null_index or -1); ``make_set()``: an empty set with
+    ``update(keys, mask)``."""
+    merged = make_set()
+    for keys, null_index in gathered:
+        keys = np.asarray(keys)
+        if not len(keys):
+            continue
+        mask = None
+        if null_index is not None and null_index >= 0:
+            mask = np.zeros(len(keys), np.uint8)
+            mask[int(null_index)] = 1
+        merged.update(keys, mask)
+    return merged
+
+
+def _host_allreduce(arr, op, group):
+    import torch
+    import torch.distributed as dist
+    t = torch.from_numpy(np.ascontiguousarray(arr).view(np.int64) if arr.dtype == np.uint64 else
+                         np.ascontiguousarray(arr))
+    dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}[op],
+                    group=group)
+    out = t.numpy()
+    return out.view(np.uint64) if arr.dtype == np.uint64 else out
+
+
+def combine_aggs_host(aggs, group=None):
+    """All-reduce aggregator grids through host memory (gloo): download, combine, upload."""
+    from . import _lib
+    import torch
+    import torch.distributed as dist
+    for agg in aggs:
+        agg._before_device_use()
+        grid = np.empty(agg.grid.length1d, agg._grid_dtype)
+        _lib.call("vh_agg_download", agg._handle, grid.ctypes.data, agg._nbytes)
+        op = _reduce_op_for(agg._kind)
+        if op == "first":
+            order = np.empty(agg.grid.length1d, agg._grid_dtype)
+            _lib.call("vh_agg_download_order", agg._handle, order.ctypes.data, agg._nbytes)
+            world = dist.get_world_size(group)
+            vals = [torch.empty_like(torch.from_numpy(grid)) for _ in range(world)]
+            ords = [torch.empty_like(torch.from_numpy(order)) for _ in range(world)]
+            dist.all_gather(vals, torch.from_numpy(grid), group=group)
+            dist.all_gather(ords, torch.from_numpy(order), group=group)
+            v, o = vals[0].numpy().copy(), ords[0].numpy().copy()
+            for r in range(1, world):
+                take = ords[r].numpy() < o
+                v[take] = vals[r].numpy()[take]
+                o[take] = ords[r].numpy()[take]
+            grid, order = v, o
+            _lib.call("vh_agg_upload_order", agg._handle, np.ascontiguousarray(order).ctypes.data, agg._nbytes)
+        else:
+            grid = _host_allreduce(grid, op, group)
+        grid = np.ascontiguousarray(grid)
+        _lib.call("vh_agg_upload", agg._handle, grid.ctypes.data, agg._nbytes)
+        agg._after_device_write()
+
+
+class ExecutorDistributed(ExecutorLocal):
+    """ExecutorLocal over this rank's row shard, combining task parts across ranks.
+
+    One process per GPU (``torch.distributed``): with ``shard_rows`` every rank holds the
+    same (e.g. memory-mapped) DataFrame and processes rows ``shard_range(n, rank, world)``;
+    without it each rank's DataFrame already is its shard.  After the local parts are
+    reduced: aggregator grids are all-reduced (RCCL on HBM grids with backend "nccl",
+    through host memory with "gloo"), min/max limits are reduced, and ordered sets are
+    merged from all ranks' key arrays (:func:`merge_key_arrays`) so every rank bins with
+    the same global ordinals.
+    """
+
+    def __init__(self, group=None, shard_rows=True, device_collectives=None, chunk_size=None):
+        import torch.distributed as dist
+        super().__init__(chunk_size)
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.shard_rows = shard_rows
+        self.device_collectives = (dist.get_backend(group) == "nccl") if device_collectives is None \
+            else device_collectives
+
+    def row_range(self, df):
+        n = df.length_unfiltered()
+        return shard_range(n, self.rank, self.world) if self.shard_rows else (0, n)
+
+    def chunk_size_for(self, df):
+        if self.chunk_size is None and df.is_device_resident():
+            i1, i2 = self.row_range(df)
+            return max(1, i2 - i1)
+        return super().chunk_size_for(df)
+
+    def combine_parts(self, parts):
+        from .taskparts import TaskPartAggregation, TaskPartMinMax, TaskPartSetCreate
+        for p in parts:
+            if isinstance(p, TaskPartAggregation):
+                aggs = p.get_aggregators()
+                if self.device_collectives:
+                    allreduce_aggs(aggs, group=self.group)
+                else:
+                    combine_aggs_host(aggs, group=self.group)
+            elif isinstance(p, TaskPartMinMax):
+                p.vmin, p.vmax = combine_minmax(p.vmin, p.vmax, group=self.group)
+            elif isinstance(p, TaskPartSetCreate):
+                p.set = combine_sets(p.set, group=self.group)
+
+
+def combine_sets(local_set, group=None):
+    """Replace a rank's ordered set by the global one (all-gather of key arrays)."""
+    import torch.distributed as dist
+    keys = local_set.key_array()
+    null_index = int(local_set.null_value) if local_set.has_null else -1
+    world = dist.get_world_size(group)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, (keys, null_index), group=group)
+    return merge_key_arrays(gathered, lambda: type(local_set)())

@@ -81,6 +81,13 @@ class ExecutorLocal:
             return max(1, df.length_unfiltered())
         return CHUNK_SIZE_HOST
 
+    def row_range(self, df):
+        """Rows this executor processes (all of them; a distributed executor its shard)."""
+        return 0, df.length_unfiltered()
+
+    def combine_parts(self, parts):
+        """Hook after the parts are reduced (a distributed executor combines across ranks)."""
+
     def _create_part(self, task, df):
         if isinstance(task, TaskAggregations):
             return TaskPartAggregation(df, task.binners, task.aggregation_descriptions)
@@ -123,17 +130,19 @@ class ExecutorLocal:
             for e in p.expressions:
                 if e not in expressions:
                     expressions.append(e)
-        n = df.length_unfiltered()
+        start, end = self.row_range(df)
         chunk_size = self.chunk_size_for(df)
         try:
-            for i1 in range(0, n, chunk_size):
-                i2 = min(n, i1 + chunk_size)
+            for i1 in range(start, end, chunk_size):
+                i2 = min(end, i1 + chunk_size)
                 filter_mask = df.evaluate_filter_mask(i1, i2) if df.filtered else None
                 blocks = {e: df.evaluate_chunk(e, i1, i2, filter_mask) for e in expressions}
                 for p in parts:
                     p.process(0, i1, i2, filter_mask, blocks)
-            for t, p in zip(tasks, parts):
+            for p in parts:
                 p.reduce([])
+            self.combine_parts(parts)
+            for t, p in zip(tasks, parts):
                 t.fulfill(p.get_result())
         except Exception as e:
             for t in tasks:
