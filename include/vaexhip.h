@@ -162,6 +162,26 @@ int vh_set_map_ordinal(vh_set *set, const void *keys, uint64_t n, int loc, void 
 int vh_minmax(const void *data, uint64_t n, int dtype, int flip_endian, const uint8_t *mask, int loc,
               double *out_min, double *out_max);
 
+/* ---- fused hash groupby (hashagg.hip) ------------------------------------
+ * groupby(key).agg({count(*), count(v), sum(v), mean(v)}) for one integer key column of
+ * <= 4 bytes and up to 2 value columns, in one hash-partitioned pass.  Replaces, for that
+ * query shape, Grouper pass 1 (ordered_set update, hash_primitives.hpp:96-281) +
+ * _ordinal_values/map_ordinal (hash_primitives.hpp:543-583) + BinnerOrdinal
+ * (superagg_binners.cpp:104-142) + AggCount/AggSum (superagg.cpp:155-192,349-389), as
+ * driven by groupby.py:97-168,484-533.  Groups come out sorted by key. */
+typedef struct vh_hashagg vh_hashagg;
+/* nonnull_mask: bit v set = the non-NaN count of value column v is read (count(v), mean);
+ * the counts of other float columns are left undefined */
+int vh_hashagg_create(int key_dtype, int nvals, const int *val_dtypes, uint32_t nonnull_mask, vh_hashagg **out);
+int vh_hashagg_destroy(vh_hashagg *h);
+/* one chunk of rows (may be called repeatedly); VH_ERR_RUNTIME on a table overflow
+ * (the caller then falls back to the ordered_set path) */
+int vh_hashagg_update(vh_hashagg *h, const void *keys, const void *const *vals, uint64_t n, int loc);
+int vh_hashagg_finish(vh_hashagg *h, uint64_t *ngroups);
+/* host outputs, ngroups items each: keys as int64, count(*) int64, per value column its sum
+ * (8 bytes: double for float columns, int64/uint64 for integers) and non-NaN count int64 */
+int vh_hashagg_read(vh_hashagg *h, int64_t *keys, int64_t *counts, void *const *sums, int64_t *const *nonnull);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,14 +1,19 @@
 #!/bin/bash
-# Build tiled.hip variants (compile-time tuning macros) as vaex_amd/libvaexhip_<name>.so for A/B runs.
-# usage: scripts/build_variants.sh name:"-DFLAG=.. -DFLAG2=.." ...
+# Build variants of one HIP source (compile-time tuning macros) as vaex_amd/libvaexhip_<name>.so
+# for A/B runs (select one with VAEX_AMD_LIB=vaex_amd/libvaexhip_<name>.so).
+# usage: SRC=hashagg scripts/build_variants.sh name:"-DFLAG=.. -DFLAG2=.." ...
 set -e
+SRC=${SRC:-tiled}
 cd "$(dirname "$0")/../vaex_amd/csrc"
 make -s
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -munsafe-fp-atomics"
+OBJS="runtime binning tiled hashset hashagg"
 for v in "$@"; do
   name=${v%%:*}; fl=${v#*:}
   mkdir -p build/var_$name
-  /opt/rocm/bin/hipcc $F $fl -c tiled.hip -o build/var_$name/tiled.o &&
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../libvaexhip_$name.so build/runtime.o build/binning.o build/hashset.o build/var_$name/tiled.o &
+  others=""
+  for o in $OBJS; do [ "$o" = "$SRC" ] || others="$others build/$o.o"; done
+  ( /opt/rocm/bin/hipcc $F $fl -c $SRC.hip -o build/var_$name/$SRC.o &&
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../libvaexhip_$name.so $others build/var_$name/$SRC.o ) &
 done
 wait

@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 STAGE=${1:-all}
 ok() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
 if [ "$STAGE" = all ] || [ "$STAGE" = tests ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
   ok $rc || exit $rc
 fi

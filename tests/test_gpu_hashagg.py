@@ -1,0 +1,192 @@
+"""Fused hash groupby (hashagg.hip) against the oracle's key -> (sum, count) restatement
+(oracle.groupby_reference: the reference's single-threaded AggSum / AggCount grids over
+the ordered_set ordinals, superagg.cpp:155-192,349-389 + groupby.py:484-533).
+
+Groups come out sorted by key, so keys, counts and integer sums are compared bit-exactly
+and float sums within 1e-6 relative (north_star; the association order differs).
+Covers every key dtype incl. the LDS table's sentinel bit patterns, every value kind,
+direct (P = 1) and partitioned paths, closed LDS tables (more keys per bucket than fit),
+region overflow (sorted / skewed keys), chunked updates, host and device columns."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _ha():
+    from vaex_amd import hashagg
+    return hashagg
+
+
+def _expected_int_sums(keys, vals, uniq):
+    inv = np.searchsorted(uniq, keys)
+    out = np.zeros(len(uniq), np.int64 if vals.dtype.kind in "i" else np.uint64)
+    np.add.at(out, inv, vals.astype(out.dtype))
+    return out
+
+
+def _run(keys, vals, chunks=1, device=False):
+    from vaex_amd.device import DeviceArray
+    ha = _ha().HashAgg(keys.dtype, [v.dtype for v in vals])
+    n = len(keys)
+    bounds = np.linspace(0, n, chunks + 1).astype(int)
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        k, vs = keys[a:b], [v[a:b] for v in vals]
+        if device:
+            k, vs = DeviceArray.from_numpy(k), [DeviceArray.from_numpy(v) for v in vs]
+        ha.update(k, vs)
+    return ha.finish()
+
+
+def _check(keys, vals, out):
+    gk, cnt, sums, nn = out
+    uniq, first_inv = np.unique(keys.astype(np.int64), return_inverse=True)
+    np.testing.assert_array_equal(gk, uniq)
+    np.testing.assert_array_equal(cnt, np.bincount(first_inv, minlength=len(uniq)))
+    for v, s, c in zip(vals, sums, nn):
+        if v.dtype.kind == "f":
+            uk, es, ec = oracle.groupby_reference(keys.astype(np.int64), v.astype(np.float64))
+            np.testing.assert_array_equal(c, ec)
+            np.testing.assert_allclose(s, es, rtol=1e-6, atol=1e-9)
+        else:
+            np.testing.assert_array_equal(s, _expected_int_sums(keys.astype(np.int64), v, uniq))
+            np.testing.assert_array_equal(c, np.bincount(first_inv, minlength=len(uniq)))
+
+
+def _keys(dtype, n, card, rng):
+    dt = np.dtype(dtype)
+    info = np.iinfo(dt)
+    span = min(card, int(info.max) - int(info.min) + 1)
+    lo = int(info.min) if dt.kind == "i" else 0
+    k = (lo + rng.integers(0, span, n)).astype(dt)
+    # the LDS table's sentinel patterns (0xFFFFFFFF / 0xFFFFFFFE as int32 bits) and extremes
+    k[:4] = np.array([-1, -2, info.min, info.max] if dt.kind == "i" else [info.max, info.max - 1, 0, 1], dtype=np.int64).astype(dt)
+    return k
+
+
+@pytest.mark.parametrize("kdtype", ["int8", "int16", "int32", "uint8", "uint16", "uint32"])
+@pytest.mark.parametrize("card", [3, 200, 60000])
+def test_key_dtypes(kdtype, card):
+    rng = np.random.default_rng(card)
+    n = 400_000
+    keys = _keys(kdtype, n, card, rng)
+    v = rng.normal(size=n)
+    v[::37] = np.nan
+    _check(keys, [v], _run(keys, [v]))
+
+
+@pytest.mark.parametrize("vdtypes", [[], ["float32"], ["int8", "float64"], ["uint16", "bool"], ["int64", "uint32"]])
+def test_value_kinds(vdtypes):
+    rng = np.random.default_rng(4)
+    n = 300_000
+    keys = rng.integers(-5000, 5000, n).astype(np.int32)
+    vals = []
+    for d in vdtypes:
+        dt = np.dtype(d)
+        if dt.kind == "f":
+            a = (rng.normal(size=n) * 100).astype(dt)
+            a[::13] = np.nan
+        elif dt.kind == "b":
+            a = rng.random(n) < 0.3
+        else:
+            info = np.iinfo(dt)
+            a = rng.integers(max(info.min, -1000), min(info.max, 1000), n).astype(dt)
+        vals.append(a)
+    _check(keys, vals, _run(keys, vals))
+
+
+@pytest.mark.parametrize("n,card", [(3_000_000, 1_000_000), (4_000_000, 4_000_000)])
+def test_high_cardinality(n, card):
+    rng = np.random.default_rng(5)
+    if card >= n:
+        keys = rng.permutation(n).astype(np.int32) * 7 - 12345
+    else:
+        keys = (5 + rng.integers(0, card, n)).astype(np.int32)
+    v = rng.normal(size=n)
+    _check(keys, [v], _run(keys, [v]))
+
+
+def test_closed_lds_tables():
+    """~8e6 distinct keys: more than P_max x 2560 fit in the LDS tables, so tables close
+    and the rest goes through the HBM-table path; results must not change."""
+    rng = np.random.default_rng(6)
+    n = 9_000_000
+    keys = rng.permutation(np.arange(n, dtype=np.int64) * 3 - 10 ** 9).astype(np.int32)[:n]
+    keys[: n // 9] = keys[n // 9: 2 * (n // 9)]  # some repeats
+    v = rng.random(n)
+    _check(keys, [v], _run(keys, [v], device=True))
+
+
+@pytest.mark.parametrize("layout", ["sorted", "heavy", "runs"])
+def test_skewed_and_sorted_keys(layout):
+    """Per-workgroup bucket fractions far from the sampled global ones: region overflow
+    rows take the HBM-table path."""
+    rng = np.random.default_rng(7)
+    n = 2_000_000
+    if layout == "sorted":
+        keys = np.sort(rng.integers(0, 300_000, n)).astype(np.int32)
+    elif layout == "heavy":
+        keys = rng.integers(0, 100_000, n).astype(np.int32)
+        keys[rng.random(n) < 0.6] = 42
+    else:
+        keys = np.repeat(np.arange(20, dtype=np.int32) * 1000, n // 20)
+    v = rng.normal(size=len(keys))
+    _check(keys, [v], _run(keys, [v]))
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_chunked_updates(device):
+    rng = np.random.default_rng(8)
+    n = 3_000_000
+    keys = rng.integers(0, 500_000, n).astype(np.uint32)
+    keys[n // 2:] += 400_000  # later chunks bring new keys: the HBM table grows across updates
+    v = rng.normal(size=n)
+    v2 = rng.integers(-50, 50, n).astype(np.int16)
+    _check(keys, [v, v2], _run(keys, [v, v2], chunks=5, device=device))
+
+
+def test_empty_and_tiny():
+    keys = np.array([], np.int32)
+    gk, cnt, sums, nn = _run(keys, [np.array([], np.float64)])
+    assert len(gk) == 0 and len(cnt) == 0
+    keys = np.array([7, -1, 7], np.int32)
+    v = np.array([1.0, np.nan, 2.0])
+    gk, cnt, sums, nn = _run(keys, [v])
+    assert gk.tolist() == [-1, 7] and cnt.tolist() == [1, 2] and nn[0].tolist() == [0, 2]
+    assert sums[0].tolist() == [0.0, 3.0]
+
+
+def test_dataframe_groupby_uses_fused_path(monkeypatch):
+    """DataFrame.groupby takes the fused path for this query shape and returns the same
+    frame as the grouper path (assume_sparse=True: ordered_set + BinnerOrdinal)."""
+    import vaex_amd
+    from vaex_amd import hashagg
+    rng = np.random.default_rng(9)
+    n = 1_000_000
+    df = vaex_amd.from_arrays(key=rng.integers(-100, 20000, n).astype(np.int32), v=rng.normal(size=n),
+                              w=rng.integers(0, 10, n).astype(np.int8))
+    agg = {"v": ["sum", "count", "mean"], "w": "sum", "n": "count"}
+    calls = []
+    orig = hashagg.HashAgg.update
+    monkeypatch.setattr(hashagg.HashAgg, "update", lambda self, *a: (calls.append(1), orig(self, *a))[1])
+    fused = df.groupby("key", agg=agg)
+    assert calls, "fused path not taken"
+    ref = df.groupby("key", agg=agg, assume_sparse=True).sort("key")
+    assert fused.get_column_names() == ref.get_column_names()
+    for c in ref.get_column_names():
+        a, b = fused[c].to_numpy(), ref[c].to_numpy()
+        assert a.dtype == b.dtype, c
+        if a.dtype.kind == "f":
+            np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-9)
+        else:
+            np.testing.assert_array_equal(a, b)
+
+
+def test_row_limit():
+    import vaex_amd
+    from vaex_amd.dataframe import RowLimitException
+    df = vaex_amd.from_arrays(key=np.arange(1000, dtype=np.int32), v=np.ones(1000))
+    with pytest.raises(RowLimitException):
+        df.groupby("key", agg={"v": "sum"}, row_limit=10)

@@ -1,0 +1,1364 @@
+// Fused hash groupby: df.groupby(key).agg({count, sum, mean}) for one integer key column
+// (<= 4-byte keys) and up to two value columns, in one pass over the data.
+//
+// The reference runs the groupby as two passes: pass 1 builds the ordered_set of the key
+// (hash_primitives.hpp:96-281, via Grouper, groupby.py:97-168), pass 2 maps every row to
+// its ordinal (_ordinal_values -> map_ordinal, hash_primitives.hpp:543-583) and scatters
+// into the AggCount/AggSum grids through BinnerOrdinal (superagg_binners.cpp:104-142,
+// superagg.cpp:155-192, 349-389).  Here both passes collapse into a hash-partitioned
+// aggregation whose per-key results equal those grids (groupby.py:484-533 output):
+//
+//   sample -- ~1 M evenly spaced rows: per fine bucket (top 12 bits of the key hash) row
+//             counts, and the sample's distinct keys in a small HBM table -> Chao1
+//             estimate of the key count -> P = 2^p buckets of <= ~1800 keys each.
+//   pass A -- workgroup w owns a row range; per 4096-row batch it hashes the keys
+//             (murmur3 fmix32), ranks rows per bucket in LDS, counting-sorts (key, value
+//             bits) by bucket through LDS and streams the runs to per-(w, bucket) regions
+//             (the tile-partition scheme of tiled.hip with buckets for tiles).
+//   pass B -- work unit = (bucket, range of pass-A workgroups): the unit's entries are
+//             aggregated in an LDS open-address table (linear probing, CAS insert,
+//             ds_add_u32 / ds_add_f64 / ds_add_u64), then merged into one HBM
+//             open-address table with global atomics (one merge per distinct key per
+//             unit, not per row).
+//   finish -- occupied HBM slots are compacted, radix-sorted by key (rocPRIM) and
+//             gathered: groups come out sorted by key (a valid sort=False order -- the
+//             reference's is hash/thread dependent -- and exactly the sort=True order).
+//
+// With P == 1 (few keys) pass A is skipped: every workgroup aggregates its row range of
+// the raw columns straight into its LDS table ("direct").
+//
+// Overflow, never wrong results: an LDS table that reaches max_used distinct keys is
+// closed -- a key not yet in it is aggregated straight into the HBM table.  The decision
+// is made by a CAS on the key's first empty probe slot (key or CLOSED), so every key is
+// either wholly in the LDS table or wholly in the HBM path.  A pass-A region that is full
+// (a sampling miss) also adds its rows to the HBM table directly.  An HBM table that grows
+// past 3/4 full is rehashed x4 after the update; one that fills up fails the update
+// (VH_ERR_RUNTIME) and the caller falls back to the ordered_set path.
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <type_traits>
+
+#include "common.hpp"
+#include "hashset.hpp"
+
+namespace vh {
+
+constexpr int HA_MAX_V = 2;
+#ifndef VH_HA_THREADS
+#define VH_HA_THREADS 512
+#endif
+constexpr int HA_THREADS = VH_HA_THREADS;  // pass A
+constexpr int HA_RPT = 8;
+constexpr int HA_BATCH = HA_THREADS * HA_RPT;
+constexpr int HB_THREADS = 1024;           // pass B / direct
+constexpr int HB_VU = 2;                   // 4-entry chunks per lane per step
+constexpr uint32_t LT_SLOTS_LOG2 = 12;     // LDS table: 4096 slots (+2 special records)
+constexpr uint32_t LT_SLOTS = 1u << LT_SLOTS_LOG2;
+constexpr uint32_t LT_MAX_USED = 2560;     // close the LDS table at 62.5 % (+ <= 1024 racing inserts)
+constexpr uint32_t LT_TARGET_KEYS = 2300;  // P is chosen so a bucket holds about this many keys
+constexpr uint32_t LT_EMPTY = 0xFFFFFFFFu, LT_CLOSED = 0xFFFFFFFEu;
+constexpr uint32_t HA_FINE_LOG2 = 12;      // sample histogram: top 12 hash bits
+constexpr uint32_t HA_MAX_P_LOG2 = 11;
+constexpr int HA_SAMPLE_BLOCKS = 256;
+constexpr uint32_t HA_DEST_OVERFLOW = 0x80000000u;
+constexpr int HA_MAX_PROBE = 1 << 14;
+
+__host__ __device__ inline uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
+
+// key bits: the key's value as int32 (signed types, sign-extended) or uint32
+template <typename K> __device__ inline uint32_t ha_kb(K v) {
+    if constexpr (std::is_signed_v<K>) return (uint32_t)(int32_t)v;
+    else return (uint32_t)v;
+}
+
+// a value as the 8 bytes pass A carries: float -> double bits, signed -> int64,
+// unsigned / bool -> uint64 (the AggSum upcast, superagg.cpp:289-346)
+__device__ inline uint64_t ha_load_val(const void *p, int dtype, uint64_t i) {
+    switch (dtype) {
+    case VH_F64: return __builtin_bit_cast(uint64_t, static_cast<const double *>(p)[i]);
+    case VH_F32: return __builtin_bit_cast(uint64_t, (double)static_cast<const float *>(p)[i]);
+    case VH_I64: return (uint64_t) static_cast<const int64_t *>(p)[i];
+    case VH_I32: return (uint64_t)(int64_t) static_cast<const int32_t *>(p)[i];
+    case VH_I16: return (uint64_t)(int64_t) static_cast<const int16_t *>(p)[i];
+    case VH_I8: return (uint64_t)(int64_t) static_cast<const int8_t *>(p)[i];
+    case VH_U64: return static_cast<const uint64_t *>(p)[i];
+    case VH_U32: return static_cast<const uint32_t *>(p)[i];
+    case VH_U16: return static_cast<const uint16_t *>(p)[i];
+    case VH_U8: return static_cast<const uint8_t *>(p)[i];
+    default: return static_cast<const uint8_t *>(p)[i] != 0;  // bool
+    }
+}
+
+// HBM open-address table (linear probing from hash64 of the zero-extended key bits)
+struct HaTable {
+    uint64_t *keys;  // SET_EMPTY = free
+    unsigned long long *cnt;
+    unsigned long long *sum[HA_MAX_V];  // double bits (float columns) or int64/uint64
+    unsigned long long *nn[HA_MAX_V];   // non-NaN counts (float columns)
+    uint64_t mask;
+    uint32_t *used, *err;               // err bit 0: past max_used (grow), bit 1: key lost
+    uint32_t max_used;
+    uint32_t vfloat;                    // bit s: value column s is floating point
+    uint32_t nnmask;                    // bit s: count the non-NaN values of column s
+    int nv;
+};
+
+__device__ inline uint64_t ha_slot(const HaTable &g, uint32_t kb) {
+    const uint64_t key = kb;
+    uint64_t pos = hash64(key) & g.mask;
+    for (int p = 0; p < HA_MAX_PROBE; p++) {
+        uint64_t cur = __hip_atomic_load(&g.keys[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == key) return pos;
+        if (cur == SET_EMPTY) {
+            cur = atomicCAS((unsigned long long *)&g.keys[pos], (unsigned long long)SET_EMPTY,
+                            (unsigned long long)key);
+            if (cur == SET_EMPTY) {
+                if (atomicAdd(g.used, 1u) >= g.max_used) atomicOr(g.err, 1u);
+                return pos;
+            }
+            if (cur == key) return pos;
+        }
+        pos = (pos + 1) & g.mask;
+    }
+    atomicOr(g.err, 2u);
+    return ~0ULL;
+}
+
+// one row straight into the HBM table (LDS table closed, or pass-A region full)
+template <int NV> __device__ inline void ha_global_row(const HaTable &g, uint32_t kb, const uint64_t *vb) {
+    const uint64_t s = ha_slot(g, kb);
+    if (s == ~0ULL) return;
+    atomicAdd(&g.cnt[s], 1ULL);
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+        if ((g.vfloat >> v) & 1) {
+            const double d = __builtin_bit_cast(double, vb[v]);
+            if (d == d) {
+                atomicAdd(reinterpret_cast<double *>(g.sum[v]) + s, d);
+                atomicAdd(&g.nn[v][s], 1ULL);
+            }
+        } else {
+            atomicAdd(&g.sum[v][s], (unsigned long long)vb[v]);
+        }
+    }
+}
+
+// ---- LDS table --------------------------------------------------------------------------
+// Per slot: key bits; one 64-bit counter word holding count(*) << 32 | non-NaN count of
+// value 0 (one ds_add_u64 updates both: a unit holds < 2^32 rows); the value sums; the
+// non-NaN count of value 1.  Records LT_SLOTS and LT_SLOTS + 1 hold the keys whose bits
+// are the CLOSED and EMPTY markers.
+struct LdsTable {
+    uint32_t *keys;                     // [LT_SLOTS]
+    unsigned long long *cn;             // [LT_SLOTS + 2]
+    unsigned long long *sum[HA_MAX_V];  // [LT_SLOTS + 2]
+    uint32_t *nn1;                      // [LT_SLOTS + 2]
+    uint32_t *used;
+};
+
+__host__ __device__ constexpr size_t lt_bytes(int nv) {
+    return (size_t)8 * (LT_SLOTS + 2) * (1 + nv) + (size_t)4 * LT_SLOTS + (nv > 1 ? (size_t)4 * (LT_SLOTS + 2) : 0) + 64;
+}
+
+template <int NV> __device__ inline LdsTable lt_layout(unsigned char *raw) {
+    LdsTable t;
+    unsigned char *p = raw;
+    t.cn = reinterpret_cast<unsigned long long *>(p);
+    p += 8 * (LT_SLOTS + 2);
+    for (int v = 0; v < NV; v++) {
+        t.sum[v] = reinterpret_cast<unsigned long long *>(p);
+        p += 8 * (LT_SLOTS + 2);
+    }
+    t.keys = reinterpret_cast<uint32_t *>(p);
+    p += 4 * LT_SLOTS;
+    t.nn1 = reinterpret_cast<uint32_t *>(p);
+    if (NV > 1) p += 4 * (LT_SLOTS + 2);
+    t.used = reinterpret_cast<uint32_t *>(p);
+    return t;
+}
+
+template <int NV> __device__ inline void lt_init(const LdsTable &t, int nthreads) {
+    for (uint32_t i = threadIdx.x; i < LT_SLOTS + 2; i += nthreads) {
+        if (i < LT_SLOTS) t.keys[i] = LT_EMPTY;
+        t.cn[i] = 0;
+#pragma unroll
+        for (int v = 0; v < NV; v++) t.sum[v][i] = 0;
+        if constexpr (NV > 1) t.nn1[i] = 0;
+    }
+    if (threadIdx.x == 0) *t.used = 0;
+}
+
+template <int NV>
+__device__ inline void lt_bump(const LdsTable &t, const HaTable &g, uint32_t slot, const uint64_t *vb) {
+    unsigned long long c = 1ULL << 32;
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+        if ((g.vfloat >> v) & 1) {
+            const double d = __builtin_bit_cast(double, vb[v]);
+            if (d == d) {
+                atomicAdd(reinterpret_cast<double *>(t.sum[v]) + slot, d);
+                if ((g.nnmask >> v) & 1) {
+                    if (v == 0) c |= 1;
+                    else atomicAdd(&t.nn1[slot], 1u);
+                }
+            }
+        } else {
+            atomicAdd(&t.sum[v][slot], (unsigned long long)vb[v]);
+        }
+    }
+    atomicAdd(&t.cn[slot], c);
+}
+
+// aggregate one entry into the LDS table (or, when its table is closed to it, the HBM table).
+// Bucketised linear probing: the key hashes to a group of 4 slots, read with one
+// ds_read_b128; a key lives at the first free slot of its group sequence at insert time,
+// so a probe ends at a hit, or at the first EMPTY (CAS: insert, or CLOSED once the table
+// is full) / CLOSED slot.  At ~50 % load a wave of 64 lanes needs ~2 group reads, where
+// one-slot linear probing waits on the longest of 64 chains.
+template <int NV>
+__device__ inline void lt_add(const LdsTable &t, const HaTable &g, uint32_t kb, const uint64_t *vb) {
+    uint32_t slot;
+    if (kb >= LT_CLOSED) {
+        slot = LT_SLOTS + (kb - LT_CLOSED);
+    } else {
+        const uint32_t h = fmix32(kb);
+        uint32_t grp = (h & (LT_SLOTS - 1)) >> 2;
+        for (;;) {
+            const uint4 q = *reinterpret_cast<const uint4 *>(t.keys + 4 * grp);
+            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+            int hit = -1, fr = -1;
+#pragma unroll
+            for (int j = 3; j >= 0; j--) {
+                if (w[j] == kb) hit = j;
+                if (w[j] >= LT_CLOSED) fr = j;
+            }
+            if (hit >= 0 && (fr < 0 || hit < fr)) {
+                slot = 4 * grp + hit;
+                break;
+            }
+            if (fr < 0) {
+                grp = (grp + 1) & (LT_SLOTS / 4 - 1);
+                continue;
+            }
+            if (w[fr] == LT_CLOSED) {
+                ha_global_row<NV>(g, kb, vb);
+                return;
+            }
+            const uint32_t pos = 4 * grp + fr;
+            const bool open = *reinterpret_cast<volatile uint32_t *>(t.used) < LT_MAX_USED;
+            const uint32_t cur = atomicCAS(&t.keys[pos], LT_EMPTY, open ? kb : LT_CLOSED);
+            if (cur == LT_EMPTY) {
+                if (!open) {
+                    ha_global_row<NV>(g, kb, vb);
+                    return;
+                }
+                atomicAdd(t.used, 1u);
+                slot = pos;
+                break;
+            }
+            if (cur == kb) {
+                slot = pos;
+                break;
+            }
+            // another key took the slot: re-read the same group
+        }
+    }
+    lt_bump<NV>(t, g, slot, vb);
+}
+
+// M entries at once: all home-group reads are issued together and the hits aggregated
+// with fire-and-forget LDS atomics; only entries whose key is not in its home group
+// (new keys, displaced keys, specials) take lt_add's probe loop.  One entry at a time, a
+// lane would wait an LDS round trip per entry.
+template <int NV, int M>
+__device__ inline void lt_add_many(const LdsTable &t, const HaTable &g, const uint32_t *kb,
+                                   const uint64_t (*vb)[NV > 0 ? NV : 1], const bool *valid) {
+    uint4 q[M];
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+        const uint32_t grp = (fmix32(kb[i]) & (LT_SLOTS - 1)) >> 2;
+        q[i] = *reinterpret_cast<const uint4 *>(t.keys + 4 * grp);
+    }
+    bool slow[M];
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+        const uint32_t base = (fmix32(kb[i]) & (LT_SLOTS - 1)) & ~3u;
+        uint32_t slot = ~0u;
+        if (q[i].w == kb[i]) slot = base + 3;
+        if (q[i].z == kb[i]) slot = base + 2;
+        if (q[i].y == kb[i]) slot = base + 1;
+        if (q[i].x == kb[i]) slot = base;
+        if (kb[i] >= LT_CLOSED) slot = ~0u;
+        slow[i] = valid[i] && slot == ~0u;
+        if (valid[i] && slot != ~0u) lt_bump<NV>(t, g, slot, vb[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < M; i++)
+        if (slow[i]) lt_add<NV>(t, g, kb[i], vb[i]);
+}
+
+// merge the LDS table into the HBM table (after a workgroup barrier)
+template <int NV> __device__ inline void lt_merge(const LdsTable &t, const HaTable &g, int nthreads) {
+    for (uint32_t i = threadIdx.x; i < LT_SLOTS + 2; i += nthreads) {
+        const unsigned long long cn = t.cn[i];
+        if (!cn) continue;
+        const uint32_t kb = i < LT_SLOTS ? t.keys[i] : LT_CLOSED + (i - LT_SLOTS);
+        const uint64_t s = ha_slot(g, kb);
+        if (s == ~0ULL) continue;
+        atomicAdd(&g.cnt[s], cn >> 32);
+#pragma unroll
+        for (int v = 0; v < NV; v++) {
+            if ((g.vfloat >> v) & 1) {
+                const double d = reinterpret_cast<const double *>(t.sum[v])[i];
+                if (d != 0.0) atomicAdd(reinterpret_cast<double *>(g.sum[v]) + s, d);
+                const uint32_t k = v == 0 ? (uint32_t)cn : t.nn1[i];
+                if (k) atomicAdd(&g.nn[v][s], (unsigned long long)k);
+            } else {
+                atomicAdd(&g.sum[v][s], t.sum[v][i]);
+            }
+        }
+    }
+}
+
+// ---- partition parameters -----------------------------------------------------------------
+struct HaParams {
+    const void *keys;
+    const void *vals[HA_MAX_V];
+    int32_t vdtype[HA_MAX_V];
+    uint32_t p_log2, P, W, pad;
+    uint64_t n, rows_per_wg, wg_stride;
+    const uint32_t *cap;   // [P]
+    const uint64_t *toff;  // [P]
+    uint32_t *fills;       // [P][W]
+    uint32_t *ent;         // W * wg_stride key bits, then W * HA_THREADS dummy slots
+    uint64_t *vbits[HA_MAX_V];
+    uint64_t dummy0;       // first dummy slot (idle lanes of the stream-out write there)
+    uint32_t debug;        // experiment switches (VH_HA_DEBUG), 0 in production
+};
+
+struct HaUnit {
+    uint32_t bucket, w_begin, w_end, pad;
+};
+
+__device__ inline void ha_lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// ---- sample -------------------------------------------------------------------------------
+template <typename K>
+__global__ __launch_bounds__(HA_THREADS) void k_ha_sample(const K *keys, uint64_t n, uint64_t block_stride,
+                                                          unsigned long long *fine_hist, uint64_t *skeys,
+                                                          uint32_t *scnt, uint64_t smask) {
+    __shared__ uint32_t h[1u << HA_FINE_LOG2];
+    for (uint32_t t = threadIdx.x; t < (1u << HA_FINE_LOG2); t += HA_THREADS) h[t] = 0;
+    __syncthreads();
+    const uint64_t row0 = blockIdx.x * block_stride;
+    for (uint64_t r = threadIdx.x; r < HA_BATCH; r += HA_THREADS) {
+        const uint64_t i = row0 + r;
+        if (i >= n) break;
+        const uint32_t kb = ha_kb(keys[i]);
+        atomicAdd(&h[fmix32(kb) >> (32 - HA_FINE_LOG2)], 1u);
+        uint64_t pos = hash64(kb) & smask;
+        for (int p = 0; p < HA_MAX_PROBE; p++) {
+            uint64_t cur = __hip_atomic_load(&skeys[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cur == SET_EMPTY)
+                cur = atomicCAS((unsigned long long *)&skeys[pos], (unsigned long long)SET_EMPTY, (unsigned long long)kb);
+            if (cur == SET_EMPTY || cur == kb) {
+                atomicAdd(&scnt[pos], 1u);
+                break;
+            }
+            pos = (pos + 1) & smask;
+        }
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < (1u << HA_FINE_LOG2); t += HA_THREADS)
+        if (h[t]) atomicAdd(&fine_hist[t], (unsigned long long)h[t]);
+}
+
+// distinct keys of the sample, and how many were seen once / twice (Chao1 inputs)
+__global__ __launch_bounds__(256) void k_ha_sample_stats(const uint32_t *scnt, uint64_t slots,
+                                                         unsigned long long *stats) {
+    uint64_t d = 0, f1 = 0, f2 = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < slots; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t c = scnt[i];
+        d += c != 0;
+        f1 += c == 1;
+        f2 += c == 2;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        d += __shfl_down(d, off, 64);
+        f1 += __shfl_down(f1, off, 64);
+        f2 += __shfl_down(f2, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&stats[0], (unsigned long long)d);
+        atomicAdd(&stats[1], (unsigned long long)f1);
+        atomicAdd(&stats[2], (unsigned long long)f2);
+    }
+}
+
+// ---- pass A -------------------------------------------------------------------------------
+__host__ __device__ constexpr size_t ha_scatter_lds_bytes(int nv, uint32_t P) {
+    return (size_t)8 * (nv + 1) * (HA_BATCH + 1) + 16 * ((size_t)P + 1) + 64;
+}
+
+// LDS of pass A: staged value bits | staged (destination, key) pairs | per-bucket hist |
+// batch offsets | region write base | region limit | wave sums
+struct HaScatterLds {
+    uint64_t *sv, *sp;
+    uint32_t *hist, *boff, *base, *lim, *wave_sums;
+};
+
+template <int NV> __device__ inline HaScatterLds ha_scatter_lds(unsigned char *raw, const HaParams &hp) {
+    HaScatterLds l;
+    l.sv = reinterpret_cast<uint64_t *>(raw);
+    l.sp = l.sv + (size_t)NV * (HA_BATCH + 1);
+    l.hist = reinterpret_cast<uint32_t *>(l.sp + HA_BATCH + 1);
+    l.boff = l.hist + hp.P + 1;  // hist[P]: the rank sink of rows past the range
+    l.base = l.boff + hp.P;
+    l.lim = l.base + hp.P;
+    l.wave_sums = l.lim + hp.P;
+    for (uint32_t t = threadIdx.x; t <= hp.P; t += HA_THREADS) l.hist[t] = 0;
+    for (uint32_t t = threadIdx.x; t < hp.P; t += HA_THREADS) {
+        l.base[t] = (uint32_t)hp.toff[t];
+        l.lim[t] = (uint32_t)hp.toff[t] + hp.cap[t];
+    }
+    return l;
+}
+
+// A batch after every row has its bucket, key bits, rank (-1 = no row) and value bits:
+// exclusive scan of the bucket histogram, counting sort of (destination, key) + values
+// into LDS, the sorted runs streamed to the regions (consecutive lanes -> consecutive
+// addresses), region bases advanced.  Rows past a region's capacity go to the HBM table.
+// The stream-out issues a fixed number of stores per lane (idle lanes write a private
+// dummy slot), so the compiler waits for the prefetched next batch with vmcnt(#stores)
+// instead of draining every store of this batch (cdna_hip_programming.md, "Pipelining
+// across barriers"); the rare overflow rows are applied after that loop.
+template <int NV>
+__device__ inline void ha_commit(const HaScatterLds &l, const HaParams &hp, const HaTable &g, uint64_t region0,
+                                 const uint32_t *bkt, const uint32_t *kb, const int32_t *rank,
+                                 const uint64_t (*vb)[NV > 0 ? NV : 1]) {
+    __shared__ uint32_t s_total, s_over;
+    const uint32_t P = hp.P;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    ha_lds_barrier();
+    {
+        const uint32_t per = (P + HA_THREADS - 1) / HA_THREADS;
+        const uint32_t t0 = threadIdx.x * per;
+        uint32_t s = 0;
+        for (uint32_t t = t0; t < t0 + per && t < P; t++) s += l.hist[t];
+        uint32_t inc = s;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += y;
+        }
+        if (lane == 63) l.wave_sums[wave] = inc;
+        ha_lds_barrier();
+        uint32_t wave_base = 0, total = 0;
+        for (int k = 0; k < HA_THREADS / 64; k++) {
+            if (k < wave) wave_base += l.wave_sums[k];
+            total += l.wave_sums[k];
+        }
+        uint32_t acc = wave_base + inc - s;
+        for (uint32_t t = t0; t < t0 + per && t < P; t++) {
+            l.boff[t] = acc;
+            acc += l.hist[t];
+        }
+        if (threadIdx.x == 0) {
+            s_total = total;
+            s_over = 0;
+        }
+    }
+    ha_lds_barrier();
+    bool over = false;
+#pragma unroll
+    for (int r = 0; r < HA_RPT; r++) {
+        const bool valid = rank[r] >= 0;
+        const uint32_t t = valid ? bkt[r] : 0u;
+        const uint32_t pos = valid ? l.boff[t] + (uint32_t)rank[r] : (uint32_t)HA_BATCH;  // slot HA_BATCH: scratch
+        const uint32_t d = l.base[t] + (uint32_t)rank[r];
+        const bool fits = d < l.lim[t];
+        over |= valid && !fits;
+        const uint32_t dest = fits ? d : (HA_DEST_OVERFLOW | t);
+        l.sp[pos] = ((uint64_t)dest << 32) | kb[r];
+#pragma unroll
+        for (int v = 0; v < NV; v++) l.sv[v * (HA_BATCH + 1) + pos] = vb[r][v];
+    }
+    if (over) s_over = 1;
+    ha_lds_barrier();
+    const uint32_t tot = s_total;
+    const uint64_t dummy = hp.dummy0 + (uint64_t)blockIdx.x * HA_THREADS + threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < HA_RPT; r++) {
+        const uint32_t k = r * HA_THREADS + threadIdx.x;
+        const uint64_t pk = l.sp[k];
+        const uint32_t dest = (uint32_t)(pk >> 32);
+        const bool ok = k < tot && !(dest & HA_DEST_OVERFLOW);
+        const uint64_t e = ok ? region0 + dest : dummy;
+        if (hp.debug & 1) {
+            asm volatile("" :: "v"(e), "v"(pk));
+            continue;
+        }
+        if constexpr (NV == 1) {  // packed {key, 0, value}: one 16-byte store per row
+            const uint64_t vbits = l.sv[k];
+            reinterpret_cast<uint4 *>(hp.ent)[e] = make_uint4((uint32_t)pk, 0u, (uint32_t)vbits, (uint32_t)(vbits >> 32));
+        } else {
+            hp.ent[e] = (uint32_t)pk;
+#pragma unroll
+            for (int v = 0; v < NV; v++) hp.vbits[v][e] = l.sv[v * (HA_BATCH + 1) + k];
+        }
+    }
+    if (s_over) {
+        for (uint32_t k = threadIdx.x; k < tot; k += HA_THREADS) {
+            const uint64_t pk = l.sp[k];
+            if (!((uint32_t)(pk >> 32) & HA_DEST_OVERFLOW)) continue;
+            uint64_t vv[NV > 0 ? NV : 1];
+#pragma unroll
+            for (int v = 0; v < NV; v++) vv[v] = l.sv[v * (HA_BATCH + 1) + k];
+            ha_global_row<NV>(g, (uint32_t)pk, vv);
+        }
+    }
+    ha_lds_barrier();
+    for (uint32_t t = threadIdx.x; t < P; t += HA_THREADS) {
+        l.base[t] += l.hist[t];
+        l.hist[t] = 0;
+    }
+    ha_lds_barrier();
+}
+
+// top p_log2 bits of the key hash (branch-free: p_log2 = 0 gives bucket 0)
+__device__ inline uint32_t ha_bucket(const HaParams &hp, uint32_t kb) {
+    return (uint32_t)(((uint64_t)fmix32(kb) << hp.p_log2) >> 32);
+}
+
+// generic pass A: any <= 4-byte key type and value dtypes, scalar loads
+template <typename K, int NV>
+__global__ __launch_bounds__(HA_THREADS) void k_ha_scatter(HaParams hp, HaTable g) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const HaScatterLds l = ha_scatter_lds<NV>(lds_raw, hp);
+    __syncthreads();
+    const uint32_t w = blockIdx.x;
+    const uint64_t row_begin = (uint64_t)w * hp.rows_per_wg;
+    const uint64_t row_end = min(hp.n, row_begin + hp.rows_per_wg);
+    const uint64_t region0 = (uint64_t)w * hp.wg_stride;
+    const K *keys = static_cast<const K *>(hp.keys);
+    for (uint64_t b0 = row_begin; b0 < row_end; b0 += HA_BATCH) {
+        uint32_t bkt[HA_RPT], kb[HA_RPT];
+        int32_t rank[HA_RPT];
+        uint64_t vb[HA_RPT][NV > 0 ? NV : 1];
+#pragma unroll
+        for (int r = 0; r < HA_RPT; r++) {
+            const uint64_t i = b0 + (uint64_t)r * HA_THREADS + threadIdx.x;
+            rank[r] = -1;
+            if (i < row_end) {
+                kb[r] = ha_kb(keys[i]);
+#pragma unroll
+                for (int v = 0; v < NV; v++) vb[r][v] = ha_load_val(hp.vals[v], hp.vdtype[v], i);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < HA_RPT; r++) {
+            const uint64_t i = b0 + (uint64_t)r * HA_THREADS + threadIdx.x;
+            if (i < row_end) {
+                bkt[r] = ha_bucket(hp, kb[r]);
+                rank[r] = (int32_t)atomicAdd(&l.hist[bkt[r]], 1u);
+            }
+        }
+        ha_commit<NV>(l, hp, g, region0, bkt, kb, rank, vb);
+    }
+    for (uint32_t t = threadIdx.x; t < hp.P; t += HA_THREADS)
+        hp.fills[(uint64_t)t * hp.W + w] = l.base[t] - (uint32_t)hp.toff[t];
+}
+
+// fast pass A: 4-byte keys and float64 values, 16-byte aligned, n a multiple of 8.  A lane
+// owns 2 x 4 consecutive rows per batch: keys as two 16-byte loads, each value column as
+// four; the next batch is prefetched into registers while this one is ranked and sorted.
+// Workgroup ranges are multiples of HA_BATCH, so a 4-row group is wholly inside or wholly
+// past the range; past-the-end groups load a clamped in-range address and are dropped.
+template <typename K, int NV>
+__global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_f64(HaParams hp, HaTable g) {
+    static_assert(sizeof(K) == 4, "fast pass A takes 4-byte keys");
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const HaScatterLds l = ha_scatter_lds<NV>(lds_raw, hp);
+    __syncthreads();
+    const uint32_t w = blockIdx.x;
+    const uint64_t row_begin = (uint64_t)w * hp.rows_per_wg;
+    const uint64_t row_end = min(hp.n, row_begin + hp.rows_per_wg);
+    const uint64_t region0 = (uint64_t)w * hp.wg_stride;
+    const K *keys = static_cast<const K *>(hp.keys);
+    const double *vcol[NV > 0 ? NV : 1];
+#pragma unroll
+    for (int v = 0; v < NV; v++) vcol[v] = static_cast<const double *>(hp.vals[v]);
+    struct Regs {
+        uint4 k[2];
+        double2 v[2][NV > 0 ? NV : 1][2];
+    };
+    auto load = [&](uint64_t b0, Regs &R) {
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const uint64_t i = b0 + 4 * ((uint64_t)q * HA_THREADS + threadIdx.x);
+            const uint64_t is = i < hp.n ? i : hp.n - 4;
+            R.k[q] = *reinterpret_cast<const uint4 *>(keys + is);
+#pragma unroll
+            for (int v = 0; v < NV; v++)
+#pragma unroll
+                for (int h = 0; h < 2; h++) R.v[q][v][h] = *reinterpret_cast<const double2 *>(vcol[v] + is + 2 * h);
+        }
+    };
+    Regs cur, nxt;
+    // prologue through nxt: cur is then written by register moves, so the loop header's
+    // wait analysis does not see cur's loads as pending (which made it drain the stores)
+    load(row_begin, cur);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): an intrinsic the wait analysis sees
+    for (uint64_t b0 = row_begin; b0 < row_end; b0 += HA_BATCH) {
+        load(b0 + HA_BATCH, nxt);
+        uint32_t bkt[HA_RPT], kb[HA_RPT];
+        int32_t rank[HA_RPT];
+        uint64_t vb[HA_RPT][NV > 0 ? NV : 1];
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const uint64_t i = b0 + 4 * ((uint64_t)q * HA_THREADS + threadIdx.x);
+            const uint32_t words[4] = {cur.k[q].x, cur.k[q].y, cur.k[q].z, cur.k[q].w};
+            const bool valid = i < row_end;  // uniform but for a range's last batch
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int r = q * 4 + j;
+                kb[r] = ha_kb(__builtin_bit_cast(K, words[j]));
+#pragma unroll
+                for (int v = 0; v < NV; v++)
+                    vb[r][v] = __builtin_bit_cast(uint64_t, (j & 1) ? cur.v[q][v][j >> 1].y : cur.v[q][v][j >> 1].x);
+                bkt[r] = ha_bucket(hp, kb[r]);
+                if (hp.debug & 4) {
+                    rank[r] = valid ? (int32_t)(bkt[r] & 7) : -1;
+                } else {
+                    const uint32_t rk = atomicAdd(&l.hist[valid ? bkt[r] : hp.P], 1u);
+                    rank[r] = valid ? (int32_t)rk : -1;
+                }
+            }
+        }
+        if (hp.debug & 2) {
+#pragma unroll
+            for (int r = 0; r < HA_RPT; r++) asm volatile("" :: "v"(rank[r]), "v"(vb[r][0]));
+        } else {
+            ha_commit<NV>(l, hp, g, region0, bkt, kb, rank, vb);
+        }
+        cur = nxt;
+    }
+    for (uint32_t t = threadIdx.x; t < hp.P; t += HA_THREADS)
+        hp.fills[(uint64_t)t * hp.W + w] = l.base[t] - (uint32_t)hp.toff[t];
+}
+
+// rows [row0, n) straight into the HBM table (the < 8-row tail of the fast pass A)
+template <typename K, int NV>
+__global__ __launch_bounds__(64) void k_ha_tail(HaParams hp, HaTable g, uint64_t row0) {
+    const uint64_t i = row0 + threadIdx.x;
+    if (i >= hp.n) return;
+    uint64_t vb[NV > 0 ? NV : 1];
+#pragma unroll
+    for (int v = 0; v < NV; v++) vb[v] = ha_load_val(hp.vals[v], hp.vdtype[v], i);
+    ha_global_row<NV>(g, ha_kb(static_cast<const K *>(hp.keys)[i]), vb);
+}
+
+// ---- pass B -------------------------------------------------------------------------------
+template <int NV>
+__global__ __launch_bounds__(HB_THREADS) void k_ha_reduce(HaParams hp, HaTable g, const HaUnit *units) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    __shared__ uint32_t s_fill[1024];
+    __shared__ uint32_t s_pre[1025];
+    __shared__ uint32_t s_pre2[NV == 1 ? 1025 : 1];
+    const HaUnit u = units[blockIdx.x];
+    const uint32_t b = u.bucket;
+    const uint32_t cap = hp.cap[b];
+    const uint32_t nw = u.w_end - u.w_begin;  // <= 1024 (host checks)
+    bool any = false;
+    for (uint32_t k = threadIdx.x; k < nw; k += HB_THREADS) {
+        const uint32_t f = min(hp.fills[(uint64_t)b * hp.W + u.w_begin + k], cap);
+        s_fill[k] = f;
+        any |= f != 0;
+    }
+    if (!__syncthreads_or(any)) return;
+    const LdsTable t = lt_layout<NV>(lds_raw);
+    lt_init<NV>(t, HB_THREADS);
+    if (threadIdx.x < 64) {
+        // exclusive scan of the 4-entry chunk counts by the first wave (16 regions per lane)
+        const uint32_t lane = threadIdx.x, k0 = lane * 16;
+        uint32_t sum = 0;
+        for (uint32_t k = k0; k < k0 + 16 && k < nw; k++) sum += (s_fill[k] + 3) >> 2;
+        uint32_t inc = sum;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(inc, off, 64);
+            if ((int)lane >= off) inc += y;
+        }
+        uint32_t acc = inc - sum;
+        for (uint32_t k = k0; k < k0 + 16 && k < nw; k++) {
+            s_pre[k] = acc;
+            acc += (s_fill[k] + 3) >> 2;
+        }
+        if (lane == 63) s_pre[nw] = inc;
+    }
+    if (NV == 1 && threadIdx.x >= 64 && threadIdx.x < 128) {
+        // exclusive scan of the region fills (entries) by the second wave
+        const uint32_t lane = threadIdx.x - 64, k0 = lane * 16;
+        uint32_t sum = 0;
+        for (uint32_t k = k0; k < k0 + 16 && k < nw; k++) sum += s_fill[k];
+        uint32_t inc = sum;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(inc, off, 64);
+            if ((int)lane >= off) inc += y;
+        }
+        uint32_t acc = inc - sum;
+        for (uint32_t k = k0; k < k0 + 16 && k < nw; k++) {
+            s_pre2[k] = acc;
+            acc += s_fill[k];
+        }
+        if (lane == 63) s_pre2[nw] = inc;
+    }
+    __syncthreads();
+    const uint32_t C = s_pre[nw];
+    const uint64_t toff_b = hp.toff[b];
+    uint32_t kk = 0;  // region of this lane's current chunk (chunk indices of a lane only grow)
+    if constexpr (NV == 1) {
+        // packed 16-byte entries {key, 0, value}, streamed one entry per lane per load:
+        // consecutive lanes read consecutive entries of the unit's flattened region stream
+        // (a wave load is 1 KB contiguous unless it crosses a region end)
+        const uint4 *pe = reinterpret_cast<const uint4 *>(hp.ent);
+        constexpr int M = HB_VU * 4;
+        const uint32_t E = s_pre2[nw];
+        uint32_t kr = 0;
+        for (uint32_t c0 = 0; c0 < E; c0 += HB_THREADS * M) {
+            uint4 ev[M];
+            bool valid[M];
+#pragma unroll
+            for (int j = 0; j < M; j++) {
+                const uint32_t c = c0 + j * HB_THREADS + threadIdx.x;
+                const uint32_t cc = c < E ? c : E - 1;
+                while (s_pre2[kr + 1] <= cc) kr++;
+                const uint64_t e = (uint64_t)(u.w_begin + kr) * hp.wg_stride + toff_b + (cc - s_pre2[kr]);
+                valid[j] = c < E;
+                ev[j] = pe[e];
+            }
+            uint32_t kb[M];
+            uint64_t vb[M][1];
+#pragma unroll
+            for (int j = 0; j < M; j++) {
+                kb[j] = ev[j].x;
+                vb[j][0] = ((uint64_t)ev[j].w << 32) | ev[j].z;
+            }
+            if (hp.debug & 8) {
+#pragma unroll
+                for (int j = 0; j < M; j++) asm volatile("" :: "v"(kb[j]), "v"(vb[j][0]));
+            } else {
+                lt_add_many<NV, M>(t, g, kb, vb, valid);
+            }
+        }
+        __syncthreads();
+        lt_merge<NV>(t, g, HB_THREADS);
+        return;
+    }
+    for (uint32_t c0 = 0; c0 < C; c0 += HB_THREADS * HB_VU) {
+        uint4 ev[HB_VU];
+        ulonglong2 vv[HB_VU][NV > 0 ? NV : 1][2];
+        uint32_t rem[HB_VU];
+#pragma unroll
+        for (int j = 0; j < HB_VU; j++) {
+            const uint32_t c = c0 + j * HB_THREADS + threadIdx.x;
+            const uint32_t cc = c < C ? c : C - 1;
+            while (s_pre[kk + 1] <= cc) kk++;
+            const uint32_t q = (cc - s_pre[kk]) * 4;
+            // regions start at multiples of 8 entries: a 4-entry chunk stays in its region
+            const uint64_t e = (uint64_t)(u.w_begin + kk) * hp.wg_stride + toff_b + q;
+            rem[j] = c < C ? min(4u, s_fill[kk] - q) : 0u;
+            ev[j] = *reinterpret_cast<const uint4 *>(hp.ent + e);
+#pragma unroll
+            for (int v = 0; v < NV; v++)
+#pragma unroll
+                for (int h = 0; h < 2; h++) vv[j][v][h] = *reinterpret_cast<const ulonglong2 *>(hp.vbits[v] + e + 2 * h);
+        }
+        uint32_t kb[HB_VU * 4];
+        uint64_t vb[HB_VU * 4][NV > 0 ? NV : 1];
+        bool valid[HB_VU * 4];
+#pragma unroll
+        for (int j = 0; j < HB_VU; j++) {
+            const uint32_t words[4] = {ev[j].x, ev[j].y, ev[j].z, ev[j].w};
+#pragma unroll
+            for (int x = 0; x < 4; x++) {
+                kb[j * 4 + x] = words[x];
+                valid[j * 4 + x] = (uint32_t)x < rem[j];
+#pragma unroll
+                for (int v = 0; v < NV; v++) vb[j * 4 + x][v] = (x & 1) ? vv[j][v][x >> 1].y : vv[j][v][x >> 1].x;
+            }
+        }
+        lt_add_many<NV, HB_VU * 4>(t, g, kb, vb, valid);
+    }
+    __syncthreads();
+    lt_merge<NV>(t, g, HB_THREADS);
+}
+
+// ---- direct (P == 1): each workgroup aggregates a row range of the raw columns ------------
+template <typename K, int NV>
+__global__ __launch_bounds__(HB_THREADS) void k_ha_direct(HaParams hp, HaTable g) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const LdsTable t = lt_layout<NV>(lds_raw);
+    lt_init<NV>(t, HB_THREADS);
+    __syncthreads();
+    const uint64_t row_begin = (uint64_t)blockIdx.x * hp.rows_per_wg;
+    const uint64_t row_end = min(hp.n, row_begin + hp.rows_per_wg);
+    const K *keys = static_cast<const K *>(hp.keys);
+    constexpr int U = 4;
+    for (uint64_t b0 = row_begin; b0 < row_end; b0 += (uint64_t)U * HB_THREADS) {
+        uint32_t kb[U];
+        uint64_t vb[U][NV > 0 ? NV : 1];
+#pragma unroll
+        for (int r = 0; r < U; r++) {
+            const uint64_t i = b0 + (uint64_t)r * HB_THREADS + threadIdx.x;
+            if (i < row_end) {
+                kb[r] = ha_kb(keys[i]);
+#pragma unroll
+                for (int v = 0; v < NV; v++) vb[r][v] = ha_load_val(hp.vals[v], hp.vdtype[v], i);
+            }
+        }
+        bool valid[U];
+#pragma unroll
+        for (int r = 0; r < U; r++) {
+            valid[r] = b0 + (uint64_t)r * HB_THREADS + threadIdx.x < row_end;
+            if (!valid[r]) kb[r] = 0;
+        }
+        lt_add_many<NV, U>(t, g, kb, vb, valid);
+    }
+    __syncthreads();
+    lt_merge<NV>(t, g, HB_THREADS);
+}
+
+// ---- table maintenance / finish -----------------------------------------------------------
+template <int NV> __global__ __launch_bounds__(256) void k_ha_rehash(HaTable src, uint64_t src_slots, HaTable dst) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < src_slots; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t k = src.keys[i];
+        if (k == SET_EMPTY) continue;
+        const uint64_t s = ha_slot(dst, (uint32_t)k);
+        if (s == ~0ULL) continue;
+        dst.cnt[s] = src.cnt[i];
+#pragma unroll
+        for (int v = 0; v < NV; v++) {
+            dst.sum[v][s] = src.sum[v][i];
+            dst.nn[v][s] = src.nn[v][i];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_ha_compact(const uint64_t *keys, uint64_t slots, int is_signed,
+                                                    uint32_t *skey, uint32_t *sslot, uint32_t *counter) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < slots; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t k = keys[i];
+        if (k == SET_EMPTY) continue;
+        const uint32_t j = atomicAdd(counter, 1u);
+        skey[j] = is_signed ? ((uint32_t)k ^ 0x80000000u) : (uint32_t)k;
+        sslot[j] = (uint32_t)i;
+    }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void k_ha_gather(HaTable g, const uint32_t *skey, const uint32_t *sslot, uint64_t m,
+                                                   int is_signed, int64_t *okey, int64_t *ocnt, uint64_t *osum,
+                                                   int64_t *onn) {
+    for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) {
+        const uint32_t s = sslot[j];
+        const uint32_t kb = is_signed ? (skey[j] ^ 0x80000000u) : skey[j];
+        okey[j] = is_signed ? (int64_t)(int32_t)kb : (int64_t)kb;
+        const uint64_t c = g.cnt[s];
+        ocnt[j] = (int64_t)c;
+#pragma unroll
+        for (int v = 0; v < NV; v++) {
+            osum[(uint64_t)v * m + j] = g.sum[v][s];
+            onn[(uint64_t)v * m + j] = ((g.vfloat >> v) & 1) ? (int64_t)g.nn[v][s] : (int64_t)c;
+        }
+    }
+}
+
+}  // namespace vh
+
+using namespace vh;
+
+struct vh_hashagg {
+    int key_dtype = VH_I32;
+    int nv = 0;
+    int vdtype[HA_MAX_V] = {VH_F64, VH_F64};
+    uint32_t vfloat = 0;
+    uint32_t nnmask = 0;  // value columns whose non-NaN count is read (count(v), mean)
+    uint64_t slots = 0;  // HBM table slots (power of two), 0 = not allocated
+    DevBuf tab;          // keys | cnt | sum[nv] | nn[nv] | used, err
+    DevBuf out;
+    uint64_t ngroups = 0;
+    bool finished = false;
+    uint64_t rows = 0;
+    HaTable view() const;
+};
+
+namespace vh {
+
+// Partition scratch shared by every hashagg of a device (the regions of a 1e9-row update
+// are ~16 GB: allocating them per query would cost more than the query).  Updates hold
+// the device's lock; they are stream-ordered on the library stream anyway.
+struct HaScratch {
+    std::mutex mu;
+    DevBuf sample, meta, entries, vbits, stage;
+};
+static HaScratch &scratch() {
+    static std::mutex g;
+    static std::map<int, std::unique_ptr<HaScratch>> m;
+    std::lock_guard<std::mutex> lk(g);
+    auto &p = m[current_device()];
+    if (!p) p = std::make_unique<HaScratch>();
+    return *p;
+}
+
+static bool key_dtype_ok(int d) {
+    return d == VH_I32 || d == VH_I16 || d == VH_I8 || d == VH_U32 || d == VH_U16 || d == VH_U8;
+}
+static bool key_signed(int d) { return d == VH_I32 || d == VH_I16 || d == VH_I8; }
+
+static uint64_t tab_bytes(uint64_t slots, int nv) { return slots * 8 * (2 + 2 * (uint64_t)nv) + 256; }
+
+static HaTable table_view(void *base, uint64_t slots, int nv, uint32_t vfloat, uint32_t nnmask = 0) {
+    HaTable g{};
+    unsigned char *p = static_cast<unsigned char *>(base);
+    g.keys = reinterpret_cast<uint64_t *>(p);
+    p += 8 * slots;
+    g.cnt = reinterpret_cast<unsigned long long *>(p);
+    p += 8 * slots;
+    for (int v = 0; v < nv; v++) {
+        g.sum[v] = reinterpret_cast<unsigned long long *>(p);
+        p += 8 * slots;
+        g.nn[v] = reinterpret_cast<unsigned long long *>(p);
+        p += 8 * slots;
+    }
+    g.used = reinterpret_cast<uint32_t *>(p);
+    g.err = g.used + 1;
+    g.mask = slots - 1;
+    g.max_used = (uint32_t)std::min<uint64_t>(slots / 4 * 3, 0xffffffffu);
+    g.vfloat = vfloat;
+    g.nnmask = nnmask;
+    g.nv = nv;
+    return g;
+}
+
+static void table_alloc(DevBuf &buf, uint64_t slots, int nv) {
+    buf.ensure(tab_bytes(slots, nv));
+    hipStream_t st = stream();
+    VH_HIP(hipMemsetAsync(buf.ptr, 0xff, 8 * slots, st));  // keys = EMPTY
+    VH_HIP(hipMemsetAsync(static_cast<char *>(buf.ptr) + 8 * slots, 0, tab_bytes(slots, nv) - 8 * slots, st));
+}
+
+template <typename F> static void dispatch_nv(int nv, F &&f) {
+    switch (nv) {
+    case 0: f(std::integral_constant<int, 0>()); break;
+    case 1: f(std::integral_constant<int, 1>()); break;
+    default: f(std::integral_constant<int, 2>());
+    }
+}
+
+#define VH_DISPATCH_KEY(code, K, ...)                                   \
+    switch (code) {                                                     \
+    case VH_I32: { using K = int32_t; __VA_ARGS__; break; }             \
+    case VH_I16: { using K = int16_t; __VA_ARGS__; break; }             \
+    case VH_I8: { using K = int8_t; __VA_ARGS__; break; }               \
+    case VH_U32: { using K = uint32_t; __VA_ARGS__; break; }            \
+    case VH_U16: { using K = uint16_t; __VA_ARGS__; break; }            \
+    case VH_U8: { using K = uint8_t; __VA_ARGS__; break; }              \
+    default: fail(VH_ERR_ARG, "hashagg: unsupported key dtype");       \
+    }
+
+static uint64_t next_pow2(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// grow (rehash) the HBM table to hold `need` keys at <= 1/2 load
+static void ensure_table(vh_hashagg *h, uint64_t need) {
+    const uint64_t want = std::max<uint64_t>(1u << 16, next_pow2(2 * need));
+    if (h->slots >= want) return;
+    if (want > (1ull << 31)) fail(VH_ERR_RUNTIME, "hashagg: too many groups for the fused hash path");
+    if (!h->slots) {
+        table_alloc(h->tab, want, h->nv);
+        h->slots = want;
+        return;
+    }
+    DevBuf nt;
+    table_alloc(nt, want, h->nv);
+    const HaTable src = table_view(h->tab.ptr, h->slots, h->nv, h->vfloat);
+    const HaTable dst = table_view(nt.ptr, want, h->nv, h->vfloat);
+    dispatch_nv(h->nv, [&](auto nvc) {
+        constexpr int NV = decltype(nvc)::value;
+        hipLaunchKernelGGL(k_ha_rehash<NV>, dim3(blocks_for(h->slots, 256, 8)), dim3(256), 0, stream(), src, h->slots, dst);
+    });
+    VH_HIP(hipGetLastError());
+    std::swap(h->tab.ptr, nt.ptr);
+    std::swap(h->tab.bytes, nt.bytes);
+    h->slots = want;
+}
+
+static uint32_t read_used(vh_hashagg *h, uint32_t *err) {
+    const HaTable g = table_view(h->tab.ptr, h->slots, h->nv, h->vfloat);
+    uint32_t ue[2];
+    VH_HIP(hipMemcpyAsync(ue, g.used, 8, hipMemcpyDeviceToHost, stream()));
+    VH_HIP(hipStreamSynchronize(stream()));
+    if (err) *err = ue[1];
+    return ue[0];
+}
+
+static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+static int blocks_per_cu(const void *kernel, int threads, size_t lds) {
+    int nb = 0;
+    VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, threads, lds));
+    return std::max(1, nb);
+}
+
+// one update over n <= 2^30 device-resident rows
+static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const void *const *vals, uint64_t n) {
+    hipStream_t st = stream();
+    const int nv = h->nv;
+    // ---- sample: fine bucket histogram + distinct estimate
+    const uint64_t sslots = 1ull << 21;
+    const uint64_t nbatch = (n + HA_BATCH - 1) / HA_BATCH;
+    const uint64_t sblocks = std::min<uint64_t>(nbatch, HA_SAMPLE_BLOCKS);
+    const uint64_t bstride = std::max<uint64_t>(HA_BATCH, n / sblocks);
+    const uint32_t FINE = 1u << HA_FINE_LOG2;
+    S.sample.ensure(sslots * 12 + 8 * FINE + 64);
+    uint64_t *skeys = S.sample.as<uint64_t>();
+    uint32_t *scnt = reinterpret_cast<uint32_t *>(skeys + sslots);
+    unsigned long long *fine = reinterpret_cast<unsigned long long *>(scnt + sslots);
+    unsigned long long *stats = fine + FINE;
+    VH_HIP(hipMemsetAsync(skeys, 0xff, 8 * sslots, st));
+    VH_HIP(hipMemsetAsync(scnt, 0, 4 * sslots + 8 * FINE + 64, st));
+    {
+        TimedScope ts("ha_sample");
+        VH_DISPATCH_KEY(h->key_dtype, K,
+                        hipLaunchKernelGGL(k_ha_sample<K>, dim3(sblocks), dim3(HA_THREADS), 0, st,
+                                           static_cast<const K *>(keys), n, bstride, fine, skeys, scnt, sslots - 1));
+        hipLaunchKernelGGL(k_ha_sample_stats, dim3(blocks_for(sslots, 256, 4)), dim3(256), 0, st, scnt, sslots, stats);
+        VH_HIP(hipGetLastError());
+    }
+    std::vector<uint64_t> fh(FINE + 3);
+    VH_HIP(hipMemcpyAsync(fh.data(), fine, 8 * (FINE + 3), hipMemcpyDeviceToHost, st));
+    VH_HIP(hipStreamSynchronize(st));
+    uint64_t sampled = 0;
+    for (uint32_t i = 0; i < FINE; i++) sampled += fh[i];
+    const double ds = (double)fh[FINE], f1 = (double)fh[FINE + 1], f2 = (double)fh[FINE + 2];
+    double dest;
+    if (sampled >= n) dest = ds;  // every row sampled: exact
+    else dest = f2 > 0 ? ds + f1 * f1 / (2 * f2) : ds + f1 * (f1 - 1) / 2;  // Chao1
+    dest = std::min<double>(dest, (double)n);
+    uint32_t used_before = h->slots ? read_used(h, nullptr) : 0;
+    ensure_table(h, (uint64_t)dest + used_before);
+    HaTable g = table_view(h->tab.ptr, h->slots, nv, h->vfloat, h->nnmask);
+
+    uint32_t p_log2 = 0;
+    static const double target_keys = getenv("VH_HA_TARGET") ? atof(getenv("VH_HA_TARGET")) : (double)LT_TARGET_KEYS;
+    static const double unit_div = getenv("VH_HA_UNIT_DIV") ? atof(getenv("VH_HA_UNIT_DIV")) : 2.0;
+    while (p_log2 < HA_MAX_P_LOG2 && dest / (double)(1u << p_log2) > target_keys) p_log2++;
+
+    HaParams hp{};
+    hp.keys = keys;
+    for (int v = 0; v < nv; v++) {
+        hp.vals[v] = vals[v];
+        hp.vdtype[v] = h->vdtype[v];
+    }
+    hp.n = n;
+    hp.p_log2 = p_log2;
+    hp.P = 1u << p_log2;
+    const size_t lt_lds = lt_bytes(nv);
+    if (p_log2 == 0) {
+        // ---- direct: one LDS table per workgroup over a contiguous row range
+        int bpc = 1;
+        VH_DISPATCH_KEY(h->key_dtype, K, dispatch_nv(nv, [&](auto nvc) {
+            constexpr int NV = decltype(nvc)::value;
+            bpc = blocks_per_cu(reinterpret_cast<const void *>(k_ha_direct<K, NV>), HB_THREADS, lt_lds);
+        }));
+        const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cu_count() * bpc,
+                                                                     (n + 4 * HB_THREADS - 1) / (4 * HB_THREADS)));
+        hp.rows_per_wg = (n + W - 1) / W;
+        TimedScope ts("ha_direct");
+        VH_DISPATCH_KEY(h->key_dtype, K, dispatch_nv(nv, [&](auto nvc) {
+            constexpr int NV = decltype(nvc)::value;
+            hipLaunchKernelGGL((k_ha_direct<K, NV>), dim3((unsigned)W), dim3(HB_THREADS), lt_lds, st, hp, g);
+        }));
+        VH_HIP(hipGetLastError());
+        return;
+    }
+    const uint32_t P = hp.P;
+    std::vector<uint64_t> bh(P, 0);
+    for (uint32_t i = 0; i < FINE; i++) bh[i >> (HA_FINE_LOG2 - p_log2)] += fh[i];
+
+    // ---- pass A geometry
+    const size_t lds_a = ha_scatter_lds_bytes(nv, P);
+    int bpc = 1;
+    VH_DISPATCH_KEY(h->key_dtype, K, dispatch_nv(nv, [&](auto nvc) {
+        constexpr int NV = decltype(nvc)::value;
+        bpc = blocks_per_cu(reinterpret_cast<const void *>(k_ha_scatter<K, NV>), HA_THREADS, lds_a);
+    }));
+    bpc = std::min(bpc, 4);
+    const uint32_t W = std::min<uint32_t>(1024, (uint32_t)cu_count() * bpc);
+    const uint64_t rows_per_wg = ((n + W - 1) / W + HA_BATCH - 1) / HA_BATCH * HA_BATCH;
+    std::vector<uint32_t> cap(P);
+    std::vector<uint64_t> toff(P);
+    uint64_t stride = 0;
+    for (uint32_t t = 0; t < P; t++) {
+        const double e = (double)rows_per_wg * (double)bh[t] / (double)std::max<uint64_t>(sampled, 1);
+        uint64_t c = (uint64_t)(e * 1.04 + 6.0 * std::sqrt(e + 1.0)) + 32;
+        c = std::min<uint64_t>((c + 7) & ~uint64_t(7), rows_per_wg + 8);
+        cap[t] = (uint32_t)c;
+        toff[t] = stride;
+        stride += c;
+    }
+    if (stride + rows_per_wg >= (uint64_t)HA_DEST_OVERFLOW) fail(VH_ERR_RUNTIME, "hashagg: region table too large");
+    const uint64_t total = stride * W + (uint64_t)W * HA_THREADS;  // regions + dummy slots
+    if (nv == 1) {
+        S.entries.ensure(16 * total + 64);  // packed {key, 0, value} entries
+    } else {
+        S.entries.ensure(4 * total + 16);
+        if (nv) S.vbits.ensure(8 * total * nv + 32);
+    }
+    // pass-B work units: buckets split over ranges of pass-A workgroups by expected size
+    std::vector<HaUnit> units;
+    const double target = std::max(1.0, (double)n / ((double)cu_count() * unit_div));
+    for (uint32_t t = 0; t < P; t++) {
+        const double e = (double)n * (double)bh[t] / (double)std::max<uint64_t>(sampled, 1);
+        const uint32_t gq = (uint32_t)std::min<double>(W, std::max(1.0, std::ceil(e / target)));
+        for (uint32_t k = 0; k < gq; k++)
+            units.push_back({t, (uint32_t)((uint64_t)W * k / gq), (uint32_t)((uint64_t)W * (k + 1) / gq), 0});
+    }
+    const uint64_t meta_bytes = 4 * (uint64_t)P + 8 * (uint64_t)P + 4 * (uint64_t)P * W + sizeof(HaUnit) * units.size() + 256;
+    S.meta.ensure(meta_bytes);
+    unsigned char *mb = S.meta.as<unsigned char>();
+    uint64_t *d_toff = reinterpret_cast<uint64_t *>(mb);
+    HaUnit *d_units = reinterpret_cast<HaUnit *>(d_toff + P);
+    uint32_t *d_cap = reinterpret_cast<uint32_t *>(d_units + units.size());
+    uint32_t *d_fills = d_cap + P;
+    VH_HIP(hipMemcpyAsync(d_toff, toff.data(), 8 * (uint64_t)P, hipMemcpyHostToDevice, st));
+    VH_HIP(hipMemcpyAsync(d_units, units.data(), sizeof(HaUnit) * units.size(), hipMemcpyHostToDevice, st));
+    VH_HIP(hipMemcpyAsync(d_cap, cap.data(), 4 * (uint64_t)P, hipMemcpyHostToDevice, st));
+    hp.W = W;
+    hp.rows_per_wg = rows_per_wg;
+    hp.wg_stride = stride;
+    hp.cap = d_cap;
+    hp.toff = d_toff;
+    hp.fills = d_fills;
+    hp.ent = S.entries.as<uint32_t>();
+    hp.dummy0 = stride * W;
+    static const uint32_t dbg = getenv("VH_HA_DEBUG") ? (uint32_t)atoi(getenv("VH_HA_DEBUG")) : 0u;
+    hp.debug = dbg;
+    if (nv != 1)
+        for (int v = 0; v < nv; v++) hp.vbits[v] = S.vbits.as<uint64_t>() + (uint64_t)v * total;
+    // the fast pass A: 4-byte keys, float64 values, 16-byte aligned columns; rows past the
+    // last multiple of 8 go straight to the HBM table
+    bool fast = dtype_itemsize(h->key_dtype) == 4 && aligned16(keys) && n >= 8;
+    for (int v = 0; v < nv; v++) fast = fast && h->vdtype[v] == VH_F64 && aligned16(vals[v]);
+    {
+        TimedScope ts(fast ? "ha_scatter_f64" : "ha_scatter");
+        if (fast) {
+            const uint64_t n8 = n & ~uint64_t(7);
+            hp.n = n8;
+            if (h->key_dtype == VH_I32) {
+                dispatch_nv(nv, [&](auto nvc) {
+                    constexpr int NV = decltype(nvc)::value;
+                    hipLaunchKernelGGL((k_ha_scatter_f64<int32_t, NV>), dim3(W), dim3(HA_THREADS), lds_a, st, hp, g);
+                    if (n8 < n) {
+                        HaParams ht = hp;
+                        ht.n = n;
+                        hipLaunchKernelGGL((k_ha_tail<int32_t, NV>), dim3(1), dim3(64), 0, st, ht, g, n8);
+                    }
+                });
+            } else {
+                dispatch_nv(nv, [&](auto nvc) {
+                    constexpr int NV = decltype(nvc)::value;
+                    hipLaunchKernelGGL((k_ha_scatter_f64<uint32_t, NV>), dim3(W), dim3(HA_THREADS), lds_a, st, hp, g);
+                    if (n8 < n) {
+                        HaParams ht = hp;
+                        ht.n = n;
+                        hipLaunchKernelGGL((k_ha_tail<uint32_t, NV>), dim3(1), dim3(64), 0, st, ht, g, n8);
+                    }
+                });
+            }
+            hp.n = n;
+        } else {
+            VH_DISPATCH_KEY(h->key_dtype, K, dispatch_nv(nv, [&](auto nvc) {
+                constexpr int NV = decltype(nvc)::value;
+                hipLaunchKernelGGL((k_ha_scatter<K, NV>), dim3(W), dim3(HA_THREADS), lds_a, st, hp, g);
+            }));
+        }
+        VH_HIP(hipGetLastError());
+    }
+    {
+        TimedScope ts("ha_reduce");
+        dispatch_nv(nv, [&](auto nvc) {
+            constexpr int NV = decltype(nvc)::value;
+            hipLaunchKernelGGL(k_ha_reduce<NV>, dim3((unsigned)units.size()), dim3(HB_THREADS), lt_lds, st, hp, g, d_units);
+        });
+        VH_HIP(hipGetLastError());
+    }
+}
+
+}  // namespace vh
+
+extern "C" {
+
+int vh_hashagg_create(int key_dtype, int nvals, const int *val_dtypes, uint32_t nonnull_mask, vh_hashagg **out) {
+    VH_API_BEGIN
+    if (!key_dtype_ok(key_dtype)) fail(VH_ERR_ARG, "hashagg: key dtype must be an integer of <= 4 bytes");
+    if (nvals < 0 || nvals > HA_MAX_V) fail(VH_ERR_ARG, "hashagg: at most 2 value columns");
+    auto h = std::make_unique<vh_hashagg>();
+    h->key_dtype = key_dtype;
+    h->nv = nvals;
+    h->nnmask = nonnull_mask & ((1u << nvals) - 1);
+    for (int v = 0; v < nvals; v++) {
+        const int d = val_dtypes[v];
+        dtype_itemsize(d);
+        h->vdtype[v] = d;
+        if (d == VH_F64 || d == VH_F32) h->vfloat |= 1u << v;
+    }
+    *out = h.release();
+    VH_API_END
+}
+
+int vh_hashagg_destroy(vh_hashagg *h) {
+    VH_API_BEGIN
+    delete h;
+    VH_API_END
+}
+
+int vh_hashagg_update(vh_hashagg *h, const void *keys, const void *const *vals, uint64_t n, int loc) {
+    VH_API_BEGIN
+    if (h->finished) fail(VH_ERR_RUNTIME, "hashagg: update after finish");
+    if (!n) return VH_OK;
+    loc = resolve_loc(keys, loc);
+    const int kisz = dtype_itemsize(h->key_dtype);
+    constexpr uint64_t CHUNK = 1ull << 30;
+    HaScratch &S = scratch();
+    std::lock_guard<std::mutex> lk(S.mu);
+    for (uint64_t r0 = 0; r0 < n; r0 += CHUNK) {
+        const uint64_t m = std::min(CHUNK, n - r0);
+        const void *kp = static_cast<const char *>(keys) + r0 * kisz;
+        const void *vp[HA_MAX_V] = {nullptr, nullptr};
+        for (int v = 0; v < h->nv; v++) vp[v] = static_cast<const char *>(vals[v]) + r0 * dtype_itemsize(h->vdtype[v]);
+        if (loc == VH_LOC_HOST) {
+            uint64_t bytes = m * kisz;
+            for (int v = 0; v < h->nv; v++) bytes += ((m * dtype_itemsize(h->vdtype[v]) + 255) & ~255ull);
+            S.stage.ensure(bytes + 512);
+            char *d = S.stage.as<char>();
+            VH_HIP(hipMemcpyAsync(d, kp, m * kisz, hipMemcpyHostToDevice, stream()));
+            uint64_t off = (m * kisz + 255) & ~255ull;
+            for (int v = 0; v < h->nv; v++) {
+                const uint64_t b = m * dtype_itemsize(h->vdtype[v]);
+                VH_HIP(hipMemcpyAsync(d + off, vp[v], b, hipMemcpyHostToDevice, stream()));
+                vp[v] = d + off;
+                off += (b + 255) & ~255ull;
+            }
+            kp = d;
+        }
+        update_device(h, S, kp, vp, m);
+        uint32_t err = 0;
+        read_used(h, &err);
+        if (err & 2) fail(VH_ERR_RUNTIME, "hashagg: hash table overflow");
+        if (err & 1) {  // past 3/4: grow now, before the next update fills it
+            const HaTable g = table_view(h->tab.ptr, h->slots, h->nv, h->vfloat);
+            const uint32_t used = read_used(h, nullptr);
+            ensure_table(h, 2 * (uint64_t)used);
+            (void)g;
+        }
+        h->rows += m;
+    }
+    VH_API_END
+}
+
+int vh_hashagg_finish(vh_hashagg *h, uint64_t *ngroups) {
+    VH_API_BEGIN
+    if (!h->finished) {
+        hipStream_t st = stream();
+        h->finished = true;
+        h->ngroups = 0;
+        if (h->slots) {
+            const uint64_t m = read_used(h, nullptr);
+            h->ngroups = m;
+            if (m) {
+                const HaTable g = table_view(h->tab.ptr, h->slots, h->nv, h->vfloat);
+                size_t tmp_bytes = 0;
+                VH_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                 (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)m, 0, 32, st));
+                // scratch: skey | sslot | skey2 | sslot2 | counter | tmp ; outputs after
+                const uint64_t a = (4 * m + 255) & ~255ull;
+                const uint64_t out_bytes = 8 * m * (2 + 2 * (uint64_t)h->nv);
+                h->out.ensure(4 * a + 256 + tmp_bytes + out_bytes + 256);
+                char *base = h->out.as<char>();
+                uint32_t *skey = reinterpret_cast<uint32_t *>(base), *sslot = reinterpret_cast<uint32_t *>(base + a);
+                uint32_t *skey2 = reinterpret_cast<uint32_t *>(base + 2 * a), *sslot2 = reinterpret_cast<uint32_t *>(base + 3 * a);
+                uint32_t *counter = reinterpret_cast<uint32_t *>(base + 4 * a);
+                void *tmp = base + 4 * a + 256;
+                char *outp = base + 4 * a + 256 + ((tmp_bytes + 255) & ~255ull);
+                VH_HIP(hipMemsetAsync(counter, 0, 4, st));
+                TimedScope ts("ha_finish");
+                const int sg = key_signed(h->key_dtype);
+                hipLaunchKernelGGL(k_ha_compact, dim3(blocks_for(h->slots, 256, 8)), dim3(256), 0, st, g.keys, h->slots,
+                                   sg, skey, sslot, counter);
+                VH_HIP(hipGetLastError());
+                VH_HIP(rocprim::radix_sort_pairs(tmp, tmp_bytes, skey, skey2, sslot, sslot2, (size_t)m, 0, 32, st));
+                int64_t *okey = reinterpret_cast<int64_t *>(outp);
+                int64_t *ocnt = okey + m;
+                uint64_t *osum = reinterpret_cast<uint64_t *>(ocnt + m);
+                int64_t *onn = reinterpret_cast<int64_t *>(osum + m * h->nv);
+                dispatch_nv(h->nv, [&](auto nvc) {
+                    constexpr int NV = decltype(nvc)::value;
+                    hipLaunchKernelGGL(k_ha_gather<NV>, dim3(blocks_for(m, 256, 8)), dim3(256), 0, st, g, skey2, sslot2, m,
+                                       sg, okey, ocnt, osum, onn);
+                });
+                VH_HIP(hipGetLastError());
+            }
+        }
+    }
+    *ngroups = h->ngroups;
+    VH_API_END
+}
+
+/* outputs (host, ngroups items each): keys as int64, count(*) int64, per value column its
+   sum (double / int64 / uint64 bits, 8 bytes) and non-NaN count int64 */
+int vh_hashagg_read(vh_hashagg *h, int64_t *keys, int64_t *counts, void *const *sums, int64_t *const *nonnull) {
+    VH_API_BEGIN
+    if (!h->finished) fail(VH_ERR_RUNTIME, "hashagg: read before finish");
+    const uint64_t m = h->ngroups;
+    if (!m) return VH_OK;
+    const uint64_t a = (4 * m + 255) & ~255ull;
+    size_t tmp_bytes = 0;
+    VH_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                     (uint32_t *)nullptr, (size_t)m, 0, 32, stream()));
+    const char *outp = h->out.as<char>() + 4 * a + 256 + ((tmp_bytes + 255) & ~255ull);
+    const int64_t *okey = reinterpret_cast<const int64_t *>(outp);
+    const int64_t *ocnt = okey + m;
+    const uint64_t *osum = reinterpret_cast<const uint64_t *>(ocnt + m);
+    const int64_t *onn = reinterpret_cast<const int64_t *>(osum + m * h->nv);
+    hipStream_t st = stream();
+    if (keys) VH_HIP(hipMemcpyAsync(keys, okey, 8 * m, hipMemcpyDeviceToHost, st));
+    if (counts) VH_HIP(hipMemcpyAsync(counts, ocnt, 8 * m, hipMemcpyDeviceToHost, st));
+    for (int v = 0; v < h->nv; v++) {
+        if (sums && sums[v]) VH_HIP(hipMemcpyAsync(sums[v], osum + (uint64_t)v * m, 8 * m, hipMemcpyDeviceToHost, st));
+        if (nonnull && nonnull[v]) VH_HIP(hipMemcpyAsync(nonnull[v], onn + (uint64_t)v * m, 8 * m, hipMemcpyDeviceToHost, st));
+    }
+    VH_HIP(hipStreamSynchronize(st));
+    VH_API_END
+}
+
+}  // extern "C"

@@ -199,6 +199,65 @@ __global__ __launch_bounds__(256) void k_minmax(const void *data, uint64_t n, in
     }
 }
 
+// Streaming form for native, unmasked, 16-B aligned columns of a numeric T: every lane
+// keeps MM_UNROLL 16-byte loads in flight, min/max are kept in T (the T -> double map is
+// monotone, so double(min T) == min of the doubles) and mapped to keys once per lane.
+// NaN fails both compares and is skipped (nanmin/nanmax, tasks.py:173-185).
+constexpr int MM_UNROLL = 4;
+template <typename T>
+__global__ __launch_bounds__(256) void k_minmax_vec(const T *data, uint64_t nvec, uint64_t *keys) {
+    constexpr int V = 16 / sizeof(T);
+    struct alignas(16) Vec { T v[V]; };
+    const Vec *src = reinterpret_cast<const Vec *>(data);
+    T lo = data[0], hi = data[0];
+    if constexpr (is_float_t<T>::value) {
+        lo = __builtin_inf();
+        hi = -__builtin_inf();
+    }
+    bool any = false;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    for (; i + (MM_UNROLL - 1) * stride < nvec; i += MM_UNROLL * stride) {
+        Vec b[MM_UNROLL];
+#pragma unroll
+        for (int u = 0; u < MM_UNROLL; u++) b[u] = src[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < MM_UNROLL; u++)
+#pragma unroll
+            for (int k = 0; k < V; k++) {
+                const T v = b[u].v[k];
+                lo = v < lo ? v : lo;
+                hi = v > hi ? v : hi;
+            }
+        any = true;
+    }
+    for (; i < nvec; i += stride) {
+        const Vec b = src[i];
+#pragma unroll
+        for (int k = 0; k < V; k++) {
+            const T v = b.v[k];
+            lo = v < lo ? v : lo;
+            hi = v > hi ? v : hi;
+        }
+        any = true;
+    }
+    uint64_t klo = ~0ULL, khi = 0ULL;
+    if (any && !(lo > hi)) {  // floats: an all-NaN lane leaves lo = inf > hi = -inf
+        klo = f64_key((double)lo);
+        khi = f64_key((double)hi);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t l2 = __shfl_down(klo, off, 64);
+        const uint64_t h2 = __shfl_down(khi, off, 64);
+        klo = l2 < klo ? l2 : klo;
+        khi = h2 > khi ? h2 : khi;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (klo != ~0ULL) atomicMin((unsigned long long *)&keys[0], (unsigned long long)klo);
+        if (khi != 0ULL) atomicMax((unsigned long long *)&keys[1], (unsigned long long)khi);
+    }
+}
+
 }  // namespace vh
 
 using namespace vh;
@@ -362,10 +421,25 @@ int vh_minmax(const void *data, uint64_t n, int dtype, int flip, const uint8_t *
     VH_HIP(hipMemcpyAsync(keys.ptr, init, 16, hipMemcpyHostToDevice, stream()));
     if (n) {
         TimedScope ts("minmax");
-        VH_DISPATCH_DTYPE(dtype, T,
-                          hipLaunchKernelGGL(k_minmax<T>, dim3(blocks_for(n, 256, 4)), dim3(256), 0, stream(),
-                                             d, n, flip, m, keys.as<uint64_t>()));
-        VH_HIP(hipGetLastError());
+        uint64_t done = 0;
+        const bool vec_ok = !flip && !m && dtype != VH_BOOL && (reinterpret_cast<uintptr_t>(d) & 15) == 0;
+        if (vec_ok && n * isz >= 16) {
+            const uint64_t nvec = n * isz / 16;
+            done = nvec * (16 / isz);
+            VH_DISPATCH_DTYPE(dtype, T,
+                              if constexpr (!std::is_same_v<T, vbool>)
+                                  hipLaunchKernelGGL(k_minmax_vec<T>, dim3(blocks_for(nvec, 256, 8)), dim3(256), 0,
+                                                     stream(), static_cast<const T *>(d), nvec, keys.as<uint64_t>()));
+            VH_HIP(hipGetLastError());
+        }
+        if (done < n) {
+            const void *rest = static_cast<const char *>(d) + done * isz;
+            VH_DISPATCH_DTYPE(dtype, T,
+                              hipLaunchKernelGGL(k_minmax<T>, dim3(blocks_for(n - done, 256, 4)), dim3(256), 0,
+                                                 stream(), rest, n - done, flip, m ? m + done : m,
+                                                 keys.as<uint64_t>()));
+            VH_HIP(hipGetLastError());
+        }
     }
     uint64_t res[2];
     VH_HIP(hipMemcpyAsync(res, keys.ptr, 16, hipMemcpyDeviceToHost, stream()));

@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cmath>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <tuple>
 
@@ -649,8 +650,27 @@ bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t
     return try_tiled_impl(plan, fa_in, n, cells, nd_f64, ws);
 }
 
+// Partition scratch shared by every grid of a device: a 1e9-row count+sum needs ~10 GB of
+// regions, which a per-grid buffer would hipMalloc/hipFree for every query (a grid lives
+// for one query).  Held under the device's lock while a bin is enqueued; reuse is ordered
+// by the library stream.
+struct TileScratch {
+    std::mutex mu;
+    DevBuf entries, values, meta;
+};
+static TileScratch &tile_scratch() {
+    static std::mutex g;
+    static std::map<int, std::unique_ptr<TileScratch>> m;
+    std::lock_guard<std::mutex> lk(g);
+    auto &p = m[current_device()];
+    if (!p) p = std::make_unique<TileScratch>();
+    return *p;
+}
+
 static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64,
-                           Workspace &ws) {
+                           Workspace &) {
+    TileScratch &ws = tile_scratch();
+    std::lock_guard<std::mutex> ws_lock(ws.mu);
     TileParams tp{};
     if (const char *dbg = getenv("VH_TILE_DEBUG")) tp.debug = (uint32_t)atoi(dbg);
     // carried values: one slot per sum aggregator; counts keyed on a matching sum's value
@@ -725,7 +745,7 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     const uint32_t W = std::min<uint32_t>(1024, (uint32_t)cu_count() * bpc);
     // pass-B work units: sum over tiles of ceil(e_t / target) <= T + 4 cu (target = n / 4 cu)
     const uint64_t max_units = (uint64_t)T + 4 * (uint64_t)cu_count() + 16;
-    DevBuf &meta = ws.tile_meta;
+    DevBuf &meta = ws.meta;
     const uint64_t meta_bytes = 8 * (uint64_t)T /*hist*/ + 4 * (uint64_t)T /*cap*/ + 8 * (uint64_t)T /*toff*/ +
                                 4 * (uint64_t)T * W /*fills*/ + 16 * max_units /*units*/ + 256;
     meta.ensure(meta_bytes);
@@ -774,8 +794,8 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     if (stride + rows_per_wg >= (uint64_t)DEST_OVERFLOW) return false;
     const uint64_t total = stride * W;
     const int ebytes = flags_mode ? 4 : 2;
-    ws.tile_entries.ensure(total * ebytes);
-    if (nv) ws.tile_values.ensure(total * 8 * nv);
+    ws.entries.ensure(total * ebytes);
+    if (nv) ws.values.ensure(total * 8 * nv);
     tp.s_log2 = s_log2;
     tp.ntiles = T;
     tp.flags_mode = flags_mode ? 1 : 0;
@@ -787,8 +807,8 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     tp.cap = d_cap;
     tp.toff = d_toff;
     tp.fills = d_fills;
-    tp.entries = ws.tile_entries.ptr;
-    for (int s = 0; s < nv; s++) tp.values[s] = ws.tile_values.as<double>() + (uint64_t)s * total;
+    tp.entries = ws.entries.ptr;
+    for (int s = 0; s < nv; s++) tp.values[s] = ws.values.as<double>() + (uint64_t)s * total;
     VH_HIP(hipMemcpyAsync(d_cap, cap.data(), 4 * (uint64_t)T, hipMemcpyHostToDevice, st));
     VH_HIP(hipMemcpyAsync(d_toff, toff.data(), 8 * (uint64_t)T, hipMemcpyHostToDevice, st));
 

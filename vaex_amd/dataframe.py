@@ -483,7 +483,13 @@ class DataFrame:
     def groupby(self, by=None, agg=None, sort=False, assume_sparse="auto", row_limit=None, copy=True,
                 progress=None, delay=False):
         """dataframe.py:6622-6683."""
-        from .groupby import GroupBy
+        from .groupby import GroupBy, parse_actions
+        if agg is not None and assume_sparse != True:  # noqa: E712
+            # one hash-partitioned pass for integer keys + count/sum/mean (hashagg.py)
+            from .hashagg import try_groupby
+            res = try_groupby(self, by, agg, lambda a, g: parse_actions(self, a, g), sort=sort, row_limit=row_limit)
+            if res is not None:
+                return res
         groupby = GroupBy(self, by=by, sort=sort, row_limit=row_limit, dense=assume_sparse != True)  # noqa: E712
         if agg is None:
             return groupby

@@ -29,7 +29,7 @@ class Grouper(BinnerBase):
         self.label = self.expression
         oset = df_original._set(self.expression, unique_limit=row_limit)
         self.bin_values = oset.key_array()
-        if self.bin_values.dtype.kind in "iu" and len(self.bin_values):
+        if self.bin_values.dtype.kind == "i" and len(self.bin_values):  # groupby.py:133-135
             self.bin_values = self.bin_values.astype(required_dtype_for_max(int(self.bin_values.max())))
         self.has_null = oset.has_null
         self.null_value = oset.null_value
@@ -171,49 +171,57 @@ class GroupByBase:
     def _agg(self, actions):
         """groupby.py:345-402: every aggregate gets edges=True on the grouper binners."""
         df = self.df
-        if isinstance(actions, dict):
-            actions = list(actions.items())
-        elif not isinstance(actions, (list, tuple)) or isinstance(actions, str):
-            actions = [actions]
         grids = {}
         self.counts = None
-
-        def add(aggregate, column_name=None, override_name=None):
-            if column_name is None or override_name is not None:
-                column_name = aggregate.pretty_name(override_name, df)
+        for column_name, aggregate in parse_actions(df, actions, self.groupby_expression):
             aggregate.edges = True
             values = df._agg(aggregate, self.binners, delay=True)
             grids[column_name] = values
             if isinstance(aggregate, vagg.AggregatorDescriptorBasic) and aggregate.name == "AggCount" \
                     and aggregate.expression == "*" and aggregate.selection in (None, False):
                 self.counts = values
-
-        for item in actions:
-            override_name = None
-            if isinstance(item, tuple):
-                name, aggregates = item
-            else:
-                aggregates, name = item, None
-            if not isinstance(aggregates, (list, tuple)) or isinstance(aggregates, str):
-                aggregates = [aggregates]
-            elif name is not None:
-                override_name = name
-            for aggregate in aggregates:
-                if isinstance(aggregate, str) and aggregate == "count":
-                    add(vagg.count(), "count" if name is None else name)
-                else:
-                    if isinstance(aggregate, str):
-                        aggregate = vagg.aggregates[aggregate]
-                    if callable(aggregate):
-                        if name is None:
-                            for column_name in df.get_column_names():
-                                if column_name not in self.groupby_expression:
-                                    add(aggregate(column_name), override_name=override_name)
-                        else:
-                            add(aggregate(name), name, override_name=override_name)
-                    else:
-                        add(aggregate, name, override_name=override_name)
         return grids
+
+
+def parse_actions(df, actions, groupby_expression):
+    """The agg= argument as [(output column name, aggregator descriptor)] (groupby.py:345-402)."""
+    if isinstance(actions, dict):
+        actions = list(actions.items())
+    elif not isinstance(actions, (list, tuple)) or isinstance(actions, str):
+        actions = [actions]
+    out = []
+
+    def add(aggregate, column_name=None, override_name=None):
+        if column_name is None or override_name is not None:
+            column_name = aggregate.pretty_name(override_name, df)
+        out.append((column_name, aggregate))
+
+    for item in actions:
+        override_name = None
+        if isinstance(item, tuple):
+            name, aggregates = item
+        else:
+            aggregates, name = item, None
+        if not isinstance(aggregates, (list, tuple)) or isinstance(aggregates, str):
+            aggregates = [aggregates]
+        elif name is not None:
+            override_name = name
+        for aggregate in aggregates:
+            if isinstance(aggregate, str) and aggregate == "count":
+                add(vagg.count(), "count" if name is None else name)
+            else:
+                if isinstance(aggregate, str):
+                    aggregate = vagg.aggregates[aggregate]
+                if callable(aggregate):
+                    if name is None:
+                        for column_name in df.get_column_names():
+                            if column_name not in groupby_expression:
+                                add(aggregate(column_name), override_name=override_name)
+                    else:
+                        add(aggregate(name), name, override_name=override_name)
+                else:
+                    add(aggregate, name, override_name=override_name)
+    return out
 
 
 class GroupBy(GroupByBase):

@@ -1,0 +1,175 @@
+"""Fused hash groupby (``libvaexhip`` ``vh_hashagg_*``, ``vaex_amd/csrc/hashagg.hip``).
+
+``groupby(key).agg(...)`` of one integer key column (<= 4 bytes) with count / sum / mean
+aggregates over at most two numeric value columns runs as ONE hash-partitioned pass over
+the data instead of the reference's two passes (ordered_set build, then
+``_ordinal_values`` + ``BinnerOrdinal`` + ``AggCount``/``AggSum``; groupby.py:97-168,
+484-533).  The per-key results are the same grids' central parts; groups come out sorted
+by key.  :func:`try_groupby` returns ``None`` for any query outside that shape (masks,
+filters, selections, other aggregators, wide keys) and the caller takes the general
+grouper path; an overflowing hash table also returns ``None`` (never a partial result).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .device import DeviceArray
+from .utils import required_dtype_for_max
+
+KEY_DTYPES = {"int8", "int16", "int32", "uint8", "uint16", "uint32"}
+VALUE_KINDS = "fiub"
+
+
+class HashAggOverflow(RuntimeError):
+    pass
+
+
+class HashAgg:
+    """Accumulates groups over one or more chunks of (key, values) rows."""
+
+    def __init__(self, key_dtype, value_dtypes, nonnull=None):
+        """nonnull[v]: the non-NaN count of value column v is needed (count(v) / mean);
+        default all."""
+        self.key_dtype = np.dtype(key_dtype)
+        self.value_dtypes = [np.dtype(d) for d in value_dtypes]
+        kcode, _ = _lib.dtype_code(self.key_dtype)
+        codes = (ctypes.c_int * max(1, len(self.value_dtypes)))(*[_lib.dtype_code(d)[0] for d in self.value_dtypes])
+        if nonnull is None:
+            nonnull = [True] * len(self.value_dtypes)
+        nnmask = sum(1 << i for i, want in enumerate(nonnull) if want)
+        h = ctypes.c_void_p()
+        _lib.call("vh_hashagg_create", kcode, len(self.value_dtypes), codes, nnmask, ctypes.byref(h))
+        self._h = h
+        self._keep = []
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            _lib.lib().vh_hashagg_destroy(h)
+            self._h = None
+
+    def update(self, keys, values):
+        n = len(keys)
+        if any(len(v) != n for v in values):
+            raise ValueError("key and value columns differ in length")
+        cols = [keys] + list(values)
+        on_device = [isinstance(c, DeviceArray) for c in cols]
+        if any(on_device) and not all(on_device):
+            cols = [c if isinstance(c, DeviceArray) else DeviceArray.from_numpy(c) for c in cols]
+            self._keep.append(cols)
+            loc = _lib.LOC_DEVICE
+        elif all(on_device):
+            loc = _lib.LOC_DEVICE
+        else:
+            cols = [np.ascontiguousarray(c) for c in cols]
+            loc = _lib.LOC_HOST
+        ptrs = [c.ptr if isinstance(c, DeviceArray) else c.ctypes.data for c in cols]
+        vals = (ctypes.c_void_p * max(1, len(values)))(*ptrs[1:])
+        rc = _lib.lib().vh_hashagg_update(self._h, ptrs[0], vals, n, loc)
+        if rc != 0:
+            msg = _lib.lib().vh_last_error().decode(errors="replace")
+            if "overflow" in msg or "too many groups" in msg:
+                raise HashAggOverflow(msg)
+            _lib.check(rc)
+
+    def finish(self):
+        m = ctypes.c_uint64()
+        _lib.call("vh_hashagg_finish", self._h, ctypes.byref(m))
+        m = m.value
+        keys = np.empty(m, np.int64)
+        counts = np.empty(m, np.int64)
+        sums = [np.empty(m, np.float64 if d.kind == "f" else (np.int64 if d.kind == "i" else np.uint64))
+                for d in self.value_dtypes]
+        nonnull = [np.empty(m, np.int64) for _ in self.value_dtypes]
+        nv = max(1, len(self.value_dtypes))
+        sp = (ctypes.c_void_p * nv)(*[s.ctypes.data for s in sums])
+        npp = (ctypes.c_void_p * nv)(*[c.ctypes.data for c in nonnull])
+        if m:
+            _lib.call("vh_hashagg_read", self._h, keys.ctypes.data, counts.ctypes.data, sp, npp)
+        return keys, counts, sums, nonnull
+
+
+def _plan(df, by, actions, parse):
+    """(key column, [(out name, op, value index)], value columns) or None if not eligible."""
+    from . import agg as vagg
+    if isinstance(by, (list, tuple)):
+        if len(by) != 1:
+            return None
+        by = by[0]
+    if not isinstance(by, str) and type(by).__name__ != "Expression":
+        return None
+    by = str(by)
+    if df.filtered or by not in df.columns or df.is_category(by):
+        return None
+    key = df.columns[by]
+    if np.ma.isMaskedArray(key) or np.dtype(key.dtype).name not in KEY_DTYPES:
+        return None
+    if isinstance(key, np.ndarray) and (key.ndim != 1 or not key.dtype.isnative):
+        return None
+    items = parse(actions, [by])
+    if items is None:
+        return None
+    value_names, ops = [], []
+    for name, a in items:
+        if getattr(a, "selection", None) not in (None, False):
+            return None
+        if isinstance(a, vagg.AggregatorDescriptorBasic) and a.name == "AggCount" and a.expression == "*":
+            ops.append((name, "count", None))
+            continue
+        short = getattr(a, "short_name", None)
+        if not ((isinstance(a, vagg.AggregatorDescriptorBasic) and a.name in ("AggCount", "AggSum"))
+                or isinstance(a, vagg.AggregatorDescriptorMean)):
+            return None
+        col = str(a.expression)
+        if col not in df.columns or col == by:
+            return None
+        c = df.columns[col]
+        dt = np.dtype(c.dtype)
+        if np.ma.isMaskedArray(c) or dt.kind not in VALUE_KINDS or not dt.isnative:
+            return None
+        if isinstance(c, np.ndarray) and c.ndim != 1:
+            return None
+        if col not in value_names:
+            value_names.append(col)
+        ops.append((name, {"count": "nonnull", "sum": "sum", "mean": "mean"}[short], value_names.index(col)))
+    if len(value_names) > 2 or not ops:
+        return None
+    return by, ops, value_names
+
+
+def try_groupby(df, by, actions, parse, sort=False, row_limit=None):
+    """The fused path of ``DataFrame.groupby(by, agg=actions)``; ``None`` = not taken."""
+    from .dataframe import DataFrame, RowLimitException
+    plan = _plan(df, by, actions, parse)
+    if plan is None:
+        return None
+    by, ops, value_names = plan
+    key = df.columns[by]
+    values = [df.columns[v] for v in value_names]
+    nonnull = [any(op in ("nonnull", "mean") and vi == i for _, op, vi in ops) for i in range(len(values))]
+    ha = HashAgg(key.dtype, [v.dtype for v in values], nonnull)
+    try:
+        ha.update(key, values)
+    except HashAggOverflow:
+        return None
+    keys, counts, sums, nonnull = ha.finish()
+    if row_limit is not None and len(keys) > row_limit:
+        raise RowLimitException(f"Resulting grouper has {len(keys):,} unique combinations, which is larger "
+                                f"than the allowed row limit of {row_limit:,}")
+    kdt = np.dtype(key.dtype)
+    labels = keys.astype(kdt)
+    if kdt.kind == "i" and len(labels):  # groupby.py:133-135
+        labels = labels.astype(required_dtype_for_max(int(labels.max())))
+    columns = {by: labels}
+    for name, op, vi in ops:
+        if op == "count":
+            columns[name] = counts
+        elif op == "nonnull":
+            columns[name] = nonnull[vi]
+        elif op == "sum":
+            columns[name] = sums[vi]
+        else:
+            with np.errstate(divide="ignore", invalid="ignore"):
+                columns[name] = sums[vi] / nonnull[vi]
+    return DataFrame(columns)
