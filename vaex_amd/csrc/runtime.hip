@@ -33,6 +33,67 @@ int current_device() {
     return d;
 }
 
+// ---- device block cache (common.hpp) ---------------------------------------------------
+namespace {
+constexpr uint64_t CACHE_MAX_BLOCK = 256ull << 20;
+constexpr uint64_t CACHE_MAX_BYTES = 2ull << 30;
+struct BlockCache {
+    std::multimap<uint64_t, void *> free;
+    uint64_t cached = 0;
+};
+std::mutex g_cache_mu;
+std::map<int, BlockCache> g_cache;
+}  // namespace
+
+void *dev_alloc(uint64_t &bytes) {
+    const uint64_t gran = bytes >= (1ull << 20) ? (1ull << 20) : 4096;
+    bytes = (bytes + gran - 1) / gran * gran;
+    const int d = current_device();
+    if (bytes <= CACHE_MAX_BLOCK) {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        BlockCache &c = g_cache[d];
+        auto it = c.free.find(bytes);
+        if (it != c.free.end()) {
+            void *p = it->second;
+            c.free.erase(it);
+            c.cached -= bytes;
+            return p;
+        }
+    }
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        {  // drop the cache and retry once
+            std::lock_guard<std::mutex> lk(g_cache_mu);
+            BlockCache &c = g_cache[d];
+            for (auto &kv : c.free) (void)hipFree(kv.second);
+            c.free.clear();
+            c.cached = 0;
+        }
+        e = hipMalloc(&p, bytes);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            fail(VH_ERR_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed: " + hipGetErrorString(e));
+        }
+    }
+    return p;
+}
+
+void dev_free(void *ptr, uint64_t bytes) {
+    if (!ptr) return;
+    if (bytes <= CACHE_MAX_BLOCK) {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        BlockCache &c = g_cache[current_device()];
+        if (c.cached + bytes <= CACHE_MAX_BYTES) {
+            c.free.emplace(bytes, ptr);
+            c.cached += bytes;
+            return;
+        }
+    }
+    (void)hipFree(ptr);
+}
+
 hipStream_t stream() {
     int d = current_device();
     std::lock_guard<std::mutex> lk(g_mu);
