@@ -165,8 +165,9 @@ def test_dataframe_groupby_uses_fused_path(monkeypatch):
     from vaex_amd import hashagg
     rng = np.random.default_rng(9)
     n = 1_000_000
-    df = vaex_amd.from_arrays(key=rng.integers(-100, 20000, n).astype(np.int32), v=rng.normal(size=n),
-                              w=rng.integers(0, 10, n).astype(np.int8))
+    # sparse keys (value span >> rows): the dense-range grouper does not apply
+    keys = (rng.integers(-100, 20000, n).astype(np.int64) * 104729 - 10 ** 9).astype(np.int32)
+    df = vaex_amd.from_arrays(key=keys, v=rng.normal(size=n), w=rng.integers(0, 10, n).astype(np.int8))
     agg = {"v": ["sum", "count", "mean"], "w": "sum", "n": "count"}
     calls = []
     orig = hashagg.HashAgg.update
@@ -190,3 +191,32 @@ def test_row_limit():
     df = vaex_amd.from_arrays(key=np.arange(1000, dtype=np.int32), v=np.ones(1000))
     with pytest.raises(RowLimitException):
         df.groupby("key", agg={"v": "sum"}, row_limit=10)
+
+
+@pytest.mark.parametrize("n", [2_000_000, 2_000_001])
+def test_dense_int32_keys_take_fast_ordinal_tile_path(n):
+    """A dense int32 key range goes to the categorical-style grid (min/max pass +
+    BinnerOrdinal) whose pass A is the fast ordinal kernel; the result equals the oracle
+    map and the fused path's.  Odd n exercises the last-row split."""
+    import vaex_amd
+    from vaex_amd import _lib
+    rng = np.random.default_rng(10)
+    keys = (5 + rng.integers(0, 300_000, n)).astype(np.int32)
+    v = rng.normal(size=n)
+    v[::53] = np.nan
+    df = vaex_amd.from_arrays(key=keys, v=v)
+    _lib.timing_reset()
+    _lib.timing_enable(True)
+    dfg = df.groupby("key", agg={"v_sum": vaex_amd.agg.sum("v"), "v_count": vaex_amd.agg.count("v"), "n": "count"})
+    _lib.synchronize()
+    _lib.timing_enable(False)
+    assert _lib.timing_read("tile_scatter_ord")[0] >= 1, "fast ordinal pass A not used"
+    uk, s, c = oracle.groupby_reference(keys, v)
+    gk = dfg["key"].to_numpy()
+    np.testing.assert_array_equal(gk, uk)
+    np.testing.assert_array_equal(dfg["v_count"].to_numpy(), c)
+    np.testing.assert_array_equal(dfg["n"].to_numpy(), np.bincount(keys)[uk])
+    np.testing.assert_allclose(dfg["v_sum"].to_numpy(), s, rtol=1e-6, atol=1e-9)
+    fk, fc, fs, fn = _run(keys, [v])
+    np.testing.assert_array_equal(fk, uk)
+    np.testing.assert_allclose(fs[0], s, rtol=1e-6, atol=1e-9)

@@ -418,6 +418,98 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan
     for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.base[t] - (uint32_t)tp.toff[t];
 }
 
+// BinnerOrdinal<int32_t> index of a loaded key, native byte order, no mask
+// (superagg_binners.cpp:104-142 with T = int32: the uint64 min_value is subtracted first)
+__device__ inline uint64_t ordinal_i32_index(int32_t raw, uint64_t min_value, uint64_t count) {
+    const int32_t value = (int32_t)((uint64_t)(int64_t)raw - min_value);
+    if (value < 0) return 1;
+    if ((uint64_t)(int64_t)value >= count) return count + 2;
+    return (uint64_t)((int64_t)value + 2);
+}
+
+// fast pass A of the groupby / categorical grid: one int32 BinnerOrdinal (native, no mask)
+// and NV float64 sums without masks -- the C3 groupby(key).agg({sum, count}) shape.
+// Keys are read as 8-byte pairs and values as 16-byte pairs, the next batch prefetched in
+// registers (same row layout and pipelining as k_tile_scatter_f64).
+template <int NV>
+__global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
+    constexpr int PAIRS = TA_RPT / 2;
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const uint32_t T = tp.ntiles;
+    const ScatterLds l = scatter_lds<NV>(lds_raw, T);
+    __shared__ uint32_t s_total;
+    scatter_lds_init(l, tp, T);
+    __syncthreads();
+    const int32_t *keys = reinterpret_cast<const int32_t *>(p.b[0].data);
+    const double *col[NV > 0 ? NV : 1];
+#pragma unroll
+    for (int s = 0; s < NV; s++) col[s] = tp.vdata[s];
+    const uint64_t min_value = p.b[0].min_value, count = p.b[0].ordinal_count, stride0 = p.b[0].stride;
+    uint32_t count_mask = 0, keyed_slot_of[MAX_FUSED_AGGS];
+    #pragma unroll
+    for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+        if (k >= fa.na) break;
+        keyed_slot_of[k] = fa.a[k].kind == VH_AGG_COUNT ? (uint32_t)tp.cnt_slot[k] : (uint32_t)tp.val_slot[k];
+        if (fa.a[k].kind == VH_AGG_COUNT && tp.cnt_slot[k] == CNT_ALWAYS) count_mask |= 1u << k;
+    }
+    const uint32_t w = blockIdx.x;
+    const uint64_t row_begin = (uint64_t)w * tp.rows_per_wg;
+    const uint64_t row_end = min(n, row_begin + tp.rows_per_wg);
+    const uint32_t smask = (1u << tp.s_log2) - 1;
+    const uint64_t region0 = (uint64_t)w * tp.wg_stride;
+    struct Regs {
+        int2 k[PAIRS];
+        double2 v[PAIRS][NV > 0 ? NV : 1];
+    };
+    auto load = [&](uint64_t b0, Regs &R) {
+#pragma unroll
+        for (int q = 0; q < PAIRS; q++) {
+            const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + threadIdx.x);
+            const uint64_t is = i < n - 2 ? i : n - 2;
+            R.k[q] = *reinterpret_cast<const int2 *>(keys + is);
+#pragma unroll
+            for (int s = 0; s < NV; s++) R.v[q][s] = *reinterpret_cast<const double2 *>(col[s] + is);
+        }
+    };
+    Regs cur, nxt;
+    load(row_begin, cur);
+    for (uint64_t b0 = row_begin; b0 < row_end; b0 += TA_BATCH) {
+        load(b0 + TA_BATCH, nxt);
+        uint32_t tile[TA_RPT], ent[TA_RPT];
+        int32_t rank[TA_RPT];
+        double vals[TA_RPT][NV > 0 ? NV : 1];
+#pragma unroll
+        for (int r = 0; r < TA_RPT; r++) {
+            const int q = r >> 1, h = r & 1;
+            const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + threadIdx.x) + h;
+            rank[r] = -1;
+            if (i < row_end) {
+                const uint64_t c = ordinal_i32_index(h ? cur.k[q].y : cur.k[q].x, min_value, count) * stride0;
+                uint32_t f = count_mask;
+#pragma unroll
+                for (int s = 0; s < NV; s++) vals[r][s] = h ? cur.v[q][s].y : cur.v[q][s].x;
+                #pragma unroll
+                for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+                    if (k >= fa.na) break;
+                    const uint32_t sl = keyed_slot_of[k];
+                    if (!((count_mask >> k) & 1)) {
+#pragma unroll
+                        for (int s = 0; s < NV; s++)
+                            if (s == (int)sl && vals[r][s] == vals[r][s]) f |= 1u << k;
+                    }
+                }
+                tile[r] = (uint32_t)(c >> tp.s_log2);
+                ent[r] = ((uint32_t)c & smask) | (f << 16);
+                if (f) rank[r] = (int32_t)atomicAdd(&l.hist[tile[r]], 1u);
+            }
+        }
+        batch_commit<NV>(l, fa, tp, T, region0, tile, ent, rank, vals, &s_total);
+        cur = nxt;
+        lds_barrier();
+    }
+    for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.base[t] - (uint32_t)tp.toff[t];
+}
+
 template <int NV>
 __device__ inline void reduce_entry(const FusedAggs &fa, const TileParams &tp, unsigned char *lds, uint32_t local,
                                     uint32_t fl, const double *v) {
@@ -628,16 +720,37 @@ template <int NV> static int scatter_blocks_per_cu_nd(int nd, bool fast, size_t 
 static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64,
                            Workspace &ws);
 
+// the fast ordinal pass A applies: one native int32 BinnerOrdinal without mask, every
+// sum a 16-byte aligned float64 column, no aggregator masks, no counts of other columns
+static bool ord_fast_ok(const BinPlan &plan, const FusedAggs &fa) {
+    if (plan.nb != 1) return false;
+    const BinnerDev &b = plan.b[0];
+    if (b.kind != 1 || b.dtype != VH_I32 || b.flip || b.mask || (reinterpret_cast<uintptr_t>(b.data) & 7)) return false;
+    for (int k = 0; k < fa.na; k++) {
+        const FusedAgg &a = fa.a[k];
+        if (a.mask) return false;
+        if (a.kind != VH_AGG_COUNT) {
+            if (!a.data || (reinterpret_cast<uintptr_t>(a.data) & 15)) return false;
+        } else if (a.data) {
+            bool keyed = false;  // count(v) of a summed column rides on that sum's value
+            for (int j = 0; j < fa.na; j++)
+                if (fa.a[j].kind != VH_AGG_COUNT && fa.a[j].data == a.data) keyed = true;
+            if (!keyed) return false;
+        }
+    }
+    return true;
+}
+
 bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64, Workspace &ws) {
     if (n < (1u << 20) || cells >= (1ull << 40)) return false;
-    if ((n & 1) && nd_f64 > 0) {
+    if ((n & 1) && (nd_f64 > 0 || ord_fast_ok(plan, fa_in))) {
         // the fast pass A reads row pairs: tile all rows but the last, which takes the
-        // global-atomic path (every binner and value column is float64 here)
+        // global-atomic path
         if (!try_tiled_impl(plan, fa_in, n - 1, cells, nd_f64, ws)) return false;
         BinPlan p1 = plan;
         FusedAggs f1 = fa_in;
         for (int d = 0; d < p1.nb; d++) {
-            p1.b[d].data = reinterpret_cast<const double *>(p1.b[d].data) + (n - 1);
+            p1.b[d].data = static_cast<const char *>(p1.b[d].data) + (n - 1) * (p1.b[d].dtype == VH_I32 ? 4 : 8);
             if (p1.b[d].mask) p1.b[d].mask += n - 1;
         }
         for (int k = 0; k < f1.na; k++) {
@@ -725,18 +838,29 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
             fast = fast && fa.a[k].data && aligned16(fa.a[k].data);
         }
     }
+    const bool ord = !fast && n % 2 == 0 && ord_fast_ok(plan, fa);
+    if (ord) for (int k = 0; k < fa.na; k++)
+        if (fa.a[k].kind != VH_AGG_COUNT) tp.vdata[tp.val_slot[k]] = fa.a[k].data;
     const size_t lds_a = scatter_lds_bytes(nv, T);
     int bpc;
     {
         static std::mutex mu;
         static std::map<std::tuple<int, int, int, bool, size_t>, int> cache;
         std::lock_guard<std::mutex> lk(mu);
-        const auto key = std::make_tuple(current_device(), nd_f64, nv, fast, lds_a);
+        const auto key = std::make_tuple(current_device(), ord ? -1 : nd_f64, nv, fast, lds_a);
         auto it = cache.find(key);
         if (it == cache.end()) {
-            const int v = nv == 0 ? scatter_blocks_per_cu_nd<0>(nd_f64, fast, lds_a)
-                                  : nv == 1 ? scatter_blocks_per_cu_nd<1>(nd_f64, fast, lds_a)
-                                            : scatter_blocks_per_cu_nd<2>(nd_f64, fast, lds_a);
+            int v = 0;
+            if (ord) {
+                const void *kf = nv == 0 ? reinterpret_cast<const void *>(k_tile_scatter_ord<0>)
+                                 : nv == 1 ? reinterpret_cast<const void *>(k_tile_scatter_ord<1>)
+                                           : reinterpret_cast<const void *>(k_tile_scatter_ord<2>);
+                VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kf, TA_THREADS, lds_a));
+            } else {
+                v = nv == 0 ? scatter_blocks_per_cu_nd<0>(nd_f64, fast, lds_a)
+                            : nv == 1 ? scatter_blocks_per_cu_nd<1>(nd_f64, fast, lds_a)
+                                      : scatter_blocks_per_cu_nd<2>(nd_f64, fast, lds_a);
+            }
             it = cache.emplace(key, v).first;
         }
         bpc = it->second;
@@ -825,12 +949,20 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
 
     // ---- pass A
     {
-        TimedScope ts(fast ? "tile_scatter_f64" : "tile_scatter");
+        TimedScope ts(fast ? "tile_scatter_f64" : ord ? "tile_scatter_ord" : "tile_scatter");
         const size_t lds = lds_a;
-        switch (nv) {
-        case 0: launch_scatter_nd<0>(nd_f64, fast, W, lds, plan, fa, tp, n); break;
-        case 1: launch_scatter_nd<1>(nd_f64, fast, W, lds, plan, fa, tp, n); break;
-        default: launch_scatter_nd<2>(nd_f64, fast, W, lds, plan, fa, tp, n);
+        if (ord) {
+            switch (nv) {
+            case 0: hipLaunchKernelGGL(k_tile_scatter_ord<0>, dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n); break;
+            case 1: hipLaunchKernelGGL(k_tile_scatter_ord<1>, dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n); break;
+            default: hipLaunchKernelGGL(k_tile_scatter_ord<2>, dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
+            }
+        } else {
+            switch (nv) {
+            case 0: launch_scatter_nd<0>(nd_f64, fast, W, lds, plan, fa, tp, n); break;
+            case 1: launch_scatter_nd<1>(nd_f64, fast, W, lds, plan, fa, tp, n); break;
+            default: launch_scatter_nd<2>(nd_f64, fast, W, lds, plan, fa, tp, n);
+            }
         }
         VH_HIP(hipGetLastError());
     }

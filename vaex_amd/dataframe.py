@@ -483,14 +483,25 @@ class DataFrame:
     def groupby(self, by=None, agg=None, sort=False, assume_sparse="auto", row_limit=None, copy=True,
                 progress=None, delay=False):
         """dataframe.py:6622-6683."""
-        from .groupby import GroupBy, parse_actions
+        from .groupby import GroupBy, _dense_range, parse_actions
+        dense_ranges = {}
         if agg is not None and assume_sparse != True:  # noqa: E712
-            # one hash-partitioned pass for integer keys + count/sum/mean (hashagg.py)
-            from .hashagg import try_groupby
-            res = try_groupby(self, by, agg, lambda a, g: parse_actions(self, a, g), sort=sort, row_limit=row_limit)
-            if res is not None:
-                return res
-        groupby = GroupBy(self, by=by, sort=sort, row_limit=row_limit, dense=assume_sparse != True)  # noqa: E712
+            # A single integer key: a dense value range bins like a categorical (min/max
+            # pass + BinnerOrdinal grid, GrouperDense); otherwise count/sum/mean run as one
+            # hash-partitioned pass (hashagg.py).
+            from .hashagg import eligible_key, try_groupby
+            key = eligible_key(self, by)
+            if key is not None:
+                rng = _dense_range(self, key)
+                if rng is not None:
+                    dense_ranges[key] = rng
+                else:
+                    res = try_groupby(self, by, agg, lambda a, g: parse_actions(self, a, g), sort=sort,
+                                      row_limit=row_limit)
+                    if res is not None:
+                        return res
+        groupby = GroupBy(self, by=by, sort=sort, row_limit=row_limit, dense=assume_sparse != True,  # noqa: E712
+                          dense_ranges=dense_ranges)
         if agg is None:
             return groupby
         return groupby.agg(agg)

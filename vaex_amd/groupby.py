@@ -145,11 +145,12 @@ class GrouperCategory(BinnerBase):
 
 
 class GroupByBase:
-    def __init__(self, df, by, sort=False, row_limit=None, dense=True):
+    def __init__(self, df, by, sort=False, row_limit=None, dense=True, dense_ranges=None):
         df_original = df
         df = df.copy()
         self.df = df
         self.sort = sort
+        self.row_limit = row_limit
         if not isinstance(by, (list, tuple)):
             by = [by]
         self.by = []
@@ -158,7 +159,7 @@ class GroupByBase:
                 self.by.append(by_value)
             elif df.is_category(by_value):
                 self.by.append(GrouperCategory(df[str(by_value)], df=df, sort=sort, row_limit=row_limit))
-            elif dense and (rng := _dense_range(df, by_value)) is not None:
+            elif dense and (rng := (dense_ranges or {}).get(str(by_value)) or _dense_range(df, by_value)) is not None:
                 self.by.append(GrouperDense(df[str(by_value)], rng[0], rng[1], df=df, row_limit=row_limit))
             else:
                 self.by.append(Grouper(df[str(by_value)], df=df, sort=sort, row_limit=row_limit,
@@ -238,6 +239,11 @@ class GroupBy(GroupByBase):
         if has_non_existing_pairs:
             counts = extract_central_part(np.asarray(counts.get()))
             mask = counts > 0
+            if self.row_limit is not None and any(getattr(b, "dense", False) for b in self.by):
+                groups = int(np.count_nonzero(mask))
+                if groups > self.row_limit:  # what the set build of Grouper raises (groupby.py:125)
+                    raise RowLimitException(f"Resulting grouper has {groups:,} unique combinations, which is "
+                                            f"larger than the allowed row limit of {self.row_limit:,}")
             coords = [c[mask] for c in np.meshgrid(*[np.asarray(b.bin_values) for b in self.by], indexing="ij")]
             for b, coord in zip(self.by, coords):
                 columns[b.label] = coord

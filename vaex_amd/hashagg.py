@@ -90,9 +90,9 @@ class HashAgg:
         return keys, counts, sums, nonnull
 
 
-def _plan(df, by, actions, parse):
-    """(key column, [(out name, op, value index)], value columns) or None if not eligible."""
-    from . import agg as vagg
+def eligible_key(df, by):
+    """The key column name when ``by`` is one plain, unmasked, native integer column of
+    <= 4 bytes on an unfiltered frame (the fused path's key), else None."""
     if isinstance(by, (list, tuple)):
         if len(by) != 1:
             return None
@@ -106,6 +106,15 @@ def _plan(df, by, actions, parse):
     if np.ma.isMaskedArray(key) or np.dtype(key.dtype).name not in KEY_DTYPES:
         return None
     if isinstance(key, np.ndarray) and (key.ndim != 1 or not key.dtype.isnative):
+        return None
+    return by
+
+
+def _plan(df, by, actions, parse):
+    """(key column, [(out name, op, value index)], value columns) or None if not eligible."""
+    from . import agg as vagg
+    by = eligible_key(df, by)
+    if by is None:
         return None
     items = parse(actions, [by])
     if items is None:
