@@ -26,7 +26,7 @@ sys.path.insert(0, ROOT)
 
 BASELINE_METRIC = "rows/sec 2D count grid 1e9×f64 + groupby-sum 1e6 keys; HBM GB/s %peak"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-TILE_KERNELS = ["tile_sample", "tile_scatter", "tile_scatter_f64", "tile_reduce"]
+TILE_KERNELS = ["tile_sample", "tile_scatter", "tile_scatter_f64", "tile_scatter_ord", "tile_reduce"]
 
 
 def parse():
@@ -314,28 +314,53 @@ def bench_host_columns(x, y, w, m, bins):
 
 def bench_groupby(n, args):
     """C3: groupby(int32 key, 1e6 distinct).agg({v: [sum, count]}) on resident columns, end to
-    end (key pass, aggregation pass, result read-back): 'auto' takes the dense-key grouper
-    (min/max pass + BinnerOrdinal), 'hash' forces the GPU ordered_set path (set build pass +
-    fused hash-probe binner)."""
+    end (every pass, result read-back into host numpy columns), best of 3:
+      auto  -- what DataFrame.groupby picks for this dense key range: one min/max pass, then
+               the BinnerOrdinal grid through the tile path (fast ordinal pass A);
+      fused -- the one-pass hash-partitioned aggregation (hashagg.hip) the frame takes for
+               sparse int keys, run on the same columns through its API;
+      hash  -- assume_sparse=True: the reference's structure, GPU ordered_set build pass +
+               fused map_ordinal/BinnerOrdinal pass.
+    Per-kernel milliseconds from HIP events on the library stream."""
     from vaex_amd import _lib
     from vaex_amd.device import DeviceArray
+    from vaex_amd.hashagg import HashAgg
     import vaex_amd
     keys = DeviceArray.random(n, "randint", seed=5, a=5, b=5 + 1_000_000, dtype="int32")
     v = DeviceArray.random(n, "normal", seed=6)
     df = vaex_amd.from_arrays(key=keys, v=v)
     out = {"rows": n, "algorithmic_bytes_per_row": 12}
-    for mode, sparse in (("auto", "auto"), ("hash", True)):
-        df.groupby("key", agg={"v": ["sum", "count"]}, assume_sparse=sparse)  # warm-up
+    names = ["minmax", "tile_sample", "tile_scatter", "tile_scatter_ord", "tile_reduce", "ha_sample",
+             "ha_scatter", "ha_scatter_f64", "ha_reduce", "ha_finish", "set_insert", "set_rank", "bin_fused_global"]
+
+    def run(mode):
+        if mode == "fused":
+            ha = HashAgg(keys.dtype, [v.dtype], [False])
+            ha.update(keys, [v])
+            return len(ha.finish()[0])
+        dfg = df.groupby("key", agg={"v": ["sum", "count"]}, assume_sparse="auto" if mode == "auto" else True)
+        return len(dfg["key"].to_numpy())
+
+    for mode in ("auto", "fused", "hash"):
+        run(mode)  # warm-up
         _lib.synchronize()
         times = []
         for _ in range(max(1, min(3, args.steps))):
+            _lib.timing_reset()
+            _lib.timing_enable(True)
             t0 = time.perf_counter()
-            dfg = df.groupby("key", agg={"v": ["sum", "count"]}, assume_sparse=sparse)
+            groups = run(mode)
             _lib.synchronize()
             times.append(time.perf_counter() - t0)
+            _lib.timing_enable(False)
         t = min(times)
-        out[mode] = {"groups": len(dfg["key"].to_numpy()), "seconds": t, "rows_per_s": n / t,
-                     "algorithmic_GBps": 12 * n / t / 1e9}
+        per = {}
+        for k in names:
+            c, ms = _lib.timing_read(k)
+            if c:
+                per[k] = round(ms, 3)
+        out[mode] = {"groups": groups, "seconds": t, "rows_per_s": n / t, "algorithmic_GBps": 12 * n / t / 1e9,
+                     "kernel_ms_last": per}
     del keys, v, df
     return out
 
