@@ -343,16 +343,30 @@ def bench_groupby(n, args):
 
     for mode in ("auto", "fused", "hash"):
         run(mode)  # warm-up
+        _lib.trace_report()
         _lib.synchronize()
         times = []
+        prof = None
+        if os.environ.get("BENCH_PROFILE_GROUPBY"):
+            import cProfile
+            prof = cProfile.Profile()
         for _ in range(max(1, min(3, args.steps))):
             _lib.timing_reset()
             _lib.timing_enable(True)
+            if prof:
+                prof.enable()
             t0 = time.perf_counter()
             groups = run(mode)
             _lib.synchronize()
             times.append(time.perf_counter() - t0)
+            if prof:
+                prof.disable()
             _lib.timing_enable(False)
+        if prof:
+            import pstats
+            print("groupby mode", mode, [round(x * 1e3, 2) for x in times], file=sys.stderr)
+            print({k: (c, round(t * 1e3, 2)) for k, (c, t) in _lib.trace_report().items()}, file=sys.stderr)
+            pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(12)
         t = min(times)
         per = {}
         for k in names:

@@ -69,6 +69,9 @@ int vh_get_device(int *device);
 int vh_synchronize(void);
 int vh_malloc(void **dptr, uint64_t bytes);
 int vh_free(void *dptr);
+/* page-locked host blocks (cached; result arrays are read back through them) */
+int vh_host_alloc(void **ptr, uint64_t bytes);
+int vh_host_free(void *ptr, uint64_t bytes);
 int vh_memcpy_htod(void *dst, const void *src, uint64_t bytes);
 int vh_memcpy_dtoh(void *dst, const void *src, uint64_t bytes);
 int vh_memcpy_dtod(void *dst, const void *src, uint64_t bytes);

@@ -153,3 +153,64 @@ def test_two_rank_set_merge_and_minmax():
         np.testing.assert_array_equal(got["keys"], ref.key_array(np.float64))
         assert int(got["null_value"]) == ref.null_value and int(got["nan_value"]) == ref.nan_value
         np.testing.assert_array_equal(got["minmax"], [np.nanmin(keys), np.nanmax(keys), 3.0, 4.0])
+
+
+def _groups_worker(rank, world, path):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from oracle import oracle
+    from vaex_amd.distributed import all_ranks_true, combine_groups, shard_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    keys, v, w = _group_data()
+    i1, i2 = shard_range(len(keys), rank, world)
+    # the per-rank fused-groupby result (what HashAgg.finish returns), from the oracle
+    uk, s, c = oracle.groupby_reference(keys[i1:i2], v[i1:i2])
+    counts = np.bincount(np.searchsorted(uk, keys[i1:i2]), minlength=len(uk)).astype(np.int64)
+    wsum = np.zeros(len(uk), np.int64)
+    np.add.at(wsum, np.searchsorted(uk, keys[i1:i2]), w[i1:i2].astype(np.int64))
+    local = (uk.astype(np.int64), counts, [s, wsum], [c, None])
+    gk, gc, gs, gn = combine_groups(local)
+    flags = [all_ranks_true(True), all_ranks_true(rank == 0)]
+    if rank == 0:
+        np.savez(path, keys=gk, counts=gc, s=gs[0], w=gs[1], nn=gn[0], flags=np.array(flags))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _group_data():
+    rng = np.random.default_rng(21)
+    n = 50_001
+    keys = (rng.integers(0, 3000, n) * 7919 - 10 ** 6).astype(np.int64)
+    v = rng.normal(size=n)
+    v[::17] = np.nan
+    w = rng.integers(-5, 6, n).astype(np.int8)
+    return keys, v, w
+
+
+def test_two_rank_fused_groupby_merge():
+    """Per-rank fused-groupby results (keys sorted, counts, float and int sums, non-NaN
+    counts) merged across ranks == the whole-column result; and the all-ranks flag used to
+    keep every rank on the same groupby route."""
+    pytest.importorskip("torch")
+    import sys
+    import torch.multiprocessing as mp
+    sys.path.insert(0, ROOT)
+    from oracle import oracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(32500 + os.getpid() % 1000)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "groups.npz")
+        mp.spawn(_groups_worker, args=(2, path), nprocs=2, join=True)
+        got = np.load(path)
+        keys, v, w = _group_data()
+        uk, s, c = oracle.groupby_reference(keys, v)
+        np.testing.assert_array_equal(got["keys"], uk)
+        np.testing.assert_array_equal(got["counts"], np.bincount(np.searchsorted(uk, keys)))
+        np.testing.assert_array_equal(got["nn"], c)
+        np.testing.assert_allclose(got["s"], s, rtol=1e-12, atol=1e-12)
+        ew = np.zeros(len(uk), np.int64)
+        np.add.at(ew, np.searchsorted(uk, keys), w.astype(np.int64))
+        np.testing.assert_array_equal(got["w"], ew)
+        assert got["flags"].tolist() == [True, False]

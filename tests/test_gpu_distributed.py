@@ -20,7 +20,9 @@ def _data():
     w = rng.random(n)
     x[::997] = np.nan
     key = rng.integers(0, 5000, n).astype(np.int32) * 7 - 300
-    return dict(x=x, y=y, w=w, key=key)
+    # sparse keys (value span >> rows): DataFrame.groupby takes the fused hash path
+    skey = (rng.integers(0, 20000, n).astype(np.int64) * 104729 - 10 ** 9).astype(np.int32)
+    return dict(x=x, y=y, w=w, key=key, skey=skey)
 
 
 def _queries(df):
@@ -36,6 +38,9 @@ def _queries(df):
         out[f"gb_{mode}_key"] = np.asarray(g["key"].to_numpy())
         out[f"gb_{mode}_sum"] = np.asarray(g["v_sum"].to_numpy())
         out[f"gb_{mode}_n"] = np.asarray(g["n"].to_numpy())
+    g = df.groupby("skey", agg={"w": ["sum", "count", "mean"]})
+    for c in g.get_column_names():
+        out[f"gb_fused_{c}"] = np.asarray(g[c].to_numpy())
     return out
 
 
@@ -67,7 +72,7 @@ def test_two_rank_executor_matches_single_process():
         got = dict(np.load(path))
     ref = _queries(vaex_amd.from_arrays(**_data()))
     for k, v in ref.items():
-        if k.endswith("sum") or k == "mean":
+        if k.endswith("sum") or k.endswith("mean") or k == "mean":
             np.testing.assert_allclose(got[k], v, rtol=1e-9, atol=1e-12, err_msg=k)
         else:
             np.testing.assert_array_equal(got[k], v, err_msg=k)

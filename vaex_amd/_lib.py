@@ -29,6 +29,8 @@ SIGNATURES = {
     "vh_synchronize": (_i32, []),
     "vh_malloc": (_i32, [_p(_vp), _u64]),
     "vh_free": (_i32, [_vp]),
+    "vh_host_alloc": (_i32, [_p(_vp), _u64]),
+    "vh_host_free": (_i32, [_vp, _u64]),
     "vh_memcpy_htod": (_i32, [_vp, _vp, _u64]),
     "vh_memcpy_dtoh": (_i32, [_vp, _vp, _u64]),
     "vh_memcpy_dtod": (_i32, [_vp, _vp, _u64]),
@@ -110,8 +112,30 @@ def check(rc):
         raise HipError(msg)
 
 
+_TRACE = {} if os.environ.get("VAEX_AMD_TRACE_CALLS") else None
+
+
 def call(name, *args):
-    check(getattr(lib(), name)(*args))
+    if _TRACE is None:
+        check(getattr(lib(), name)(*args))
+        return
+    import time
+    t0 = time.perf_counter()
+    try:
+        check(getattr(lib(), name)(*args))
+    finally:
+        n, tot = _TRACE.get(name, (0, 0.0))
+        _TRACE[name] = (n + 1, tot + time.perf_counter() - t0)
+
+
+def trace_report(reset=True):
+    """{C-ABI function: (calls, seconds)} since the last report (VAEX_AMD_TRACE_CALLS=1)."""
+    if _TRACE is None:
+        return {}
+    out = dict(_TRACE)
+    if reset:
+        _TRACE.clear()
+    return out
 
 
 def dtype_code(dtype):
@@ -151,3 +175,26 @@ def timing_read(kernel):
     n, ms = ctypes.c_uint64(), ctypes.c_double()
     call("vh_timing_read", kernel.encode(), ctypes.byref(n), ctypes.byref(ms))
     return n.value, ms.value
+
+
+class _PinnedBlock:
+    """A page-locked host block (vh_host_alloc) that numpy arrays view; returned to the
+    library's block cache when the last array over it is gone."""
+
+    def __init__(self, n, dtype):
+        dtype = np.dtype(dtype)
+        self.nbytes = max(1, n * dtype.itemsize)
+        p = ctypes.c_void_p()
+        check(lib().vh_host_alloc(ctypes.byref(p), self.nbytes))
+        self.ptr = p.value
+        self.__array_interface__ = {"shape": (n,), "typestr": dtype.str, "data": (self.ptr, False), "version": 3}
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            lib().vh_host_free(self.ptr, self.nbytes)
+            self.ptr = None
+
+
+def pinned_empty(n, dtype):
+    """1-d numpy array of n items in page-locked memory (fast D2H read-back target)."""
+    return np.asarray(_PinnedBlock(int(n), dtype))

@@ -510,10 +510,6 @@ __device__ inline void ha_commit(const HaScatterLds &l, const HaParams &hp, cons
         const uint32_t dest = (uint32_t)(pk >> 32);
         const bool ok = k < tot && !(dest & HA_DEST_OVERFLOW);
         const uint64_t e = ok ? region0 + dest : dummy;
-        if (hp.debug & 1) {
-            asm volatile("" :: "v"(e), "v"(pk));
-            continue;
-        }
         if constexpr (NV == 1) {  // packed {key, 0, value}: one 16-byte store per row
             const uint64_t vbits = l.sv[k];
             reinterpret_cast<uint4 *>(hp.ent)[e] = make_uint4((uint32_t)pk, 0u, (uint32_t)vbits, (uint32_t)(vbits >> 32));
@@ -643,20 +639,11 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_f64(HaParams hp, HaTa
                 for (int v = 0; v < NV; v++)
                     vb[r][v] = __builtin_bit_cast(uint64_t, (j & 1) ? cur.v[q][v][j >> 1].y : cur.v[q][v][j >> 1].x);
                 bkt[r] = ha_bucket(hp, kb[r]);
-                if (hp.debug & 4) {
-                    rank[r] = valid ? (int32_t)(bkt[r] & 7) : -1;
-                } else {
-                    const uint32_t rk = atomicAdd(&l.hist[valid ? bkt[r] : hp.P], 1u);
-                    rank[r] = valid ? (int32_t)rk : -1;
-                }
+                const uint32_t rk = atomicAdd(&l.hist[valid ? bkt[r] : hp.P], 1u);
+                rank[r] = valid ? (int32_t)rk : -1;
             }
         }
-        if (hp.debug & 2) {
-#pragma unroll
-            for (int r = 0; r < HA_RPT; r++) asm volatile("" :: "v"(rank[r]), "v"(vb[r][0]));
-        } else {
-            ha_commit<NV>(l, hp, g, region0, bkt, kb, rank, vb);
-        }
+        ha_commit<NV>(l, hp, g, region0, bkt, kb, rank, vb);
         cur = nxt;
     }
     for (uint32_t t = threadIdx.x; t < hp.P; t += HA_THREADS)
@@ -862,12 +849,22 @@ template <int NV> __global__ __launch_bounds__(256) void k_ha_rehash(HaTable src
 
 __global__ __launch_bounds__(256) void k_ha_compact(const uint64_t *keys, uint64_t slots, int is_signed,
                                                     uint32_t *skey, uint32_t *sslot, uint32_t *counter) {
-    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < slots; i += (uint64_t)gridDim.x * 256) {
-        const uint64_t k = keys[i];
-        if (k == SET_EMPTY) continue;
-        const uint32_t j = atomicAdd(counter, 1u);
-        skey[j] = is_signed ? ((uint32_t)k ^ 0x80000000u) : (uint32_t)k;
-        sslot[j] = (uint32_t)i;
+    // one counter add per wave (ballot + popcount), not per occupied slot
+    const int lane = threadIdx.x & 63;
+    const uint64_t step = (uint64_t)gridDim.x * 256;
+    for (uint64_t i0 = blockIdx.x * 256ull; i0 < slots; i0 += step) {
+        const uint64_t i = i0 + threadIdx.x;
+        const uint64_t k = i < slots ? keys[i] : SET_EMPTY;
+        const bool occ = k != SET_EMPTY;
+        const uint64_t m = __ballot(occ);
+        uint32_t base = 0;
+        if (lane == 0 && m) base = atomicAdd(counter, (uint32_t)__popcll(m));
+        base = __shfl(base, 0, 64);
+        if (occ) {
+            const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+            skey[j] = is_signed ? ((uint32_t)k ^ 0x80000000u) : (uint32_t)k;
+            sslot[j] = (uint32_t)i;
+        }
     }
 }
 

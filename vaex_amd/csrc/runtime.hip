@@ -94,6 +94,19 @@ void dev_free(void *ptr, uint64_t bytes) {
     (void)hipFree(ptr);
 }
 
+// ---- pinned host block cache (vh_host_alloc / vh_host_free) ---------------------------
+// Result arrays (grids, groupby columns) are read back through page-locked blocks: a
+// pageable D2H runs at ~5-10 GB/s, page-locked at PCIe/xGMI rate, and hipHostMalloc itself
+// is slow, so freed blocks are kept (sizes rounded to 64 KiB, <= 1 GiB cached).
+namespace {
+constexpr uint64_t HCACHE_MAX_BYTES = 1ull << 30;
+std::mutex g_hcache_mu;
+std::multimap<uint64_t, void *> g_hcache;
+uint64_t g_hcached = 0;
+}  // namespace
+
+static uint64_t host_round(uint64_t bytes) { return (std::max<uint64_t>(bytes, 1) + 65535) & ~uint64_t(65535); }
+
 hipStream_t stream() {
     int d = current_device();
     std::lock_guard<std::mutex> lk(g_mu);
@@ -372,6 +385,45 @@ int vh_free(void *dptr) {
     VH_API_BEGIN
     VH_HIP(hipStreamSynchronize(stream()));
     VH_HIP(hipFree(dptr));
+    VH_API_END
+}
+
+int vh_host_alloc(void **ptr, uint64_t bytes) {
+    VH_API_BEGIN
+    const uint64_t b = host_round(bytes);
+    {
+        std::lock_guard<std::mutex> lk(g_hcache_mu);
+        auto it = g_hcache.find(b);
+        if (it != g_hcache.end()) {
+            *ptr = it->second;
+            g_hcache.erase(it);
+            g_hcached -= b;
+            return VH_OK;
+        }
+    }
+    void *p = nullptr;
+    hipError_t e = hipHostMalloc(&p, b, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        fail(VH_ERR_NOMEM, "hipHostMalloc of " + std::to_string(b) + " bytes failed");
+    }
+    *ptr = p;
+    VH_API_END
+}
+
+int vh_host_free(void *ptr, uint64_t bytes) {
+    VH_API_BEGIN
+    if (!ptr) return VH_OK;
+    const uint64_t b = host_round(bytes);
+    {
+        std::lock_guard<std::mutex> lk(g_hcache_mu);
+        if (g_hcached + b <= HCACHE_MAX_BYTES) {
+            g_hcache.emplace(b, ptr);
+            g_hcached += b;
+            return VH_OK;
+        }
+    }
+    VH_HIP(hipHostFree(ptr));
     VH_API_END
 }
 

@@ -211,6 +211,58 @@ class ExecutorDistributed(ExecutorLocal):
                 p.set = combine_sets(p.set, group=self.group)
 
 
+def all_ranks_true(flag, group=None):
+    """Logical AND of a per-rank flag (a MIN all-reduce)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32)
+    if dist.get_backend(group) == "nccl":
+        t = t.cuda()
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
+
+
+def merge_groups(parts):
+    """Merge per-rank fused-groupby results ``(keys, counts, sums, nonnull)`` (each sorted by
+    key, hashagg.py) into one key-sorted result: counts and integer sums add exactly, float
+    sums add in rank order.  ``nonnull`` entries may be None (not requested)."""
+    parts = [p for p in parts if len(p[0])]
+    if not parts:
+        return None
+    nv = len(parts[0][2])
+    keys = np.concatenate([p[0] for p in parts])
+    uniq, inv = np.unique(keys, return_inverse=True)
+    m = len(uniq)
+    counts = np.zeros(m, np.int64)
+    np.add.at(counts, inv, np.concatenate([p[1] for p in parts]))
+    sums, nonnull = [], []
+    for v in range(nv):
+        cat = np.concatenate([p[2][v] for p in parts])
+        out = np.zeros(m, cat.dtype)
+        np.add.at(out, inv, cat)
+        sums.append(out)
+        if parts[0][3][v] is None:
+            nonnull.append(None)
+        else:
+            nn = np.zeros(m, np.int64)
+            np.add.at(nn, inv, np.concatenate([p[3][v] for p in parts]))
+            nonnull.append(nn)
+    return uniq, counts, sums, nonnull
+
+
+def combine_groups(local, group=None):
+    """All-gather every rank's fused-groupby result and merge (:func:`merge_groups`)."""
+    import torch.distributed as dist
+    keys, counts, sums, nonnull = local
+    payload = (np.asarray(keys), np.asarray(counts), [np.asarray(s) for s in sums],
+               [None if c is None else np.asarray(c) for c in nonnull])
+    world = dist.get_world_size(group)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, payload, group=group)
+    merged = merge_groups(gathered)
+    return local if merged is None else merged
+
+
 def combine_sets(local_set, group=None):
     """Replace a rank's ordered set by the global one (all-gather of key arrays)."""
     import torch.distributed as dist

@@ -90,13 +90,22 @@ class GrouperDense(BinnerBase):
         self.min_value = int(vmin)
         self.N = int(vmax) - int(vmin) + 1
         dtype = self.df.data_type(self.expression)
-        self.bin_values = np.arange(int(vmin), int(vmax) + 1, dtype=np.int64)
-        if len(self.bin_values):
-            lo, hi = int(self.bin_values[0]), int(self.bin_values[-1])
-            self.bin_values = self.bin_values.astype(required_dtype_for_max(max(abs(lo), abs(hi))))
+        self.value_dtype = required_dtype_for_max(max(abs(int(vmin)), abs(int(vmax))))
+        self._bin_values = None
         self.sort_indices = None
         self.binner = self.df._binner_ordinal(self.expression, self.N, self.min_value)
         self.key_dtype = dtype
+
+    @property
+    def bin_values(self):
+        """min_value .. max (built on demand: a single-key groupby only needs the occupied ones)."""
+        if self._bin_values is None:
+            self._bin_values = np.arange(self.min_value, self.min_value + self.N, dtype=np.int64).astype(self.value_dtype)
+        return self._bin_values
+
+    def occupied_values(self, mask):
+        """Labels of the cells where mask is set (mask over the N central cells)."""
+        return (np.flatnonzero(mask) + self.min_value).astype(self.value_dtype)
 
     def labels(self):
         return self.bin_values.tolist()
@@ -244,7 +253,10 @@ class GroupBy(GroupByBase):
                 if groups > self.row_limit:  # what the set build of Grouper raises (groupby.py:125)
                     raise RowLimitException(f"Resulting grouper has {groups:,} unique combinations, which is "
                                             f"larger than the allowed row limit of {self.row_limit:,}")
-            coords = [c[mask] for c in np.meshgrid(*[np.asarray(b.bin_values) for b in self.by], indexing="ij")]
+            if len(self.by) == 1 and isinstance(self.by[0], GrouperDense):
+                coords = [self.by[0].occupied_values(mask)]
+            else:
+                coords = [c[mask] for c in np.meshgrid(*[np.asarray(b.bin_values) for b in self.by], indexing="ij")]
             for b, coord in zip(self.by, coords):
                 columns[b.label] = coord
             for k, v in arrays.items():

@@ -37,6 +37,7 @@ class HashAgg:
         codes = (ctypes.c_int * max(1, len(self.value_dtypes)))(*[_lib.dtype_code(d)[0] for d in self.value_dtypes])
         if nonnull is None:
             nonnull = [True] * len(self.value_dtypes)
+        self.nonnull = list(nonnull)
         nnmask = sum(1 << i for i, want in enumerate(nonnull) if want)
         h = ctypes.c_void_p()
         _lib.call("vh_hashagg_create", kcode, len(self.value_dtypes), codes, nnmask, ctypes.byref(h))
@@ -77,14 +78,15 @@ class HashAgg:
         m = ctypes.c_uint64()
         _lib.call("vh_hashagg_finish", self._h, ctypes.byref(m))
         m = m.value
-        keys = np.empty(m, np.int64)
-        counts = np.empty(m, np.int64)
-        sums = [np.empty(m, np.float64 if d.kind == "f" else (np.int64 if d.kind == "i" else np.uint64))
+        # page-locked result columns: the read-back is one fast DMA per column
+        keys = _lib.pinned_empty(m, np.int64)
+        counts = _lib.pinned_empty(m, np.int64)
+        sums = [_lib.pinned_empty(m, np.float64 if d.kind == "f" else (np.int64 if d.kind == "i" else np.uint64))
                 for d in self.value_dtypes]
-        nonnull = [np.empty(m, np.int64) for _ in self.value_dtypes]
+        nonnull = [_lib.pinned_empty(m, np.int64) if want else None for want in self.nonnull]
         nv = max(1, len(self.value_dtypes))
         sp = (ctypes.c_void_p * nv)(*[s.ctypes.data for s in sums])
-        npp = (ctypes.c_void_p * nv)(*[c.ctypes.data for c in nonnull])
+        npp = (ctypes.c_void_p * nv)(*[c.ctypes.data if c is not None else None for c in nonnull])
         if m:
             _lib.call("vh_hashagg_read", self._h, keys.ctypes.data, counts.ctypes.data, sp, npp)
         return keys, counts, sums, nonnull
@@ -158,11 +160,27 @@ def try_groupby(df, by, actions, parse, sort=False, row_limit=None):
     values = [df.columns[v] for v in value_names]
     nonnull = [any(op in ("nonnull", "mean") and vi == i for _, op, vi in ops) for i in range(len(values))]
     ha = HashAgg(key.dtype, [v.dtype for v in values], nonnull)
+    # the executor's row range (a distributed executor: this rank's shard) in its chunks
+    executor = df.executor
+    start, end = executor.row_range(df)
+    chunk = max(1, executor.chunk_size_for(df))
+    ok = True
     try:
-        ha.update(key, values)
+        for i1 in range(start, end, chunk):
+            i2 = min(end, i1 + chunk)
+            ha.update(key[i1:i2], [v[i1:i2] for v in values])
     except HashAggOverflow:
+        ok = False
+    distributed = getattr(executor, "world", 1) > 1
+    if distributed:  # every rank takes the same route, or the collectives below would hang
+        from .distributed import all_ranks_true
+        ok = all_ranks_true(ok, group=executor.group)
+    if not ok:
         return None
     keys, counts, sums, nonnull = ha.finish()
+    if distributed:  # ExecutorDistributed: merge the ranks' groups
+        from .distributed import combine_groups
+        keys, counts, sums, nonnull = combine_groups((keys, counts, sums, nonnull), group=executor.group)
     if row_limit is not None and len(keys) > row_limit:
         raise RowLimitException(f"Resulting grouper has {len(keys):,} unique combinations, which is larger "
                                 f"than the allowed row limit of {row_limit:,}")

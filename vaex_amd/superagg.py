@@ -273,7 +273,7 @@ class Aggregator:
     # ---- host image / device coherence --------------------------------------
     def _ensure_host(self):
         if self._host is None:
-            self._host = np.empty(self._grid.length1d, self._grid_dtype)
+            self._host = _lib.pinned_empty(self._grid.length1d, self._grid_dtype)
             self._device_newer = True
         if self._device_newer:
             _lib.call("vh_agg_download", self._handle, self._host.ctypes.data, self._nbytes)
