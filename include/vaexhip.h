@@ -166,8 +166,8 @@ int vh_minmax(const void *data, uint64_t n, int dtype, int flip_endian, const ui
               double *out_min, double *out_max);
 
 /* ---- fused hash groupby (hashagg.hip) ------------------------------------
- * groupby(key).agg({count(*), count(v), sum(v), mean(v)}) for one integer key column of
- * <= 4 bytes and up to 2 value columns, in one hash-partitioned pass.  Replaces, for that
+ * groupby(key).agg({count(*), count(v), sum(v), mean(v)}) for one integer key column
+ * (any width) and up to 2 value columns, in one hash-partitioned pass.  Replaces, for that
  * query shape, Grouper pass 1 (ordered_set update, hash_primitives.hpp:96-281) +
  * _ordinal_values/map_ordinal (hash_primitives.hpp:543-583) + BinnerOrdinal
  * (superagg_binners.cpp:104-142) + AggCount/AggSum (superagg.cpp:155-192,349-389), as
@@ -184,6 +184,11 @@ int vh_hashagg_finish(vh_hashagg *h, uint64_t *ngroups);
 /* host outputs, ngroups items each: keys as int64, count(*) int64, per value column its sum
  * (8 bytes: double for float columns, int64/uint64 for integers) and non-NaN count int64 */
 int vh_hashagg_read(vh_hashagg *h, int64_t *keys, int64_t *counts, void *const *sums, int64_t *const *nonnull);
+/* combined int64 key of a multi-key groupby, out[i] = sum_j (cols[j][i] - mins[j]) * mults[j]
+ * (the cartesian ordinal of groupby.py:248-288 _combine, first key most significant);
+ * HBM columns and output, up to 8 integer key columns */
+int vh_combine_keys(uint64_t n, int nkeys, const void *const *cols, const int *dtypes, const int64_t *mins,
+                    const int64_t *mults, int64_t *out);
 
 #ifdef __cplusplus
 }

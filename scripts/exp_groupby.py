@@ -12,7 +12,7 @@ from vaex_amd.device import DeviceArray  # noqa: E402
 mode = sys.argv[1]
 n = int(float(sys.argv[2])) if len(sys.argv) > 2 else 10 ** 9
 card = int(float(sys.argv[3])) if len(sys.argv) > 3 else 10 ** 6
-keys = DeviceArray.random(n, "randint", seed=5, a=5, b=5 + card, dtype="int32")
+keys = DeviceArray.random(n, "randint", seed=5, a=5, b=5 + card, dtype=os.environ.get("KEYDT", "int32"))
 v = DeviceArray.random(n, "normal", seed=6)
 df = vaex_amd.from_arrays(key=keys, v=v)
 sparse = {"auto": "auto", "hash": True, "fused": None}[mode]

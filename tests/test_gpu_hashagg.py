@@ -42,16 +42,19 @@ def _run(keys, vals, chunks=1, device=False):
 
 def _check(keys, vals, out):
     gk, cnt, sums, nn = out
-    uniq, first_inv = np.unique(keys.astype(np.int64), return_inverse=True)
+    # sorted in the key's own order (uint64 keys above 2**63 sort last)
+    uniq, first_inv = np.unique(keys, return_inverse=True)
+    ordinal = first_inv.astype(np.int64)
+    assert gk.dtype == (np.uint64 if keys.dtype == np.uint64 else np.int64)
     np.testing.assert_array_equal(gk, uniq)
     np.testing.assert_array_equal(cnt, np.bincount(first_inv, minlength=len(uniq)))
     for v, s, c in zip(vals, sums, nn):
         if v.dtype.kind == "f":
-            uk, es, ec = oracle.groupby_reference(keys.astype(np.int64), v.astype(np.float64))
+            uk, es, ec = oracle.groupby_reference(ordinal, v.astype(np.float64))
             np.testing.assert_array_equal(c, ec)
             np.testing.assert_allclose(s, es, rtol=1e-6, atol=1e-9)
         else:
-            np.testing.assert_array_equal(s, _expected_int_sums(keys.astype(np.int64), v, uniq))
+            np.testing.assert_array_equal(s, _expected_int_sums(ordinal, v, np.arange(len(uniq))))
             np.testing.assert_array_equal(c, np.bincount(first_inv, minlength=len(uniq)))
 
 
@@ -60,13 +63,22 @@ def _keys(dtype, n, card, rng):
     info = np.iinfo(dt)
     span = min(card, int(info.max) - int(info.min) + 1)
     lo = int(info.min) if dt.kind == "i" else 0
-    k = (lo + rng.integers(0, span, n)).astype(dt)
-    # the LDS table's sentinel patterns (0xFFFFFFFF / 0xFFFFFFFE as int32 bits) and extremes
-    k[:4] = np.array([-1, -2, info.min, info.max] if dt.kind == "i" else [info.max, info.max - 1, 0, 1], dtype=np.int64).astype(dt)
+    if dt.itemsize == 8:
+        # 64-bit keys: a sparse spread over the whole range (the hash, not the span, matters)
+        pool = rng.integers(np.iinfo(np.int64).min, np.iinfo(np.int64).max, card, dtype=np.int64, endpoint=True)
+        k = pool[rng.integers(0, card, n)].view(dt)
+    else:
+        k = (lo + rng.integers(0, span, n)).astype(dt)
+    # the table sentinels (all-ones / all-ones - 1 key bits, the HBM table's side slot for
+    # 64-bit keys) and extremes
+    if dt.kind == "i":
+        k[:4] = np.array([-1, -2, info.min, info.max], dtype=np.int64).astype(dt)
+    else:
+        k[:4] = np.array([info.max, info.max - 1, 0, 1], dtype=np.uint64).astype(dt)
     return k
 
 
-@pytest.mark.parametrize("kdtype", ["int8", "int16", "int32", "uint8", "uint16", "uint32"])
+@pytest.mark.parametrize("kdtype", ["int8", "int16", "int32", "int64", "uint8", "uint16", "uint32", "uint64"])
 @pytest.mark.parametrize("card", [3, 200, 60000])
 def test_key_dtypes(kdtype, card):
     rng = np.random.default_rng(card)
@@ -220,3 +232,55 @@ def test_dense_int32_keys_take_fast_ordinal_tile_path(n):
     fk, fc, fs, fn = _run(keys, [v])
     np.testing.assert_array_equal(fk, uk)
     np.testing.assert_allclose(fs[0], s, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("n,card", [(3_000_000, 1_000_000), (600_000, 3)])
+@pytest.mark.parametrize("kdtype", ["int64", "uint64"])
+def test_64bit_keys_partitioned_and_chunked(kdtype, n, card):
+    """64-bit keys through the partitioned path (many buckets), chunked device updates, the
+    all-ones key in the HBM table's side slot in every chunk."""
+    rng = np.random.default_rng(card + 1)
+    keys = _keys(kdtype, n, card, rng)
+    keys[n // 2] = keys[0]
+    v = rng.normal(size=n)
+    w = rng.integers(-5, 5, n).astype(np.int32)
+    _check(keys, [v, w], _run(keys, [v, w], chunks=3, device=True))
+
+
+def test_64bit_keys_that_collide_in_low_bits():
+    """Keys equal in their low 32 bits (and in their high 32 bits) stay distinct groups."""
+    lo = np.arange(1000, dtype=np.int64)
+    keys = np.concatenate([lo, lo + (1 << 32), lo + (7 << 40), (lo << 32) | 5, lo]).astype(np.int64)
+    rng = np.random.default_rng(3)
+    keys = keys[rng.permutation(len(keys))]
+    v = rng.normal(size=len(keys))
+    _check(keys, [v], _run(keys, [v]))
+
+
+@pytest.mark.parametrize("dtypes", [["int32", "int8"], ["uint16", "int64", "int32"], ["uint32", "uint32"]])
+def test_combine_keys(dtypes):
+    """vh_combine_keys = the cartesian ordinal of groupby.py:248-288 (first key most
+    significant), bit-exact against numpy."""
+    import ctypes
+    from vaex_amd import _lib
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(len(dtypes))
+    n = 1_000_003
+    cols = []
+    for d in dtypes:
+        info = np.iinfo(d)
+        lo = max(int(info.min), -1000)
+        cols.append(rng.integers(lo, lo + 700, n).astype(d))
+    mins = [int(c.min()) for c in cols]
+    spans = [int(c.max()) - m + 1 for c, m in zip(cols, mins)]
+    mults = [int(np.prod(spans[i + 1:], dtype=np.int64)) for i in range(len(cols))]
+    expect = np.zeros(n, np.int64)
+    for c, m, k in zip(cols, mins, mults):
+        expect += (c.astype(np.int64) - m) * k
+    dcols = [DeviceArray.from_numpy(c) for c in cols]
+    out = DeviceArray.empty(n, np.int64)
+    k = len(cols)
+    _lib.call("vh_combine_keys", n, k, (ctypes.c_void_p * k)(*[c.ptr for c in dcols]),
+              (ctypes.c_int * k)(*[_lib.dtype_code(np.dtype(d))[0] for d in dtypes]),
+              (ctypes.c_int64 * k)(*mins), (ctypes.c_int64 * k)(*mults), out.ptr)
+    np.testing.assert_array_equal(out.to_numpy(), expect)

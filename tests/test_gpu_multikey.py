@@ -1,0 +1,158 @@
+"""Multi-key groupby (groupby.py:248-333 ``_combine`` / ``combine='auto'``): the keys are
+combined on the GPU into one int64 cartesian ordinal (``vh_combine_keys``) and take the
+single-key routes (dense grid, fused hash pass, set grouper for other aggregators), or,
+with >= 10 rows per cell, the cartesian grid of dense groupers.
+
+The checker is numpy: ``np.unique`` over the row tuples gives the groups in lexicographic
+order (the reference's ``sort=True`` order), ``np.bincount`` the counts and sums.  Counts,
+labels and integer sums are bit-exact; float sums within 1e-6 relative (north_star)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _expected(keys, v):
+    tup = np.stack([k.astype(np.int64) for k in keys], axis=1)
+    uniq, inv = np.unique(tup, axis=0, return_inverse=True)
+    inv = inv.ravel()
+    ok = ~np.isnan(v)
+    return (uniq, np.bincount(inv, minlength=len(uniq)),
+            np.bincount(inv[ok], weights=v[ok], minlength=len(uniq)),
+            np.bincount(inv[ok], minlength=len(uniq)), inv)
+
+
+def _frame(keys, v, device):
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    cols = {f"k{i}": k for i, k in enumerate(keys)}
+    cols["v"] = v
+    if device:
+        cols = {name: DeviceArray.from_numpy(c) for name, c in cols.items()}
+    return vaex_amd.from_arrays(**cols)
+
+
+def _check(keys, v, res, sort_result=False):
+    uniq, cnt, s, nn, _ = _expected(keys, v)
+    names = [f"k{i}" for i in range(len(keys))]
+    got = [res[n].to_numpy() for n in names]
+    order = np.lexsort(got[::-1]) if sort_result else np.arange(len(got[0]))
+    for j, g in enumerate(got):
+        np.testing.assert_array_equal(g[order].astype(np.int64), uniq[:, j])
+    np.testing.assert_array_equal(res["n"].to_numpy()[order], cnt)
+    np.testing.assert_array_equal(res["v_count"].to_numpy()[order], nn)
+    np.testing.assert_allclose(res["v_sum"].to_numpy()[order], s, rtol=1e-6, atol=1e-9)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        np.testing.assert_allclose(res["v_mean"].to_numpy()[order], s / nn, rtol=1e-6, atol=1e-9)
+
+
+def _agg():
+    import vaex_amd
+    return {"n": "count", "v_sum": vaex_amd.agg.sum("v"), "v_count": vaex_amd.agg.count("v"),
+            "v_mean": vaex_amd.agg.mean("v")}
+
+
+def _spy(monkeypatch):
+    from vaex_amd import _lib
+    calls = []
+    orig = _lib.call
+    monkeypatch.setattr(_lib, "call", lambda name, *a: (calls.append(name), orig(name, *a))[1])
+    return calls
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_sparse_keys_combine_into_fused_hash(monkeypatch, device):
+    """Two int32 keys whose cartesian span (1e10) is far beyond the rows: combined key,
+    fused hash pass; groups in lexicographic key order."""
+    rng = np.random.default_rng(1)
+    n = 1_000_000
+    k0 = (rng.integers(-50_000, 50_000, n)).astype(np.int32)
+    k1 = (rng.integers(0, 3, n) * 40_000 + 7).astype(np.int32)
+    v = rng.normal(size=n)
+    v[::41] = np.nan
+    df = _frame([k0, k1], v, device)
+    calls = _spy(monkeypatch)
+    res = df.groupby(["k0", "k1"], agg=_agg())
+    assert "vh_combine_keys" in calls and "vh_hashagg_create" in calls
+    assert res.get_column_names()[:2] == ["k0", "k1"]
+    _check([k0, k1], v, res)
+
+
+def test_combined_dense_range_takes_grid_path(monkeypatch):
+    """Spans 300 x 400 with 100k rows: occupancy < 10 -> combined, and the combined range
+    (120000 <= 4 n) bins as a dense BinnerOrdinal grid."""
+    rng = np.random.default_rng(2)
+    n = 100_000
+    k0 = rng.integers(-150, 150, n).astype(np.int16)
+    k1 = rng.integers(1000, 1400, n).astype(np.uint32)
+    v = rng.normal(size=n)
+    df = _frame([k0, k1], v, True)
+    calls = _spy(monkeypatch)
+    res = df.groupby(["k0", "k1"], agg=_agg())
+    assert "vh_combine_keys" in calls and "vh_hashagg_create" not in calls
+    _check([k0, k1], v, res)
+    assert res["k0"].to_numpy().dtype == np.int16 and res["k1"].to_numpy().dtype == np.uint32
+
+
+def test_high_occupancy_keeps_cartesian_grid(monkeypatch):
+    """10 x 20 cells over 100k rows: >= 10 rows per cell, no combine (groupby.py:329-333)."""
+    rng = np.random.default_rng(3)
+    n = 100_000
+    k0 = rng.integers(0, 10, n).astype(np.int8)
+    k1 = rng.integers(-10, 10, n).astype(np.int64)
+    v = rng.normal(size=n)
+    df = _frame([k0, k1], v, False)
+    calls = _spy(monkeypatch)
+    res = df.groupby(["k0", "k1"], agg=_agg())
+    assert "vh_combine_keys" not in calls
+    _check([k0, k1], v, res)
+
+
+def test_three_keys_mixed_dtypes_other_aggregators():
+    """min / max are not fused aggregators: the combined key goes through the set grouper;
+    compared against numpy per group.  Result order: lexicographic after sorting."""
+    rng = np.random.default_rng(4)
+    n = 300_000
+    k0 = rng.integers(0, 60_000, n).astype(np.uint16)
+    k1 = (rng.integers(-5, 5, n) * 10 ** 9).astype(np.int64)
+    k2 = rng.integers(-100, 100, n).astype(np.int8)
+    v = rng.normal(size=n)
+    import vaex_amd
+    df = _frame([k0, k1, k2], v, True)
+    res = df.groupby(["k0", "k1", "k2"], agg={"lo": vaex_amd.agg.min("v"), "hi": vaex_amd.agg.max("v"),
+                                              "n": "count"})
+    uniq, cnt, _, _, inv = _expected([k0, k1, k2], v)
+    got = [res[c].to_numpy() for c in ("k0", "k1", "k2")]
+    order = np.lexsort(got[::-1])
+    for j, g in enumerate(got):
+        np.testing.assert_array_equal(g[order].astype(np.int64), uniq[:, j])
+    np.testing.assert_array_equal(res["n"].to_numpy()[order], cnt)
+    lo = np.full(len(uniq), np.inf)
+    hi = np.full(len(uniq), -np.inf)
+    np.minimum.at(lo, inv, v)
+    np.maximum.at(hi, inv, v)
+    np.testing.assert_array_equal(res["lo"].to_numpy()[order], lo)
+    np.testing.assert_array_equal(res["hi"].to_numpy()[order], hi)
+
+
+def test_same_frame_as_uncombined_path():
+    """Same groups, values and label dtypes as assume_sparse=True (per-key set groupers +
+    cartesian grid, filtered by count > 0)."""
+    rng = np.random.default_rng(5)
+    n = 200_000
+    k0 = rng.integers(0, 700, n).astype(np.int32)
+    k1 = rng.integers(-3000, 3000, n).astype(np.int32)
+    v = rng.normal(size=n)
+    df = _frame([k0, k1], v, True)
+    a = df.groupby(["k0", "k1"], agg=_agg())
+    b = df.groupby(["k0", "k1"], agg=_agg(), assume_sparse=True)
+    assert a.get_column_names() == b.get_column_names()
+    oa = np.lexsort([a["k1"].to_numpy(), a["k0"].to_numpy()])
+    ob = np.lexsort([b["k1"].to_numpy(), b["k0"].to_numpy()])
+    for c in a.get_column_names():
+        x, y = a[c].to_numpy()[oa], b[c].to_numpy()[ob]
+        assert x.dtype == y.dtype, c
+        if x.dtype.kind == "f":
+            np.testing.assert_allclose(x, y, rtol=1e-6, atol=1e-9)
+        else:
+            np.testing.assert_array_equal(x, y)

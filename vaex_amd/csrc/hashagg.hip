@@ -1,5 +1,6 @@
 // Fused hash groupby: df.groupby(key).agg({count, sum, mean}) for one integer key column
-// (<= 4-byte keys) and up to two value columns, in one pass over the data.
+// (1-, 2-, 4- or 8-byte keys; a multi-key groupby first combines its keys into one int64,
+// groupby.py:248-288) and up to two value columns, in one pass over the data.
 //
 // The reference runs the groupby as two passes: pass 1 builds the ordered_set of the key
 // (hash_primitives.hpp:96-281, via Grouper, groupby.py:97-168), pass 2 maps every row to
@@ -10,22 +11,27 @@
 //
 //   sample -- ~1 M evenly spaced rows: per fine bucket (top 12 bits of the key hash) row
 //             counts, and the sample's distinct keys in a small HBM table -> Chao1
-//             estimate of the key count -> P = 2^p buckets of <= ~1800 keys each.
+//             estimate of the key count -> P = 2^p buckets of <= ~2300 keys each.
 //   pass A -- workgroup w owns a row range; per 4096-row batch it hashes the keys
-//             (murmur3 fmix32), ranks rows per bucket in LDS, counting-sorts (key, value
-//             bits) by bucket through LDS and streams the runs to per-(w, bucket) regions
-//             (the tile-partition scheme of tiled.hip with buckets for tiles).
+//             (murmur3 fmix32 / splitmix64 finaliser), ranks rows per bucket in LDS,
+//             counting-sorts (key, value bits) by bucket through LDS and streams the runs
+//             to per-(w, bucket) regions (the tile-partition scheme of tiled.hip with
+//             buckets for tiles).
 //   pass B -- work unit = (bucket, range of pass-A workgroups): the unit's entries are
-//             aggregated in an LDS open-address table (linear probing, CAS insert,
-//             ds_add_u32 / ds_add_f64 / ds_add_u64), then merged into one HBM
-//             open-address table with global atomics (one merge per distinct key per
-//             unit, not per row).
+//             aggregated in an LDS open-address table (4-slot groups, CAS insert,
+//             ds_add_u64 / ds_add_f64), then merged into one HBM open-address table with
+//             global atomics (one merge per distinct key per unit, not per row).
 //   finish -- occupied HBM slots are compacted, radix-sorted by key (rocPRIM) and
 //             gathered: groups come out sorted by key (a valid sort=False order -- the
 //             reference's is hash/thread dependent -- and exactly the sort=True order).
 //
 // With P == 1 (few keys) pass A is skipped: every workgroup aggregates its row range of
 // the raw columns straight into its LDS table ("direct").
+//
+// Key bits KB: uint32_t for keys of <= 4 bytes (the value as int32 / uint32), uint64_t for
+// 8-byte keys.  The two all-ones patterns of KB mark EMPTY / CLOSED LDS slots; keys with
+// those bits (e.g. -1, -2) live in two side records.  The HBM table stores keys as uint64
+// (EMPTY = all ones); an 8-byte key with that pattern lives in a side slot after the table.
 //
 // Overflow, never wrong results: an LDS table that reaches max_used distinct keys is
 // closed -- a key not yet in it is aggregated straight into the HBM table.  The decision
@@ -50,19 +56,15 @@
 namespace vh {
 
 constexpr int HA_MAX_V = 2;
-#ifndef VH_HA_THREADS
-#define VH_HA_THREADS 512
-#endif
-constexpr int HA_THREADS = VH_HA_THREADS;  // pass A
+constexpr int HA_THREADS = 512;            // pass A
 constexpr int HA_RPT = 8;
 constexpr int HA_BATCH = HA_THREADS * HA_RPT;
 constexpr int HB_THREADS = 1024;           // pass B / direct
-constexpr int HB_VU = 2;                   // 4-entry chunks per lane per step
+constexpr int HB_M = 8;                    // entries per lane per pass-B step
 constexpr uint32_t LT_SLOTS_LOG2 = 12;     // LDS table: 4096 slots (+2 special records)
 constexpr uint32_t LT_SLOTS = 1u << LT_SLOTS_LOG2;
 constexpr uint32_t LT_MAX_USED = 2560;     // close the LDS table at 62.5 % (+ <= 1024 racing inserts)
 constexpr uint32_t LT_TARGET_KEYS = 2300;  // P is chosen so a bucket holds about this many keys
-constexpr uint32_t LT_EMPTY = 0xFFFFFFFFu, LT_CLOSED = 0xFFFFFFFEu;
 constexpr uint32_t HA_FINE_LOG2 = 12;      // sample histogram: top 12 hash bits
 constexpr uint32_t HA_MAX_P_LOG2 = 11;
 constexpr int HA_SAMPLE_BLOCKS = 256;
@@ -78,11 +80,21 @@ __host__ __device__ inline uint32_t fmix32(uint32_t h) {
     return h;
 }
 
-// key bits: the key's value as int32 (signed types, sign-extended) or uint32
-template <typename K> __device__ inline uint32_t ha_kb(K v) {
-    if constexpr (std::is_signed_v<K>) return (uint32_t)(int32_t)v;
+// 32-bit hash of the key bits: its top bits pick the bucket, its low bits the LDS group
+__device__ inline uint32_t ha_h(uint32_t kb) { return fmix32(kb); }
+__device__ inline uint32_t ha_h(uint64_t kb) { return (uint32_t)(hash64(kb) >> 32); }
+
+template <typename K> using kb_t = std::conditional_t<sizeof(K) == 8, uint64_t, uint32_t>;
+
+// key bits: <= 4-byte keys as int32 (signed, sign-extended) / uint32; 8-byte keys verbatim
+template <typename K> __device__ inline kb_t<K> ha_kb(K v) {
+    if constexpr (sizeof(K) == 8) return __builtin_bit_cast(uint64_t, v);
+    else if constexpr (std::is_signed_v<K>) return (uint32_t)(int32_t)v;
     else return (uint32_t)v;
 }
+
+template <typename KB> __host__ __device__ constexpr KB kb_empty() { return ~KB(0); }
+template <typename KB> __host__ __device__ constexpr KB kb_closed() { return ~KB(0) - 1; }
 
 // a value as the 8 bytes pass A carries: float -> double bits, signed -> int64,
 // unsigned / bool -> uint64 (the AggSum upcast, superagg.cpp:289-346)
@@ -102,7 +114,8 @@ __device__ inline uint64_t ha_load_val(const void *p, int dtype, uint64_t i) {
     }
 }
 
-// HBM open-address table (linear probing from hash64 of the zero-extended key bits)
+// HBM open-address table (linear probing from hash64 of the key bits); slot `mask + 1` is
+// the side slot of the 8-byte key whose bits equal EMPTY
 struct HaTable {
     uint64_t *keys;  // SET_EMPTY = free
     unsigned long long *cnt;
@@ -116,8 +129,8 @@ struct HaTable {
     int nv;
 };
 
-__device__ inline uint64_t ha_slot(const HaTable &g, uint32_t kb) {
-    const uint64_t key = kb;
+__device__ inline uint64_t ha_slot(const HaTable &g, uint64_t key) {
+    if (key == SET_EMPTY) return g.mask + 1;
     uint64_t pos = hash64(key) & g.mask;
     for (int p = 0; p < HA_MAX_PROBE; p++) {
         uint64_t cur = __hip_atomic_load(&g.keys[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -138,8 +151,8 @@ __device__ inline uint64_t ha_slot(const HaTable &g, uint32_t kb) {
 }
 
 // one row straight into the HBM table (LDS table closed, or pass-A region full)
-template <int NV> __device__ inline void ha_global_row(const HaTable &g, uint32_t kb, const uint64_t *vb) {
-    const uint64_t s = ha_slot(g, kb);
+template <int NV> __device__ inline void ha_global_row(const HaTable &g, uint64_t key, const uint64_t *vb) {
+    const uint64_t s = ha_slot(g, key);
     if (s == ~0ULL) return;
     atomicAdd(&g.cnt[s], 1ULL);
 #pragma unroll
@@ -161,20 +174,20 @@ template <int NV> __device__ inline void ha_global_row(const HaTable &g, uint32_
 // value 0 (one ds_add_u64 updates both: a unit holds < 2^32 rows); the value sums; the
 // non-NaN count of value 1.  Records LT_SLOTS and LT_SLOTS + 1 hold the keys whose bits
 // are the CLOSED and EMPTY markers.
-struct LdsTable {
-    uint32_t *keys;                     // [LT_SLOTS]
+template <typename KB> struct LdsTable {
+    KB *keys;                           // [LT_SLOTS]
     unsigned long long *cn;             // [LT_SLOTS + 2]
     unsigned long long *sum[HA_MAX_V];  // [LT_SLOTS + 2]
     uint32_t *nn1;                      // [LT_SLOTS + 2]
     uint32_t *used;
 };
 
-__host__ __device__ constexpr size_t lt_bytes(int nv) {
-    return (size_t)8 * (LT_SLOTS + 2) * (1 + nv) + (size_t)4 * LT_SLOTS + (nv > 1 ? (size_t)4 * (LT_SLOTS + 2) : 0) + 64;
+__host__ __device__ constexpr size_t lt_bytes(int nv, int kbsize) {
+    return (size_t)8 * (LT_SLOTS + 2) * (1 + nv) + (size_t)kbsize * LT_SLOTS + (nv > 1 ? (size_t)4 * (LT_SLOTS + 2) : 0) + 64;
 }
 
-template <int NV> __device__ inline LdsTable lt_layout(unsigned char *raw) {
-    LdsTable t;
+template <typename KB, int NV> __device__ inline LdsTable<KB> lt_layout(unsigned char *raw) {
+    LdsTable<KB> t;
     unsigned char *p = raw;
     t.cn = reinterpret_cast<unsigned long long *>(p);
     p += 8 * (LT_SLOTS + 2);
@@ -182,17 +195,17 @@ template <int NV> __device__ inline LdsTable lt_layout(unsigned char *raw) {
         t.sum[v] = reinterpret_cast<unsigned long long *>(p);
         p += 8 * (LT_SLOTS + 2);
     }
-    t.keys = reinterpret_cast<uint32_t *>(p);
-    p += 4 * LT_SLOTS;
+    t.keys = reinterpret_cast<KB *>(p);
+    p += sizeof(KB) * LT_SLOTS;
     t.nn1 = reinterpret_cast<uint32_t *>(p);
     if (NV > 1) p += 4 * (LT_SLOTS + 2);
     t.used = reinterpret_cast<uint32_t *>(p);
     return t;
 }
 
-template <int NV> __device__ inline void lt_init(const LdsTable &t, int nthreads) {
+template <typename KB, int NV> __device__ inline void lt_init(const LdsTable<KB> &t, int nthreads) {
     for (uint32_t i = threadIdx.x; i < LT_SLOTS + 2; i += nthreads) {
-        if (i < LT_SLOTS) t.keys[i] = LT_EMPTY;
+        if (i < LT_SLOTS) t.keys[i] = kb_empty<KB>();
         t.cn[i] = 0;
 #pragma unroll
         for (int v = 0; v < NV; v++) t.sum[v][i] = 0;
@@ -201,8 +214,8 @@ template <int NV> __device__ inline void lt_init(const LdsTable &t, int nthreads
     if (threadIdx.x == 0) *t.used = 0;
 }
 
-template <int NV>
-__device__ inline void lt_bump(const LdsTable &t, const HaTable &g, uint32_t slot, const uint64_t *vb) {
+template <typename KB, int NV>
+__device__ inline void lt_bump(const LdsTable<KB> &t, const HaTable &g, uint32_t slot, const uint64_t *vb) {
     unsigned long long c = 1ULL << 32;
 #pragma unroll
     for (int v = 0; v < NV; v++) {
@@ -222,28 +235,37 @@ __device__ inline void lt_bump(const LdsTable &t, const HaTable &g, uint32_t slo
     atomicAdd(&t.cn[slot], c);
 }
 
+// four consecutive key slots: one ds_read_b128 (4-byte keys) or two (8-byte keys)
+template <typename KB> struct alignas(16) KB4 {
+    KB v[4];
+};
+
+__device__ inline uint32_t lt_cas(uint32_t *p, uint32_t cmp, uint32_t val) { return atomicCAS(p, cmp, val); }
+__device__ inline uint64_t lt_cas(uint64_t *p, uint64_t cmp, uint64_t val) {
+    return atomicCAS(reinterpret_cast<unsigned long long *>(p), (unsigned long long)cmp, (unsigned long long)val);
+}
+
 // aggregate one entry into the LDS table (or, when its table is closed to it, the HBM table).
-// Bucketised linear probing: the key hashes to a group of 4 slots, read with one
-// ds_read_b128; a key lives at the first free slot of its group sequence at insert time,
-// so a probe ends at a hit, or at the first EMPTY (CAS: insert, or CLOSED once the table
-// is full) / CLOSED slot.  At ~50 % load a wave of 64 lanes needs ~2 group reads, where
-// one-slot linear probing waits on the longest of 64 chains.
-template <int NV>
-__device__ inline void lt_add(const LdsTable &t, const HaTable &g, uint32_t kb, const uint64_t *vb) {
+// Bucketised linear probing: the key hashes to a group of 4 slots, read at once; a key
+// lives at the first free slot of its group sequence at insert time, so a probe ends at a
+// hit, or at the first EMPTY (CAS: insert, or CLOSED once the table is full) / CLOSED slot.
+// At ~50 % load a wave of 64 lanes needs ~2 group reads, where one-slot linear probing
+// waits on the longest of 64 chains.
+template <typename KB, int NV>
+__device__ inline void lt_add(const LdsTable<KB> &t, const HaTable &g, KB kb, const uint64_t *vb) {
+    constexpr KB EMPTY = kb_empty<KB>(), CLOSED = kb_closed<KB>();
     uint32_t slot;
-    if (kb >= LT_CLOSED) {
-        slot = LT_SLOTS + (kb - LT_CLOSED);
+    if (kb >= CLOSED) {
+        slot = LT_SLOTS + (uint32_t)(kb - CLOSED);
     } else {
-        const uint32_t h = fmix32(kb);
-        uint32_t grp = (h & (LT_SLOTS - 1)) >> 2;
+        uint32_t grp = (ha_h(kb) & (LT_SLOTS - 1)) >> 2;
         for (;;) {
-            const uint4 q = *reinterpret_cast<const uint4 *>(t.keys + 4 * grp);
-            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+            const KB4<KB> q = *reinterpret_cast<const KB4<KB> *>(t.keys + 4 * grp);
             int hit = -1, fr = -1;
 #pragma unroll
             for (int j = 3; j >= 0; j--) {
-                if (w[j] == kb) hit = j;
-                if (w[j] >= LT_CLOSED) fr = j;
+                if (q.v[j] == kb) hit = j;
+                if (q.v[j] >= CLOSED) fr = j;
             }
             if (hit >= 0 && (fr < 0 || hit < fr)) {
                 slot = 4 * grp + hit;
@@ -253,16 +275,16 @@ __device__ inline void lt_add(const LdsTable &t, const HaTable &g, uint32_t kb, 
                 grp = (grp + 1) & (LT_SLOTS / 4 - 1);
                 continue;
             }
-            if (w[fr] == LT_CLOSED) {
-                ha_global_row<NV>(g, kb, vb);
+            if (q.v[fr] == CLOSED) {
+                ha_global_row<NV>(g, (uint64_t)kb, vb);
                 return;
             }
             const uint32_t pos = 4 * grp + fr;
             const bool open = *reinterpret_cast<volatile uint32_t *>(t.used) < LT_MAX_USED;
-            const uint32_t cur = atomicCAS(&t.keys[pos], LT_EMPTY, open ? kb : LT_CLOSED);
-            if (cur == LT_EMPTY) {
+            const KB cur = lt_cas(&t.keys[pos], EMPTY, open ? kb : CLOSED);
+            if (cur == EMPTY) {
                 if (!open) {
-                    ha_global_row<NV>(g, kb, vb);
+                    ha_global_row<NV>(g, (uint64_t)kb, vb);
                     return;
                 }
                 atomicAdd(t.used, 1u);
@@ -276,47 +298,46 @@ __device__ inline void lt_add(const LdsTable &t, const HaTable &g, uint32_t kb, 
             // another key took the slot: re-read the same group
         }
     }
-    lt_bump<NV>(t, g, slot, vb);
+    lt_bump<KB, NV>(t, g, slot, vb);
 }
 
 // M entries at once: all home-group reads are issued together and the hits aggregated
 // with fire-and-forget LDS atomics; only entries whose key is not in its home group
 // (new keys, displaced keys, specials) take lt_add's probe loop.  One entry at a time, a
 // lane would wait an LDS round trip per entry.
-template <int NV, int M>
-__device__ inline void lt_add_many(const LdsTable &t, const HaTable &g, const uint32_t *kb,
+template <typename KB, int NV, int M>
+__device__ inline void lt_add_many(const LdsTable<KB> &t, const HaTable &g, const KB *kb,
                                    const uint64_t (*vb)[NV > 0 ? NV : 1], const bool *valid) {
-    uint4 q[M];
+    KB4<KB> q[M];
 #pragma unroll
     for (int i = 0; i < M; i++) {
-        const uint32_t grp = (fmix32(kb[i]) & (LT_SLOTS - 1)) >> 2;
-        q[i] = *reinterpret_cast<const uint4 *>(t.keys + 4 * grp);
+        const uint32_t grp = (ha_h(kb[i]) & (LT_SLOTS - 1)) >> 2;
+        q[i] = *reinterpret_cast<const KB4<KB> *>(t.keys + 4 * grp);
     }
     bool slow[M];
 #pragma unroll
     for (int i = 0; i < M; i++) {
-        const uint32_t base = (fmix32(kb[i]) & (LT_SLOTS - 1)) & ~3u;
+        const uint32_t base = (ha_h(kb[i]) & (LT_SLOTS - 1)) & ~3u;
         uint32_t slot = ~0u;
-        if (q[i].w == kb[i]) slot = base + 3;
-        if (q[i].z == kb[i]) slot = base + 2;
-        if (q[i].y == kb[i]) slot = base + 1;
-        if (q[i].x == kb[i]) slot = base;
-        if (kb[i] >= LT_CLOSED) slot = ~0u;
+#pragma unroll
+        for (int j = 3; j >= 0; j--)
+            if (q[i].v[j] == kb[i]) slot = base + j;
+        if (kb[i] >= kb_closed<KB>()) slot = ~0u;
         slow[i] = valid[i] && slot == ~0u;
-        if (valid[i] && slot != ~0u) lt_bump<NV>(t, g, slot, vb[i]);
+        if (valid[i] && slot != ~0u) lt_bump<KB, NV>(t, g, slot, vb[i]);
     }
 #pragma unroll
     for (int i = 0; i < M; i++)
-        if (slow[i]) lt_add<NV>(t, g, kb[i], vb[i]);
+        if (slow[i]) lt_add<KB, NV>(t, g, kb[i], vb[i]);
 }
 
 // merge the LDS table into the HBM table (after a workgroup barrier)
-template <int NV> __device__ inline void lt_merge(const LdsTable &t, const HaTable &g, int nthreads) {
+template <typename KB, int NV> __device__ inline void lt_merge(const LdsTable<KB> &t, const HaTable &g, int nthreads) {
     for (uint32_t i = threadIdx.x; i < LT_SLOTS + 2; i += nthreads) {
         const unsigned long long cn = t.cn[i];
         if (!cn) continue;
-        const uint32_t kb = i < LT_SLOTS ? t.keys[i] : LT_CLOSED + (i - LT_SLOTS);
-        const uint64_t s = ha_slot(g, kb);
+        const KB kb = i < LT_SLOTS ? t.keys[i] : (KB)(kb_closed<KB>() + (i - LT_SLOTS));
+        const uint64_t s = ha_slot(g, (uint64_t)kb);
         if (s == ~0ULL) continue;
         atomicAdd(&g.cnt[s], cn >> 32);
 #pragma unroll
@@ -343,10 +364,11 @@ struct HaParams {
     const uint32_t *cap;   // [P]
     const uint64_t *toff;  // [P]
     uint32_t *fills;       // [P][W]
-    uint32_t *ent;         // W * wg_stride key bits, then W * HA_THREADS dummy slots
+    // regions: NV == 1 packed 16-byte entries {key bits (8 B), value bits (8 B)}; otherwise
+    // a key-bits array and NV value-bits arrays.  W * HA_THREADS dummy slots follow.
+    void *ent;
     uint64_t *vbits[HA_MAX_V];
     uint64_t dummy0;       // first dummy slot (idle lanes of the stream-out write there)
-    uint32_t debug;        // experiment switches (VH_HA_DEBUG), 0 in production
 };
 
 struct HaUnit {
@@ -371,14 +393,16 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_sample(const K *keys, uint64_
     for (uint64_t r = threadIdx.x; r < HA_BATCH; r += HA_THREADS) {
         const uint64_t i = row0 + r;
         if (i >= n) break;
-        const uint32_t kb = ha_kb(keys[i]);
-        atomicAdd(&h[fmix32(kb) >> (32 - HA_FINE_LOG2)], 1u);
-        uint64_t pos = hash64(kb) & smask;
+        const auto kb = ha_kb(keys[i]);
+        atomicAdd(&h[ha_h(kb) >> (32 - HA_FINE_LOG2)], 1u);
+        const uint64_t key = (uint64_t)kb;
+        if (key == SET_EMPTY) continue;  // the estimate can miss one key
+        uint64_t pos = hash64(key) & smask;
         for (int p = 0; p < HA_MAX_PROBE; p++) {
             uint64_t cur = __hip_atomic_load(&skeys[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (cur == SET_EMPTY)
-                cur = atomicCAS((unsigned long long *)&skeys[pos], (unsigned long long)SET_EMPTY, (unsigned long long)kb);
-            if (cur == SET_EMPTY || cur == kb) {
+                cur = atomicCAS((unsigned long long *)&skeys[pos], (unsigned long long)SET_EMPTY, (unsigned long long)key);
+            if (cur == SET_EMPTY || cur == key) {
                 atomicAdd(&scnt[pos], 1u);
                 break;
             }
@@ -413,22 +437,25 @@ __global__ __launch_bounds__(256) void k_ha_sample_stats(const uint32_t *scnt, u
 }
 
 // ---- pass A -------------------------------------------------------------------------------
-__host__ __device__ constexpr size_t ha_scatter_lds_bytes(int nv, uint32_t P) {
-    return (size_t)8 * (nv + 1) * (HA_BATCH + 1) + 16 * ((size_t)P + 1) + 64;
+__host__ __device__ constexpr size_t ha_scatter_lds_bytes(int nv, int kbsize, uint32_t P) {
+    return ((size_t)8 * nv + kbsize + 4) * (HA_BATCH + 1) + 16 * ((size_t)P + 1) + 64;
 }
 
-// LDS of pass A: staged value bits | staged (destination, key) pairs | per-bucket hist |
-// batch offsets | region write base | region limit | wave sums
-struct HaScatterLds {
-    uint64_t *sv, *sp;
+// LDS of pass A: staged value bits | staged key bits | staged destinations | per-bucket
+// hist | batch offsets | region write base | region limit | wave sums
+template <typename KB> struct HaScatterLds {
+    uint64_t *sv;
+    KB *sk;
+    uint32_t *sd;
     uint32_t *hist, *boff, *base, *lim, *wave_sums;
 };
 
-template <int NV> __device__ inline HaScatterLds ha_scatter_lds(unsigned char *raw, const HaParams &hp) {
-    HaScatterLds l;
+template <typename KB, int NV> __device__ inline HaScatterLds<KB> ha_scatter_lds(unsigned char *raw, const HaParams &hp) {
+    HaScatterLds<KB> l;
     l.sv = reinterpret_cast<uint64_t *>(raw);
-    l.sp = l.sv + (size_t)NV * (HA_BATCH + 1);
-    l.hist = reinterpret_cast<uint32_t *>(l.sp + HA_BATCH + 1);
+    l.sk = reinterpret_cast<KB *>(l.sv + (size_t)NV * (HA_BATCH + 1));
+    l.sd = reinterpret_cast<uint32_t *>(l.sk + HA_BATCH + 1);
+    l.hist = l.sd + HA_BATCH + 1;
     l.boff = l.hist + hp.P + 1;  // hist[P]: the rank sink of rows past the range
     l.base = l.boff + hp.P;
     l.lim = l.base + hp.P;
@@ -447,11 +474,11 @@ template <int NV> __device__ inline HaScatterLds ha_scatter_lds(unsigned char *r
 // addresses), region bases advanced.  Rows past a region's capacity go to the HBM table.
 // The stream-out issues a fixed number of stores per lane (idle lanes write a private
 // dummy slot), so the compiler waits for the prefetched next batch with vmcnt(#stores)
-// instead of draining every store of this batch (cdna_hip_programming.md, "Pipelining
-// across barriers"); the rare overflow rows are applied after that loop.
-template <int NV>
-__device__ inline void ha_commit(const HaScatterLds &l, const HaParams &hp, const HaTable &g, uint64_t region0,
-                                 const uint32_t *bkt, const uint32_t *kb, const int32_t *rank,
+// instead of draining every store of this batch; the rare overflow rows are applied after
+// that loop.
+template <typename KB, int NV>
+__device__ inline void ha_commit(const HaScatterLds<KB> &l, const HaParams &hp, const HaTable &g, uint64_t region0,
+                                 const uint32_t *bkt, const KB *kb, const int32_t *rank,
                                  const uint64_t (*vb)[NV > 0 ? NV : 1]) {
     __shared__ uint32_t s_total, s_over;
     const uint32_t P = hp.P;
@@ -494,8 +521,8 @@ __device__ inline void ha_commit(const HaScatterLds &l, const HaParams &hp, cons
         const uint32_t d = l.base[t] + (uint32_t)rank[r];
         const bool fits = d < l.lim[t];
         over |= valid && !fits;
-        const uint32_t dest = fits ? d : (HA_DEST_OVERFLOW | t);
-        l.sp[pos] = ((uint64_t)dest << 32) | kb[r];
+        l.sd[pos] = fits ? d : (HA_DEST_OVERFLOW | t);
+        l.sk[pos] = kb[r];
 #pragma unroll
         for (int v = 0; v < NV; v++) l.sv[v * (HA_BATCH + 1) + pos] = vb[r][v];
     }
@@ -506,27 +533,27 @@ __device__ inline void ha_commit(const HaScatterLds &l, const HaParams &hp, cons
 #pragma unroll
     for (int r = 0; r < HA_RPT; r++) {
         const uint32_t k = r * HA_THREADS + threadIdx.x;
-        const uint64_t pk = l.sp[k];
-        const uint32_t dest = (uint32_t)(pk >> 32);
+        const uint32_t dest = l.sd[k];
+        const uint64_t key = (uint64_t)l.sk[k];
         const bool ok = k < tot && !(dest & HA_DEST_OVERFLOW);
         const uint64_t e = ok ? region0 + dest : dummy;
-        if constexpr (NV == 1) {  // packed {key, 0, value}: one 16-byte store per row
+        if constexpr (NV == 1) {  // packed {key, value}: one 16-byte store per row
             const uint64_t vbits = l.sv[k];
-            reinterpret_cast<uint4 *>(hp.ent)[e] = make_uint4((uint32_t)pk, 0u, (uint32_t)vbits, (uint32_t)(vbits >> 32));
+            reinterpret_cast<uint4 *>(hp.ent)[e] =
+                make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)vbits, (uint32_t)(vbits >> 32));
         } else {
-            hp.ent[e] = (uint32_t)pk;
+            reinterpret_cast<KB *>(hp.ent)[e] = (KB)key;
 #pragma unroll
             for (int v = 0; v < NV; v++) hp.vbits[v][e] = l.sv[v * (HA_BATCH + 1) + k];
         }
     }
     if (s_over) {
         for (uint32_t k = threadIdx.x; k < tot; k += HA_THREADS) {
-            const uint64_t pk = l.sp[k];
-            if (!((uint32_t)(pk >> 32) & HA_DEST_OVERFLOW)) continue;
+            if (!(l.sd[k] & HA_DEST_OVERFLOW)) continue;
             uint64_t vv[NV > 0 ? NV : 1];
 #pragma unroll
             for (int v = 0; v < NV; v++) vv[v] = l.sv[v * (HA_BATCH + 1) + k];
-            ha_global_row<NV>(g, (uint32_t)pk, vv);
+            ha_global_row<NV>(g, (uint64_t)l.sk[k], vv);
         }
     }
     ha_lds_barrier();
@@ -538,15 +565,16 @@ __device__ inline void ha_commit(const HaScatterLds &l, const HaParams &hp, cons
 }
 
 // top p_log2 bits of the key hash (branch-free: p_log2 = 0 gives bucket 0)
-__device__ inline uint32_t ha_bucket(const HaParams &hp, uint32_t kb) {
-    return (uint32_t)(((uint64_t)fmix32(kb) << hp.p_log2) >> 32);
+template <typename KB> __device__ inline uint32_t ha_bucket(const HaParams &hp, KB kb) {
+    return (uint32_t)(((uint64_t)ha_h(kb) << hp.p_log2) >> 32);
 }
 
-// generic pass A: any <= 4-byte key type and value dtypes, scalar loads
+// generic pass A: any key type and value dtypes, scalar loads
 template <typename K, int NV>
 __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter(HaParams hp, HaTable g) {
+    using KB = kb_t<K>;
     extern __shared__ __align__(16) unsigned char lds_raw[];
-    const HaScatterLds l = ha_scatter_lds<NV>(lds_raw, hp);
+    const HaScatterLds<KB> l = ha_scatter_lds<KB, NV>(lds_raw, hp);
     __syncthreads();
     const uint32_t w = blockIdx.x;
     const uint64_t row_begin = (uint64_t)w * hp.rows_per_wg;
@@ -554,13 +582,15 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter(HaParams hp, HaTable 
     const uint64_t region0 = (uint64_t)w * hp.wg_stride;
     const K *keys = static_cast<const K *>(hp.keys);
     for (uint64_t b0 = row_begin; b0 < row_end; b0 += HA_BATCH) {
-        uint32_t bkt[HA_RPT], kb[HA_RPT];
+        uint32_t bkt[HA_RPT];
+        KB kb[HA_RPT];
         int32_t rank[HA_RPT];
         uint64_t vb[HA_RPT][NV > 0 ? NV : 1];
 #pragma unroll
         for (int r = 0; r < HA_RPT; r++) {
             const uint64_t i = b0 + (uint64_t)r * HA_THREADS + threadIdx.x;
             rank[r] = -1;
+            kb[r] = 0;
             if (i < row_end) {
                 kb[r] = ha_kb(keys[i]);
 #pragma unroll
@@ -575,22 +605,25 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter(HaParams hp, HaTable 
                 rank[r] = (int32_t)atomicAdd(&l.hist[bkt[r]], 1u);
             }
         }
-        ha_commit<NV>(l, hp, g, region0, bkt, kb, rank, vb);
+        ha_commit<KB, NV>(l, hp, g, region0, bkt, kb, rank, vb);
     }
     for (uint32_t t = threadIdx.x; t < hp.P; t += HA_THREADS)
         hp.fills[(uint64_t)t * hp.W + w] = l.base[t] - (uint32_t)hp.toff[t];
 }
 
-// fast pass A: 4-byte keys and float64 values, 16-byte aligned, n a multiple of 8.  A lane
-// owns 2 x 4 consecutive rows per batch: keys as two 16-byte loads, each value column as
-// four; the next batch is prefetched into registers while this one is ranked and sorted.
-// Workgroup ranges are multiples of HA_BATCH, so a 4-row group is wholly inside or wholly
-// past the range; past-the-end groups load a clamped in-range address and are dropped.
+// fast pass A: 4- or 8-byte keys and float64 values, 16-byte aligned, n a multiple of 8.
+// A lane owns 8 rows per batch in groups of KPL consecutive rows (one 16-byte key load
+// each: KPL = 4 for 4-byte keys, 2 for 8-byte keys) and each value column as KPL / 2
+// 16-byte loads; the next batch is prefetched into registers while this one is ranked and
+// sorted.  Workgroup ranges are multiples of HA_BATCH, so a group is wholly inside or
+// wholly past the range; past-the-end groups load a clamped in-range address and drop.
 template <typename K, int NV>
 __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_f64(HaParams hp, HaTable g) {
-    static_assert(sizeof(K) == 4, "fast pass A takes 4-byte keys");
+    static_assert(sizeof(K) == 4 || sizeof(K) == 8, "fast pass A takes 4- or 8-byte keys");
+    using KB = kb_t<K>;
+    constexpr int KPL = 16 / sizeof(K), GROUPS = HA_RPT / KPL;
     extern __shared__ __align__(16) unsigned char lds_raw[];
-    const HaScatterLds l = ha_scatter_lds<NV>(lds_raw, hp);
+    const HaScatterLds<KB> l = ha_scatter_lds<KB, NV>(lds_raw, hp);
     __syncthreads();
     const uint32_t w = blockIdx.x;
     const uint64_t row_begin = (uint64_t)w * hp.rows_per_wg;
@@ -601,39 +634,39 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_f64(HaParams hp, HaTa
 #pragma unroll
     for (int v = 0; v < NV; v++) vcol[v] = static_cast<const double *>(hp.vals[v]);
     struct Regs {
-        uint4 k[2];
-        double2 v[2][NV > 0 ? NV : 1][2];
+        uint4 k[GROUPS];
+        double2 v[GROUPS][NV > 0 ? NV : 1][KPL / 2];
     };
     auto load = [&](uint64_t b0, Regs &R) {
 #pragma unroll
-        for (int q = 0; q < 2; q++) {
-            const uint64_t i = b0 + 4 * ((uint64_t)q * HA_THREADS + threadIdx.x);
-            const uint64_t is = i < hp.n ? i : hp.n - 4;
+        for (int q = 0; q < GROUPS; q++) {
+            const uint64_t i = b0 + KPL * ((uint64_t)q * HA_THREADS + threadIdx.x);
+            const uint64_t is = i < hp.n ? i : hp.n - KPL;
             R.k[q] = *reinterpret_cast<const uint4 *>(keys + is);
 #pragma unroll
             for (int v = 0; v < NV; v++)
 #pragma unroll
-                for (int h = 0; h < 2; h++) R.v[q][v][h] = *reinterpret_cast<const double2 *>(vcol[v] + is + 2 * h);
+                for (int h = 0; h < KPL / 2; h++) R.v[q][v][h] = *reinterpret_cast<const double2 *>(vcol[v] + is + 2 * h);
         }
     };
     Regs cur, nxt;
-    // prologue through nxt: cur is then written by register moves, so the loop header's
-    // wait analysis does not see cur's loads as pending (which made it drain the stores)
     load(row_begin, cur);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): an intrinsic the wait analysis sees
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): cur is not pending at the loop header
     for (uint64_t b0 = row_begin; b0 < row_end; b0 += HA_BATCH) {
         load(b0 + HA_BATCH, nxt);
-        uint32_t bkt[HA_RPT], kb[HA_RPT];
+        uint32_t bkt[HA_RPT];
+        KB kb[HA_RPT];
         int32_t rank[HA_RPT];
         uint64_t vb[HA_RPT][NV > 0 ? NV : 1];
 #pragma unroll
-        for (int q = 0; q < 2; q++) {
-            const uint64_t i = b0 + 4 * ((uint64_t)q * HA_THREADS + threadIdx.x);
-            const uint32_t words[4] = {cur.k[q].x, cur.k[q].y, cur.k[q].z, cur.k[q].w};
+        for (int q = 0; q < GROUPS; q++) {
+            const uint64_t i = b0 + KPL * ((uint64_t)q * HA_THREADS + threadIdx.x);
             const bool valid = i < row_end;  // uniform but for a range's last batch
+            KB words[KPL];
+            __builtin_memcpy(words, &cur.k[q], 16);
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int r = q * 4 + j;
+            for (int j = 0; j < KPL; j++) {
+                const int r = q * KPL + j;
                 kb[r] = ha_kb(__builtin_bit_cast(K, words[j]));
 #pragma unroll
                 for (int v = 0; v < NV; v++)
@@ -643,7 +676,7 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_f64(HaParams hp, HaTa
                 rank[r] = valid ? (int32_t)rk : -1;
             }
         }
-        ha_commit<NV>(l, hp, g, region0, bkt, kb, rank, vb);
+        ha_commit<KB, NV>(l, hp, g, region0, bkt, kb, rank, vb);
         cur = nxt;
     }
     for (uint32_t t = threadIdx.x; t < hp.P; t += HA_THREADS)
@@ -658,16 +691,19 @@ __global__ __launch_bounds__(64) void k_ha_tail(HaParams hp, HaTable g, uint64_t
     uint64_t vb[NV > 0 ? NV : 1];
 #pragma unroll
     for (int v = 0; v < NV; v++) vb[v] = ha_load_val(hp.vals[v], hp.vdtype[v], i);
-    ha_global_row<NV>(g, ha_kb(static_cast<const K *>(hp.keys)[i]), vb);
+    ha_global_row<NV>(g, (uint64_t)ha_kb(static_cast<const K *>(hp.keys)[i]), vb);
 }
 
 // ---- pass B -------------------------------------------------------------------------------
-template <int NV>
+// One work unit = one bucket x a range of pass-A workgroups.  The unit's regions are read
+// as one flat stream of entries (prefix sums of the region fills in LDS), one entry per
+// lane per load: consecutive lanes read consecutive entries (a wave's load is contiguous
+// unless it crosses a region end); a lane finds the region of its entry by a forward scan.
+template <typename KB, int NV>
 __global__ __launch_bounds__(HB_THREADS) void k_ha_reduce(HaParams hp, HaTable g, const HaUnit *units) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
     __shared__ uint32_t s_fill[1024];
     __shared__ uint32_t s_pre[1025];
-    __shared__ uint32_t s_pre2[NV == 1 ? 1025 : 1];
     const HaUnit u = units[blockIdx.x];
     const uint32_t b = u.bucket;
     const uint32_t cap = hp.cap[b];
@@ -679,28 +715,11 @@ __global__ __launch_bounds__(HB_THREADS) void k_ha_reduce(HaParams hp, HaTable g
         any |= f != 0;
     }
     if (!__syncthreads_or(any)) return;
-    const LdsTable t = lt_layout<NV>(lds_raw);
-    lt_init<NV>(t, HB_THREADS);
+    const LdsTable<KB> t = lt_layout<KB, NV>(lds_raw);
+    lt_init<KB, NV>(t, HB_THREADS);
     if (threadIdx.x < 64) {
-        // exclusive scan of the 4-entry chunk counts by the first wave (16 regions per lane)
+        // exclusive scan of the region fills by the first wave (16 regions per lane)
         const uint32_t lane = threadIdx.x, k0 = lane * 16;
-        uint32_t sum = 0;
-        for (uint32_t k = k0; k < k0 + 16 && k < nw; k++) sum += (s_fill[k] + 3) >> 2;
-        uint32_t inc = sum;
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(inc, off, 64);
-            if ((int)lane >= off) inc += y;
-        }
-        uint32_t acc = inc - sum;
-        for (uint32_t k = k0; k < k0 + 16 && k < nw; k++) {
-            s_pre[k] = acc;
-            acc += (s_fill[k] + 3) >> 2;
-        }
-        if (lane == 63) s_pre[nw] = inc;
-    }
-    if (NV == 1 && threadIdx.x >= 64 && threadIdx.x < 128) {
-        // exclusive scan of the region fills (entries) by the second wave
-        const uint32_t lane = threadIdx.x - 64, k0 = lane * 16;
         uint32_t sum = 0;
         for (uint32_t k = k0; k < k0 + 16 && k < nw; k++) sum += s_fill[k];
         uint32_t inc = sum;
@@ -710,134 +729,88 @@ __global__ __launch_bounds__(HB_THREADS) void k_ha_reduce(HaParams hp, HaTable g
         }
         uint32_t acc = inc - sum;
         for (uint32_t k = k0; k < k0 + 16 && k < nw; k++) {
-            s_pre2[k] = acc;
+            s_pre[k] = acc;
             acc += s_fill[k];
         }
-        if (lane == 63) s_pre2[nw] = inc;
+        if (lane == 63) s_pre[nw] = inc;
     }
     __syncthreads();
-    const uint32_t C = s_pre[nw];
+    const uint32_t E = s_pre[nw];
     const uint64_t toff_b = hp.toff[b];
-    uint32_t kk = 0;  // region of this lane's current chunk (chunk indices of a lane only grow)
-    if constexpr (NV == 1) {
-        // packed 16-byte entries {key, 0, value}, streamed one entry per lane per load:
-        // consecutive lanes read consecutive entries of the unit's flattened region stream
-        // (a wave load is 1 KB contiguous unless it crosses a region end)
-        const uint4 *pe = reinterpret_cast<const uint4 *>(hp.ent);
-        constexpr int M = HB_VU * 4;
-        const uint32_t E = s_pre2[nw];
-        uint32_t kr = 0;
-        for (uint32_t c0 = 0; c0 < E; c0 += HB_THREADS * M) {
-            uint4 ev[M];
-            bool valid[M];
+    uint32_t kr = 0;  // region of this lane's current entry (entry indices of a lane only grow)
+    for (uint32_t c0 = 0; c0 < E; c0 += HB_THREADS * HB_M) {
+        KB kb[HB_M];
+        uint64_t vb[HB_M][NV > 0 ? NV : 1];
+        bool valid[HB_M];
 #pragma unroll
-            for (int j = 0; j < M; j++) {
-                const uint32_t c = c0 + j * HB_THREADS + threadIdx.x;
-                const uint32_t cc = c < E ? c : E - 1;
-                while (s_pre2[kr + 1] <= cc) kr++;
-                const uint64_t e = (uint64_t)(u.w_begin + kr) * hp.wg_stride + toff_b + (cc - s_pre2[kr]);
-                valid[j] = c < E;
-                ev[j] = pe[e];
-            }
-            uint32_t kb[M];
-            uint64_t vb[M][1];
-#pragma unroll
-            for (int j = 0; j < M; j++) {
-                kb[j] = ev[j].x;
-                vb[j][0] = ((uint64_t)ev[j].w << 32) | ev[j].z;
-            }
-            if (hp.debug & 8) {
-#pragma unroll
-                for (int j = 0; j < M; j++) asm volatile("" :: "v"(kb[j]), "v"(vb[j][0]));
-            } else {
-                lt_add_many<NV, M>(t, g, kb, vb, valid);
-            }
-        }
-        __syncthreads();
-        lt_merge<NV>(t, g, HB_THREADS);
-        return;
-    }
-    for (uint32_t c0 = 0; c0 < C; c0 += HB_THREADS * HB_VU) {
-        uint4 ev[HB_VU];
-        ulonglong2 vv[HB_VU][NV > 0 ? NV : 1][2];
-        uint32_t rem[HB_VU];
-#pragma unroll
-        for (int j = 0; j < HB_VU; j++) {
+        for (int j = 0; j < HB_M; j++) {
             const uint32_t c = c0 + j * HB_THREADS + threadIdx.x;
-            const uint32_t cc = c < C ? c : C - 1;
-            while (s_pre[kk + 1] <= cc) kk++;
-            const uint32_t q = (cc - s_pre[kk]) * 4;
-            // regions start at multiples of 8 entries: a 4-entry chunk stays in its region
-            const uint64_t e = (uint64_t)(u.w_begin + kk) * hp.wg_stride + toff_b + q;
-            rem[j] = c < C ? min(4u, s_fill[kk] - q) : 0u;
-            ev[j] = *reinterpret_cast<const uint4 *>(hp.ent + e);
+            const uint32_t cc = c < E ? c : E - 1;
+            while (s_pre[kr + 1] <= cc) kr++;
+            const uint64_t e = (uint64_t)(u.w_begin + kr) * hp.wg_stride + toff_b + (cc - s_pre[kr]);
+            valid[j] = c < E;
+            if constexpr (NV == 1) {
+                const uint4 q = reinterpret_cast<const uint4 *>(hp.ent)[e];
+                kb[j] = (KB)(((uint64_t)q.y << 32) | q.x);
+                vb[j][0] = ((uint64_t)q.w << 32) | q.z;
+            } else {
+                kb[j] = reinterpret_cast<const KB *>(hp.ent)[e];
 #pragma unroll
-            for (int v = 0; v < NV; v++)
-#pragma unroll
-                for (int h = 0; h < 2; h++) vv[j][v][h] = *reinterpret_cast<const ulonglong2 *>(hp.vbits[v] + e + 2 * h);
-        }
-        uint32_t kb[HB_VU * 4];
-        uint64_t vb[HB_VU * 4][NV > 0 ? NV : 1];
-        bool valid[HB_VU * 4];
-#pragma unroll
-        for (int j = 0; j < HB_VU; j++) {
-            const uint32_t words[4] = {ev[j].x, ev[j].y, ev[j].z, ev[j].w};
-#pragma unroll
-            for (int x = 0; x < 4; x++) {
-                kb[j * 4 + x] = words[x];
-                valid[j * 4 + x] = (uint32_t)x < rem[j];
-#pragma unroll
-                for (int v = 0; v < NV; v++) vb[j * 4 + x][v] = (x & 1) ? vv[j][v][x >> 1].y : vv[j][v][x >> 1].x;
+                for (int v = 0; v < NV; v++) vb[j][v] = hp.vbits[v][e];
             }
         }
-        lt_add_many<NV, HB_VU * 4>(t, g, kb, vb, valid);
+        lt_add_many<KB, NV, HB_M>(t, g, kb, vb, valid);
     }
     __syncthreads();
-    lt_merge<NV>(t, g, HB_THREADS);
+    lt_merge<KB, NV>(t, g, HB_THREADS);
 }
 
 // ---- direct (P == 1): each workgroup aggregates a row range of the raw columns ------------
 template <typename K, int NV>
 __global__ __launch_bounds__(HB_THREADS) void k_ha_direct(HaParams hp, HaTable g) {
+    using KB = kb_t<K>;
     extern __shared__ __align__(16) unsigned char lds_raw[];
-    const LdsTable t = lt_layout<NV>(lds_raw);
-    lt_init<NV>(t, HB_THREADS);
+    const LdsTable<KB> t = lt_layout<KB, NV>(lds_raw);
+    lt_init<KB, NV>(t, HB_THREADS);
     __syncthreads();
     const uint64_t row_begin = (uint64_t)blockIdx.x * hp.rows_per_wg;
     const uint64_t row_end = min(hp.n, row_begin + hp.rows_per_wg);
     const K *keys = static_cast<const K *>(hp.keys);
     constexpr int U = 4;
     for (uint64_t b0 = row_begin; b0 < row_end; b0 += (uint64_t)U * HB_THREADS) {
-        uint32_t kb[U];
+        KB kb[U];
         uint64_t vb[U][NV > 0 ? NV : 1];
+        bool valid[U];
 #pragma unroll
         for (int r = 0; r < U; r++) {
             const uint64_t i = b0 + (uint64_t)r * HB_THREADS + threadIdx.x;
-            if (i < row_end) {
+            valid[r] = i < row_end;
+            kb[r] = 0;
+            if (valid[r]) {
                 kb[r] = ha_kb(keys[i]);
 #pragma unroll
                 for (int v = 0; v < NV; v++) vb[r][v] = ha_load_val(hp.vals[v], hp.vdtype[v], i);
             }
         }
-        bool valid[U];
-#pragma unroll
-        for (int r = 0; r < U; r++) {
-            valid[r] = b0 + (uint64_t)r * HB_THREADS + threadIdx.x < row_end;
-            if (!valid[r]) kb[r] = 0;
-        }
-        lt_add_many<NV, U>(t, g, kb, vb, valid);
+        lt_add_many<KB, NV, U>(t, g, kb, vb, valid);
     }
     __syncthreads();
-    lt_merge<NV>(t, g, HB_THREADS);
+    lt_merge<KB, NV>(t, g, HB_THREADS);
 }
 
 // ---- table maintenance / finish -----------------------------------------------------------
 template <int NV> __global__ __launch_bounds__(256) void k_ha_rehash(HaTable src, uint64_t src_slots, HaTable dst) {
-    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < src_slots; i += (uint64_t)gridDim.x * 256) {
-        const uint64_t k = src.keys[i];
-        if (k == SET_EMPTY) continue;
-        const uint64_t s = ha_slot(dst, (uint32_t)k);
-        if (s == ~0ULL) continue;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i <= src_slots; i += (uint64_t)gridDim.x * 256) {
+        uint64_t s;
+        if (i == src_slots) {  // the side slot keeps its place
+            if (!src.cnt[i]) continue;
+            s = dst.mask + 1;
+        } else {
+            const uint64_t k = src.keys[i];
+            if (k == SET_EMPTY) continue;
+            s = ha_slot(dst, k);
+            if (s == ~0ULL) continue;
+        }
         dst.cnt[s] = src.cnt[i];
 #pragma unroll
         for (int v = 0; v < NV; v++) {
@@ -847,35 +820,50 @@ template <int NV> __global__ __launch_bounds__(256) void k_ha_rehash(HaTable src
     }
 }
 
-__global__ __launch_bounds__(256) void k_ha_compact(const uint64_t *keys, uint64_t slots, int is_signed,
-                                                    uint32_t *skey, uint32_t *sslot, uint32_t *counter) {
-    // one counter add per wave (ballot + popcount), not per occupied slot
+// sortable key bits: signed keys with the sign bit flipped (radix order = value order)
+template <typename KB> __device__ inline KB ha_sortable(uint64_t key, int is_signed) {
+    const KB k = (KB)key;
+    return is_signed ? (KB)(k ^ ((KB)1 << (8 * sizeof(KB) - 1))) : k;
+}
+
+template <typename KB>
+__global__ __launch_bounds__(256) void k_ha_compact(const uint64_t *keys, const unsigned long long *cnt, uint64_t slots,
+                                                    int is_signed, KB *skey, uint32_t *sslot, uint32_t *counter) {
+    // one counter add per wave (ballot + popcount), not per occupied slot; i == slots is the
+    // side slot (occupied when it counted rows)
     const int lane = threadIdx.x & 63;
     const uint64_t step = (uint64_t)gridDim.x * 256;
-    for (uint64_t i0 = blockIdx.x * 256ull; i0 < slots; i0 += step) {
+    for (uint64_t i0 = blockIdx.x * 256ull; i0 <= slots; i0 += step) {
         const uint64_t i = i0 + threadIdx.x;
-        const uint64_t k = i < slots ? keys[i] : SET_EMPTY;
-        const bool occ = k != SET_EMPTY;
+        bool occ = false;
+        uint64_t k = SET_EMPTY;
+        if (i < slots) {
+            k = keys[i];
+            occ = k != SET_EMPTY;
+        } else if (i == slots) {
+            occ = cnt[i] != 0;
+        }
         const uint64_t m = __ballot(occ);
         uint32_t base = 0;
         if (lane == 0 && m) base = atomicAdd(counter, (uint32_t)__popcll(m));
         base = __shfl(base, 0, 64);
         if (occ) {
             const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-            skey[j] = is_signed ? ((uint32_t)k ^ 0x80000000u) : (uint32_t)k;
+            skey[j] = ha_sortable<KB>(k, is_signed);
             sslot[j] = (uint32_t)i;
         }
     }
 }
 
-template <int NV>
-__global__ __launch_bounds__(256) void k_ha_gather(HaTable g, const uint32_t *skey, const uint32_t *sslot, uint64_t m,
+template <typename KB, int NV>
+__global__ __launch_bounds__(256) void k_ha_gather(HaTable g, const KB *skey, const uint32_t *sslot, uint64_t m,
                                                    int is_signed, int64_t *okey, int64_t *ocnt, uint64_t *osum,
                                                    int64_t *onn) {
     for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) {
         const uint32_t s = sslot[j];
-        const uint32_t kb = is_signed ? (skey[j] ^ 0x80000000u) : skey[j];
-        okey[j] = is_signed ? (int64_t)(int32_t)kb : (int64_t)kb;
+        const KB kb = ha_sortable<KB>((uint64_t)skey[j], is_signed);  // the flip is its own inverse
+        if constexpr (sizeof(KB) == 4) okey[j] = is_signed ? (int64_t)(int32_t)kb : (int64_t)kb;
+        else okey[j] = (int64_t)kb;
         const uint64_t c = g.cnt[s];
         ocnt[j] = (int64_t)c;
 #pragma unroll
@@ -883,6 +871,38 @@ __global__ __launch_bounds__(256) void k_ha_gather(HaTable g, const uint32_t *sk
             osum[(uint64_t)v * m + j] = g.sum[v][s];
             onn[(uint64_t)v * m + j] = ((g.vfloat >> v) & 1) ? (int64_t)g.nn[v][s] : (int64_t)c;
         }
+    }
+}
+
+// combined key of a multi-key groupby: sum_j (key_j - min_j) * mult_j as int64
+// (groupby.py:248-288 _combine: the cartesian ordinal, first key most significant)
+constexpr int HC_MAX_KEYS = 8;
+struct HcParams {
+    const void *col[HC_MAX_KEYS];
+    int32_t dtype[HC_MAX_KEYS];
+    int64_t min[HC_MAX_KEYS];
+    int64_t mult[HC_MAX_KEYS];
+    int nkeys;
+};
+
+__device__ inline int64_t hc_load(const void *p, int dtype, uint64_t i) {
+    switch (dtype) {
+    case VH_I64: return static_cast<const int64_t *>(p)[i];
+    case VH_I32: return static_cast<const int32_t *>(p)[i];
+    case VH_I16: return static_cast<const int16_t *>(p)[i];
+    case VH_I8: return static_cast<const int8_t *>(p)[i];
+    case VH_U64: return (int64_t) static_cast<const uint64_t *>(p)[i];
+    case VH_U32: return static_cast<const uint32_t *>(p)[i];
+    case VH_U16: return static_cast<const uint16_t *>(p)[i];
+    default: return static_cast<const uint8_t *>(p)[i];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_combine_keys(HcParams p, uint64_t n, int64_t *out) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        int64_t c = 0;
+        for (int j = 0; j < p.nkeys; j++) c += (hc_load(p.col[j], p.dtype[j], i) - p.min[j]) * p.mult[j];
+        out[i] = c;
     }
 }
 
@@ -897,12 +917,11 @@ struct vh_hashagg {
     uint32_t vfloat = 0;
     uint32_t nnmask = 0;  // value columns whose non-NaN count is read (count(v), mean)
     uint64_t slots = 0;  // HBM table slots (power of two), 0 = not allocated
-    DevBuf tab;          // keys | cnt | sum[nv] | nn[nv] | used, err
+    DevBuf tab;          // keys | cnt | sum[nv] | nn[nv] (slots + 1 each) | used, err
     DevBuf out;
     uint64_t ngroups = 0;
     bool finished = false;
     uint64_t rows = 0;
-    HaTable view() const;
 };
 
 namespace vh {
@@ -923,25 +942,26 @@ static HaScratch &scratch() {
     return *p;
 }
 
-static bool key_dtype_ok(int d) {
-    return d == VH_I32 || d == VH_I16 || d == VH_I8 || d == VH_U32 || d == VH_U16 || d == VH_U8;
-}
-static bool key_signed(int d) { return d == VH_I32 || d == VH_I16 || d == VH_I8; }
+static bool key_dtype_ok(int d) { return d != VH_F64 && d != VH_F32 && d != VH_BOOL; }
+static bool key_signed(int d) { return d == VH_I64 || d == VH_I32 || d == VH_I16 || d == VH_I8; }
+static int key_bits_size(int d) { return dtype_itemsize(d) == 8 ? 8 : 4; }
 
-static uint64_t tab_bytes(uint64_t slots, int nv) { return slots * 8 * (2 + 2 * (uint64_t)nv) + 256; }
+// table arrays hold slots + 1 entries (the side slot); 8 spare words for used / err
+static uint64_t tab_bytes(uint64_t slots, int nv) { return (slots + 1) * 8 * (2 + 2 * (uint64_t)nv) + 256; }
 
 static HaTable table_view(void *base, uint64_t slots, int nv, uint32_t vfloat, uint32_t nnmask = 0) {
     HaTable g{};
     unsigned char *p = static_cast<unsigned char *>(base);
+    const uint64_t a = 8 * (slots + 1);
     g.keys = reinterpret_cast<uint64_t *>(p);
-    p += 8 * slots;
+    p += a;
     g.cnt = reinterpret_cast<unsigned long long *>(p);
-    p += 8 * slots;
+    p += a;
     for (int v = 0; v < nv; v++) {
         g.sum[v] = reinterpret_cast<unsigned long long *>(p);
-        p += 8 * slots;
+        p += a;
         g.nn[v] = reinterpret_cast<unsigned long long *>(p);
-        p += 8 * slots;
+        p += a;
     }
     g.used = reinterpret_cast<uint32_t *>(p);
     g.err = g.used + 1;
@@ -956,8 +976,9 @@ static HaTable table_view(void *base, uint64_t slots, int nv, uint32_t vfloat, u
 static void table_alloc(DevBuf &buf, uint64_t slots, int nv) {
     buf.ensure(tab_bytes(slots, nv));
     hipStream_t st = stream();
-    VH_HIP(hipMemsetAsync(buf.ptr, 0xff, 8 * slots, st));  // keys = EMPTY
-    VH_HIP(hipMemsetAsync(static_cast<char *>(buf.ptr) + 8 * slots, 0, tab_bytes(slots, nv) - 8 * slots, st));
+    const uint64_t a = 8 * (slots + 1);
+    VH_HIP(hipMemsetAsync(buf.ptr, 0xff, a, st));  // keys = EMPTY
+    VH_HIP(hipMemsetAsync(static_cast<char *>(buf.ptr) + a, 0, tab_bytes(slots, nv) - a, st));
 }
 
 template <typename F> static void dispatch_nv(int nv, F &&f) {
@@ -970,14 +991,21 @@ template <typename F> static void dispatch_nv(int nv, F &&f) {
 
 #define VH_DISPATCH_KEY(code, K, ...)                                   \
     switch (code) {                                                     \
+    case VH_I64: { using K = int64_t; __VA_ARGS__; break; }             \
     case VH_I32: { using K = int32_t; __VA_ARGS__; break; }             \
     case VH_I16: { using K = int16_t; __VA_ARGS__; break; }             \
     case VH_I8: { using K = int8_t; __VA_ARGS__; break; }               \
+    case VH_U64: { using K = uint64_t; __VA_ARGS__; break; }            \
     case VH_U32: { using K = uint32_t; __VA_ARGS__; break; }            \
     case VH_U16: { using K = uint16_t; __VA_ARGS__; break; }            \
     case VH_U8: { using K = uint8_t; __VA_ARGS__; break; }              \
     default: fail(VH_ERR_ARG, "hashagg: unsupported key dtype");       \
     }
+
+template <typename F> static void dispatch_kb(int key_dtype, F &&f) {
+    if (key_bits_size(key_dtype) == 8) f(uint64_t());
+    else f(uint32_t());
+}
 
 static uint64_t next_pow2(uint64_t x) {
     uint64_t p = 1;
@@ -998,10 +1026,11 @@ static void ensure_table(vh_hashagg *h, uint64_t need) {
     DevBuf nt;
     table_alloc(nt, want, h->nv);
     const HaTable src = table_view(h->tab.ptr, h->slots, h->nv, h->vfloat);
-    const HaTable dst = table_view(nt.ptr, want, h->nv, h->vfloat);
+    HaTable dst = table_view(nt.ptr, want, h->nv, h->vfloat);
     dispatch_nv(h->nv, [&](auto nvc) {
         constexpr int NV = decltype(nvc)::value;
-        hipLaunchKernelGGL(k_ha_rehash<NV>, dim3(blocks_for(h->slots, 256, 8)), dim3(256), 0, stream(), src, h->slots, dst);
+        hipLaunchKernelGGL(k_ha_rehash<NV>, dim3(blocks_for(h->slots + 1, 256, 8)), dim3(256), 0, stream(), src,
+                           h->slots, dst);
     });
     VH_HIP(hipGetLastError());
     std::swap(h->tab.ptr, nt.ptr);
@@ -1009,6 +1038,7 @@ static void ensure_table(vh_hashagg *h, uint64_t need) {
     h->slots = want;
 }
 
+// used slots (not counting the side slot) and the error word
 static uint32_t read_used(vh_hashagg *h, uint32_t *err) {
     const HaTable g = table_view(h->tab.ptr, h->slots, h->nv, h->vfloat);
     uint32_t ue[2];
@@ -1030,6 +1060,7 @@ static int blocks_per_cu(const void *kernel, int threads, size_t lds) {
 static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const void *const *vals, uint64_t n) {
     hipStream_t st = stream();
     const int nv = h->nv;
+    const int kbs = key_bits_size(h->key_dtype);
     // ---- sample: fine bucket histogram + distinct estimate
     const uint64_t sslots = 1ull << 21;
     const uint64_t nbatch = (n + HA_BATCH - 1) / HA_BATCH;
@@ -1066,9 +1097,7 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     HaTable g = table_view(h->tab.ptr, h->slots, nv, h->vfloat, h->nnmask);
 
     uint32_t p_log2 = 0;
-    static const double target_keys = getenv("VH_HA_TARGET") ? atof(getenv("VH_HA_TARGET")) : (double)LT_TARGET_KEYS;
-    static const double unit_div = getenv("VH_HA_UNIT_DIV") ? atof(getenv("VH_HA_UNIT_DIV")) : 2.0;
-    while (p_log2 < HA_MAX_P_LOG2 && dest / (double)(1u << p_log2) > target_keys) p_log2++;
+    while (p_log2 < HA_MAX_P_LOG2 && dest / (double)(1u << p_log2) > LT_TARGET_KEYS) p_log2++;
 
     HaParams hp{};
     hp.keys = keys;
@@ -1079,7 +1108,7 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     hp.n = n;
     hp.p_log2 = p_log2;
     hp.P = 1u << p_log2;
-    const size_t lt_lds = lt_bytes(nv);
+    const size_t lt_lds = lt_bytes(nv, kbs);
     if (p_log2 == 0) {
         // ---- direct: one LDS table per workgroup over a contiguous row range
         int bpc = 1;
@@ -1103,7 +1132,7 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     for (uint32_t i = 0; i < FINE; i++) bh[i >> (HA_FINE_LOG2 - p_log2)] += fh[i];
 
     // ---- pass A geometry
-    const size_t lds_a = ha_scatter_lds_bytes(nv, P);
+    const size_t lds_a = ha_scatter_lds_bytes(nv, kbs, P);
     int bpc = 1;
     VH_DISPATCH_KEY(h->key_dtype, K, dispatch_nv(nv, [&](auto nvc) {
         constexpr int NV = decltype(nvc)::value;
@@ -1126,14 +1155,14 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     if (stride + rows_per_wg >= (uint64_t)HA_DEST_OVERFLOW) fail(VH_ERR_RUNTIME, "hashagg: region table too large");
     const uint64_t total = stride * W + (uint64_t)W * HA_THREADS;  // regions + dummy slots
     if (nv == 1) {
-        S.entries.ensure(16 * total + 64);  // packed {key, 0, value} entries
+        S.entries.ensure(16 * total + 64);  // packed {key, value} entries
     } else {
-        S.entries.ensure(4 * total + 16);
+        S.entries.ensure((uint64_t)kbs * total + 16);
         if (nv) S.vbits.ensure(8 * total * nv + 32);
     }
     // pass-B work units: buckets split over ranges of pass-A workgroups by expected size
     std::vector<HaUnit> units;
-    const double target = std::max(1.0, (double)n / ((double)cu_count() * unit_div));
+    const double target = std::max(1.0, (double)n / ((double)cu_count() * 2));
     for (uint32_t t = 0; t < P; t++) {
         const double e = (double)n * (double)bh[t] / (double)std::max<uint64_t>(sampled, 1);
         const uint32_t gq = (uint32_t)std::min<double>(W, std::max(1.0, std::ceil(e / target)));
@@ -1156,41 +1185,37 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     hp.cap = d_cap;
     hp.toff = d_toff;
     hp.fills = d_fills;
-    hp.ent = S.entries.as<uint32_t>();
+    hp.ent = S.entries.ptr;
     hp.dummy0 = stride * W;
-    static const uint32_t dbg = getenv("VH_HA_DEBUG") ? (uint32_t)atoi(getenv("VH_HA_DEBUG")) : 0u;
-    hp.debug = dbg;
     if (nv != 1)
         for (int v = 0; v < nv; v++) hp.vbits[v] = S.vbits.as<uint64_t>() + (uint64_t)v * total;
-    // the fast pass A: 4-byte keys, float64 values, 16-byte aligned columns; rows past the
-    // last multiple of 8 go straight to the HBM table
-    bool fast = dtype_itemsize(h->key_dtype) == 4 && aligned16(keys) && n >= 8;
+    // the fast pass A: 4- or 8-byte keys, float64 values, 16-byte aligned columns; rows past
+    // the last multiple of 8 go straight to the HBM table
+    const int kisz = dtype_itemsize(h->key_dtype);
+    bool fast = (kisz == 4 || kisz == 8) && aligned16(keys) && n >= 8;
     for (int v = 0; v < nv; v++) fast = fast && h->vdtype[v] == VH_F64 && aligned16(vals[v]);
     {
         TimedScope ts(fast ? "ha_scatter_f64" : "ha_scatter");
         if (fast) {
             const uint64_t n8 = n & ~uint64_t(7);
             hp.n = n8;
-            if (h->key_dtype == VH_I32) {
+            auto launch = [&](auto kc) {
+                using K = decltype(kc);
                 dispatch_nv(nv, [&](auto nvc) {
                     constexpr int NV = decltype(nvc)::value;
-                    hipLaunchKernelGGL((k_ha_scatter_f64<int32_t, NV>), dim3(W), dim3(HA_THREADS), lds_a, st, hp, g);
+                    hipLaunchKernelGGL((k_ha_scatter_f64<K, NV>), dim3(W), dim3(HA_THREADS), lds_a, st, hp, g);
                     if (n8 < n) {
                         HaParams ht = hp;
                         ht.n = n;
-                        hipLaunchKernelGGL((k_ha_tail<int32_t, NV>), dim3(1), dim3(64), 0, st, ht, g, n8);
+                        hipLaunchKernelGGL((k_ha_tail<K, NV>), dim3(1), dim3(64), 0, st, ht, g, n8);
                     }
                 });
-            } else {
-                dispatch_nv(nv, [&](auto nvc) {
-                    constexpr int NV = decltype(nvc)::value;
-                    hipLaunchKernelGGL((k_ha_scatter_f64<uint32_t, NV>), dim3(W), dim3(HA_THREADS), lds_a, st, hp, g);
-                    if (n8 < n) {
-                        HaParams ht = hp;
-                        ht.n = n;
-                        hipLaunchKernelGGL((k_ha_tail<uint32_t, NV>), dim3(1), dim3(64), 0, st, ht, g, n8);
-                    }
-                });
+            };
+            switch (h->key_dtype) {
+            case VH_I32: launch(int32_t()); break;
+            case VH_U32: launch(uint32_t()); break;
+            case VH_I64: launch(int64_t()); break;
+            default: launch(uint64_t());
             }
             hp.n = n;
         } else {
@@ -1203,12 +1228,34 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     }
     {
         TimedScope ts("ha_reduce");
-        dispatch_nv(nv, [&](auto nvc) {
-            constexpr int NV = decltype(nvc)::value;
-            hipLaunchKernelGGL(k_ha_reduce<NV>, dim3((unsigned)units.size()), dim3(HB_THREADS), lt_lds, st, hp, g, d_units);
+        dispatch_kb(h->key_dtype, [&](auto kbc) {
+            using KB = decltype(kbc);
+            dispatch_nv(nv, [&](auto nvc) {
+                constexpr int NV = decltype(nvc)::value;
+                hipLaunchKernelGGL((k_ha_reduce<KB, NV>), dim3((unsigned)units.size()), dim3(HB_THREADS), lt_lds, st, hp,
+                                   g, d_units);
+            });
         });
         VH_HIP(hipGetLastError());
     }
+}
+
+static size_t sort_tmp_bytes(int kbs, uint64_t m) {
+    size_t tmp = 0;
+    if (kbs == 8)
+        VH_HIP(rocprim::radix_sort_pairs(nullptr, tmp, (uint64_t *)nullptr, (uint64_t *)nullptr, (uint32_t *)nullptr,
+                                         (uint32_t *)nullptr, (size_t)m, 0, 64, stream()));
+    else
+        VH_HIP(rocprim::radix_sort_pairs(nullptr, tmp, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                         (uint32_t *)nullptr, (size_t)m, 0, 32, stream()));
+    return tmp;
+}
+
+// out buffer: skey | skey2 | sslot | sslot2 | counter | sort tmp | okey ocnt osum onn
+static char *out_results(vh_hashagg *h, uint64_t m, size_t tmp_bytes) {
+    const int kbs = key_bits_size(h->key_dtype);
+    const uint64_t ak = (kbs * m + 255) & ~255ull, as = (4 * m + 255) & ~255ull;
+    return h->out.as<char>() + 2 * ak + 2 * as + 256 + ((tmp_bytes + 255) & ~255ull);
 }
 
 }  // namespace vh
@@ -1217,7 +1264,8 @@ extern "C" {
 
 int vh_hashagg_create(int key_dtype, int nvals, const int *val_dtypes, uint32_t nonnull_mask, vh_hashagg **out) {
     VH_API_BEGIN
-    if (!key_dtype_ok(key_dtype)) fail(VH_ERR_ARG, "hashagg: key dtype must be an integer of <= 4 bytes");
+    dtype_itemsize(key_dtype);
+    if (!key_dtype_ok(key_dtype)) fail(VH_ERR_ARG, "hashagg: the key must be an integer column");
     if (nvals < 0 || nvals > HA_MAX_V) fail(VH_ERR_ARG, "hashagg: at most 2 value columns");
     auto h = std::make_unique<vh_hashagg>();
     h->key_dtype = key_dtype;
@@ -1254,7 +1302,7 @@ int vh_hashagg_update(vh_hashagg *h, const void *keys, const void *const *vals, 
         const void *vp[HA_MAX_V] = {nullptr, nullptr};
         for (int v = 0; v < h->nv; v++) vp[v] = static_cast<const char *>(vals[v]) + r0 * dtype_itemsize(h->vdtype[v]);
         if (loc == VH_LOC_HOST) {
-            uint64_t bytes = m * kisz;
+            uint64_t bytes = (m * kisz + 255) & ~255ull;
             for (int v = 0; v < h->nv; v++) bytes += ((m * dtype_itemsize(h->vdtype[v]) + 255) & ~255ull);
             S.stage.ensure(bytes + 512);
             char *d = S.stage.as<char>();
@@ -1270,14 +1318,9 @@ int vh_hashagg_update(vh_hashagg *h, const void *keys, const void *const *vals, 
         }
         update_device(h, S, kp, vp, m);
         uint32_t err = 0;
-        read_used(h, &err);
+        const uint32_t used = read_used(h, &err);
         if (err & 2) fail(VH_ERR_RUNTIME, "hashagg: hash table overflow");
-        if (err & 1) {  // past 3/4: grow now, before the next update fills it
-            const HaTable g = table_view(h->tab.ptr, h->slots, h->nv, h->vfloat);
-            const uint32_t used = read_used(h, nullptr);
-            ensure_table(h, 2 * (uint64_t)used);
-            (void)g;
-        }
+        if (err & 1) ensure_table(h, 2 * (uint64_t)used);  // past 3/4: grow before the next update
         h->rows += m;
     }
     VH_API_END
@@ -1290,38 +1333,44 @@ int vh_hashagg_finish(vh_hashagg *h, uint64_t *ngroups) {
         h->finished = true;
         h->ngroups = 0;
         if (h->slots) {
-            const uint64_t m = read_used(h, nullptr);
+            const HaTable g = table_view(h->tab.ptr, h->slots, h->nv, h->vfloat);
+            uint64_t side = 0;
+            VH_HIP(hipMemcpyAsync(&side, g.cnt + h->slots, 8, hipMemcpyDeviceToHost, st));
+            const uint64_t m = read_used(h, nullptr) + (side ? 1 : 0);
             h->ngroups = m;
             if (m) {
-                const HaTable g = table_view(h->tab.ptr, h->slots, h->nv, h->vfloat);
-                size_t tmp_bytes = 0;
-                VH_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                                 (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)m, 0, 32, st));
-                // scratch: skey | sslot | skey2 | sslot2 | counter | tmp ; outputs after
-                const uint64_t a = (4 * m + 255) & ~255ull;
+                const int kbs = key_bits_size(h->key_dtype);
+                const size_t tmp_bytes = sort_tmp_bytes(kbs, m);
+                const uint64_t ak = (kbs * m + 255) & ~255ull, as = (4 * m + 255) & ~255ull;
                 const uint64_t out_bytes = 8 * m * (2 + 2 * (uint64_t)h->nv);
-                h->out.ensure(4 * a + 256 + tmp_bytes + out_bytes + 256);
+                h->out.ensure(2 * ak + 2 * as + 256 + ((tmp_bytes + 255) & ~255ull) + out_bytes + 256);
                 char *base = h->out.as<char>();
-                uint32_t *skey = reinterpret_cast<uint32_t *>(base), *sslot = reinterpret_cast<uint32_t *>(base + a);
-                uint32_t *skey2 = reinterpret_cast<uint32_t *>(base + 2 * a), *sslot2 = reinterpret_cast<uint32_t *>(base + 3 * a);
-                uint32_t *counter = reinterpret_cast<uint32_t *>(base + 4 * a);
-                void *tmp = base + 4 * a + 256;
-                char *outp = base + 4 * a + 256 + ((tmp_bytes + 255) & ~255ull);
+                char *skey = base, *skey2 = base + ak;
+                uint32_t *sslot = reinterpret_cast<uint32_t *>(base + 2 * ak);
+                uint32_t *sslot2 = reinterpret_cast<uint32_t *>(base + 2 * ak + as);
+                uint32_t *counter = reinterpret_cast<uint32_t *>(base + 2 * ak + 2 * as);
+                void *tmp = base + 2 * ak + 2 * as + 256;
+                char *outp = out_results(h, m, tmp_bytes);
                 VH_HIP(hipMemsetAsync(counter, 0, 4, st));
                 TimedScope ts("ha_finish");
                 const int sg = key_signed(h->key_dtype);
-                hipLaunchKernelGGL(k_ha_compact, dim3(blocks_for(h->slots, 256, 8)), dim3(256), 0, st, g.keys, h->slots,
-                                   sg, skey, sslot, counter);
-                VH_HIP(hipGetLastError());
-                VH_HIP(rocprim::radix_sort_pairs(tmp, tmp_bytes, skey, skey2, sslot, sslot2, (size_t)m, 0, 32, st));
                 int64_t *okey = reinterpret_cast<int64_t *>(outp);
                 int64_t *ocnt = okey + m;
                 uint64_t *osum = reinterpret_cast<uint64_t *>(ocnt + m);
                 int64_t *onn = reinterpret_cast<int64_t *>(osum + m * h->nv);
-                dispatch_nv(h->nv, [&](auto nvc) {
-                    constexpr int NV = decltype(nvc)::value;
-                    hipLaunchKernelGGL(k_ha_gather<NV>, dim3(blocks_for(m, 256, 8)), dim3(256), 0, st, g, skey2, sslot2, m,
-                                       sg, okey, ocnt, osum, onn);
+                dispatch_kb(h->key_dtype, [&](auto kbc) {
+                    using KB = decltype(kbc);
+                    hipLaunchKernelGGL(k_ha_compact<KB>, dim3(blocks_for(h->slots + 1, 256, 8)), dim3(256), 0, st, g.keys,
+                                       g.cnt, h->slots, sg, reinterpret_cast<KB *>(skey), sslot, counter);
+                    VH_HIP(hipGetLastError());
+                    size_t tb = tmp_bytes;
+                    VH_HIP(rocprim::radix_sort_pairs(tmp, tb, reinterpret_cast<KB *>(skey), reinterpret_cast<KB *>(skey2),
+                                                     sslot, sslot2, (size_t)m, 0, 8 * (int)sizeof(KB), st));
+                    dispatch_nv(h->nv, [&](auto nvc) {
+                        constexpr int NV = decltype(nvc)::value;
+                        hipLaunchKernelGGL((k_ha_gather<KB, NV>), dim3(blocks_for(m, 256, 8)), dim3(256), 0, st, g,
+                                           reinterpret_cast<const KB *>(skey2), sslot2, m, sg, okey, ocnt, osum, onn);
+                    });
                 });
                 VH_HIP(hipGetLastError());
             }
@@ -1331,18 +1380,14 @@ int vh_hashagg_finish(vh_hashagg *h, uint64_t *ngroups) {
     VH_API_END
 }
 
-/* outputs (host, ngroups items each): keys as int64, count(*) int64, per value column its
-   sum (double / int64 / uint64 bits, 8 bytes) and non-NaN count int64 */
+/* outputs (host, ngroups items each): keys as int64 (uint64 keys: their bits), count(*)
+   int64, per value column its sum (double / int64 / uint64 bits, 8 bytes) and non-NaN count */
 int vh_hashagg_read(vh_hashagg *h, int64_t *keys, int64_t *counts, void *const *sums, int64_t *const *nonnull) {
     VH_API_BEGIN
     if (!h->finished) fail(VH_ERR_RUNTIME, "hashagg: read before finish");
     const uint64_t m = h->ngroups;
     if (!m) return VH_OK;
-    const uint64_t a = (4 * m + 255) & ~255ull;
-    size_t tmp_bytes = 0;
-    VH_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                     (uint32_t *)nullptr, (size_t)m, 0, 32, stream()));
-    const char *outp = h->out.as<char>() + 4 * a + 256 + ((tmp_bytes + 255) & ~255ull);
+    const char *outp = out_results(h, m, sort_tmp_bytes(key_bits_size(h->key_dtype), m));
     const int64_t *okey = reinterpret_cast<const int64_t *>(outp);
     const int64_t *ocnt = okey + m;
     const uint64_t *osum = reinterpret_cast<const uint64_t *>(ocnt + m);
@@ -1355,6 +1400,30 @@ int vh_hashagg_read(vh_hashagg *h, int64_t *keys, int64_t *counts, void *const *
         if (nonnull && nonnull[v]) VH_HIP(hipMemcpyAsync(nonnull[v], onn + (uint64_t)v * m, 8 * m, hipMemcpyDeviceToHost, st));
     }
     VH_HIP(hipStreamSynchronize(st));
+    VH_API_END
+}
+
+int vh_combine_keys(uint64_t n, int nkeys, const void *const *cols, const int *dtypes, const int64_t *mins,
+                    const int64_t *mults, int64_t *out) {
+    VH_API_BEGIN
+    if (nkeys < 1 || nkeys > HC_MAX_KEYS) fail(VH_ERR_ARG, "combine_keys: 1..8 key columns");
+    HcParams p{};
+    p.nkeys = nkeys;
+    for (int j = 0; j < nkeys; j++) {
+        dtype_itemsize(dtypes[j]);
+        if (!key_dtype_ok(dtypes[j])) fail(VH_ERR_ARG, "combine_keys: integer key columns only");
+        if (resolve_loc(cols[j], VH_LOC_AUTO) != VH_LOC_DEVICE) fail(VH_ERR_ARG, "combine_keys: device columns only");
+        p.col[j] = cols[j];
+        p.dtype[j] = dtypes[j];
+        p.min[j] = mins[j];
+        p.mult[j] = mults[j];
+    }
+    if (resolve_loc(out, VH_LOC_AUTO) != VH_LOC_DEVICE) fail(VH_ERR_ARG, "combine_keys: device output only");
+    if (n) {
+        TimedScope ts("combine_keys");
+        hipLaunchKernelGGL(k_combine_keys, dim3(blocks_for(n, 256, 8)), dim3(256), 0, stream(), p, n, out);
+        VH_HIP(hipGetLastError());
+    }
     VH_API_END
 }
 

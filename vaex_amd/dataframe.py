@@ -483,8 +483,12 @@ class DataFrame:
     def groupby(self, by=None, agg=None, sort=False, assume_sparse="auto", row_limit=None, copy=True,
                 progress=None, delay=False):
         """dataframe.py:6622-6683."""
-        from .groupby import GroupBy, _dense_range, parse_actions
+        from .groupby import GroupBy, _dense_range, groupby_multikey, parse_actions
         dense_ranges = {}
+        if agg is not None and assume_sparse != True and isinstance(by, (list, tuple)) and len(by) > 1:  # noqa: E712
+            res = groupby_multikey(self, by, agg, sort=sort, row_limit=row_limit)
+            if res is not None:
+                return res
         if agg is not None and assume_sparse != True:  # noqa: E712
             # A single integer key: a dense value range bins like a categorical (min/max
             # pass + BinnerOrdinal grid, GrouperDense); otherwise count/sum/mean run as one

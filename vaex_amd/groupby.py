@@ -13,7 +13,7 @@ import numpy as np
 
 from . import agg as vagg
 from .dataframe import DataFrame, Expression, RowLimitException
-from .utils import extract_central_part, required_dtype_for_max
+from .utils import extract_central_part, label_dtype
 
 
 class BinnerBase:
@@ -30,7 +30,8 @@ class Grouper(BinnerBase):
         oset = df_original._set(self.expression, unique_limit=row_limit)
         self.bin_values = oset.key_array()
         if self.bin_values.dtype.kind == "i" and len(self.bin_values):  # groupby.py:133-135
-            self.bin_values = self.bin_values.astype(required_dtype_for_max(int(self.bin_values.max())))
+            self.bin_values = self.bin_values.astype(
+                label_dtype(self.bin_values.dtype, self.bin_values.min(), self.bin_values.max()))
         self.has_null = oset.has_null
         self.null_value = oset.null_value
         self.sort_indices = None
@@ -90,7 +91,7 @@ class GrouperDense(BinnerBase):
         self.min_value = int(vmin)
         self.N = int(vmax) - int(vmin) + 1
         dtype = self.df.data_type(self.expression)
-        self.value_dtype = required_dtype_for_max(max(abs(int(vmin)), abs(int(vmax))))
+        self.value_dtype = label_dtype(dtype, vmin, vmax)
         self._bin_values = None
         self.sort_indices = None
         self.binner = self.df._binner_ordinal(self.expression, self.N, self.min_value)
@@ -130,6 +131,103 @@ def _dense_range(df, expression):
     if span > DENSE_KEY_MAX or span > 4 * n + 1024:
         return None
     return int(vmin), int(vmax)
+
+
+COMBINE_OCCUPANCY = 10  # groupby.py:329-333: combine when rows / cells < 10
+COMBINED_KEY = "__vaex_amd_combined_key"
+
+
+def _key_ranges(df, by):
+    """[(name, min, max)] when every key of a multi-key groupby is a plain unmasked native
+    integer column of an unfiltered frame with exact (< 2**53) limits, else None."""
+    if df.filtered or len(by) < 2:
+        return None
+    names = []
+    for b in by:
+        if not isinstance(b, str) and not isinstance(b, Expression):
+            return None
+        name = str(b)
+        col = df.columns.get(name)
+        if col is None or df.is_category(name) or np.ma.isMaskedArray(col) or name in names:
+            return None
+        dt = np.dtype(col.dtype)
+        if dt.kind not in "iu" or not dt.isnative or (isinstance(col, np.ndarray) and col.ndim != 1):
+            return None
+        names.append(name)
+    if df.length_unfiltered() == 0:
+        return None
+    promises = [df.minmax(name, delay=True) for name in names]
+    df.execute()
+    out = []
+    for name, p in zip(names, promises):
+        vmin, vmax = (int(x) for x in p.get())
+        if not (abs(vmin) < 2 ** 53 and abs(vmax) < 2 ** 53):
+            return None
+        out.append((name, vmin, vmax))
+    return out
+
+
+def groupby_multikey(df, by, agg, sort=False, row_limit=None):
+    """Multi-key ``groupby(by=[k1, k2, ...], agg=...)`` over integer keys (groupby.py:248-333).
+
+    With enough rows per cell (rows / prod(spans) >= 10, the reference's ``combine='auto'``
+    test) every key becomes a dense grouper and the cartesian grid is binned directly.
+    Otherwise the keys are combined on the GPU into one int64 key, the cartesian ordinal
+    ``sum_j (k_j - min_j) * prod(span_{j+1..})`` (``vh_combine_keys``, first key most
+    significant), which takes the single-key routes (dense grid, fused hash pass, or the
+    set grouper for other aggregators); the labels are decoded back per key.  The
+    reference combines the per-key set ordinals instead of value offsets; both give the
+    lexicographic order of ``sort=True``.  Returns None when the keys do not qualify
+    (non-integer, masked, filtered frame, spans whose product reaches 2**62)."""
+    import ctypes
+    from . import _lib
+    from .device import DeviceArray
+    ranges = _key_ranges(df, by)
+    if ranges is None:
+        return None
+    spans = [vmax - vmin + 1 for _, vmin, vmax in ranges]
+    cells = 1
+    for sp in spans:
+        cells *= sp
+    if cells >= 2 ** 62:
+        return None
+    n = df.length_unfiltered()
+    names = [name for name, _, _ in ranges]
+    if n / cells >= COMBINE_OCCUPANCY and all(sp <= DENSE_KEY_MAX for sp in spans):
+        dense_ranges = {name: (vmin, vmax) for name, vmin, vmax in ranges}
+        return GroupBy(df, by=names, sort=sort, row_limit=row_limit, dense_ranges=dense_ranges).agg(agg)
+    mults = [1] * len(spans)
+    for i in range(len(spans) - 2, -1, -1):
+        mults[i] = mults[i + 1] * spans[i + 1]
+    cols, keep = [], []
+    for name in names:
+        c = df.columns[name]
+        if not isinstance(c, DeviceArray):
+            c = DeviceArray.from_numpy(np.ascontiguousarray(c))
+            keep.append(c)
+        cols.append(c)
+    combined = DeviceArray.empty(n, np.int64)
+    k = len(cols)
+    _lib.call("vh_combine_keys", n, k, (ctypes.c_void_p * k)(*[c.ptr for c in cols]),
+              (ctypes.c_int * k)(*[_lib.dtype_code(c.dtype)[0] for c in cols]),
+              (ctypes.c_int64 * k)(*[vmin for _, vmin, _ in ranges]), (ctypes.c_int64 * k)(*mults), combined.ptr)
+    del keep
+    # the aggregators are named against the original frame (callables expand over its
+    # non-key columns), then evaluated on a copy that also holds the combined key
+    actions = [(name, a) for name, a in parse_actions(df, agg, names)]
+    tmp = df.copy()
+    tmp.add_column(COMBINED_KEY, combined)
+    res = tmp.groupby(COMBINED_KEY, agg=actions, sort=sort, row_limit=row_limit)
+    ck = np.asarray(res.columns[COMBINED_KEY], dtype=np.int64)
+    columns = {}
+    for (name, vmin, vmax), sp, mult in zip(ranges, spans, mults):
+        kd = np.dtype(df.columns[name].dtype)
+        labels = (ck // mult) % sp + vmin
+        columns[name] = labels.astype(label_dtype(kd, vmin, vmax) if len(labels) else kd)
+    for name, values in res.columns.items():
+        if name != COMBINED_KEY:
+            columns[name] = values
+    return DataFrame(columns)
 
 
 class GrouperCategory(BinnerBase):

@@ -1,6 +1,6 @@
 """Fused hash groupby (``libvaexhip`` ``vh_hashagg_*``, ``vaex_amd/csrc/hashagg.hip``).
 
-``groupby(key).agg(...)`` of one integer key column (<= 4 bytes) with count / sum / mean
+``groupby(key).agg(...)`` of one integer key column (any width) with count / sum / mean
 aggregates over at most two numeric value columns runs as ONE hash-partitioned pass over
 the data instead of the reference's two passes (ordered_set build, then
 ``_ordinal_values`` + ``BinnerOrdinal`` + ``AggCount``/``AggSum``; groupby.py:97-168,
@@ -15,9 +15,9 @@ import numpy as np
 
 from . import _lib
 from .device import DeviceArray
-from .utils import required_dtype_for_max
+from .utils import label_dtype
 
-KEY_DTYPES = {"int8", "int16", "int32", "uint8", "uint16", "uint32"}
+KEY_DTYPES = {"int8", "int16", "int32", "int64", "uint8", "uint16", "uint32", "uint64"}
 VALUE_KINDS = "fiub"
 
 
@@ -89,12 +89,14 @@ class HashAgg:
         npp = (ctypes.c_void_p * nv)(*[c.ctypes.data if c is not None else None for c in nonnull])
         if m:
             _lib.call("vh_hashagg_read", self._h, keys.ctypes.data, counts.ctypes.data, sp, npp)
+        if self.key_dtype == np.uint64:
+            keys = keys.view(np.uint64)  # the library returns the key bits
         return keys, counts, sums, nonnull
 
 
 def eligible_key(df, by):
-    """The key column name when ``by`` is one plain, unmasked, native integer column of
-    <= 4 bytes on an unfiltered frame (the fused path's key), else None."""
+    """The key column name when ``by`` is one plain, unmasked, native integer column on an
+    unfiltered frame (the fused path's key), else None."""
     if isinstance(by, (list, tuple)):
         if len(by) != 1:
             return None
@@ -186,8 +188,8 @@ def try_groupby(df, by, actions, parse, sort=False, row_limit=None):
                                 f"than the allowed row limit of {row_limit:,}")
     kdt = np.dtype(key.dtype)
     labels = keys.astype(kdt)
-    if kdt.kind == "i" and len(labels):  # groupby.py:133-135
-        labels = labels.astype(required_dtype_for_max(int(labels.max())))
+    if len(labels):  # groupby.py:131-133 (keys are sorted)
+        labels = labels.astype(label_dtype(kdt, labels[0], labels[-1]))
     columns = {by: labels}
     for name, op, vi in ops:
         if op == "count":

@@ -30,6 +30,20 @@ def required_dtype_for_max(N, signed=True):
     raise ValueError(f"Cannot store a max value on {N} inside an uint64/int64")
 
 
+def label_dtype(key_dtype, vmin, vmax):
+    """dtype of groupby labels for an integer key spanning [vmin, vmax]: signed keys are
+    down-cast to ``required_dtype_for_max(max)`` (groupby.py:131-133), unsigned keep their
+    dtype.  Unlike the reference, a minimum below that dtype's range widens it instead of
+    wrapping (the reference's astype would wrap e.g. int32 -1000 into int8)."""
+    key_dtype = np.dtype(key_dtype)
+    if key_dtype.kind != "i":
+        return key_dtype
+    dt = required_dtype_for_max(int(vmax))
+    while int(vmin) < np.iinfo(dt).min:
+        dt = required_dtype_for_max(np.iinfo(dt).max + 1)
+    return dt
+
+
 def _expand_shape(shape, dimension):
     """utils.py:793-798."""
     if isinstance(shape, (tuple, list)):
