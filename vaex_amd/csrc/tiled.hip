@@ -186,12 +186,12 @@ __device__ inline uint32_t block_exclusive_scan(const uint32_t *in, uint32_t *ou
 struct ScatterLds {
     double *sv;
     uint64_t *sp;
-    uint32_t *hist, *boff, *base, *lim, *wave_sums;
+    uint32_t *hist, *boff, *base, *lim, *dbase, *wave_sums;
 };
 
 // LDS bytes of pass A (must match scatter_lds)
 __host__ __device__ inline size_t scatter_lds_bytes(int nv, uint32_t T) {
-    return (size_t)8 * nv * TA_BATCH + (size_t)8 * TA_BATCH + 16 * (size_t)T + 64;
+    return (size_t)8 * nv * TA_BATCH + (size_t)8 * TA_BATCH + 20 * (size_t)T + 64;
 }
 
 template <int NV> __device__ inline ScatterLds scatter_lds(unsigned char *raw, uint32_t T) {
@@ -202,7 +202,8 @@ template <int NV> __device__ inline ScatterLds scatter_lds(unsigned char *raw, u
     l.boff = l.hist + T;
     l.base = l.boff + T;
     l.lim = l.base + T;
-    l.wave_sums = l.lim + T;
+    l.dbase = l.lim + T;
+    l.wave_sums = l.dbase + T;
     return l;
 }
 
@@ -279,6 +280,91 @@ __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, co
     }
 }
 
+// Batch commit of the fast kernels, three LDS barriers per batch:
+//   B1 (every rank taken) -> wave 0 scans the tile histogram: boff = exclusive offsets,
+//   dbase = region write base - boff (a row sorted to position k of tile t goes to
+//   dbase[t] + k), then advances base and clears hist -> B2 -> rows stage their sorted
+//   (tile << 16 | cell) key and values -> B3 -> sorted runs streamed to the regions.
+// The next batch's ranking may start while slower waves still stream: it only touches
+// hist, which the scan already cleared; boff/dbase/sp/sv are rewritten only after the next
+// B1, which every wave reaches after its stream-out.
+__device__ inline void fast_scan(const ScatterLds &l, uint32_t T) {
+    if (threadIdx.x >= 64) return;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t per = (T + 63) / 64;
+    const uint32_t t0 = lane * per;
+    uint32_t s = 0;
+    for (uint32_t t = t0; t < t0 + per && t < T; t++) s += l.hist[t];
+    uint32_t inc = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(inc, off, 64);
+        if ((int)lane >= off) inc += y;
+    }
+    uint32_t acc = inc - s;
+    for (uint32_t t = t0; t < t0 + per && t < T; t++) {
+        const uint32_t h = l.hist[t], b = l.base[t];
+        l.boff[t] = acc;
+        l.dbase[t] = b - acc;
+        l.base[t] = b + h;
+        l.hist[t] = 0;
+        acc += h;
+    }
+    if (lane == 63) l.wave_sums[0] = inc;
+}
+
+template <int NV>
+__device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &fa, const TileParams &tp, uint32_t T,
+                                         uint64_t region0, const uint32_t *key, const int32_t *rank,
+                                         const double (*vals)[NV > 0 ? NV : 1], uint32_t count_mask,
+                                         const uint32_t *keyed_slot_of) {
+    uint32_t *sk = reinterpret_cast<uint32_t *>(l.sp);
+    lds_barrier();
+    fast_scan(l, T);
+    lds_barrier();
+    const uint32_t tot = l.wave_sums[0];
+#pragma unroll
+    for (int r = 0; r < TA_RPT; r++) {
+        if (rank[r] < 0) continue;
+        const uint32_t pos = l.boff[key[r] >> 16] + (uint32_t)rank[r];
+        sk[pos] = key[r];
+#pragma unroll
+        for (int s = 0; s < NV; s++) l.sv[s * TA_BATCH + pos] = vals[r][s];
+    }
+    lds_barrier();
+    for (uint32_t k = threadIdx.x; k < tot; k += TA_THREADS) {
+        const uint32_t kk = sk[k];
+        const uint32_t t = kk >> 16;
+        const uint32_t dest = l.dbase[t] + k;
+        if (dest < l.lim[t]) {
+            const uint64_t e = region0 + dest;
+            reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)kk;
+#pragma unroll
+            for (int s = 0; s < NV; s++) tp.values[s][e] = l.sv[s * TA_BATCH + k];
+        } else {
+            // region overflow (a sampling miss): apply the staged row with global atomics
+            const uint64_t c = ((uint64_t)t << tp.s_log2) | (kk & 0xffffu);
+            #pragma unroll
+            for (int a = 0; a < MAX_FUSED_AGGS; a++) {
+                if (a >= fa.na) break;
+                bool take = (count_mask >> a) & 1;
+                if constexpr (NV > 0) {
+                    if (!take) {
+                        const double v = l.sv[keyed_slot_of[a] * TA_BATCH + k];
+                        take = v == v;
+                    }
+                }
+                if (!take) continue;
+                if (fa.a[a].kind == VH_AGG_COUNT) {
+                    atomicAdd((unsigned long long *)fa.a[a].grid + c, 1ULL);
+                } else if constexpr (NV > 0) {
+                    atomicAdd(reinterpret_cast<double *>(fa.a[a].grid) + c, l.sv[tp.val_slot[a] * TA_BATCH + k]);
+                }
+            }
+        }
+    }
+}
+
 // generic pass A: any binner kinds/dtypes, masks and keep flags
 template <int ND, int NV>
 __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
@@ -335,7 +421,6 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const uint32_t T = tp.ntiles;
     const ScatterLds l = scatter_lds<NV>(lds_raw, T);
-    __shared__ uint32_t s_total;
     scatter_lds_init(l, tp, T);
     __syncthreads();
     const double *col[NC];
@@ -374,7 +459,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan
     load(row_begin, cur);
     for (uint64_t b0 = row_begin; b0 < row_end; b0 += TA_BATCH) {
         load(b0 + TA_BATCH, nxt);
-        uint32_t tile[TA_RPT], ent[TA_RPT];
+        uint32_t key[TA_RPT];
         int32_t rank[TA_RPT];
         double vals[TA_RPT][NV > 0 ? NV : 1];
 #pragma unroll
@@ -402,19 +487,18 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan
                             if (s == (int)sl && vals[r][s] == vals[r][s]) f |= 1u << k;
                     }
                 }
-                tile[r] = (uint32_t)(c >> tp.s_log2);
-                ent[r] = ((uint32_t)c & smask) | (f << 16);
-                if (f && !(tp.debug & 4)) rank[r] = (int32_t)atomicAdd(&l.hist[tile[r]], 1u);
-                if (tp.debug & 4) asm volatile("" :: "v"(ent[r]), "v"(tile[r]));
+                const uint32_t t = (uint32_t)(c >> tp.s_log2);
+                key[r] = (t << 16) | ((uint32_t)c & smask);
+                if (f) rank[r] = (int32_t)atomicAdd(&l.hist[t], 1u);
             }
         }
-        if (!(tp.debug & 2)) batch_commit<NV>(l, fa, tp, T, region0, tile, ent, rank, vals, &s_total);
+        batch_commit_fast<NV>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
 #pragma unroll
         for (int q = 0; q < PAIRS; q++)
 #pragma unroll
             for (int c = 0; c < NC; c++) cur[q][c] = nxt[q][c];
-        lds_barrier();
     }
+    lds_barrier();
     for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.base[t] - (uint32_t)tp.toff[t];
 }
 
@@ -437,7 +521,6 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const uint32_t T = tp.ntiles;
     const ScatterLds l = scatter_lds<NV>(lds_raw, T);
-    __shared__ uint32_t s_total;
     scatter_lds_init(l, tp, T);
     __syncthreads();
     const int32_t *keys = reinterpret_cast<const int32_t *>(p.b[0].data);
@@ -475,7 +558,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
     load(row_begin, cur);
     for (uint64_t b0 = row_begin; b0 < row_end; b0 += TA_BATCH) {
         load(b0 + TA_BATCH, nxt);
-        uint32_t tile[TA_RPT], ent[TA_RPT];
+        uint32_t key[TA_RPT];
         int32_t rank[TA_RPT];
         double vals[TA_RPT][NV > 0 ? NV : 1];
 #pragma unroll
@@ -498,15 +581,15 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
                             if (s == (int)sl && vals[r][s] == vals[r][s]) f |= 1u << k;
                     }
                 }
-                tile[r] = (uint32_t)(c >> tp.s_log2);
-                ent[r] = ((uint32_t)c & smask) | (f << 16);
-                if (f) rank[r] = (int32_t)atomicAdd(&l.hist[tile[r]], 1u);
+                const uint32_t t = (uint32_t)(c >> tp.s_log2);
+                key[r] = (t << 16) | ((uint32_t)c & smask);
+                if (f) rank[r] = (int32_t)atomicAdd(&l.hist[t], 1u);
             }
         }
-        batch_commit<NV>(l, fa, tp, T, region0, tile, ent, rank, vals, &s_total);
+        batch_commit_fast<NV>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
         cur = nxt;
-        lds_barrier();
     }
+    lds_barrier();
     for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.base[t] - (uint32_t)tp.toff[t];
 }
 
