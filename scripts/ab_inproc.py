@@ -1,0 +1,74 @@
+"""Same-process A/B of library builds on the C2 workload: the builds are loaded side by
+side and their steps interleaved, so clock and box drift hit every build alike.
+
+usage: python scripts/ab_inproc.py lib1.so lib2.so ... [--rows 1e9] [--rounds 12]
+Prints the median step / per-kernel times per build (count+sum and count-only)."""
+import argparse
+import gc
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from vaex_amd import _lib, superagg  # noqa: E402
+from vaex_amd.device import DeviceArray  # noqa: E402
+
+KERNELS = ["tile_sample", "tile_scatter_f64", "tile_reduce"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--rows", type=float, default=1e9)
+    ap.add_argument("--rounds", type=int, default=12)
+    a = ap.parse_args()
+    libs = [_lib.load_library(os.path.abspath(p)) for p in a.libs]
+    _lib._lib = libs[0]
+    n = int(a.rows)
+    x = DeviceArray.random(n, "normal", seed=2)
+    y = DeviceArray.random(n, "normal", seed=3)
+    w = DeviceArray.random(n, "uniform", seed=4)
+
+    def step(with_sum):
+        bx = superagg.BinnerScalar_float64("x", -4.0, 4.0, 1024)
+        by = superagg.BinnerScalar_float64("y", -4.0, 4.0, 1024)
+        bx.set_data(x)
+        by.set_data(y)
+        grid = superagg.Grid([bx, by])
+        aggs = [superagg.AggCount_int64(grid)]
+        if with_sum:
+            aggs.append(superagg.AggSum_float64(grid))
+            aggs[1].set_data(w, 0)
+        grid.bin(aggs)
+
+    res = {(i, ws): {k: [] for k in KERNELS} for i in range(len(libs)) for ws in (True, False)}
+    for rnd in range(a.rounds + 1):
+        for i, L in enumerate(libs):
+            _lib._lib = L
+            for ws in (True, False):
+                _lib.synchronize()
+                _lib.timing_reset()
+                _lib.timing_enable(True)
+                step(ws)
+                _lib.synchronize()
+                _lib.timing_enable(False)
+                gc.collect()
+                if rnd == 0:
+                    continue  # warm-up round
+                for k in KERNELS:
+                    c, ms = _lib.timing_read(k)
+                    if c:
+                        res[(i, ws)][k].append(ms / c)
+        print(f"round {rnd} done", flush=True)
+    _lib._lib = libs[0]
+    for ws in (True, False):
+        print("count+sum" if ws else "count-only")
+        for i, p in enumerate(a.libs):
+            med = {k: round(statistics.median(v), 3) for k, v in res[(i, ws)].items() if v}
+            mn = {k: round(min(v), 3) for k, v in res[(i, ws)].items() if v}
+            print(f"  {os.path.basename(p):28s} median {med}  min {mn}")
+
+
+if __name__ == "__main__":
+    main()

@@ -312,3 +312,29 @@ def test_host_staging_multiple_chunks():
     c = sa().AggCount_int64(grid)
     grid.bin([c])
     np.testing.assert_array_equal(np.asarray(c), _oracle_grid([spec], "count"))
+
+
+@pytest.mark.parametrize("bins,nsums", [(3000, 1), (4000, 2), (2000, 0)])
+def test_tiled_path_many_tiles(bins, nsums):
+    """Grids with 1000-4000 tiles: the multi-batch staging of pass A no longer fits the LDS,
+    so the one-batch fast kernel (or the global-atomic path) takes over; same results."""
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(bins)
+    n = 3_000_000
+    x, y = rng.uniform(-1.1, 1.1, n), rng.uniform(-1.1, 1.1, n)
+    ws = [rng.random(n) for _ in range(nsums)]
+    bx = oracle.Binner("scalar", x, vmin=-1, vmax=1, bins=bins)
+    by = oracle.Binner("scalar", y, vmin=-1, vmax=1, bins=bins)
+    gx, gy = sa().BinnerScalar_float64("x", -1, 1, bins), sa().BinnerScalar_float64("y", -1, 1, bins)
+    gx.set_data(DeviceArray.from_numpy(x))
+    gy.set_data(DeviceArray.from_numpy(y))
+    grid = sa().Grid([gx, gy])
+    aggs = [sa().AggCount_int64(grid)]
+    for w in ws:
+        s = sa().AggSum_float64(grid)
+        s.set_data(DeviceArray.from_numpy(w), 0)
+        aggs.append(s)
+    grid.bin(aggs)
+    np.testing.assert_array_equal(np.asarray(aggs[0]), _oracle_grid([bx, by], "count"))
+    for a, w in zip(aggs[1:], ws):
+        np.testing.assert_allclose(np.asarray(a), _oracle_grid([bx, by], "sum", data=w), rtol=1e-6, atol=1e-12)

@@ -89,21 +89,26 @@ class HipError(RuntimeError):
     """A failed libvaexhip call (the reference raises RuntimeError from its C++ too)."""
 
 
+def load_library(path):
+    """ctypes handle of a libvaexhip build with every C-ABI signature bound."""
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} is missing: the HIP library must be built "
+            "(python -c 'import __graft_entry__ as g; g.build()' or make -C vaex_amd/csrc)")
+    L = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    if L.vh_abi_version() != 1:
+        raise ImportError("libvaexhip ABI version mismatch")
+    return L
+
+
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(
-                f"{LIB_PATH} is missing: the HIP library must be built "
-                "(python -c 'import __graft_entry__ as g; g.build()' or make -C vaex_amd/csrc)")
-        L = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in SIGNATURES.items():
-            f = getattr(L, name)
-            f.restype = res
-            f.argtypes = args
-        if L.vh_abi_version() != 1:
-            raise ImportError("libvaexhip ABI version mismatch")
-        _lib = L
+        _lib = load_library(LIB_PATH)
     return _lib
 
 

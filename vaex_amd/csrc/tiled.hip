@@ -46,6 +46,9 @@ constexpr int TA_THREADS = VH_TA_THREADS;
 #ifndef VH_TA_RPT
 #define VH_TA_RPT 8
 #endif
+#ifndef VH_TA_DRAIN
+#define VH_TA_DRAIN 1  // fast pass A: the prefetched batch lands before the commit's stores
+#endif
 #ifndef VH_TB_THREADS
 #define VH_TB_THREADS 1024
 #endif
@@ -57,6 +60,7 @@ constexpr int TB_THREADS = VH_TB_THREADS;
 #endif
 constexpr uint64_t TILE_LDS_BUDGET = VH_TILE_LDS_KB * 1024;
 constexpr uint32_t TILE_MAX_TILES = 4096;
+constexpr size_t LDS_MAX_BYTES = 160 * 1024;  // per workgroup on gfx950
 constexpr int TA_WG_PER_CU = 4;
 constexpr int SAMPLE_BLOCKS = 512;
 
@@ -207,6 +211,32 @@ template <int NV> __device__ inline ScatterLds scatter_lds(unsigned char *raw, u
     return l;
 }
 
+// rows per thread of one commit of the fast f64 pass A: with sums, SB batches are ranked
+// into one commit, so each (workgroup, tile) run is SB times longer (fewer, longer region
+// stores; the kernel already runs one workgroup per CU on registers)
+#ifndef VH_TA_SB
+#define VH_TA_SB 3
+#endif
+__host__ __device__ constexpr int fast_sb(int nv) { return nv == 0 ? 1 : nv == 1 ? VH_TA_SB : (VH_TA_SB < 2 ? VH_TA_SB : 2); }
+
+// LDS of the fast kernels: staged values | staged 4-byte keys | tile arrays
+__host__ __device__ inline size_t fast_lds_bytes(int nv, uint32_t T, uint32_t cap) {
+    return (size_t)8 * nv * cap + (size_t)4 * cap + 20 * (size_t)T + 64;
+}
+
+template <int NV> __device__ inline ScatterLds fast_lds(unsigned char *raw, uint32_t T, uint32_t cap) {
+    ScatterLds l;
+    l.sv = reinterpret_cast<double *>(raw);
+    l.sp = reinterpret_cast<uint64_t *>(raw + (size_t)8 * NV * cap);
+    l.hist = reinterpret_cast<uint32_t *>(raw + (size_t)8 * NV * cap + (size_t)4 * cap);
+    l.boff = l.hist + T;
+    l.base = l.boff + T;
+    l.lim = l.base + T;
+    l.dbase = l.lim + T;
+    l.wave_sums = l.dbase + T;
+    return l;
+}
+
 // per-workgroup init: zero the histogram; a tile's region of this workgroup is
 // [toff, toff + cap) inside the workgroup's block, written from base upwards
 __device__ inline void scatter_lds_init(const ScatterLds &l, const TileParams &tp, uint32_t T) {
@@ -313,23 +343,24 @@ __device__ inline void fast_scan(const ScatterLds &l, uint32_t T) {
     if (lane == 63) l.wave_sums[0] = inc;
 }
 
-template <int NV>
+template <int NV, int R>
 __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &fa, const TileParams &tp, uint32_t T,
                                          uint64_t region0, const uint32_t *key, const int32_t *rank,
                                          const double (*vals)[NV > 0 ? NV : 1], uint32_t count_mask,
                                          const uint32_t *keyed_slot_of) {
+    constexpr uint32_t CAP = R * TA_THREADS;
     uint32_t *sk = reinterpret_cast<uint32_t *>(l.sp);
     lds_barrier();
     fast_scan(l, T);
     lds_barrier();
     const uint32_t tot = l.wave_sums[0];
 #pragma unroll
-    for (int r = 0; r < TA_RPT; r++) {
+    for (int r = 0; r < R; r++) {
         if (rank[r] < 0) continue;
         const uint32_t pos = l.boff[key[r] >> 16] + (uint32_t)rank[r];
         sk[pos] = key[r];
 #pragma unroll
-        for (int s = 0; s < NV; s++) l.sv[s * TA_BATCH + pos] = vals[r][s];
+        for (int s = 0; s < NV; s++) l.sv[s * CAP + pos] = vals[r][s];
     }
     lds_barrier();
     for (uint32_t k = threadIdx.x; k < tot; k += TA_THREADS) {
@@ -340,7 +371,7 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
             const uint64_t e = region0 + dest;
             reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)kk;
 #pragma unroll
-            for (int s = 0; s < NV; s++) tp.values[s][e] = l.sv[s * TA_BATCH + k];
+            for (int s = 0; s < NV; s++) tp.values[s][e] = l.sv[s * CAP + k];
         } else {
             // region overflow (a sampling miss): apply the staged row with global atomics
             const uint64_t c = ((uint64_t)t << tp.s_log2) | (kk & 0xffffu);
@@ -350,7 +381,7 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
                 bool take = (count_mask >> a) & 1;
                 if constexpr (NV > 0) {
                     if (!take) {
-                        const double v = l.sv[keyed_slot_of[a] * TA_BATCH + k];
+                        const double v = l.sv[keyed_slot_of[a] * CAP + k];
                         take = v == v;
                     }
                 }
@@ -358,7 +389,7 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
                 if (fa.a[a].kind == VH_AGG_COUNT) {
                     atomicAdd((unsigned long long *)fa.a[a].grid + c, 1ULL);
                 } else if constexpr (NV > 0) {
-                    atomicAdd(reinterpret_cast<double *>(fa.a[a].grid) + c, l.sv[tp.val_slot[a] * TA_BATCH + k]);
+                    atomicAdd(reinterpret_cast<double *>(fa.a[a].grid) + c, l.sv[tp.val_slot[a] * CAP + k]);
                 }
             }
         }
@@ -401,44 +432,62 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter(BinPlan p, 
     for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.base[t] - (uint32_t)tp.toff[t];
 }
 
-// BinnerScalar<double> index from a loaded value (superagg_binners.cpp:42-53)
-__device__ inline uint64_t scalar_f64_index(double v, double vmin, double scale, uint64_t bins) {
+// BinnerScalar<double> index from a loaded value (superagg_binners.cpp:42-53),
+// branch-free in 32 bits (the tile path has cells < 2^28): every candidate is computed
+// and selected, so a wave runs no exec-masked branches.  The
+// conversion of an out-of-range or NaN product is never selected.
+__device__ inline uint32_t scalar_f64_index32(double v, double vmin, double scale, double bins_d, uint32_t bins2) {
     const double scaled = (v - vmin) * scale;
-    if (scaled != scaled) return 0;
-    if (scaled < 0) return 1;
-    if (scaled >= 1) return bins + 2;
-    return (uint64_t)(int64_t)((int)(scaled * (double)bins) + 2);
+    const uint32_t inner = (uint32_t)((int)(scaled * bins_d) + 2);
+    uint32_t idx = scaled >= 1 ? bins2 : inner;
+    idx = scaled < 0 ? 1u : idx;
+    return scaled != scaled ? 0u : idx;
 }
 
 // fast pass A: ND native float64 scalar binners without masks, NV float64 sums without
 // masks, counts unconditional or keyed on a carried value (mean).  Rows are read as
-// 16-byte pairs and the next batch is prefetched into registers while the current one
-// is ranked, sorted and written.
-template <int ND, int NV>
+// 16-byte pairs; the next batch loads into a second register buffer while the current
+// one is ranked, sorted and written.
+template <int ND, int NV, int SB>
 __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
     constexpr int NC = ND + NV;
     constexpr int PAIRS = TA_RPT / 2;
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const uint32_t T = tp.ntiles;
-    const ScatterLds l = scatter_lds<NV>(lds_raw, T);
+    const ScatterLds l = fast_lds<NV>(lds_raw, T, SB * TA_BATCH);
     scatter_lds_init(l, tp, T);
     __syncthreads();
     const double *col[NC];
+    double vmin[ND > 0 ? ND : 1], scale[ND > 0 ? ND : 1], bins_d[ND > 0 ? ND : 1];
+    uint32_t bins2[ND > 0 ? ND : 1], stride[ND > 0 ? ND : 1];
 #pragma unroll
-    for (int d = 0; d < ND; d++) col[d] = reinterpret_cast<const double *>(p.b[d].data);
+    for (int d = 0; d < ND; d++) {
+        col[d] = reinterpret_cast<const double *>(p.b[d].data);
+        vmin[d] = p.b[d].vmin;
+        scale[d] = p.b[d].scale;
+        bins_d[d] = (double)p.b[d].bins;
+        bins2[d] = (uint32_t)p.b[d].bins + 2;
+        stride[d] = (uint32_t)p.b[d].stride;
+    }
 #pragma unroll
     for (int s = 0; s < NV; s++) col[ND + s] = tp.vdata[s];
-    uint32_t count_mask = 0, keyed_slot_of[MAX_FUSED_AGGS];
+    // take flags: count(*) always; a sum, or a count keyed on a summed column, takes the
+    // row when that value is not NaN (nan_keyed[s] = the aggregators keyed on slot s)
+    uint32_t count_mask = 0, keyed_slot_of[MAX_FUSED_AGGS], nan_keyed[NV > 0 ? NV : 1] = {};
     #pragma unroll
     for (int k = 0; k < MAX_FUSED_AGGS; k++) {
         if (k >= fa.na) break;
         keyed_slot_of[k] = fa.a[k].kind == VH_AGG_COUNT ? (uint32_t)tp.cnt_slot[k] : (uint32_t)tp.val_slot[k];
         if (fa.a[k].kind == VH_AGG_COUNT && tp.cnt_slot[k] == CNT_ALWAYS) count_mask |= 1u << k;
+        else
+#pragma unroll
+            for (int s = 0; s < NV; s++)
+                if ((uint32_t)s == keyed_slot_of[k]) nan_keyed[s] |= 1u << k;
     }
     const uint32_t w = blockIdx.x;
     const uint64_t row_begin = (uint64_t)w * tp.rows_per_wg;
     const uint64_t row_end = min(n, row_begin + tp.rows_per_wg);
-    const uint32_t smask = (1u << tp.s_log2) - 1;
+    const uint32_t smask = (1u << tp.s_log2) - 1, s_log2 = tp.s_log2;
     const uint64_t region0 = (uint64_t)w * tp.wg_stride;
     // Branch-free 16-byte loads: n is even on this path (the host bins an odd last row
     // separately) and workgroup ranges are multiples of TA_BATCH, so a pair is either
@@ -455,48 +504,56 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan
             for (int c = 0; c < NC; c++) dst[q][c] = *reinterpret_cast<const double2 *>(col[c] + is);
         }
     };
-    double2 cur[PAIRS][NC], nxt[PAIRS][NC];
-    load(row_begin, cur);
-    for (uint64_t b0 = row_begin; b0 < row_end; b0 += TA_BATCH) {
-        load(b0 + TA_BATCH, nxt);
-        uint32_t key[TA_RPT];
-        int32_t rank[TA_RPT];
-        double vals[TA_RPT][NV > 0 ? NV : 1];
+    // rank the rows of one batch: cell, take flags, (tile << 16 | cell) key, rank in tile
+    auto rows = [&](uint64_t b0, const double2 (&cur)[PAIRS][NC], uint32_t *key, int32_t *rank,
+                    double (*vals)[NV > 0 ? NV : 1]) {
 #pragma unroll
         for (int r = 0; r < TA_RPT; r++) {
             const int q = r >> 1, h = r & 1;
             const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + threadIdx.x) + h;
-            rank[r] = -1;
-            if (i < row_end) {
-                uint64_t c = 0;
+            uint32_t c = 0;
 #pragma unroll
-                for (int d = 0; d < ND; d++) {
-                    const double v = h ? cur[q][d].y : cur[q][d].x;
-                    c += scalar_f64_index(v, p.b[d].vmin, p.b[d].scale, p.b[d].bins) * p.b[d].stride;
-                }
-                uint32_t f = count_mask;
-#pragma unroll
-                for (int s = 0; s < NV; s++) vals[r][s] = h ? cur[q][ND + s].y : cur[q][ND + s].x;
-                #pragma unroll
-                for (int k = 0; k < MAX_FUSED_AGGS; k++) {
-                    if (k >= fa.na) break;
-                    const uint32_t sl = keyed_slot_of[k];
-                    if (!((count_mask >> k) & 1)) {
-#pragma unroll
-                        for (int s = 0; s < NV; s++)
-                            if (s == (int)sl && vals[r][s] == vals[r][s]) f |= 1u << k;
-                    }
-                }
-                const uint32_t t = (uint32_t)(c >> tp.s_log2);
-                key[r] = (t << 16) | ((uint32_t)c & smask);
-                if (f) rank[r] = (int32_t)atomicAdd(&l.hist[t], 1u);
+            for (int d = 0; d < ND; d++) {
+                const double v = h ? cur[q][d].y : cur[q][d].x;
+                c += scalar_f64_index32(v, vmin[d], scale[d], bins_d[d], bins2[d]) * stride[d];
             }
+            uint32_t f = count_mask;
+#pragma unroll
+            for (int s = 0; s < NV; s++) {
+                vals[r][s] = h ? cur[q][ND + s].y : cur[q][ND + s].x;
+                f |= vals[r][s] == vals[r][s] ? nan_keyed[s] : 0u;
+            }
+            f = i < row_end ? f : 0u;
+            const uint32_t t = c >> s_log2;
+            key[r] = (t << 16) | (c & smask);
+            rank[r] = -1;
+            if (f) rank[r] = (int32_t)atomicAdd(&l.hist[t], 1u);
         }
-        batch_commit_fast<NV>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
+    };
+    double2 cur[PAIRS][NC], nxt[PAIRS][NC];
+    load(row_begin, cur);
+    for (uint64_t b0 = row_begin; b0 < row_end; b0 += SB * TA_BATCH) {
+        uint32_t key[SB * TA_RPT];
+        int32_t rank[SB * TA_RPT];
+        double vals[SB * TA_RPT][NV > 0 ? NV : 1];
+        // the last prefetch stays in flight across the commit: it is moved into cur only
+        // after the commit (a copy before it would wait for those loads)
 #pragma unroll
-        for (int q = 0; q < PAIRS; q++)
+        for (int sb = 0; sb < SB; sb++) {
+            load(b0 + (sb + 1) * TA_BATCH, nxt);
+            rows(b0 + sb * TA_BATCH, cur, key + sb * TA_RPT, rank + sb * TA_RPT, vals + sb * TA_RPT);
+            if (sb + 1 < SB || VH_TA_DRAIN)
 #pragma unroll
-            for (int c = 0; c < NC; c++) cur[q][c] = nxt[q][c];
+                for (int q = 0; q < PAIRS; q++)
+#pragma unroll
+                    for (int c = 0; c < NC; c++) cur[q][c] = nxt[q][c];
+        }
+        batch_commit_fast<NV, SB * TA_RPT>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
+        if (!VH_TA_DRAIN)
+#pragma unroll
+            for (int q = 0; q < PAIRS; q++)
+#pragma unroll
+                for (int c = 0; c < NC; c++) cur[q][c] = nxt[q][c];
     }
     lds_barrier();
     for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.base[t] - (uint32_t)tp.toff[t];
@@ -586,7 +643,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
                 if (f) rank[r] = (int32_t)atomicAdd(&l.hist[t], 1u);
             }
         }
-        batch_commit_fast<NV>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
+        batch_commit_fast<NV, TA_RPT>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
         cur = nxt;
     }
     lds_barrier();
@@ -754,12 +811,18 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
     }
 }
 
+// fast: 0 = generic kernel, 1 = fast kernel one batch per commit, 2 = fast kernel with
+// fast_sb(NV) batches per commit (when its LDS fits)
 template <int ND, int NV>
-static void launch_scatter(bool fast, unsigned grid, size_t lds, const BinPlan &plan, const FusedAggs &fa,
+static void launch_scatter(int fast, unsigned grid, size_t lds, const BinPlan &plan, const FusedAggs &fa,
                            const TileParams &tp, uint64_t n) {
     if constexpr (ND > 0) {
-        if (fast) {
-            hipLaunchKernelGGL((k_tile_scatter_f64<ND, NV>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
+        if (fast == 2) {
+            hipLaunchKernelGGL((k_tile_scatter_f64<ND, NV, fast_sb(NV)>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
+            return;
+        }
+        if (fast == 1) {
+            hipLaunchKernelGGL((k_tile_scatter_f64<ND, NV, 1>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
             return;
         }
     }
@@ -767,23 +830,27 @@ static void launch_scatter(bool fast, unsigned grid, size_t lds, const BinPlan &
 }
 
 template <int NV>
-static void launch_scatter_nd(int nd, bool fast, unsigned grid, size_t lds, const BinPlan &plan, const FusedAggs &fa,
+static void launch_scatter_nd(int nd, int fast, unsigned grid, size_t lds, const BinPlan &plan, const FusedAggs &fa,
                               const TileParams &tp, uint64_t n) {
     switch (nd) {
     case 1: launch_scatter<1, NV>(fast, grid, lds, plan, fa, tp, n); break;
     case 2: launch_scatter<2, NV>(fast, grid, lds, plan, fa, tp, n); break;
     case 3: launch_scatter<3, NV>(fast, grid, lds, plan, fa, tp, n); break;
-    default: launch_scatter<0, NV>(false, grid, lds, plan, fa, tp, n);
+    default: launch_scatter<0, NV>(0, grid, lds, plan, fa, tp, n);
     }
 }
 
 static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-template <int ND, int NV> static int scatter_blocks_per_cu(bool fast, size_t lds) {
+template <int ND, int NV> static int scatter_blocks_per_cu(int fast, size_t lds) {
     int nb = 0;
     if constexpr (ND > 0) {
-        if (fast) {
-            VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter_f64<ND, NV>, TA_THREADS, lds));
+        if (fast == 2) {
+            VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter_f64<ND, NV, fast_sb(NV)>, TA_THREADS, lds));
+            return nb;
+        }
+        if (fast == 1) {
+            VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter_f64<ND, NV, 1>, TA_THREADS, lds));
             return nb;
         }
     }
@@ -791,12 +858,12 @@ template <int ND, int NV> static int scatter_blocks_per_cu(bool fast, size_t lds
     return nb;
 }
 
-template <int NV> static int scatter_blocks_per_cu_nd(int nd, bool fast, size_t lds) {
+template <int NV> static int scatter_blocks_per_cu_nd(int nd, int fast, size_t lds) {
     switch (nd) {
     case 1: return scatter_blocks_per_cu<1, NV>(fast, lds);
     case 2: return scatter_blocks_per_cu<2, NV>(fast, lds);
     case 3: return scatter_blocks_per_cu<3, NV>(fast, lds);
-    default: return scatter_blocks_per_cu<0, NV>(false, lds);
+    default: return scatter_blocks_per_cu<0, NV>(0, lds);
     }
 }
 
@@ -924,13 +991,18 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     const bool ord = !fast && n % 2 == 0 && ord_fast_ok(plan, fa);
     if (ord) for (int k = 0; k < fa.na; k++)
         if (fa.a[k].kind != VH_AGG_COUNT) tp.vdata[tp.val_slot[k]] = fa.a[k].data;
-    const size_t lds_a = scatter_lds_bytes(nv, T);
+    // fast kernel: several batches per commit when that staging fits the LDS
+    const int fast_mode = !fast ? 0 : fast_lds_bytes(nv, T, (uint32_t)(fast_sb(nv) * TA_BATCH)) <= LDS_MAX_BYTES ? 2 : 1;
+    const size_t lds_a = fast_mode == 2   ? fast_lds_bytes(nv, T, (uint32_t)(fast_sb(nv) * TA_BATCH))
+                         : fast_mode == 1 ? fast_lds_bytes(nv, T, (uint32_t)TA_BATCH)
+                                          : scatter_lds_bytes(nv, T);
+    if (lds_a > LDS_MAX_BYTES) return false;  // very many tiles: the global-atomic path
     int bpc;
     {
         static std::mutex mu;
-        static std::map<std::tuple<int, int, int, bool, size_t>, int> cache;
+        static std::map<std::tuple<int, int, int, int, size_t>, int> cache;
         std::lock_guard<std::mutex> lk(mu);
-        const auto key = std::make_tuple(current_device(), ord ? -1 : nd_f64, nv, fast, lds_a);
+        const auto key = std::make_tuple(current_device(), ord ? -1 : nd_f64, nv, fast_mode, lds_a);
         auto it = cache.find(key);
         if (it == cache.end()) {
             int v = 0;
@@ -940,9 +1012,9 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
                                            : reinterpret_cast<const void *>(k_tile_scatter_ord<2>);
                 VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kf, TA_THREADS, lds_a));
             } else {
-                v = nv == 0 ? scatter_blocks_per_cu_nd<0>(nd_f64, fast, lds_a)
-                            : nv == 1 ? scatter_blocks_per_cu_nd<1>(nd_f64, fast, lds_a)
-                                      : scatter_blocks_per_cu_nd<2>(nd_f64, fast, lds_a);
+                v = nv == 0 ? scatter_blocks_per_cu_nd<0>(nd_f64, fast_mode, lds_a)
+                            : nv == 1 ? scatter_blocks_per_cu_nd<1>(nd_f64, fast_mode, lds_a)
+                                      : scatter_blocks_per_cu_nd<2>(nd_f64, fast_mode, lds_a);
             }
             it = cache.emplace(key, v).first;
         }
@@ -1042,9 +1114,9 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
             }
         } else {
             switch (nv) {
-            case 0: launch_scatter_nd<0>(nd_f64, fast, W, lds, plan, fa, tp, n); break;
-            case 1: launch_scatter_nd<1>(nd_f64, fast, W, lds, plan, fa, tp, n); break;
-            default: launch_scatter_nd<2>(nd_f64, fast, W, lds, plan, fa, tp, n);
+            case 0: launch_scatter_nd<0>(nd_f64, fast_mode, W, lds, plan, fa, tp, n); break;
+            case 1: launch_scatter_nd<1>(nd_f64, fast_mode, W, lds, plan, fa, tp, n); break;
+            default: launch_scatter_nd<2>(nd_f64, fast_mode, W, lds, plan, fa, tp, n);
             }
         }
         VH_HIP(hipGetLastError());
