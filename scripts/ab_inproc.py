@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT)
 from vaex_amd import _lib, superagg  # noqa: E402
 from vaex_amd.device import DeviceArray  # noqa: E402
 
-KERNELS = ["tile_sample", "tile_scatter_f64", "tile_reduce"]
+KERNELS = ["tile_sample", "tile_scatter_f64", "tile_scatter_ord", "tile_reduce", "minmax"]
 
 
 def main():
@@ -22,6 +22,7 @@ def main():
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--rows", type=float, default=1e9)
     ap.add_argument("--rounds", type=int, default=12)
+    ap.add_argument("--workloads", default="c2sum,c2count", help="c2sum,c2count,c3")
     a = ap.parse_args()
     libs = [_lib.load_library(os.path.abspath(p)) for p in a.libs]
     _lib._lib = libs[0]
@@ -29,8 +30,17 @@ def main():
     x = DeviceArray.random(n, "normal", seed=2)
     y = DeviceArray.random(n, "normal", seed=3)
     w = DeviceArray.random(n, "uniform", seed=4)
+    workloads = a.workloads.split(",")
+    if "c3" in workloads:
+        import vaex_amd
+        keys = DeviceArray.random(n, "randint", seed=5, a=5, b=5 + 10 ** 6, dtype="int32")
+        df3 = vaex_amd.from_arrays(key=keys, v=x)
 
-    def step(with_sum):
+    def step(wl):
+        if wl == "c3":
+            df3.groupby("key", agg={"v_sum": vaex_amd.agg.sum("v"), "v_count": vaex_amd.agg.count("v")})
+            return
+        with_sum = wl == "c2sum"
         bx = superagg.BinnerScalar_float64("x", -4.0, 4.0, 1024)
         by = superagg.BinnerScalar_float64("y", -4.0, 4.0, 1024)
         bx.set_data(x)
@@ -42,11 +52,11 @@ def main():
             aggs[1].set_data(w, 0)
         grid.bin(aggs)
 
-    res = {(i, ws): {k: [] for k in KERNELS} for i in range(len(libs)) for ws in (True, False)}
+    res = {(i, wl): {k: [] for k in KERNELS} for i in range(len(libs)) for wl in workloads}
     for rnd in range(a.rounds + 1):
         for i, L in enumerate(libs):
             _lib._lib = L
-            for ws in (True, False):
+            for ws in workloads:
                 _lib.synchronize()
                 _lib.timing_reset()
                 _lib.timing_enable(True)
@@ -62,8 +72,8 @@ def main():
                         res[(i, ws)][k].append(ms / c)
         print(f"round {rnd} done", flush=True)
     _lib._lib = libs[0]
-    for ws in (True, False):
-        print("count+sum" if ws else "count-only")
+    for ws in workloads:
+        print(ws)
         for i, p in enumerate(a.libs):
             med = {k: round(statistics.median(v), 3) for k, v in res[(i, ws)].items() if v}
             mn = {k: round(min(v), 3) for k, v in res[(i, ws)].items() if v}

@@ -572,30 +572,35 @@ __device__ inline uint64_t ordinal_i32_index(int32_t raw, uint64_t min_value, ui
 // and NV float64 sums without masks -- the C3 groupby(key).agg({sum, count}) shape.
 // Keys are read as 8-byte pairs and values as 16-byte pairs, the next batch prefetched in
 // registers (same row layout and pipelining as k_tile_scatter_f64).
-template <int NV>
+template <int NV, int SB>
 __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
     constexpr int PAIRS = TA_RPT / 2;
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const uint32_t T = tp.ntiles;
-    const ScatterLds l = scatter_lds<NV>(lds_raw, T);
+    const ScatterLds l = fast_lds<NV>(lds_raw, T, SB * TA_BATCH);
     scatter_lds_init(l, tp, T);
     __syncthreads();
     const int32_t *keys = reinterpret_cast<const int32_t *>(p.b[0].data);
     const double *col[NV > 0 ? NV : 1];
 #pragma unroll
     for (int s = 0; s < NV; s++) col[s] = tp.vdata[s];
-    const uint64_t min_value = p.b[0].min_value, count = p.b[0].ordinal_count, stride0 = p.b[0].stride;
-    uint32_t count_mask = 0, keyed_slot_of[MAX_FUSED_AGGS];
+    const uint64_t min_value = p.b[0].min_value, count = p.b[0].ordinal_count;
+    const uint32_t stride0 = (uint32_t)p.b[0].stride;
+    uint32_t count_mask = 0, keyed_slot_of[MAX_FUSED_AGGS], nan_keyed[NV > 0 ? NV : 1] = {};
     #pragma unroll
     for (int k = 0; k < MAX_FUSED_AGGS; k++) {
         if (k >= fa.na) break;
         keyed_slot_of[k] = fa.a[k].kind == VH_AGG_COUNT ? (uint32_t)tp.cnt_slot[k] : (uint32_t)tp.val_slot[k];
         if (fa.a[k].kind == VH_AGG_COUNT && tp.cnt_slot[k] == CNT_ALWAYS) count_mask |= 1u << k;
+        else
+#pragma unroll
+            for (int s = 0; s < NV; s++)
+                if ((uint32_t)s == keyed_slot_of[k]) nan_keyed[s] |= 1u << k;
     }
     const uint32_t w = blockIdx.x;
     const uint64_t row_begin = (uint64_t)w * tp.rows_per_wg;
     const uint64_t row_end = min(n, row_begin + tp.rows_per_wg);
-    const uint32_t smask = (1u << tp.s_log2) - 1;
+    const uint32_t smask = (1u << tp.s_log2) - 1, s_log2 = tp.s_log2;
     const uint64_t region0 = (uint64_t)w * tp.wg_stride;
     struct Regs {
         int2 k[PAIRS];
@@ -611,40 +616,39 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
             for (int s = 0; s < NV; s++) R.v[q][s] = *reinterpret_cast<const double2 *>(col[s] + is);
         }
     };
-    Regs cur, nxt;
-    load(row_begin, cur);
-    for (uint64_t b0 = row_begin; b0 < row_end; b0 += TA_BATCH) {
-        load(b0 + TA_BATCH, nxt);
-        uint32_t key[TA_RPT];
-        int32_t rank[TA_RPT];
-        double vals[TA_RPT][NV > 0 ? NV : 1];
+    auto rows = [&](uint64_t b0, const Regs &cur, uint32_t *key, int32_t *rank, double (*vals)[NV > 0 ? NV : 1]) {
 #pragma unroll
         for (int r = 0; r < TA_RPT; r++) {
             const int q = r >> 1, h = r & 1;
             const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + threadIdx.x) + h;
-            rank[r] = -1;
-            if (i < row_end) {
-                const uint64_t c = ordinal_i32_index(h ? cur.k[q].y : cur.k[q].x, min_value, count) * stride0;
-                uint32_t f = count_mask;
+            const uint32_t c = (uint32_t)ordinal_i32_index(h ? cur.k[q].y : cur.k[q].x, min_value, count) * stride0;
+            uint32_t f = count_mask;
 #pragma unroll
-                for (int s = 0; s < NV; s++) vals[r][s] = h ? cur.v[q][s].y : cur.v[q][s].x;
-                #pragma unroll
-                for (int k = 0; k < MAX_FUSED_AGGS; k++) {
-                    if (k >= fa.na) break;
-                    const uint32_t sl = keyed_slot_of[k];
-                    if (!((count_mask >> k) & 1)) {
-#pragma unroll
-                        for (int s = 0; s < NV; s++)
-                            if (s == (int)sl && vals[r][s] == vals[r][s]) f |= 1u << k;
-                    }
-                }
-                const uint32_t t = (uint32_t)(c >> tp.s_log2);
-                key[r] = (t << 16) | ((uint32_t)c & smask);
-                if (f) rank[r] = (int32_t)atomicAdd(&l.hist[t], 1u);
+            for (int s = 0; s < NV; s++) {
+                vals[r][s] = h ? cur.v[q][s].y : cur.v[q][s].x;
+                f |= vals[r][s] == vals[r][s] ? nan_keyed[s] : 0u;
             }
+            f = i < row_end ? f : 0u;
+            const uint32_t t = c >> s_log2;
+            key[r] = (t << 16) | (c & smask);
+            rank[r] = -1;
+            if (f) rank[r] = (int32_t)atomicAdd(&l.hist[t], 1u);
         }
-        batch_commit_fast<NV, TA_RPT>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
-        cur = nxt;
+    };
+    Regs cur, nxt;
+    load(row_begin, cur);
+    for (uint64_t b0 = row_begin; b0 < row_end; b0 += SB * TA_BATCH) {
+        uint32_t key[SB * TA_RPT];
+        int32_t rank[SB * TA_RPT];
+        double vals[SB * TA_RPT][NV > 0 ? NV : 1];
+#pragma unroll
+        for (int sb = 0; sb < SB; sb++) {
+            load(b0 + (sb + 1) * TA_BATCH, nxt);
+            rows(b0 + sb * TA_BATCH, cur, key + sb * TA_RPT, rank + sb * TA_RPT, vals + sb * TA_RPT);
+            if (sb + 1 < SB || VH_TA_DRAIN) cur = nxt;
+        }
+        batch_commit_fast<NV, SB * TA_RPT>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
+        if (!VH_TA_DRAIN) cur = nxt;
     }
     lds_barrier();
     for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.base[t] - (uint32_t)tp.toff[t];
@@ -867,6 +871,15 @@ template <int NV> static int scatter_blocks_per_cu_nd(int nd, int fast, size_t l
     }
 }
 
+static const void *ord_kernel(int nv, int fast_mode) {
+    if (nv == 0) return reinterpret_cast<const void *>(k_tile_scatter_ord<0, 1>);
+    if (nv == 1)
+        return fast_mode == 2 ? reinterpret_cast<const void *>(k_tile_scatter_ord<1, fast_sb(1)>)
+                              : reinterpret_cast<const void *>(k_tile_scatter_ord<1, 1>);
+    return fast_mode == 2 ? reinterpret_cast<const void *>(k_tile_scatter_ord<2, fast_sb(2)>)
+                          : reinterpret_cast<const void *>(k_tile_scatter_ord<2, 1>);
+}
+
 static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64,
                            Workspace &ws);
 
@@ -992,7 +1005,7 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     if (ord) for (int k = 0; k < fa.na; k++)
         if (fa.a[k].kind != VH_AGG_COUNT) tp.vdata[tp.val_slot[k]] = fa.a[k].data;
     // fast kernel: several batches per commit when that staging fits the LDS
-    const int fast_mode = !fast ? 0 : fast_lds_bytes(nv, T, (uint32_t)(fast_sb(nv) * TA_BATCH)) <= LDS_MAX_BYTES ? 2 : 1;
+    const int fast_mode = !(fast || ord) ? 0 : fast_lds_bytes(nv, T, (uint32_t)(fast_sb(nv) * TA_BATCH)) <= LDS_MAX_BYTES ? 2 : 1;
     const size_t lds_a = fast_mode == 2   ? fast_lds_bytes(nv, T, (uint32_t)(fast_sb(nv) * TA_BATCH))
                          : fast_mode == 1 ? fast_lds_bytes(nv, T, (uint32_t)TA_BATCH)
                                           : scatter_lds_bytes(nv, T);
@@ -1007,9 +1020,7 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         if (it == cache.end()) {
             int v = 0;
             if (ord) {
-                const void *kf = nv == 0 ? reinterpret_cast<const void *>(k_tile_scatter_ord<0>)
-                                 : nv == 1 ? reinterpret_cast<const void *>(k_tile_scatter_ord<1>)
-                                           : reinterpret_cast<const void *>(k_tile_scatter_ord<2>);
+                const void *kf = ord_kernel(nv, fast_mode);
                 VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kf, TA_THREADS, lds_a));
             } else {
                 v = nv == 0 ? scatter_blocks_per_cu_nd<0>(nd_f64, fast_mode, lds_a)
@@ -1108,9 +1119,14 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         const size_t lds = lds_a;
         if (ord) {
             switch (nv) {
-            case 0: hipLaunchKernelGGL(k_tile_scatter_ord<0>, dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n); break;
-            case 1: hipLaunchKernelGGL(k_tile_scatter_ord<1>, dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n); break;
-            default: hipLaunchKernelGGL(k_tile_scatter_ord<2>, dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
+            case 0: hipLaunchKernelGGL((k_tile_scatter_ord<0, 1>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n); break;
+            case 1:
+                if (fast_mode == 2) hipLaunchKernelGGL((k_tile_scatter_ord<1, fast_sb(1)>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
+                else hipLaunchKernelGGL((k_tile_scatter_ord<1, 1>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
+                break;
+            default:
+                if (fast_mode == 2) hipLaunchKernelGGL((k_tile_scatter_ord<2, fast_sb(2)>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
+                else hipLaunchKernelGGL((k_tile_scatter_ord<2, 1>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
             }
         } else {
             switch (nv) {
