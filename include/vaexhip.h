@@ -150,6 +150,10 @@ int vh_set_create(int dtype, vh_set **out);
 int vh_set_destroy(vh_set *set);
 /* update(keys[, mask]) hash_primitives.hpp:96-281 (mask: 1 = null) */
 int vh_set_update(vh_set *set, const void *keys, const uint8_t *mask, uint64_t n, int loc);
+/* update with only the rows where select[i] != 0 (a filtered / selected chunk, without
+ * compacting it first; ordinals follow the first selected occurrence) */
+int vh_set_update_selected(vh_set *set, const void *keys, const uint8_t *mask, const uint8_t *select, uint64_t n,
+                           int loc);
 /* assigns ordinals (first-appearance order); called implicitly by the readers */
 int vh_set_seal(vh_set *set);
 /* len(set), nan_count, null_count, nan_value, null_value (ordinals; 0x7fffffff if absent) */
@@ -184,6 +188,14 @@ int vh_hashagg_finish(vh_hashagg *h, uint64_t *ngroups);
 /* host outputs, ngroups items each: keys as int64, count(*) int64, per value column its sum
  * (8 bytes: double for float columns, int64/uint64 for integers) and non-NaN count int64 */
 int vh_hashagg_read(vh_hashagg *h, int64_t *keys, int64_t *counts, void *const *sums, int64_t *const *nonnull);
+/* ---- expressions on HBM columns (expr.hip) ----------------------------------
+ * out[i] = program(cols[.][i]) for i < n: the device evaluation of a virtual column,
+ * selection or filter (the reference evaluates them with numpy per chunk, cpu.py:542-581,
+ * execution.py:337-341).  code: stack program compiled by vaex_amd/expr.py (op | arg << 8),
+ * consts: 64-bit constant bit patterns; HBM columns and output. */
+int vh_expr_eval(const uint32_t *code, int ncode, const uint64_t *consts, int nconsts, const void *const *cols,
+                 const int *col_dtypes, int ncols, uint64_t n, int out_dtype, void *out);
+
 /* combined int64 key of a multi-key groupby, out[i] = sum_j (cols[j][i] - mins[j]) * mults[j]
  * (the cartesian ordinal of groupby.py:248-288 _combine, first key most significant);
  * HBM columns and output, up to 8 integer key columns */

@@ -69,6 +69,7 @@ SIGNATURES = {
     "vh_set_create": (_i32, [_i32, _p(_vp)]),
     "vh_set_destroy": (_i32, [_vp]),
     "vh_set_update": (_i32, [_vp, _vp, _vp, _u64, _i32]),
+    "vh_set_update_selected": (_i32, [_vp, _vp, _vp, _vp, _u64, _i32]),
     "vh_set_seal": (_i32, [_vp]),
     "vh_set_info": (_i32, [_vp, _p(_i64), _p(_i64), _p(_i64), _p(_i64), _p(_i64)]),
     "vh_set_key_array": (_i32, [_vp, _vp]),
@@ -80,6 +81,7 @@ SIGNATURES = {
     "vh_hashagg_finish": (_i32, [_vp, _p(_u64)]),
     "vh_hashagg_read": (_i32, [_vp, _vp, _vp, _p(_vp), _p(_vp)]),
     "vh_combine_keys": (_i32, [_u64, _i32, _p(_vp), _p(_i32), _p(_i64), _p(_i64), _vp]),
+    "vh_expr_eval": (_i32, [_p(ctypes.c_uint32), _i32, _p(_u64), _i32, _p(_vp), _p(_i32), _i32, _u64, _i32, _vp]),
 }
 
 _lib = None

@@ -32,7 +32,7 @@ struct vh_set {
     int dtype = VH_I64;
     uint64_t cap = 0;
     DevBuf tab, lut, ctr;
-    DevBuf stage_keys, stage_mask;
+    DevBuf stage_keys, stage_mask, stage_select;
     DevBuf c_slot, c_first, c_ord, c_bits;
     uint64_t rows_seen = 0;
     // the reference flushes NaN/null rows after the regular keys of the update call that
@@ -49,11 +49,13 @@ struct vh_set {
 namespace vh {
 
 template <typename T>
-__global__ __launch_bounds__(256) void k_set_insert(const T *keys, const uint8_t *mask, uint64_t n, uint64_t row0,
-                                                    uint64_t *tab, uint64_t cap_mask, uint64_t limit, uint64_t *ctr) {
+__global__ __launch_bounds__(256) void k_set_insert(const T *keys, const uint8_t *mask, const uint8_t *select, uint64_t n,
+                                                    uint64_t row0, uint64_t *tab, uint64_t cap_mask, uint64_t limit,
+                                                    uint64_t *ctr) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t row = row0 + i;
+        if (select && !select[i]) continue;  // filtered out / not selected
         if (mask && mask[i]) {
             atomicMin((unsigned long long *)&ctr[C_NULL_FIRST], (unsigned long long)row);
             atomicAdd((unsigned long long *)&ctr[C_NULL_COUNT], 1ULL);
@@ -436,8 +438,7 @@ int vh_set_destroy(vh_set *s) {
     VH_API_END
 }
 
-int vh_set_update(vh_set *s, const void *keys, const uint8_t *mask, uint64_t n, int loc) {
-    VH_API_BEGIN
+static void set_update(vh_set *s, const void *keys, const uint8_t *mask, const uint8_t *select, uint64_t n, int loc) {
     loc = resolve_loc(keys, loc);
     const int isz = dtype_itemsize(s->dtype);
     // Chunks start at cap/4 rows and double after every chunk that did not need the table
@@ -450,6 +451,7 @@ int vh_set_update(vh_set *s, const void *keys, const uint8_t *mask, uint64_t n, 
         len = std::min({want, stage_max, n - row0});
         const void *dk = reinterpret_cast<const char *>(keys) + row0 * isz;
         const uint8_t *dm = mask ? mask + row0 : nullptr;
+        const uint8_t *ds = select ? select + row0 : nullptr;
         if (loc == VH_LOC_HOST) {
             s->stage_keys.ensure(len * isz);
             VH_HIP(hipMemcpyAsync(s->stage_keys.ptr, dk, len * isz, hipMemcpyHostToDevice, stream()));
@@ -459,6 +461,11 @@ int vh_set_update(vh_set *s, const void *keys, const uint8_t *mask, uint64_t n, 
                 VH_HIP(hipMemcpyAsync(s->stage_mask.ptr, dm, len, hipMemcpyHostToDevice, stream()));
                 dm = s->stage_mask.as<uint8_t>();
             }
+            if (select) {
+                s->stage_select.ensure(len);
+                VH_HIP(hipMemcpyAsync(s->stage_select.ptr, ds, len, hipMemcpyHostToDevice, stream()));
+                ds = s->stage_select.as<uint8_t>();
+            }
         }
         bool grew = false;
         for (int attempt = 0;; attempt++) {
@@ -467,7 +474,7 @@ int vh_set_update(vh_set *s, const void *keys, const uint8_t *mask, uint64_t n, 
                 const uint64_t limit = s->cap / 4 * 3;
                 VH_DISPATCH_DTYPE(s->dtype, T,
                                   hipLaunchKernelGGL(k_set_insert<T>, dim3(std::min<uint64_t>(blocks_for(len, 256), 1 << 16)),
-                                                     dim3(256), 0, stream(), reinterpret_cast<const T *>(dk), dm, len,
+                                                     dim3(256), 0, stream(), reinterpret_cast<const T *>(dk), dm, ds, len,
                                                      s->rows_seen + row0, s->tab.as<uint64_t>(), s->cap - 1, limit,
                                                      s->ctr.as<uint64_t>()));
                 VH_HIP(hipGetLastError());
@@ -495,6 +502,18 @@ int vh_set_update(vh_set *s, const void *keys, const uint8_t *mask, uint64_t n, 
     }
     s->sealed = false;
     VH_HIP(hipStreamSynchronize(stream()));
+}
+
+int vh_set_update(vh_set *s, const void *keys, const uint8_t *mask, uint64_t n, int loc) {
+    VH_API_BEGIN
+    set_update(s, keys, mask, nullptr, n, loc);
+    VH_API_END
+}
+
+int vh_set_update_selected(vh_set *s, const void *keys, const uint8_t *mask, const uint8_t *select, uint64_t n,
+                           int loc) {
+    VH_API_BEGIN
+    set_update(s, keys, mask, select, n, loc);
     VH_API_END
 }
 

@@ -217,7 +217,10 @@ template <int NV> __device__ inline ScatterLds scatter_lds(unsigned char *raw, u
 #ifndef VH_TA_SB
 #define VH_TA_SB 3
 #endif
-__host__ __device__ constexpr int fast_sb(int nv) { return nv == 0 ? 1 : nv == 1 ? VH_TA_SB : (VH_TA_SB < 2 ? VH_TA_SB : 2); }
+#ifndef VH_TA_SB0
+#define VH_TA_SB0 1  // count-only commits
+#endif
+__host__ __device__ constexpr int fast_sb(int nv) { return nv == 0 ? VH_TA_SB0 : nv == 1 ? VH_TA_SB : (VH_TA_SB < 2 ? VH_TA_SB : 2); }
 
 // LDS of the fast kernels: staged values | staged 4-byte keys | tile arrays
 __host__ __device__ inline size_t fast_lds_bytes(int nv, uint32_t T, uint32_t cap) {

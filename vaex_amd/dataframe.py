@@ -211,6 +211,9 @@ class DataFrame:
         return name
 
     def __getitem__(self, item):
+        if isinstance(item, Expression) and str(item) not in self.columns and \
+                str(item) not in self.virtual_columns and self.data_type(item).kind == "b":
+            return self.filter(item)  # df[df.x > 0] (dataframe.py __getitem__: boolean expression = filter)
         if isinstance(item, (str, Expression)):
             return Expression(self, str(item))
         raise TypeError(item)
@@ -257,6 +260,9 @@ class DataFrame:
 
     def _eval_host(self, expression, i1, i2, filter_mask=None):
         expression = str(expression)
+        if isinstance(filter_mask, DeviceArray):
+            # HBM frame: chunks stay whole, the parts apply the filter as a row mask
+            filter_mask = None
         if expression in self.columns:
             col = self.columns[expression]
             if isinstance(col, DeviceArray):
@@ -265,6 +271,8 @@ class DataFrame:
                 return col[i1:i2]
             block = col[i1:i2]
             return block[filter_mask] if filter_mask is not None else block
+        if self.is_device_resident():
+            return self._eval_device(expression, i1, i2)
         if expression in self.virtual_columns:
             return self._eval_host(self.virtual_columns[expression], i1, i2, filter_mask)
         ns = {"np": np, "_ordinal_values": _ordinal_values}
@@ -285,6 +293,15 @@ class DataFrame:
         value = np.asarray(value) if not np.ma.isMaskedArray(value) else value
         return value[filter_mask] if filter_mask is not None else value
 
+    def _eval_device(self, expression, i1, i2):
+        """An expression over HBM columns, evaluated by the device expression kernel into
+        a new HBM column (expr.py); unsupported syntax raises rather than leaving the GPU."""
+        from .expr import UnsupportedExpression, compile_expression
+        try:
+            return compile_expression(self, expression).evaluate(self, i1, i2)
+        except UnsupportedExpression as e:
+            raise NotImplementedError(f"expression {expression!r} over HBM columns: {e}") from None
+
     def evaluate_chunk(self, expression, i1, i2, filter_mask=None):
         return self._eval_host(expression, i1, i2, filter_mask)
 
@@ -292,17 +309,50 @@ class DataFrame:
         i1 = 0 if i1 is None else i1
         i2 = self._length if i2 is None else i2
         fm = self.evaluate_filter_mask(i1, i2) if (filtered and self.filtered) else None
+        if isinstance(fm, DeviceArray):
+            # the filtered rows of an HBM frame, read back (the compaction happens on the host)
+            v = self._eval_host(expression, i1, i2)
+            v = v.to_numpy() if isinstance(v, DeviceArray) else np.asarray(v)
+            return v[fm.to_numpy().astype(bool)]
         return self._eval_host(expression, i1, i2, fm)
 
     def evaluate_filter_mask(self, i1, i2):
+        if self.is_device_resident():
+            return self._eval_device(self._filter, i1, i2)
         return np.asarray(self._eval_host(self._filter, i1, i2), dtype=bool)
 
     def data_type(self, expression):
         expression = str(expression)
         if expression in self.columns:
             return np.dtype(self.columns[expression].dtype)
+        if self.is_device_resident():
+            from .expr import UnsupportedExpression, compile_expression
+            try:
+                return compile_expression(self, expression).dtype
+            except UnsupportedExpression as e:
+                raise NotImplementedError(f"expression {expression!r} over HBM columns: {e}") from None
         v = self._eval_host(expression, 0, min(self._length, 16))
         return np.dtype(v.dtype)
+
+    def _selection_expression(self, selection):
+        if selection is True:
+            selection = "default"
+        if isinstance(selection, str) and selection in self.selection_expressions:
+            selection = self.selection_expressions[selection]
+        return str(selection)
+
+    def device_keep_mask(self, i1, i2, selection=None, invert=False):
+        """HBM frame: one device mask of the rows a part takes (filter & selection), or its
+        complement (invert: the skip mask of the min/max kernel); None = every row."""
+        parts = []
+        if self._filter is not None:
+            parts.append(f"({self._filter})")
+        if selection not in (None, False):
+            parts.append(f"({self._selection_expression(selection)})")
+        if not parts:
+            return None
+        expr = " & ".join(parts)
+        return self._eval_device(f"~({expr})" if invert else expr, i1, i2)
 
     # ---- selections --------------------------------------------------------------
     def select(self, expression, name="default"):
@@ -316,10 +366,10 @@ class DataFrame:
 
     def evaluate_selection_mask(self, selection, i1=0, i2=None, filter_mask=None, cache=False):
         i2 = self._length if i2 is None else i2
-        if selection is True:
-            selection = "default"
-        if isinstance(selection, str) and selection in self.selection_expressions:
-            selection = self.selection_expressions[selection]
+        if isinstance(filter_mask, DeviceArray) or (filter_mask is None and self.is_device_resident()):
+            # HBM frame: the device mask of (filter &) selection over the whole chunk
+            return self.device_keep_mask(i1, i2, selection)
+        selection = self._selection_expression(selection)
         mask = self._eval_host(str(selection), i1, i2, filter_mask)
         if np.ma.isMaskedArray(mask):
             mask = mask.data & ~np.ma.getmaskarray(mask)

@@ -59,6 +59,9 @@ class _OrderedSetBase:
         if rest and (isinstance(rest[0], (np.ndarray, list, DeviceArray)) or rest[0] is None):
             mask = rest.pop(0)
         mask = kwargs.pop("mask", mask)
+        # select (this build): only rows where select != 0 enter the set (a filtered or
+        # selected chunk, evaluated on the device, without compacting it)
+        select = kwargs.pop("select", None)
         return_values = kwargs.get("return_values", False)
         if np.ma.isMaskedArray(ar):
             m = np.ma.getmaskarray(ar)
@@ -72,7 +75,12 @@ class _OrderedSetBase:
         if mask is not None:
             mkeep = np.ascontiguousarray(mask, dtype=np.uint8) if not isinstance(mask, DeviceArray) else mask
             mptr = mkeep.ctypes.data if isinstance(mkeep, np.ndarray) else mkeep.ptr
-        _lib.call("vh_set_update", self._handle, kptr, mptr, n, loc)
+        if select is not None:
+            skeep = select if isinstance(select, DeviceArray) else np.ascontiguousarray(select, dtype=np.uint8)
+            sptr = skeep.ptr if isinstance(skeep, DeviceArray) else skeep.ctypes.data
+            _lib.call("vh_set_update_selected", self._handle, kptr, mptr, sptr, n, loc)
+        else:
+            _lib.call("vh_set_update", self._handle, kptr, mptr, n, loc)
         if return_values:
             ordinals = self.map_ordinal(ar).astype(np.int64)
             if mask is not None:

@@ -95,7 +95,8 @@ class TaskPartAggregation:
     def process(self, thread_index, i1, i2, filter_mask, blocks):
         """cpu.py:501-583 with ``blocks`` a dict expression -> chunk buffer."""
         N = i2 - i1
-        if filter_mask is not None:
+        device_filter = isinstance(filter_mask, DeviceArray)  # HBM frame: chunk whole, filter as mask
+        if filter_mask is not None and not device_filter:
             N = int(np.sum(filter_mask))
         references = []
         for binner in self.grid.binners:
@@ -115,12 +116,17 @@ class TaskPartAggregation:
                 all_aggregators.append(agg)
                 selection_mask = None
                 if not (selection is None or selection is False):
-                    selection_mask = np.asarray(self.df.evaluate_selection_mask(selection, i1=i1, i2=i2,
-                                                                                filter_mask=filter_mask))
+                    selection_mask = self.df.evaluate_selection_mask(selection, i1=i1, i2=i2, filter_mask=filter_mask)
+                    if not isinstance(selection_mask, DeviceArray):
+                        selection_mask = np.asarray(selection_mask)
+                elif device_filter:
+                    selection_mask = filter_mask
                 for i, expression in enumerate(desc.expressions):
                     block, mask = _split_masked(blocks[expression])
                     block = _prepare(block)
                     if mask is not None:
+                        if isinstance(selection_mask, DeviceArray):
+                            raise NotImplementedError("masked host columns in a filtered / selected HBM frame")
                         selection_mask = ~mask if selection_mask is None else (selection_mask & ~mask)
                     agg.set_data(block, i)
                     references.append(block)
@@ -167,6 +173,18 @@ class TaskPartSetCreate:
 
     def process(self, thread_index, i1, i2, filter_mask, blocks):
         ar = blocks[self.expression]
+        if isinstance(ar, DeviceArray):
+            # HBM frame: filter & selection as one device mask, the set skips the other rows
+            keep = None
+            if isinstance(filter_mask, DeviceArray) or self.selection:
+                keep = self.df.device_keep_mask(i1, i2, self.selection or None)
+            if len(ar):
+                if keep is not None:
+                    self.set.update(ar, select=keep)
+                else:
+                    self.set.update(ar)
+            self._check_row_limit()
+            return
         if self.selection:
             sel = self.df.evaluate_selection_mask(self.selection, i1=i1, i2=i2, filter_mask=filter_mask)
             ar = ar[np.asarray(sel)]
@@ -208,21 +226,26 @@ class TaskPartMinMax:
         import ctypes
         block, mask = _split_masked(blocks[self.expression])
         block = _prepare(block)
-        skip = None
-        if mask is not None:
-            skip = mask
-        if self.selection not in (None, False):
-            sel = np.asarray(self.df.evaluate_selection_mask(self.selection, i1=i1, i2=i2, filter_mask=filter_mask))
-            skip = ~sel if skip is None else (skip | ~sel)
         code, flip = _lib.dtype_code(block.dtype)
         lo, hi = ctypes.c_double(), ctypes.c_double()
         if isinstance(block, DeviceArray):
-            ptr, loc = block.ptr, _lib.LOC_DEVICE
+            # HBM frame: skip = ~(filter & selection), evaluated on the device
+            skip = None
+            if isinstance(filter_mask, DeviceArray) or self.selection not in (None, False):
+                skip = self.df.device_keep_mask(i1, i2, self.selection if self.selection not in (None, False) else None,
+                                                invert=True)
+            _lib.call("vh_minmax", block.ptr, len(block), code, flip, None if skip is None else skip.ptr,
+                      _lib.LOC_DEVICE, ctypes.byref(lo), ctypes.byref(hi))
         else:
-            ptr, loc = block.ctypes.data, _lib.LOC_HOST
-        skip_arr = None if skip is None else np.ascontiguousarray(skip, dtype=np.uint8)
-        _lib.call("vh_minmax", ptr, len(block), code, flip, None if skip_arr is None else skip_arr.ctypes.data, loc,
-                  ctypes.byref(lo), ctypes.byref(hi))
+            skip = None
+            if mask is not None:
+                skip = mask
+            if self.selection not in (None, False):
+                sel = np.asarray(self.df.evaluate_selection_mask(self.selection, i1=i1, i2=i2, filter_mask=filter_mask))
+                skip = ~sel if skip is None else (skip | ~sel)
+            skip_arr = None if skip is None else np.ascontiguousarray(skip, dtype=np.uint8)
+            _lib.call("vh_minmax", block.ctypes.data, len(block), code, flip,
+                      None if skip_arr is None else skip_arr.ctypes.data, _lib.LOC_HOST, ctypes.byref(lo), ctypes.byref(hi))
         self.vmin = np.nanmin([self.vmin, lo.value]) if not np.isnan(lo.value) else self.vmin
         self.vmax = np.nanmax([self.vmax, hi.value]) if not np.isnan(hi.value) else self.vmax
 
