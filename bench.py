@@ -216,7 +216,7 @@ def main():
 
 
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_c2.json")
-PMC_KERNEL = {"tile_scatter_f64": "k_tile_scatter_f64<2, 1>", "tile_scatter": "k_tile_scatter<2, 1>",
+PMC_KERNEL = {"tile_scatter_f64": "k_tile_scatter_f64<2, 1,", "tile_scatter": "k_tile_scatter<2, 1>",
               "tile_reduce": "k_tile_reduce<1>"}
 
 
@@ -234,7 +234,7 @@ def pmc_traffic(timer, n, bins):
     if pmc.get("rows") != n or pmc.get("bins") != bins or timer not in PMC_KERNEL:
         return None
     for name, k in pmc["kernels"].items():
-        if name.endswith(PMC_KERNEL[timer]) and k.get("fetch_bytes_x2") is not None and k.get("write_bytes") is not None:
+        if PMC_KERNEL[timer] in name and k.get("fetch_bytes_x2") is not None and k.get("write_bytes") is not None:
             return {"bytes": int(k["fetch_bytes_x2"] + k["write_bytes"]),
                     "source": f"{os.path.relpath(PMC_FILE, ROOT)} ({pmc.get('source')}): 2*FETCH_SIZE + WRITE_SIZE"}
     return None
