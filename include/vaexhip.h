@@ -52,7 +52,9 @@ enum vh_agg_kind {
     VH_AGG_MIN = 2,        /* AggMin_<t>        superagg.cpp:241-287 */
     VH_AGG_MAX = 3,        /* AggMax_<t>        superagg.cpp:194-239 */
     VH_AGG_FIRST = 4,      /* AggFirst_<t>      superagg.cpp:436-511 */
-    VH_AGG_SUM_MOMENT = 5  /* AggSumMoment_<t>  superagg.cpp:391-434 */
+    VH_AGG_SUM_MOMENT = 5, /* AggSumMoment_<t>  superagg.cpp:391-434 */
+    VH_AGG_NUNIQUE = 6     /* AggNUnique_<t>    agg_hash_primitive.cpp:6-102; create arg: bit 0
+                              dropmissing, bit 1 dropnan */
 };
 
 typedef struct vh_binner vh_binner;
@@ -134,6 +136,9 @@ int vh_agg_set_data(vh_agg *agg, const void *ptr, uint64_t length, int itemsize,
                     int loc);
 int vh_agg_set_data_mask(vh_agg *agg, const uint8_t *mask, uint64_t length, int ndim, int loc); /* 1 = keep */
 int vh_agg_clear_data_mask(vh_agg *agg);
+/* AggNUnique::set_selection_mask (agg_hash_primitive.cpp:82-89): with a selection set, rows
+ * whose data mask is 0 are outside the selection (skipped), not missing values */
+int vh_agg_set_selection_mask(vh_agg *agg, const uint8_t *mask, uint64_t length, int ndim, int loc);
 /* __sizeof__ (grid bytes, agg.hpp:162-164), grid dtype and itemsize */
 int vh_agg_info(const vh_agg *agg, uint64_t *bytes, int *grid_dtype, uint64_t *itemsize);
 /* buffer protocol (agg.hpp:166-179): the grid is copied to/from a host image */

@@ -259,6 +259,44 @@ def compute_grid(binners, kind, data=None, data2=None, mask=None, n=None, dtype=
     return _fortran_view(grid, shape)
 
 
+def nunique_grid(binners, data, mask=None, selection=False, dropmissing=False, dropnan=False, n=None):
+    """AggNUnique over all rows (agg_hash_primitive.cpp:24-60 with the counter's count(),
+    hash.hpp:208-222): per cell  distinct + (nulls > 0) + (nans > 0), minus the null / nan
+    ROW counts when dropmissing / dropnan (the reference subtracts counts, not presence).
+    mask: aggregator data mask (1 = keep); selection: a selection mask was set, so rows
+    with mask 0 are outside it and not seen.  Values compare with == (-0.0 == 0.0)."""
+    data = np.asarray(data)
+    if n is None:
+        n = len(data)
+    shape = grid_shape(binners)
+    length = int(np.prod(shape)) if shape else 1
+    idx = (bin_indices(binners, n) if binners else np.zeros(n, np.uint64)).astype(np.int64)
+    name, flip = _dtype_info(data)
+    vals = data.byteswap().view(data.dtype.newbyteorder()) if flip else data
+    keep = np.ones(n, bool) if mask is None else np.asarray(mask).astype(bool)
+    seen = keep if selection else np.ones(n, bool)
+    nulls = np.bincount(idx[seen & ~keep], minlength=length)
+    v = vals[keep & seen]
+    c = idx[keep & seen]
+    if v.dtype.kind == "f":
+        isnan = np.isnan(v)
+        nans = np.bincount(c[isnan], minlength=length)
+        v, c = v[~isnan].astype(np.float64), c[~isnan]
+        v = np.where(v == 0, 0.0, v)  # -0.0 and 0.0 are one key
+        bits = v.view(np.int64)
+    else:
+        nans = np.zeros(length, np.int64)
+        bits = v.astype(np.int64)
+    pairs = np.unique(np.stack([c, bits], axis=1), axis=0) if len(c) else np.zeros((0, 2), np.int64)
+    distinct = np.bincount(pairs[:, 0], minlength=length)
+    out = distinct + (nulls > 0) + (nans > 0)
+    if dropmissing:
+        out = out - nulls
+    if dropnan:
+        out = out - nans
+    return _fortran_view(out.astype(np.int64), shape)
+
+
 def extract_central_part(ar):
     """utils.py:919-920."""
     return ar[(slice(2, -1),) * ar.ndim]

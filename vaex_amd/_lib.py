@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("VAEX_AMD_LIB", os.path.join(HERE, "libvaexhip.so"))
 DTYPES = ["float64", "float32", "int64", "int32", "int16", "int8",
           "uint64", "uint32", "uint16", "uint8", "bool"]
 DTYPE_CODE = {name: i for i, name in enumerate(DTYPES)}
-AGG_KIND = {"AggCount": 0, "AggSum": 1, "AggMin": 2, "AggMax": 3, "AggFirst": 4, "AggSumMoment": 5}
+AGG_KIND = {"AggCount": 0, "AggSum": 1, "AggMin": 2, "AggMax": 3, "AggFirst": 4, "AggSumMoment": 5, "AggNUnique": 6}
 LOC_AUTO, LOC_HOST, LOC_DEVICE = 0, 1, 2
 
 # every symbol the header declares, with (restype, argtypes)
@@ -59,6 +59,7 @@ SIGNATURES = {
     "vh_agg_set_data": (_i32, [_vp, _vp, _u64, _i32, _i32, _i32, _i32]),
     "vh_agg_set_data_mask": (_i32, [_vp, _vp, _u64, _i32, _i32]),
     "vh_agg_clear_data_mask": (_i32, [_vp]),
+    "vh_agg_set_selection_mask": (_i32, [_vp, _vp, _u64, _i32, _i32]),
     "vh_agg_info": (_i32, [_vp, _p(_u64), _p(_i32), _p(_u64)]),
     "vh_agg_download": (_i32, [_vp, _vp, _u64]),
     "vh_agg_upload": (_i32, [_vp, _vp, _u64]),

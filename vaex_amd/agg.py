@@ -112,6 +112,31 @@ class AggregatorDescriptorBasic(AggregatorDescriptor):
         return grid
 
 
+class AggregatorDescriptorNUnique(AggregatorDescriptorBasic):
+    """agg.py:123-144: AggNUnique_<t>(grid, dropmissing, dropnan), int64 output."""
+
+    def __init__(self, name, expression, short_name, dropmissing, dropnan, selection=None, edges=False):
+        super().__init__(name, expression, short_name, selection=selection, edges=edges)
+        self.dropmissing = dropmissing
+        self.dropnan = dropnan
+
+    def encode(self):
+        spec = super().encode()
+        if self.dropmissing:
+            spec["dropmissing"] = self.dropmissing
+        if self.dropnan:
+            spec["dropnan"] = self.dropnan
+        return spec
+
+    def _prepare_types(self, df):
+        super()._prepare_types(df)
+        self.dtype_out = np.dtype("int64")
+
+    def _create_operation(self, grid):
+        agg_op_type = find_type_from_dtype(superagg, self.name + "_", self.dtype_in)
+        return agg_op_type(grid, self.dropmissing, self.dropnan)
+
+
 class AggregatorDescriptorMulti(AggregatorDescriptor):
     def __init__(self, name, expression, short_name, selection=None, edges=False):
         self.name = name
@@ -247,5 +272,13 @@ def var(expression, ddof=0, selection=None, edges=False):
 
 @register
 def nunique(expression, dropna=False, dropnan=False, dropmissing=False, selection=None, edges=False):
-    """Out of scope for this build (a per-cell hash, not the scatter-add path)."""
-    raise NotImplementedError("nunique is outside the binned-statistics hot path this build implements")
+    """Aggregator that calculates the number of unique items per bin (agg.py:277-288).
+
+    :param dropmissing: do not count missing values
+    :param dropnan: do not count nan values
+    :param dropna: short for both"""
+    if dropna:
+        dropnan = True
+        dropmissing = True
+    return AggregatorDescriptorNUnique("AggNUnique", expression, "nunique", dropmissing, dropnan,
+                                       selection=selection, edges=edges)

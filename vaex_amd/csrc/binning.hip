@@ -46,16 +46,6 @@ struct vh_grid {
     Workspace ws;
 };
 
-struct vh_agg {
-    vh_grid *grid = nullptr;
-    int kind = 0, dtype = VH_F64, flip = 0;
-    uint32_t moment = 0;
-    int grid_dtype = VH_I64;
-    int grid_isz = 8;
-    DevBuf g, g2;          // grid, AggFirst order grid
-    DevBuf s_key, s_row;   // AggFirst per-chunk scratch
-    ColumnRef data, data2, mask;
-};
 
 namespace vh {
 
@@ -639,16 +629,17 @@ int vh_grid_info(const vh_grid *g, int *dims, uint64_t *shapes, uint64_t *stride
 
 int vh_agg_create(vh_grid *grid, int kind, int dtype, int flip, uint32_t arg, vh_agg **out) {
     VH_API_BEGIN
-    if (kind < VH_AGG_COUNT || kind > VH_AGG_SUM_MOMENT) fail(VH_ERR_ARG, "unknown aggregator kind");
+    if (kind < VH_AGG_COUNT || kind > VH_AGG_NUNIQUE) fail(VH_ERR_ARG, "unknown aggregator kind");
     dtype_itemsize(dtype);
     std::unique_ptr<vh_agg> a(new vh_agg());
     a->grid = grid;
+    a->L = grid->length1d;
     a->kind = kind;
     a->dtype = dtype;
     a->flip = flip ? 1 : 0;
     a->moment = arg;
     switch (kind) {
-    case VH_AGG_COUNT: a->grid_dtype = VH_I64; break;
+    case VH_AGG_COUNT: case VH_AGG_NUNIQUE: a->grid_dtype = VH_I64; break;
     case VH_AGG_SUM: case VH_AGG_SUM_MOMENT: a->grid_dtype = upcast_dtype(dtype); break;
     default: a->grid_dtype = dtype;
     }
@@ -660,7 +651,8 @@ int vh_agg_create(vh_grid *grid, int kind, int dtype, int flip, uint32_t arg, vh
         a->s_key.ensure(L * 8);
         a->s_row.ensure(L * 8);
     }
-    init_agg_grid(a.get());
+    if (kind == VH_AGG_NUNIQUE) nunique_init(a.get());
+    else init_agg_grid(a.get());
     *out = a.release();
     VH_API_END
 }
@@ -695,6 +687,17 @@ int vh_agg_clear_data_mask(vh_agg *a) {
     VH_API_END
 }
 
+int vh_agg_set_selection_mask(vh_agg *a, const uint8_t *mask, uint64_t length, int ndim, int loc) {
+    VH_API_BEGIN
+    (void)length;
+    (void)loc;
+    if (ndim != 1) fail(VH_ERR_RUNTIME, "Expected a 1d array");
+    // as agg_hash_primitive.cpp:46-47 only its presence matters: rows whose data mask is 0
+    // are then outside the selection (not missing)
+    a->has_selection = mask != nullptr;
+    VH_API_END
+}
+
 int vh_agg_info(const vh_agg *a, uint64_t *bytes, int *grid_dtype, uint64_t *itemsize) {
     VH_API_BEGIN
     if (bytes) *bytes = a->grid->length1d * a->grid_isz;
@@ -706,6 +709,7 @@ int vh_agg_info(const vh_agg *a, uint64_t *bytes, int *grid_dtype, uint64_t *ite
 int vh_agg_download(vh_agg *a, void *host, uint64_t bytes) {
     VH_API_BEGIN
     if (bytes != a->grid->length1d * a->grid_isz) fail(VH_ERR_ARG, "download size mismatch");
+    nunique_finalize(a);
     VH_HIP(hipMemcpyAsync(host, a->g.ptr, bytes, hipMemcpyDeviceToHost, stream()));
     VH_HIP(hipStreamSynchronize(stream()));
     VH_API_END
@@ -732,6 +736,7 @@ int vh_agg_upload_order(vh_agg *a, const void *host, uint64_t bytes) {
 int vh_agg_upload(vh_agg *a, const void *host, uint64_t bytes) {
     VH_API_BEGIN
     if (bytes != a->grid->length1d * a->grid_isz) fail(VH_ERR_ARG, "upload size mismatch");
+    if (a->kind == VH_AGG_NUNIQUE) return VH_OK;  // a derived grid (recomputed when read)
     VH_HIP(hipMemcpyAsync(a->g.ptr, host, bytes, hipMemcpyHostToDevice, stream()));
     VH_HIP(hipStreamSynchronize(stream()));
     VH_API_END
@@ -739,6 +744,7 @@ int vh_agg_upload(vh_agg *a, const void *host, uint64_t bytes) {
 
 int vh_agg_device_ptr(vh_agg *a, void **grid_dptr, void **grid2_dptr) {
     VH_API_BEGIN
+    nunique_finalize(a);
     if (grid_dptr) *grid_dptr = a->g.ptr;
     if (grid2_dptr) *grid2_dptr = a->g2.ptr;
     VH_API_END
@@ -774,6 +780,9 @@ int vh_agg_reduce(vh_agg *a, vh_agg *const *others, int nothers) {
             VH_DISPATCH_DTYPE(a->dtype, T,
                               hipLaunchKernelGGL(k_reduce_first<T>, grd, blk, 0, stream(), a->g.as<T>(),
                                                  a->g2.as<T>(), o->g.as<T>(), o->g2.as<T>(), L));
+            break;
+        case VH_AGG_NUNIQUE:
+            nunique_merge(a, o);  // counter::merge (hash_primitives.hpp:393-415)
             break;
         }
         VH_HIP(hipGetLastError());
@@ -838,6 +847,7 @@ static AggDev agg_dev(vh_agg *a, Stager &st) {
     d.dtype = a->dtype;
     d.flip = a->flip;
     d.moment = a->moment;
+    d.has_selection = a->has_selection ? 1 : 0;
     d.data = st.get(a->data);
     d.data2 = st.get(a->data2);
     d.mask = reinterpret_cast<const uint8_t *>(st.get(a->mask));
@@ -952,6 +962,9 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                         hipLaunchKernelGGL(k_first_b<T>, grd, blk, 0, stream(), ad, idx, len, row0);
                         hipLaunchKernelGGL(k_first_c<T>, dim3(blocks_for(L, 256)), blk, 0, stream(), ad, L, row0);
                     });
+                    break;
+                case VH_AGG_NUNIQUE:
+                    nunique_collect(aggs[k], ad, idx, len);
                     break;
                 }
                 VH_HIP(hipGetLastError());

@@ -9,6 +9,7 @@
 struct vh_grid;
 struct vh_agg;
 
+
 namespace vh {
 
 constexpr int MAX_DIM = 16;          // agg.hpp:25
@@ -44,6 +45,7 @@ struct BinPlan {
 struct AggDev {
     int32_t kind, dtype, flip;
     uint32_t moment;
+    int32_t has_selection, pad;
     const void *data;
     const void *data2;
     const uint8_t *mask;
@@ -104,4 +106,30 @@ void launch_fused(const BinPlan &plan, FusedAggs &fa, uint64_t n, uint64_t cells
 // (tiled.hip); returns false when the plan is not eligible
 bool try_tiled(const BinPlan &plan, const FusedAggs &fa, uint64_t n, uint64_t cells, int nd_f64, Workspace &ws);
 
+}  // namespace vh
+
+struct vh_agg {
+    vh_grid *grid = nullptr;
+    int kind = 0, dtype = VH_F64, flip = 0;
+    uint32_t moment = 0;   // AggSumMoment moment; AggNUnique: bit 0 dropmissing, bit 1 dropnan
+    int grid_dtype = VH_I64;
+    int grid_isz = 8;
+    vh::DevBuf g, g2;          // grid, AggFirst order grid / AggNUnique per-cell null counts
+    vh::DevBuf s_key, s_row;   // AggFirst per-chunk scratch / AggNUnique per-cell nan counts
+    vh::ColumnRef data, data2, mask;
+    // AggNUnique (agg_hash_primitive.cpp:6-102): the (cell, value) pairs seen so far, kept
+    // as an unordered list, deduplicated by sort when the grid is read or the list grows
+    bool has_selection = false;
+    bool nu_dirty = false;
+    uint64_t L = 0;        // grid length1d
+    uint64_t nu_n = 0;
+    vh::DevBuf nu_cell, nu_val;
+};
+
+namespace vh {
+// AggNUnique (nunique.hip)
+void nunique_init(vh_agg *a);
+void nunique_collect(vh_agg *a, const AggDev &ad, const uint64_t *idx, uint64_t len);
+void nunique_merge(vh_agg *a, vh_agg *o);
+void nunique_finalize(vh_agg *a);
 }  // namespace vh

@@ -1,0 +1,270 @@
+// AggNUnique on the GPU: the number of distinct values per grid cell
+// (packages/vaex-core/src/agg_hash_primitive.cpp:6-102).
+//
+// The reference keeps one hash counter per cell.  Here every chunk appends the (cell,
+// value) pairs of its rows to one list in HBM (missing / NaN rows only bump per-cell
+// counters); when the grid is read the list is sorted by (cell, value) with two stable
+// radix passes, equal neighbours collapse, and each cell counts its distinct values.  The
+// deduplicated list is kept, so later chunks and reduce() keep appending to it.
+//
+// Per cell, as the reference computes it (agg_hash_primitive.cpp:24-38, hash.hpp:208-222):
+//   distinct + (null rows > 0) + (nan rows > 0)
+//            - (dropmissing ? null rows : 0) - (dropnan ? nan rows : 0)
+// Rows outside a selection (a selection mask is set and the row's data mask is 0) are not
+// seen at all; without a selection a data-mask 0 row is a missing value.  Values compare
+// as the hash map's equal_to: -0.0 == 0.0; NaN never enters the list.
+#include <cstring>
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "common.hpp"
+#include "engine.hpp"
+
+namespace vh {
+
+constexpr uint64_t NU_COMPACT_AT = uint64_t(1) << 28;  // pairs before an eager dedup
+
+template <typename T> __device__ inline T nu_load(const void *p, uint64_t i, int flip) {
+    T v = static_cast<const T *>(p)[i];
+    if constexpr (!std::is_same_v<T, vbool>) {
+        if (flip) v = bswap_v(v);
+    }
+    return v;
+}
+
+// the value's key bits and whether it is NaN
+template <typename T> __device__ inline uint64_t nu_bits(T v, bool *nan) {
+    *nan = false;
+    if constexpr (std::is_same_v<T, double> || std::is_same_v<T, float>) {
+        const double d = (double)v;
+        if (d != d) {
+            *nan = true;
+            return 0;
+        }
+        return __builtin_bit_cast(uint64_t, d == 0.0 ? 0.0 : d);
+    } else if constexpr (std::is_same_v<T, vbool>) {
+        return v.v ? 1 : 0;
+    } else if constexpr (std::is_signed_v<T>) {
+        return (uint64_t)(int64_t)v;
+    } else {
+        return (uint64_t)v;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_nu_collect(AggDev a, const uint64_t *idx, uint64_t n, uint64_t *null_cnt,
+                                                    uint64_t *nan_cnt, uint64_t *out_cell, uint64_t *out_val,
+                                                    unsigned long long *counter) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = idx[i];
+        bool emit = false;
+        uint64_t bits = 0;
+        const bool masked = a.mask && a.mask[i] == 0;
+        if (masked && a.has_selection) {
+            // outside the selection / filter: not seen (agg_hash_primitive.cpp:46-47)
+        } else if (masked) {
+            atomicAdd((unsigned long long *)&null_cnt[c], 1ULL);
+        } else {
+            bool nan;
+            bits = nu_bits<T>(nu_load<T>(a.data, i, a.flip), &nan);
+            if (nan) atomicAdd((unsigned long long *)&nan_cnt[c], 1ULL);
+            else emit = true;
+        }
+        // wave-aggregated slot reservation
+        const uint64_t ballot = __ballot(emit);
+        if (!ballot) continue;
+        const int lane = threadIdx.x & 63;
+        const int leader = __ffsll((unsigned long long)ballot) - 1;
+        unsigned long long base = 0;
+        if (lane == leader) base = atomicAdd(counter, (unsigned long long)__popcll(ballot));
+        base = __shfl(base, leader, 64);
+        if (emit) {
+            const uint64_t pos = base + __popcll(ballot & ((1ull << lane) - 1));
+            out_cell[pos] = c;
+            out_val[pos] = bits;
+        }
+    }
+}
+
+// after the (cell, value) sort: the first of each run of equal pairs counts for its cell
+// and is written to the deduplicated list
+__global__ __launch_bounds__(256) void k_nu_unique(const uint64_t *cell, const uint64_t *val, uint64_t n,
+                                                   uint64_t *distinct, uint64_t *out_cell, uint64_t *out_val,
+                                                   unsigned long long *counter) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const bool first = i == 0 || cell[i] != cell[i - 1] || val[i] != val[i - 1];
+        if (first) atomicAdd((unsigned long long *)&distinct[cell[i]], 1ULL);
+        const uint64_t ballot = __ballot(first);
+        if (!ballot) continue;
+        const int lane = threadIdx.x & 63;
+        const int leader = __ffsll((unsigned long long)ballot) - 1;
+        unsigned long long base = 0;
+        if (lane == leader) base = atomicAdd(counter, (unsigned long long)__popcll(ballot));
+        base = __shfl(base, leader, 64);
+        if (first) {
+            const uint64_t pos = base + __popcll(ballot & ((1ull << lane) - 1));
+            out_cell[pos] = cell[i];
+            out_val[pos] = val[i];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_nu_grid(const uint64_t *distinct, const uint64_t *null_cnt,
+                                                 const uint64_t *nan_cnt, uint64_t L, uint32_t flags, int64_t *grid) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < L; i += (uint64_t)gridDim.x * blockDim.x) {
+        int64_t v = (int64_t)distinct[i] + (null_cnt[i] ? 1 : 0) + (nan_cnt[i] ? 1 : 0);
+        if (flags & 1) v -= (int64_t)null_cnt[i];
+        if (flags & 2) v -= (int64_t)nan_cnt[i];
+        grid[i] = v;
+    }
+}
+
+__global__ void k_nu_add(uint64_t *a, const uint64_t *b, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        a[i] += b[i];
+}
+
+static unsigned bits_for(uint64_t v) {
+    unsigned b = 1;
+    while (b < 64 && (v >> b)) b++;
+    return b;
+}
+
+static uint64_t read_counter(const DevBuf &b) {
+    uint64_t v = 0;
+    VH_HIP(hipMemcpyAsync(&v, b.ptr, 8, hipMemcpyDeviceToHost, stream()));
+    VH_HIP(hipStreamSynchronize(stream()));
+    return v;
+}
+
+// room for `extra` more pairs (the list is copied into a doubled buffer)
+static void nu_reserve(vh_agg *a, uint64_t extra) {
+    const uint64_t need = (a->nu_n + extra) * 8;
+    if (need <= a->nu_cell.bytes) return;
+    uint64_t cap = std::max<uint64_t>(need, a->nu_cell.bytes * 2);
+    cap = std::max<uint64_t>(cap, 1 << 16);
+    DevBuf nc, nv;
+    nc.ensure(cap);
+    nv.ensure(cap);
+    if (a->nu_n) {
+        VH_HIP(hipMemcpyAsync(nc.ptr, a->nu_cell.ptr, a->nu_n * 8, hipMemcpyDeviceToDevice, stream()));
+        VH_HIP(hipMemcpyAsync(nv.ptr, a->nu_val.ptr, a->nu_n * 8, hipMemcpyDeviceToDevice, stream()));
+    }
+    VH_HIP(hipStreamSynchronize(stream()));
+    std::swap(a->nu_cell.ptr, nc.ptr);
+    std::swap(a->nu_cell.bytes, nc.bytes);
+    std::swap(a->nu_val.ptr, nv.ptr);
+    std::swap(a->nu_val.bytes, nv.bytes);
+}
+
+// sort the list by (cell, value), count distinct pairs per cell into `distinct` (L
+// counters, or a scratch when null) and replace the list by its deduplicated form
+static void nu_dedup(vh_agg *a, uint64_t *distinct) {
+    const uint64_t n = a->nu_n, L = a->L;
+    hipStream_t st = stream();
+    if (distinct) VH_HIP(hipMemsetAsync(distinct, 0, L * 8, st));
+    if (!n) return;
+    TimedScope ts("nunique_dedup");
+    DevBuf c1, v1, c2, v2, tmp, ctr, dscratch;
+    c1.ensure(n * 8);
+    v1.ensure(n * 8);
+    c2.ensure(n * 8);
+    v2.ensure(n * 8);
+    ctr.ensure(8);
+    const unsigned cbits = bits_for(L);
+    size_t t1 = 0, t2 = 0;
+    VH_HIP(rocprim::radix_sort_pairs(nullptr, t1, (uint64_t *)nullptr, (uint64_t *)nullptr, (uint64_t *)nullptr,
+                                     (uint64_t *)nullptr, (size_t)n, 0, 64, st));
+    VH_HIP(rocprim::radix_sort_pairs(nullptr, t2, (uint64_t *)nullptr, (uint64_t *)nullptr, (uint64_t *)nullptr,
+                                     (uint64_t *)nullptr, (size_t)n, 0, cbits, st));
+    tmp.ensure(std::max<size_t>(std::max(t1, t2), 16));
+    // LSD: by value, then stably by cell
+    size_t tb = tmp.bytes;
+    VH_HIP(rocprim::radix_sort_pairs(tmp.ptr, tb, a->nu_val.as<uint64_t>(), v1.as<uint64_t>(),
+                                     a->nu_cell.as<uint64_t>(), c1.as<uint64_t>(), (size_t)n, 0, 64, st));
+    tb = tmp.bytes;
+    VH_HIP(rocprim::radix_sort_pairs(tmp.ptr, tb, c1.as<uint64_t>(), c2.as<uint64_t>(), v1.as<uint64_t>(),
+                                     v2.as<uint64_t>(), (size_t)n, 0, cbits, st));
+    uint64_t *dist = distinct;
+    if (!dist) {
+        dscratch.ensure(L * 8);
+        dist = dscratch.as<uint64_t>();
+        VH_HIP(hipMemsetAsync(dist, 0, L * 8, st));
+    }
+    VH_HIP(hipMemsetAsync(ctr.ptr, 0, 8, st));
+    hipLaunchKernelGGL(k_nu_unique, dim3(blocks_for(n, 256)), dim3(256), 0, st, c2.as<uint64_t>(), v2.as<uint64_t>(),
+                       n, dist, a->nu_cell.as<uint64_t>(), a->nu_val.as<uint64_t>(),
+                       reinterpret_cast<unsigned long long *>(ctr.ptr));
+    VH_HIP(hipGetLastError());
+    a->nu_n = read_counter(ctr);
+}
+
+void nunique_init(vh_agg *a) {
+    const uint64_t L = a->L;
+    a->g2.ensure(std::max<uint64_t>(L, 1) * 8);
+    a->s_key.ensure(std::max<uint64_t>(L, 1) * 8);
+    VH_HIP(hipMemsetAsync(a->g.ptr, 0, L * 8, stream()));
+    VH_HIP(hipMemsetAsync(a->g2.ptr, 0, L * 8, stream()));
+    VH_HIP(hipMemsetAsync(a->s_key.ptr, 0, L * 8, stream()));
+    VH_HIP(hipStreamSynchronize(stream()));
+    a->nu_n = 0;
+    a->nu_dirty = false;
+}
+
+void nunique_collect(vh_agg *a, const AggDev &ad, const uint64_t *idx, uint64_t len) {
+    if (!len) return;
+    if (a->nu_n + len > NU_COMPACT_AT && a->nu_n) nu_dedup(a, nullptr);
+    nu_reserve(a, len);
+    DevBuf ctr;
+    ctr.ensure(8);
+    VH_HIP(hipMemsetAsync(ctr.ptr, 0, 8, stream()));
+    {
+        TimedScope ts("nunique_collect");
+        VH_DISPATCH_DTYPE(ad.dtype, T,
+                          hipLaunchKernelGGL(k_nu_collect<T>, dim3(blocks_for(len, 256)), dim3(256), 0, stream(), ad,
+                                             idx, len, a->g2.as<uint64_t>(), a->s_key.as<uint64_t>(),
+                                             a->nu_cell.as<uint64_t>() + a->nu_n, a->nu_val.as<uint64_t>() + a->nu_n,
+                                             reinterpret_cast<unsigned long long *>(ctr.ptr)));
+        VH_HIP(hipGetLastError());
+    }
+    a->nu_n += read_counter(ctr);
+    a->nu_dirty = true;
+}
+
+void nunique_merge(vh_agg *a, vh_agg *o) {
+    nunique_finalize(o);  // deduplicated first: fewer pairs to copy
+    const uint64_t L = a->L;
+    nu_reserve(a, o->nu_n);
+    if (o->nu_n) {
+        VH_HIP(hipMemcpyAsync(a->nu_cell.as<uint64_t>() + a->nu_n, o->nu_cell.ptr, o->nu_n * 8,
+                              hipMemcpyDeviceToDevice, stream()));
+        VH_HIP(hipMemcpyAsync(a->nu_val.as<uint64_t>() + a->nu_n, o->nu_val.ptr, o->nu_n * 8,
+                              hipMemcpyDeviceToDevice, stream()));
+    }
+    a->nu_n += o->nu_n;
+    if (L) {
+        hipLaunchKernelGGL(k_nu_add, dim3(blocks_for(L, 256)), dim3(256), 0, stream(), a->g2.as<uint64_t>(),
+                           o->g2.as<uint64_t>(), L);
+        hipLaunchKernelGGL(k_nu_add, dim3(blocks_for(L, 256)), dim3(256), 0, stream(), a->s_key.as<uint64_t>(),
+                           o->s_key.as<uint64_t>(), L);
+        VH_HIP(hipGetLastError());
+    }
+    a->nu_dirty = true;
+}
+
+void nunique_finalize(vh_agg *a) {
+    if (a->kind != VH_AGG_NUNIQUE || !a->nu_dirty) return;
+    const uint64_t L = a->L;
+    DevBuf distinct;
+    distinct.ensure(std::max<uint64_t>(L, 1) * 8);
+    nu_dedup(a, distinct.as<uint64_t>());
+    if (L) {
+        hipLaunchKernelGGL(k_nu_grid, dim3(blocks_for(L, 256)), dim3(256), 0, stream(), distinct.as<uint64_t>(),
+                           a->g2.as<uint64_t>(), a->s_key.as<uint64_t>(), L, a->moment, a->g.as<int64_t>());
+        VH_HIP(hipGetLastError());
+    }
+    VH_HIP(hipStreamSynchronize(stream()));
+    a->nu_dirty = false;
+}
+
+}  // namespace vh

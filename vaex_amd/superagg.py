@@ -342,6 +342,26 @@ class Aggregator:
             self._handle = None
 
 
+class _AggNUniqueBase(Aggregator):
+    """AggNUnique_<t>(grid, dropmissing, dropnan) (agg_hash_primitive.cpp:6-102,
+    superagg.cpp add_agg): distinct values per cell, an int64 grid derived from the
+    (cell, value) pairs kept in HBM."""
+
+    _kind = "AggNUnique"
+
+    def __init__(self, grid, dropmissing=False, dropnan=False):
+        super().__init__(grid, (1 if dropmissing else 0) | (2 if dropnan else 0))
+        self.dropmissing, self.dropnan = bool(dropmissing), bool(dropnan)
+
+    def set_selection_mask(self, ar):
+        ptr, length, itemsize, ndim, loc, keep = _column(ar)
+        _lib.call("vh_agg_set_selection_mask", self._handle, ptr, length, ndim, loc)
+        self._refs["selection"] = keep
+
+    def _before_device_use(self):
+        pass  # the grid is derived from the pairs: writes through a view do not feed back
+
+
 def _register():
     ns = globals()
     for dtype in DTYPES:
@@ -353,6 +373,7 @@ def _register():
             for kind in ("AggCount", "AggSum", "AggMin", "AggMax", "AggFirst", "AggSumMoment"):
                 name = kind + "_" + postfix
                 ns[name] = type(name, (Aggregator,), dict(attrs, _kind=kind))
+            ns["AggNUnique_" + postfix] = type("AggNUnique_" + postfix, (_AggNUniqueBase,), dict(attrs))
 
 
 _register()

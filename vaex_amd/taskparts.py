@@ -121,6 +121,10 @@ class TaskPartAggregation:
                         selection_mask = np.asarray(selection_mask)
                 elif device_filter:
                     selection_mask = filter_mask
+                if selection_mask is not None and hasattr(agg, "set_selection_mask"):
+                    # nunique tells rows outside the selection (or an HBM frame's filter)
+                    # from missing values (cpu.py:551-554)
+                    agg.set_selection_mask(selection_mask)
                 for i, expression in enumerate(desc.expressions):
                     block, mask = _split_masked(blocks[expression])
                     block = _prepare(block)
