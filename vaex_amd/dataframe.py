@@ -560,6 +560,24 @@ class DataFrame:
             return groupby
         return groupby.agg(agg)
 
+    def export_hdf5(self, path, **kwargs):
+        """dataframe.py export_hdf5: numeric columns (host or HBM) as vaex's HDF5 layout
+        version 2, contiguous and 4 KiB aligned so the file maps back without copies."""
+        from .hdf5 import export_hdf5
+        export_hdf5(self, path)
+
+    def export_arrow(self, path, **kwargs):
+        import pyarrow as pa
+        cols = {}
+        for name in self.get_column_names():
+            v = self.columns.get(name)
+            v = v.to_numpy() if isinstance(v, DeviceArray) else np.asarray(self.evaluate(name) if v is None else v)
+            cols[name] = pa.array(v)
+        with pa.OSFile(str(path), "wb") as sink:
+            table = pa.table(cols)
+            with pa.ipc.new_file(sink, table.schema) as w:
+                w.write_table(table)
+
     def binby(self, by=None, agg=None, sort=False, copy=True, delay=False, progress=None):
         from .groupby import BinBy
         binby = BinBy(self, by=by, sort=sort)
