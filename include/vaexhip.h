@@ -139,6 +139,12 @@ int vh_agg_clear_data_mask(vh_agg *agg);
 /* AggNUnique::set_selection_mask (agg_hash_primitive.cpp:82-89): with a selection set, rows
  * whose data mask is 0 are outside the selection (skipped), not missing values */
 int vh_agg_set_selection_mask(vh_agg *agg, const uint8_t *mask, uint64_t length, int ndim, int loc);
+/* AggNUnique state to / from host memory (multi-GPU combine, counter::merge
+ * hash_primitives.hpp:393-415): export with null arrays returns the deduplicated pair
+ * count in *n; nulls / nans hold one count per grid cell; import appends and adds */
+int vh_agg_nunique_export(vh_agg *agg, uint64_t *n, uint64_t *cells, uint64_t *vals, uint64_t *nulls, uint64_t *nans);
+int vh_agg_nunique_import(vh_agg *agg, uint64_t n, const uint64_t *cells, const uint64_t *vals, const uint64_t *nulls,
+                          const uint64_t *nans);
 /* __sizeof__ (grid bytes, agg.hpp:162-164), grid dtype and itemsize */
 int vh_agg_info(const vh_agg *agg, uint64_t *bytes, int *grid_dtype, uint64_t *itemsize);
 /* buffer protocol (agg.hpp:166-179): the grid is copied to/from a host image */

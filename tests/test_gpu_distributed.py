@@ -22,7 +22,8 @@ def _data():
     key = rng.integers(0, 5000, n).astype(np.int32) * 7 - 300
     # sparse keys (value span >> rows): DataFrame.groupby takes the fused hash path
     skey = (rng.integers(0, 20000, n).astype(np.int64) * 104729 - 10 ** 9).astype(np.int32)
-    return dict(x=x, y=y, w=w, key=key, skey=skey)
+    c = rng.integers(0, 40, n).astype(np.int16)
+    return dict(x=x, y=y, w=w, key=key, skey=skey, c=c)
 
 
 def _queries(df):
@@ -38,6 +39,10 @@ def _queries(df):
         out[f"gb_{mode}_key"] = np.asarray(g["key"].to_numpy())
         out[f"gb_{mode}_sum"] = np.asarray(g["v_sum"].to_numpy())
         out[f"gb_{mode}_n"] = np.asarray(g["n"].to_numpy())
+    g = df.groupby("key", agg={"nu": __import__("vaex_amd").agg.nunique("c"),
+                               "nu_sel": __import__("vaex_amd").agg.nunique("c", selection="x > 0")}, sort=True)
+    out["gb_nunique"] = np.asarray(g["nu"].to_numpy())
+    out["gb_nunique_sel"] = np.asarray(g["nu_sel"].to_numpy())
     g = df.groupby("skey", agg={"w": ["sum", "count", "mean"]})
     for c in g.get_column_names():
         out[f"gb_fused_{c}"] = np.asarray(g[c].to_numpy())

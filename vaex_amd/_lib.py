@@ -60,6 +60,8 @@ SIGNATURES = {
     "vh_agg_set_data_mask": (_i32, [_vp, _vp, _u64, _i32, _i32]),
     "vh_agg_clear_data_mask": (_i32, [_vp]),
     "vh_agg_set_selection_mask": (_i32, [_vp, _vp, _u64, _i32, _i32]),
+    "vh_agg_nunique_export": (_i32, [_vp, _p(_u64), _vp, _vp, _vp, _vp]),
+    "vh_agg_nunique_import": (_i32, [_vp, _u64, _vp, _vp, _vp, _vp]),
     "vh_agg_info": (_i32, [_vp, _p(_u64), _p(_i32), _p(_u64)]),
     "vh_agg_download": (_i32, [_vp, _vp, _u64]),
     "vh_agg_upload": (_i32, [_vp, _vp, _u64]),

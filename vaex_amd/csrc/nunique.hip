@@ -268,3 +268,50 @@ void nunique_finalize(vh_agg *a) {
 }
 
 }  // namespace vh
+
+using namespace vh;
+
+// Pairs and per-cell missing / NaN counts of an AggNUnique, to host memory and back: the
+// multi-GPU combine gathers them from every rank (distributed.py), like counter::merge
+// merges the per-thread counters (hash_primitives.hpp:393-415).
+extern "C" int vh_agg_nunique_export(vh_agg *a, uint64_t *n, uint64_t *cells, uint64_t *vals, uint64_t *nulls,
+                                     uint64_t *nans) {
+    VH_API_BEGIN
+    if (a->kind != VH_AGG_NUNIQUE) fail(VH_ERR_ARG, "not an AggNUnique");
+    nunique_finalize(a);  // deduplicated
+    if (n) *n = a->nu_n;
+    hipStream_t st = stream();
+    if (cells && a->nu_n) VH_HIP(hipMemcpyAsync(cells, a->nu_cell.ptr, a->nu_n * 8, hipMemcpyDeviceToHost, st));
+    if (vals && a->nu_n) VH_HIP(hipMemcpyAsync(vals, a->nu_val.ptr, a->nu_n * 8, hipMemcpyDeviceToHost, st));
+    if (nulls) VH_HIP(hipMemcpyAsync(nulls, a->g2.ptr, a->L * 8, hipMemcpyDeviceToHost, st));
+    if (nans) VH_HIP(hipMemcpyAsync(nans, a->s_key.ptr, a->L * 8, hipMemcpyDeviceToHost, st));
+    VH_HIP(hipStreamSynchronize(st));
+    VH_API_END
+}
+
+extern "C" int vh_agg_nunique_import(vh_agg *a, uint64_t n, const uint64_t *cells, const uint64_t *vals,
+                                     const uint64_t *nulls, const uint64_t *nans) {
+    VH_API_BEGIN
+    if (a->kind != VH_AGG_NUNIQUE) fail(VH_ERR_ARG, "not an AggNUnique");
+    hipStream_t st = stream();
+    for (uint64_t i = 0; i < n; i++)
+        if (cells[i] >= a->L) fail(VH_ERR_ARG, "nunique import: cell index out of range");
+    nu_reserve(a, n);
+    if (n) {
+        VH_HIP(hipMemcpyAsync(a->nu_cell.as<uint64_t>() + a->nu_n, cells, n * 8, hipMemcpyHostToDevice, st));
+        VH_HIP(hipMemcpyAsync(a->nu_val.as<uint64_t>() + a->nu_n, vals, n * 8, hipMemcpyHostToDevice, st));
+    }
+    a->nu_n += n;
+    DevBuf tmp;
+    tmp.ensure(a->L * 16);
+    VH_HIP(hipMemcpyAsync(tmp.ptr, nulls, a->L * 8, hipMemcpyHostToDevice, st));
+    VH_HIP(hipMemcpyAsync(tmp.as<uint64_t>() + a->L, nans, a->L * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_nu_add, dim3(blocks_for(a->L, 256)), dim3(256), 0, st, a->g2.as<uint64_t>(), tmp.as<uint64_t>(),
+                       a->L);
+    hipLaunchKernelGGL(k_nu_add, dim3(blocks_for(a->L, 256)), dim3(256), 0, st, a->s_key.as<uint64_t>(),
+                       tmp.as<uint64_t>() + a->L, a->L);
+    VH_HIP(hipGetLastError());
+    VH_HIP(hipStreamSynchronize(st));
+    a->nu_dirty = true;
+    VH_API_END
+}

@@ -164,6 +164,41 @@ def combine_aggs_host(aggs, group=None):
         agg._after_device_write()
 
 
+def nunique_state(agg):
+    """(cells, values, nulls, nans) of an AggNUnique as host arrays (deduplicated pairs)."""
+    import ctypes
+    from . import _lib
+    n = ctypes.c_uint64()
+    _lib.call("vh_agg_nunique_export", agg._handle, ctypes.byref(n), None, None, None, None)
+    L = agg.grid.length1d
+    cells, vals = np.empty(n.value, np.uint64), np.empty(n.value, np.uint64)
+    nulls, nans = np.empty(L, np.uint64), np.empty(L, np.uint64)
+    _lib.call("vh_agg_nunique_export", agg._handle, ctypes.byref(n), cells.ctypes.data, vals.ctypes.data,
+              nulls.ctypes.data, nans.ctypes.data)
+    return cells, vals, nulls, nans
+
+
+def combine_nunique(agg, group=None):
+    """AggNUnique across ranks: every rank gathers the others' (cell, value) pairs and
+    missing / NaN counts and merges them into its own (counter::merge,
+    hash_primitives.hpp:393-415); distinct values are not additive, so no grid all-reduce."""
+    import torch.distributed as dist
+    from . import _lib
+    mine = nunique_state(agg)
+    world = dist.get_world_size(group)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, mine, group=group)
+    me = dist.get_rank(group)
+    for r, (cells, vals, nulls, nans) in enumerate(gathered):
+        if r == me:
+            continue
+        cells, vals = np.ascontiguousarray(cells, np.uint64), np.ascontiguousarray(vals, np.uint64)
+        nulls, nans = np.ascontiguousarray(nulls, np.uint64), np.ascontiguousarray(nans, np.uint64)
+        _lib.call("vh_agg_nunique_import", agg._handle, len(cells), cells.ctypes.data, vals.ctypes.data,
+                  nulls.ctypes.data, nans.ctypes.data)
+    agg._after_device_write()
+
+
 class ExecutorDistributed(ExecutorLocal):
     """ExecutorLocal over this rank's row shard, combining task parts across ranks.
 
@@ -201,6 +236,9 @@ class ExecutorDistributed(ExecutorLocal):
         for p in parts:
             if isinstance(p, TaskPartAggregation):
                 aggs = p.get_aggregators()
+                for agg in [a for a in aggs if a._kind == "AggNUnique"]:
+                    combine_nunique(agg, group=self.group)
+                aggs = [a for a in aggs if a._kind != "AggNUnique"]
                 if self.device_collectives:
                     allreduce_aggs(aggs, group=self.group)
                 else:
