@@ -104,8 +104,10 @@ class GrouperDense(BinnerBase):
             self._bin_values = np.arange(self.min_value, self.min_value + self.N, dtype=np.int64).astype(self.value_dtype)
         return self._bin_values
 
-    def occupied_values(self, mask):
+    def occupied_values(self, mask, all_set=False):
         """Labels of the cells where mask is set (mask over the N central cells)."""
+        if all_set:
+            return np.arange(self.min_value, self.min_value + self.N, dtype=np.int64).astype(self.value_dtype)
         return (np.flatnonzero(mask) + self.min_value).astype(self.value_dtype)
 
     def labels(self):
@@ -351,14 +353,15 @@ class GroupBy(GroupByBase):
                 if groups > self.row_limit:  # what the set build of Grouper raises (groupby.py:125)
                     raise RowLimitException(f"Resulting grouper has {groups:,} unique combinations, which is "
                                             f"larger than the allowed row limit of {self.row_limit:,}")
+            every = bool(mask.all())  # every cell occupied (e.g. a dense key range): no compaction
             if len(self.by) == 1 and isinstance(self.by[0], GrouperDense):
-                coords = [self.by[0].occupied_values(mask)]
+                coords = [self.by[0].occupied_values(mask, all_set=every)]
             else:
                 coords = [c[mask] for c in np.meshgrid(*[np.asarray(b.bin_values) for b in self.by], indexing="ij")]
             for b, coord in zip(self.by, coords):
                 columns[b.label] = coord
             for k, v in arrays.items():
-                columns[k] = v[mask]
+                columns[k] = v if every and v.ndim == 1 else v[mask]
         else:
             columns[self.by[0].label] = np.asarray(self.by[0].bin_values)
             for k, v in arrays.items():

@@ -271,6 +271,14 @@ class Aggregator:
         return self._nbytes
 
     # ---- host image / device coherence --------------------------------------
+    def _release_host(self):
+        """The current host image now belongs to a result array (which keeps this object,
+        and so the image, alive through its base): later reads get a fresh image."""
+        self._released = self._host
+        self._host = None
+        self._exposed = False
+        self._device_newer = True
+
     def _ensure_host(self):
         if self._host is None:
             self._host = _lib.pinned_empty(self._grid.length1d, self._grid_dtype)

@@ -159,7 +159,14 @@ class TaskPartAggregation:
             dtype_out = np.dtype(desc.dtype_out)
             if dtype_out.kind in "mM" or result.dtype.itemsize == dtype_out.itemsize:
                 result = result.view(dtype_out.newbyteorder("=") if dtype_out.byteorder not in "<=|" else dtype_out)
-            results.append(result.copy())
+            host = getattr(aggs[0], "_host", None) if len(aggs) == 1 and not selection_waslist else None
+            if host is not None and result.ndim <= 1 and result.flags.c_contiguous and np.may_share_memory(result, host):
+                # the part is done with its aggregator: hand its (page-locked) host image over
+                # instead of copying it (cpu.py:605 copies because its grids are reused)
+                aggs[0]._release_host()
+                results.append(result)
+            else:
+                results.append(result.copy())
         return results
 
 
