@@ -54,7 +54,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    # BENCH_FORCE_DIST=1: the N>1 code path (RCCL init, grid all-reduce, max-over-ranks
+    # timing) on a single rank, to exercise it on a one-GPU box
+    if world > 1 or os.environ.get("BENCH_FORCE_DIST"):
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
