@@ -1,0 +1,42 @@
+"""h2o groupby G1 (benchmarks/groupbyh2o.py:15-93 with fixtures.py:38-70's columns) on HBM
+columns: q1-q5, q7, q10 timed end to end.  usage: python scripts/exp_h2o.py [rows] [q...]"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import vaex_amd  # noqa: E402
+from vaex_amd import _lib  # noqa: E402
+from vaex_amd.device import DeviceArray  # noqa: E402
+
+n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 10 ** 8
+which = sys.argv[2:] or ["q1", "q2", "q3", "q4", "q5", "q7", "q10"]
+rng = np.random.default_rng(0)
+i1_100 = rng.integers(5, 105, n).astype(np.int8)
+i4_1M = rng.integers(5, 1_000_005, n).astype(np.int32)
+i1_10 = rng.integers(5, 15, n).astype(np.int8)
+x4 = rng.normal(size=n).astype(np.float32)
+d = {k: DeviceArray.from_numpy(v) for k, v in dict(i1_100=i1_100, i4_1M=i4_1M, i1_10=i1_10, x4=x4).items()}
+df = vaex_amd.from_arrays(**d)
+for a, b in [("id1", "i1_100"), ("id2", "i1_100"), ("id3", "i4_1M"), ("id4", "i1_100"), ("id5", "i1_100"),
+             ("id6", "i4_1M"), ("v1", "i1_10"), ("v2", "i1_10"), ("v3", "x4")]:
+    df.columns[a] = df.columns[b]  # the benchmark's aliases (df['id1'] = df['i1_100'])
+Q = {
+    "q1": lambda: df.groupby(["id1"]).agg({"v1": "sum"}),
+    "q2": lambda: df.groupby(["id1", "id2"]).agg({"v1": "sum"}),
+    "q3": lambda: df.groupby(["id3"]).agg({"v1": "sum", "v3": "mean"}),
+    "q4": lambda: df.groupby(["id4"]).agg({"v1": "mean", "v2": "mean", "v3": "mean"}),
+    "q5": lambda: df.groupby(["id6"]).agg({"v1": "sum", "v2": "sum", "v3": "sum"}),
+    "q7": lambda: df.groupby(["id3"]).agg({"v1": "max", "v2": "min"}),
+    "q10": lambda: df.groupby(["id1", "id2", "id3", "id4", "id5", "id6"]).agg({"v3": "sum", "v1": "count"}),
+}
+for q in which:
+    for it in range(3):
+        _lib.synchronize()
+        t0 = time.perf_counter()
+        r = Q[q]()
+        _lib.synchronize()
+        t = time.perf_counter() - t0
+    print(f"{q}: {t * 1e3:.2f} ms  {n / t / 1e9:.2f} G rows/s  groups {len(r)}", flush=True)

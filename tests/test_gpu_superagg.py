@@ -338,3 +338,79 @@ def test_tiled_path_many_tiles(bins, nsums):
     np.testing.assert_array_equal(np.asarray(aggs[0]), _oracle_grid([bx, by], "count"))
     for a, w in zip(aggs[1:], ws):
         np.testing.assert_allclose(np.asarray(a), _oracle_grid([bx, by], "sum", data=w), rtol=1e-6, atol=1e-12)
+
+
+@pytest.mark.parametrize("dtype", ["int8", "int32", "uint16", "uint64", "float32", "bool", "int64"])
+def test_tile_path_generic_dtype_sums(dtype):
+    """count / sum of non-float64 columns over a 1e5+ cell grid take the tile path with
+    per-dtype loads (integer sums accumulate as 64-bit integers, float32 as float64):
+    bit-exact integer sums and counts, float sums within 1e-6."""
+    from vaex_amd import _lib
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(len(dtype))
+    n = 3_000_001
+    key = rng.integers(0, 200_000, n).astype(np.int32)
+    if dtype == "bool":
+        v = rng.random(n) > 0.5
+    elif dtype == "float32":
+        v = rng.normal(size=n).astype(np.float32)
+        v[::77] = np.nan
+    else:
+        info = np.iinfo(dtype)
+        v = rng.integers(max(info.min, -100), min(info.max, 100), n).astype(dtype)
+        if dtype == "uint64":
+            v[::5] = np.uint64(2 ** 63 + 12345)
+    spec = oracle.Binner("ordinal", key, ordinal_count=200_000, min_value=0)
+    b = sa().BinnerOrdinal_int32("key", 200_000, 0)
+    b.set_data(DeviceArray.from_numpy(key))
+    grid = sa().Grid([b])
+    s = getattr(sa(), "AggSum_" + dtype)(grid)
+    s.set_data(DeviceArray.from_numpy(v), 0)
+    c = getattr(sa(), "AggCount_" + dtype)(grid)
+    c.set_data(DeviceArray.from_numpy(v), 0)
+    _lib.timing_reset()
+    _lib.timing_enable(True)
+    grid.bin([s, c])
+    _lib.synchronize()
+    _lib.timing_enable(False)
+    assert _lib.timing_read("tile_reduce")[0] >= 1, "tile path not used"
+    exp_s = _oracle_grid([spec], "sum", data=v)
+    exp_c = _oracle_grid([spec], "count", data=v)
+    np.testing.assert_array_equal(np.asarray(c), exp_c)
+    if dtype == "float32":
+        np.testing.assert_allclose(np.asarray(s), exp_s, rtol=1e-6, atol=1e-9)
+    else:
+        np.testing.assert_array_equal(np.asarray(s), exp_s)
+
+
+def test_tile_path_three_sums_in_groups():
+    """Three sums (h2o q5's shape: two int8 columns and a float32 one) run as two tile
+    passes of at most two carried values each."""
+    from vaex_amd import _lib
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(5)
+    n = 2_000_000
+    key = rng.integers(0, 300_000, n).astype(np.int32)
+    v1 = rng.integers(5, 15, n).astype(np.int8)
+    v2 = rng.integers(-5, 5, n).astype(np.int8)
+    v3 = rng.normal(size=n).astype(np.float32)
+    spec = oracle.Binner("ordinal", key, ordinal_count=300_000, min_value=0)
+    b = sa().BinnerOrdinal_int32("key", 300_000, 0)
+    b.set_data(DeviceArray.from_numpy(key))
+    grid = sa().Grid([b])
+    aggs = []
+    for v in (v1, v2, v3):
+        a = getattr(sa(), "AggSum_" + v.dtype.name)(grid)
+        a.set_data(DeviceArray.from_numpy(v), 0)
+        aggs.append(a)
+    c = sa().AggCount_int64(grid)
+    _lib.timing_reset()
+    _lib.timing_enable(True)
+    grid.bin(aggs + [c])
+    _lib.synchronize()
+    _lib.timing_enable(False)
+    assert _lib.timing_read("tile_reduce")[0] == 2
+    np.testing.assert_array_equal(np.asarray(aggs[0]), _oracle_grid([spec], "sum", data=v1))
+    np.testing.assert_array_equal(np.asarray(aggs[1]), _oracle_grid([spec], "sum", data=v2))
+    np.testing.assert_allclose(np.asarray(aggs[2]), _oracle_grid([spec], "sum", data=v3), rtol=1e-6, atol=1e-9)
+    np.testing.assert_array_equal(np.asarray(c), _oracle_grid([spec], "count"))

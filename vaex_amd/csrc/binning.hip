@@ -181,6 +181,78 @@ __global__ __launch_bounds__(256) void k_agg(AggDev a, const uint64_t *idx, uint
     }
 }
 
+// Small grids (<= LDS_AGG_MAX_BYTES of cells): every workgroup aggregates into its own LDS
+// copy of the grid in the same pass that bins the rows (no indices1d round trip, no global
+// atomic per row -- a few hundred cells hit by every row would serialise on them), then
+// flushes it with one global atomic per touched cell.  Per-row semantics exactly as k_agg.
+constexpr uint64_t LDS_AGG_MAX_BYTES = 96 * 1024;
+
+template <int KIND, typename T> struct LdsCell {
+    using G = typename Upcast<T>::type;
+    using type = std::conditional_t<KIND == VH_AGG_MIN || KIND == VH_AGG_MAX, T,
+                                    std::conditional_t<KIND == VH_AGG_COUNT, unsigned long long, G>>;
+};
+
+template <int KIND, typename T>
+__global__ __launch_bounds__(256) void k_agg_lds(BinPlan p, AggDev a, uint64_t n, uint64_t L, T fill) {
+    using G = typename Upcast<T>::type;
+    using C = typename LdsCell<KIND, T>::type;
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    C *g = reinterpret_cast<C *>(lds_raw);
+    for (uint64_t c = threadIdx.x; c < L; c += blockDim.x) {
+        if constexpr (KIND == VH_AGG_MIN || KIND == VH_AGG_MAX) g[c] = fill;
+        else g[c] = (C)0;
+    }
+    __syncthreads();
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+        if (a.mask && a.mask[j] != 1) continue;
+        const uint64_t c = plan_index(p, j);
+        if constexpr (KIND == VH_AGG_COUNT) {
+            if (a.data) {
+                T v = load_v<T>(a.data, j, a.flip);
+                if (is_nan_v(v)) continue;
+            }
+            atomicAdd(g + c, 1ULL);
+        } else if constexpr (KIND == VH_AGG_SUM) {
+            T v = load_v<T>(a.data, j, a.flip);
+            if (is_nan_v(v)) continue;
+            atomic_add_grid<G>(g + c, upcast_v(v));
+        } else if constexpr (KIND == VH_AGG_MIN || KIND == VH_AGG_MAX) {
+            T v = load_v<T>(a.data, j, a.flip);
+            if (is_nan_v(v)) continue;
+            atomic_minmax<T>(g + c, v, KIND == VH_AGG_MAX);
+        } else if constexpr (KIND == VH_AGG_SUM_MOMENT) {
+            G value = upcast_v(reinterpret_cast<const T *>(a.data)[j]);
+            if (a.flip) value = bswap_v(value);
+            if (is_nan_v(value)) continue;
+            double pw;
+            if (a.moment == 0) pw = 1.0;
+            else if (a.moment == 1) pw = (double)value;
+            else if (a.moment == 2) pw = (double)value * (double)value;
+            else pw = pow((double)value, (double)a.moment);
+            atomic_add_grid<G>(g + c, (G)pw);
+        }
+    }
+    __syncthreads();
+    for (uint64_t c = threadIdx.x; c < L; c += blockDim.x) {
+        const C v = g[c];
+        if constexpr (KIND == VH_AGG_MIN || KIND == VH_AGG_MAX) {
+            using W = std::conditional_t<sizeof(T) == 8, uint64_t,
+                                         std::conditional_t<sizeof(T) == 4, uint32_t,
+                                                            std::conditional_t<sizeof(T) == 2, uint16_t, uint8_t>>>;
+            W vb, fb;
+            __builtin_memcpy(&vb, &v, sizeof(T));
+            __builtin_memcpy(&fb, &fill, sizeof(T));
+            if (vb != fb)
+                atomic_minmax<T>(reinterpret_cast<T *>(a.grid) + c, v, KIND == VH_AGG_MAX);
+        } else if constexpr (KIND == VH_AGG_COUNT) {
+            if (v) atomicAdd((unsigned long long *)a.grid + c, v);
+        } else {
+            if (v != (C)0) atomic_add_grid<G>(reinterpret_cast<G *>(a.grid) + c, v);
+        }
+    }
+}
+
 // AggFirst (superagg.cpp:481-505).  Per chunk: (A) min order key per cell,
 // (B) lowest row holding that key, (C) per cell: take it if strictly smaller
 // than the grid's order -- ties go to the earliest row, as a serial pass does.
@@ -886,7 +958,13 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
         note(aggs[k]->mask);
     }
     const uint64_t L = g->length1d;
-    const uint64_t chunk_max = any_host ? (uint64_t(1) << 24) : (all_fusable ? length : (uint64_t(1) << 26));
+    // count / sum of other native dtypes without masks on grids beyond the LDS sub-grid size
+    bool tile_generic = !all_fusable && naggs <= MAX_FUSED_AGGS && L * 8 > LDS_AGG_MAX_BYTES;
+    for (int k = 0; k < naggs && tile_generic; k++) {
+        const vh_agg *a = aggs[k];
+        tile_generic = (a->kind == VH_AGG_COUNT || (a->kind == VH_AGG_SUM && a->data.set)) && !a->mask.set && !a->flip;
+    }
+    const uint64_t chunk_max = any_host ? (uint64_t(1) << 24) : ((all_fusable || tile_generic) ? length : (uint64_t(1) << 26));
     HostPipe &pipe = g->ws.pipe;
     if (any_host) {
         pipe.cols.clear();
@@ -924,20 +1002,88 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                 fa.a[k].data = reinterpret_cast<const double *>(ad.data);
                 fa.a[k].mask = ad.mask;
                 fa.a[k].grid = ad.grid;
+                fa.a[k].dtype = ad.dtype;
+                fa.a[k].vint = 0;
             }
             launch_fused(plan, fa, len, L, scalar_f64_dims(g), g->ws);
+        } else if (tile_generic && [&] {
+                       // count / sum of any native dtype over a grid too large for LDS: the
+                       // tile-partitioned path with per-dtype loads, in groups of at most two
+                       // sums (the values a pass-A row carries); all groups or none (the
+                       // eligibility of the first decides, they share the plan)
+                       std::vector<std::vector<int>> groups(1);
+                       int sums = 0;
+                       for (int k = 0; k < naggs; k++) {
+                           if (aggs[k]->kind == VH_AGG_SUM && sums == 2) {
+                               groups.emplace_back();
+                               sums = 0;
+                           }
+                           if (aggs[k]->kind == VH_AGG_SUM) sums++;
+                           groups.back().push_back(k);
+                       }
+                       for (size_t gi = 0; gi < groups.size(); gi++) {
+                           FusedAggs fa{};
+                           fa.na = (int)groups[gi].size();
+                           fa.generic_vals = 1;
+                           for (int j = 0; j < fa.na; j++) {
+                               AggDev ad = agg_dev(aggs[groups[gi][j]], st);
+                               fa.a[j].kind = ad.kind;
+                               fa.a[j].data = reinterpret_cast<const double *>(ad.data);
+                               fa.a[j].mask = nullptr;
+                               fa.a[j].grid = ad.grid;
+                               fa.a[j].dtype = ad.dtype;
+                               fa.a[j].vint = ad.kind == VH_AGG_SUM && ad.dtype != VH_F64 && ad.dtype != VH_F32;
+                           }
+                           if (!try_tiled(plan, fa, len, L, scalar_f64_dims(g), g->ws)) {
+                               if (gi == 0) return false;
+                               fail(VH_ERR_RUNTIME, "tiled binning: aggregator group not eligible");
+                           }
+                       }
+                       return true;
+                   }()) {
+            // done by the tile path
         } else {
             std::vector<AggDev> ads;
             for (int k = 0; k < naggs; k++) ads.push_back(agg_dev(aggs[k], st));
-            g->ws.idx.ensure(len * 8);
-            uint64_t *idx = g->ws.idx.as<uint64_t>();
-            {
+            // small grids: LDS sub-grid per workgroup for every kind but AggFirst / AggNUnique
+            const bool small = L * 8 <= LDS_AGG_MAX_BYTES;
+            auto lds_ok = [&](int kind) { return small && kind != VH_AGG_FIRST && kind != VH_AGG_NUNIQUE; };
+            uint64_t *idx = nullptr;
+            for (int k = 0; k < naggs && !idx; k++) {
+                if (lds_ok(ads[k].kind)) continue;
+                g->ws.idx.ensure(len * 8);
+                idx = g->ws.idx.as<uint64_t>();
                 TimedScope ts("bin_indices");
                 hipLaunchKernelGGL(k_indices, dim3(blocks_for(len, 256)), dim3(256), 0, stream(), plan, len, idx);
                 VH_HIP(hipGetLastError());
             }
             for (int k = 0; k < naggs; k++) {
                 AggDev &ad = ads[k];
+                if (lds_ok(ad.kind)) {
+                    TimedScope ts("bin_aggregate_lds");
+                    dim3 grd(blocks_for(len, 256, 4)), blk(256);
+                    const size_t shm = (size_t)((L * 8 + 15) & ~uint64_t(15));
+                    const bool mx = ad.kind == VH_AGG_MAX;
+                    switch (ad.kind) {
+                    case VH_AGG_COUNT:
+                        VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg_lds<VH_AGG_COUNT, T>), grd, blk, shm, stream(), plan, ad, len, L, T{}));
+                        break;
+                    case VH_AGG_SUM:
+                        VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg_lds<VH_AGG_SUM, T>), grd, blk, shm, stream(), plan, ad, len, L, T{}));
+                        break;
+                    case VH_AGG_MIN:
+                        VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg_lds<VH_AGG_MIN, T>), grd, blk, shm, stream(), plan, ad, len, L, minmax_fill<T>(false)));
+                        break;
+                    case VH_AGG_MAX:
+                        VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg_lds<VH_AGG_MAX, T>), grd, blk, shm, stream(), plan, ad, len, L, minmax_fill<T>(mx)));
+                        break;
+                    case VH_AGG_SUM_MOMENT:
+                        VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg_lds<VH_AGG_SUM_MOMENT, T>), grd, blk, shm, stream(), plan, ad, len, L, T{}));
+                        break;
+                    }
+                    VH_HIP(hipGetLastError());
+                    continue;
+                }
                 dim3 grd(blocks_for(len, 256)), blk(256);
                 TimedScope ts("bin_aggregate");
                 switch (ad.kind) {

@@ -59,14 +59,18 @@ struct AggDev {
 struct FusedAgg {
     int32_t kind;
     uint32_t lds_off;
-    const double *data;   // nullptr for count(*)
+    const double *data;   // nullptr for count(*); of `dtype` (float64 unless generic_vals)
     const uint8_t *mask;  // 1 = keep
-    void *grid;           // int64 counts / float64 sums, length1d cells
+    void *grid;           // int64 counts / upcast sums (float64, int64 or uint64), length1d cells
+    int32_t dtype;        // data dtype code
+    int32_t vint;         // the sum accumulates 64-bit integers (integer / bool data), not float64
 };
 
 struct FusedAggs {
     int32_t na;
     uint32_t lds_words;
+    int32_t generic_vals;  // some data is not float64: tile path with per-dtype loads only
+    int32_t pad;
     FusedAgg a[MAX_FUSED_AGGS];
 };
 

@@ -99,6 +99,35 @@ template <int ND> __device__ inline uint64_t cell_of(const BinPlan &p, uint64_t 
     }
 }
 
+// a value as the 64-bit slot pass A carries: float data as float64 (NaN kept), integer
+// and bool data as int64 / uint64 bits (the AggSum upcast, superagg.cpp:289-346)
+__device__ inline double load_slot_value(const void *p, int dtype, uint64_t i, bool *nan) {
+    *nan = false;
+    switch (dtype) {
+    case VH_F64: {
+        const double d = static_cast<const double *>(p)[i];
+        *nan = d != d;
+        return d;
+    }
+    case VH_F32: {
+        const double d = (double)static_cast<const float *>(p)[i];
+        *nan = d != d;
+        return d;
+    }
+    case VH_I64: return __builtin_bit_cast(double, static_cast<const int64_t *>(p)[i]);
+    case VH_I32: return __builtin_bit_cast(double, (int64_t) static_cast<const int32_t *>(p)[i]);
+    case VH_I16: return __builtin_bit_cast(double, (int64_t) static_cast<const int16_t *>(p)[i]);
+    case VH_I8: return __builtin_bit_cast(double, (int64_t) static_cast<const int8_t *>(p)[i]);
+    case VH_U64: return __builtin_bit_cast(double, static_cast<const uint64_t *>(p)[i]);
+    case VH_U32: return __builtin_bit_cast(double, (uint64_t) static_cast<const uint32_t *>(p)[i]);
+    case VH_U16: return __builtin_bit_cast(double, (uint64_t) static_cast<const uint16_t *>(p)[i]);
+    default: {
+        const uint8_t b = static_cast<const uint8_t *>(p)[i];
+        return __builtin_bit_cast(double, (uint64_t)(dtype == VH_BOOL ? (b ? 1 : 0) : b));
+    }
+    }
+}
+
 // keep flags of a row (bit k: aggregator k takes the row) and the carried values
 template <int NV>
 __device__ inline uint32_t row_contrib(const FusedAggs &fa, const TileParams &tp, uint64_t i, double *vals) {
@@ -110,13 +139,16 @@ __device__ inline uint32_t row_contrib(const FusedAggs &fa, const TileParams &tp
         bool keep = !a.mask || a.mask[i] == 1;
         double v = 0.0;
         if (a.data) {
-            v = a.data[i];
-            keep = keep && (v == v);
+            bool nan;
+            v = load_slot_value(a.data, a.dtype, i, &nan);
+            keep = keep && !nan;
         }
         if (keep) f |= 1u << k;
         if constexpr (NV > 0) {
             const int s = tp.val_slot[k];
-            if (s >= 0 && s < NV) vals[s] = keep ? v : __builtin_nan("");
+            // a dropped row carries NaN (float sums skip it) or 0 (integer sums add nothing;
+            // masks with integer data are not taken by the tile path)
+            if (s >= 0 && s < NV) vals[s] = keep ? v : (a.vint ? 0.0 : __builtin_nan(""));
         }
     }
     return f;
@@ -301,7 +333,12 @@ __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, co
                 if (fa.a[a].kind == VH_AGG_COUNT) {
                     atomicAdd((unsigned long long *)fa.a[a].grid + c, 1ULL);
                 } else if constexpr (NV > 0) {
-                    atomicAdd(reinterpret_cast<double *>(fa.a[a].grid) + c, l.sv[tp.val_slot[a] * TA_BATCH + k]);
+                    const double v = l.sv[tp.val_slot[a] * TA_BATCH + k];
+                    if (fa.a[a].vint)
+                        atomicAdd(reinterpret_cast<unsigned long long *>(fa.a[a].grid) + c,
+                                  __builtin_bit_cast(unsigned long long, v));
+                    else
+                        atomicAdd(reinterpret_cast<double *>(fa.a[a].grid) + c, v);
                 }
             }
         }
@@ -678,7 +715,11 @@ __device__ inline void reduce_entry(const FusedAggs &fa, const TileParams &tp, u
         } else {
 #pragma unroll
             for (int s = 0; s < NV; s++) {
-                if (s == tp.val_slot[k] && v[s] == v[s])
+                if (s != tp.val_slot[k]) continue;
+                if (fa.a[k].vint)  // integer sums: two's-complement 64-bit adds of the upcast value
+                    atomicAdd(reinterpret_cast<unsigned long long *>(lds + fa.a[k].lds_off) + local,
+                              __builtin_bit_cast(unsigned long long, v[s]));
+                else if (v[s] == v[s])
                     atomicAdd(reinterpret_cast<double *>(lds + fa.a[k].lds_off) + local, v[s]);
             }
         }
@@ -810,6 +851,9 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
             if (fa.a[k].kind == VH_AGG_COUNT) {
                 const uint32_t v = reinterpret_cast<const uint32_t *>(lds_raw + fa.a[k].lds_off)[i];
                 if (v) atomicAdd((unsigned long long *)fa.a[k].grid + c0 + i, (unsigned long long)v);
+            } else if (fa.a[k].vint) {
+                const unsigned long long v = reinterpret_cast<const unsigned long long *>(lds_raw + fa.a[k].lds_off)[i];
+                if (v) atomicAdd(reinterpret_cast<unsigned long long *>(fa.a[k].grid) + c0 + i, v);
             } else {
                 const double v = reinterpret_cast<const double *>(lds_raw + fa.a[k].lds_off)[i];
                 if (v != 0.0) atomicAdd(reinterpret_cast<double *>(fa.a[k].grid) + c0 + i, v);
@@ -896,7 +940,7 @@ static bool ord_fast_ok(const BinPlan &plan, const FusedAggs &fa) {
         const FusedAgg &a = fa.a[k];
         if (a.mask) return false;
         if (a.kind != VH_AGG_COUNT) {
-            if (!a.data || (reinterpret_cast<uintptr_t>(a.data) & 15)) return false;
+            if (!a.data || a.dtype != VH_F64 || (reinterpret_cast<uintptr_t>(a.data) & 15)) return false;
         } else if (a.data) {
             bool keyed = false;  // count(v) of a summed column rides on that sum's value
             for (int j = 0; j < fa.na; j++)
@@ -909,7 +953,7 @@ static bool ord_fast_ok(const BinPlan &plan, const FusedAggs &fa) {
 
 bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64, Workspace &ws) {
     if (n < (1u << 20) || cells >= (1ull << 40)) return false;
-    if ((n & 1) && (nd_f64 > 0 || ord_fast_ok(plan, fa_in))) {
+    if ((n & 1) && !fa_in.generic_vals && (nd_f64 > 0 || ord_fast_ok(plan, fa_in))) {
         // the fast pass A reads row pairs: tile all rows but the last, which takes the
         // global-atomic path
         if (!try_tiled_impl(plan, fa_in, n - 1, cells, nd_f64, ws)) return false;
@@ -964,9 +1008,11 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     for (int k = 0; k < fa_in.na; k++) {
         const FusedAgg &a = fa_in.a[k];
         if (a.kind != VH_AGG_COUNT || (!a.data && !a.mask)) continue;
+        if (!a.mask && a.dtype != VH_F64 && a.dtype != VH_F32) continue;  // integers: never NaN
         tp.cnt_slot[k] = CNT_FLAG;
         for (int j = 0; j < fa_in.na; j++)
-            if (fa_in.a[j].kind != VH_AGG_COUNT && fa_in.a[j].data == a.data && fa_in.a[j].mask == a.mask && a.data)
+            if (fa_in.a[j].kind != VH_AGG_COUNT && fa_in.a[j].data == a.data && fa_in.a[j].mask == a.mask && a.data &&
+                !fa_in.a[j].vint)
                 tp.cnt_slot[k] = tp.val_slot[j];
         if (tp.cnt_slot[k] == CNT_FLAG) flags_mode = true;
     }
@@ -1001,8 +1047,9 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         if (fa.a[k].mask) fast = false;
         if (fa.a[k].kind != VH_AGG_COUNT) {
             tp.vdata[tp.val_slot[k]] = fa.a[k].data;
-            fast = fast && fa.a[k].data && aligned16(fa.a[k].data);
+            fast = fast && fa.a[k].data && fa.a[k].dtype == VH_F64 && aligned16(fa.a[k].data);
         }
+        if (fa.a[k].kind == VH_AGG_COUNT && fa.a[k].data && fa.a[k].dtype != VH_F64) fast = false;
     }
     const bool ord = !fast && n % 2 == 0 && ord_fast_ok(plan, fa);
     if (ord) for (int k = 0; k < fa.na; k++)
