@@ -189,20 +189,21 @@ def _group_data():
     return keys, v, w
 
 
-def test_two_rank_fused_groupby_merge():
+@pytest.mark.parametrize("world", [2, 3])
+def test_two_rank_fused_groupby_merge(world):
     """Per-rank fused-groupby results (keys sorted, counts, float and int sums, non-NaN
-    counts) merged across ranks == the whole-column result; and the all-ranks flag used to
-    keep every rank on the same groupby route."""
+    counts) merged across ranks by the hash-partition all-to-all == the whole-column
+    result; and the all-ranks flag used to keep every rank on the same groupby route."""
     pytest.importorskip("torch")
     import sys
     import torch.multiprocessing as mp
     sys.path.insert(0, ROOT)
     from oracle import oracle
     os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(32500 + os.getpid() % 1000)
+    os.environ["MASTER_PORT"] = str(32500 + 10 * world + os.getpid() % 1000)
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "groups.npz")
-        mp.spawn(_groups_worker, args=(2, path), nprocs=2, join=True)
+        mp.spawn(_groups_worker, args=(world, path), nprocs=world, join=True)
         got = np.load(path)
         keys, v, w = _group_data()
         uk, s, c = oracle.groupby_reference(keys, v)
@@ -214,3 +215,57 @@ def test_two_rank_fused_groupby_merge():
         np.add.at(ew, np.searchsorted(uk, keys), w.astype(np.int64))
         np.testing.assert_array_equal(got["w"], ew)
         assert got["flags"].tolist() == [True, False]
+
+
+def _u64_groups_worker(rank, world, path):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from vaex_amd.distributed import combine_groups, shard_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    keys = _u64_keys()
+    i1, i2 = shard_range(len(keys), rank, world)
+    uk, inv = np.unique(keys[i1:i2], return_inverse=True)
+    counts = np.bincount(inv, minlength=len(uk)).astype(np.int64)
+    usum = np.zeros(len(uk), np.uint64)
+    np.add.at(usum, inv, (keys[i1:i2] >> np.uint64(40)))
+    gk, gc, gs, gn = combine_groups((uk, counts, [usum], [None]))
+    if rank == world - 1:
+        np.savez(path, keys=gk, counts=gc, s=gs[0], nn_none=np.array([gn[0] is None]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _u64_keys():
+    rng = np.random.default_rng(5)
+    base = rng.integers(0, 2 ** 63, 400, dtype=np.uint64) * np.uint64(2) + np.uint64(1)
+    return base[rng.integers(0, 400, 20_000)]
+
+
+def test_hash_partition_merge_uint64_keys():
+    """uint64 keys above 2**63 keep unsigned order and exact unsigned sums through the
+    all-to-all (three ranks, one of them may own no group); owners are in range."""
+    pytest.importorskip("torch")
+    import sys
+    import torch.multiprocessing as mp
+    sys.path.insert(0, ROOT)
+    from vaex_amd.distributed import group_owner
+    keys = _u64_keys()
+    own = group_owner(keys, 3)
+    assert own.min() >= 0 and own.max() < 3
+    np.testing.assert_array_equal(own, group_owner(keys.copy(), 3))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(33700 + os.getpid() % 1000)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "u64.npz")
+        mp.spawn(_u64_groups_worker, args=(3, path), nprocs=3, join=True)
+        got = np.load(path)
+        uk, inv = np.unique(keys, return_inverse=True)
+        assert got["keys"].dtype == np.uint64
+        np.testing.assert_array_equal(got["keys"], uk)
+        np.testing.assert_array_equal(got["counts"], np.bincount(inv))
+        es = np.zeros(len(uk), np.uint64)
+        np.add.at(es, inv, keys >> np.uint64(40))
+        np.testing.assert_array_equal(got["s"], es)
+        assert bool(got["nn_none"][0])

@@ -81,3 +81,38 @@ def test_two_rank_executor_matches_single_process():
             np.testing.assert_allclose(got[k], v, rtol=1e-9, atol=1e-12, err_msg=k)
         else:
             np.testing.assert_array_equal(got[k], v, err_msg=k)
+
+
+def _nccl_groups_worker(rank, world, path):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world)
+    from vaex_amd.distributed import combine_groups
+    rng = np.random.default_rng(3)
+    keys = np.unique(rng.integers(-10 ** 12, 10 ** 12, 70_000))
+    counts = rng.integers(1, 9, len(keys)).astype(np.int64)
+    sums = rng.normal(size=len(keys))
+    nn = rng.integers(0, 9, len(keys)).astype(np.int64)
+    gk, gc, gs, gn = combine_groups((keys, counts, [sums], [nn]))
+    np.savez(path, keys=keys, counts=counts, sums=sums, nn=nn, gk=gk, gc=gc, gs=gs[0], gn=gn[0])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rccl_group_exchange_single_rank():
+    """The hash-partition all-to-all + all-gather of groupby results on HBM tensors over RCCL
+    (one rank on the box's GPU): the exchange must hand back every group bit-exactly."""
+    pytest.importorskip("torch")
+    import torch.multiprocessing as mp
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(34500 + os.getpid() % 1000)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "g.npz")
+        mp.spawn(_nccl_groups_worker, args=(1, path), nprocs=1, join=True)
+        got = np.load(path)
+    for a, b in (("keys", "gk"), ("counts", "gc"), ("sums", "gs"), ("nn", "gn")):
+        np.testing.assert_array_equal(got[a], got[b], err_msg=a)

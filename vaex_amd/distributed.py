@@ -288,17 +288,108 @@ def merge_groups(parts):
     return uniq, counts, sums, nonnull
 
 
+def group_owner(keys, world):
+    """Owner rank of each group key: splitmix64 of the key's 64-bit pattern modulo the world
+    size (SURVEY.md §8e hash partition).  ``keys``: int64 / uint64 array."""
+    z = np.ascontiguousarray(keys).view(np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    z = z ^ (z >> np.uint64(31))
+    return (z % np.uint64(world)).astype(np.int64)
+
+
+def _pack_groups(keys, counts, sums, nonnull):
+    """Rows of 64-bit words [key, count, sum_0.., nonnull_v..] (bit patterns, int64)."""
+    cols = [np.ascontiguousarray(keys).view(np.int64), np.ascontiguousarray(counts, np.int64)]
+    cols += [np.ascontiguousarray(s).view(np.int64) for s in sums]
+    cols += [np.ascontiguousarray(c, np.int64) for c in nonnull if c is not None]
+    return np.stack(cols, axis=1) if cols[0].size else np.empty((0, len(cols)), np.int64)
+
+
+def _unpack_groups(mat, key_dtype, sum_dtypes, has_nonnull):
+    mat = np.ascontiguousarray(mat)
+    keys = mat[:, 0].copy().view(key_dtype)
+    counts = mat[:, 1].copy()
+    sums = [mat[:, 2 + v].copy().view(dt) for v, dt in enumerate(sum_dtypes)]
+    nonnull, c = [], 2 + len(sum_dtypes)
+    for want in has_nonnull:
+        nonnull.append(mat[:, c].copy() if want else None)
+        c += int(bool(want))
+    return keys, counts, sums, nonnull
+
+
+def _exchange(mat, send_counts, group, device):
+    """All-to-all of packed group rows (rows already ordered by destination rank)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    ncol = mat.shape[1]
+    sc = torch.tensor(send_counts, dtype=torch.int64, device=device)
+    rc = torch.empty(world, dtype=torch.int64, device=device)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv_counts = [int(r) for r in rc.cpu()]
+    src = torch.from_numpy(np.ascontiguousarray(mat).reshape(-1)).to(device)
+    dst = torch.empty(sum(recv_counts) * ncol, dtype=torch.int64, device=device)
+    dist.all_to_all_single(dst, src, [r * ncol for r in recv_counts], [s * ncol for s in send_counts],
+                           group=group)
+    return dst.cpu().numpy().reshape(-1, ncol), recv_counts
+
+
+def _all_gather_rows(mat, group, device):
+    """All-gather of a variable number of packed rows per rank (sizes first, then padded)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    ncol = mat.shape[1]
+    n = torch.tensor([mat.shape[0]], dtype=torch.int64, device=device)
+    sizes = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s) for s in torch.cat(sizes).cpu()]
+    top = max(sizes)
+    buf = np.zeros((top, ncol), np.int64)
+    buf[:mat.shape[0]] = mat
+    t = torch.from_numpy(buf.reshape(-1)).to(device)
+    outs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(outs, t, group=group)
+    return [o.cpu().numpy().reshape(top, ncol)[:s] for o, s in zip(outs, sizes)]
+
+
 def combine_groups(local, group=None):
-    """All-gather every rank's fused-groupby result and merge (:func:`merge_groups`)."""
+    """Merge every rank's fused-groupby result by hash partition: each group
+    row goes to its owner rank (:func:`group_owner`) in one all-to-all, owners merge what
+    they received (:func:`merge_groups`, senders in rank order, so float sums add in the
+    same order as a merge of all ranks' parts), and the disjoint owner results are
+    all-gathered so every rank holds the whole key-sorted result.  Each group crosses the
+    links twice (to its owner, then to every rank) instead of every rank receiving every
+    other rank's full table.  Over "nccl" the exchanges run on HBM tensors (RCCL / xGMI),
+    over "gloo" through host memory."""
     import torch.distributed as dist
     keys, counts, sums, nonnull = local
-    payload = (np.asarray(keys), np.asarray(counts), [np.asarray(s) for s in sums],
-               [None if c is None else np.asarray(c) for c in nonnull])
+    keys = np.asarray(keys)
+    key_dtype = keys.dtype if keys.dtype == np.uint64 else np.dtype(np.int64)
+    sums = [np.asarray(s) for s in sums]
+    sum_dtypes = [s.dtype for s in sums]
+    has_nn = [c is not None for c in nonnull]
     world = dist.get_world_size(group)
-    gathered = [None] * world
-    dist.all_gather_object(gathered, payload, group=group)
-    merged = merge_groups(gathered)
-    return local if merged is None else merged
+    device = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    mat = _pack_groups(keys.astype(key_dtype, copy=False), counts, sums, nonnull)
+    owner = group_owner(mat[:, 0], world)
+    order = np.argsort(owner, kind="stable")  # keeps each destination's rows key-sorted
+    send_counts = np.bincount(owner, minlength=world).tolist()
+    recv, recv_counts = _exchange(mat[order], send_counts, group, device)
+    parts, at = [], 0
+    for r in recv_counts:
+        parts.append(_unpack_groups(recv[at:at + r], key_dtype, sum_dtypes, has_nn))
+        at += r
+    merged = merge_groups(parts)
+    if merged is None:
+        merged = _unpack_groups(np.empty((0, mat.shape[1]), np.int64), key_dtype, sum_dtypes, has_nn)
+    owned = _pack_groups(*merged)
+    gathered = np.concatenate(_all_gather_rows(owned, group, device), axis=0)
+    out = _unpack_groups(gathered, key_dtype, sum_dtypes, has_nn)
+    order = np.argsort(out[0], kind="stable")
+    return (out[0][order], out[1][order], [s[order] for s in out[2]],
+            [None if c is None else c[order] for c in out[3]])
 
 
 def combine_sets(local_set, group=None):
