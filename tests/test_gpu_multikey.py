@@ -156,3 +156,42 @@ def test_same_frame_as_uncombined_path():
             np.testing.assert_allclose(x, y, rtol=1e-6, atol=1e-9)
         else:
             np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_spans_overflowing_62_bits_recombine(device, monkeypatch):
+    """Cartesian span >= 2**62 (the reference's 64-bit overflow recursion, groupby.py:256-287):
+    leading keys are combined, re-ordinalised through sorted GPU sets, then combined with the
+    rest; the h2o q10 shape (six keys, aliased columns) included."""
+    rng = np.random.default_rng(44)
+    n = 40_000
+    keys = [(rng.integers(0, 60, n) * (2 ** 21) - 2 ** 25).astype(np.int64) for _ in range(4)]
+    keys[2] = rng.integers(-3, 4, n).astype(np.int8)
+    v = rng.normal(size=n)
+    v[::13] = np.nan
+    calls = _spy(monkeypatch)
+    res = _frame(keys, v, device).groupby([f"k{i}" for i in range(4)], agg=_agg(), sort=True)
+    assert calls.count("vh_combine_keys") >= 2
+    _check(keys, v, res)
+    # h2o q10: id1/id2/id4/id5 alias one int8 column, id3/id6 one int32 column
+    a = rng.integers(5, 105, n).astype(np.int8)
+    b = rng.integers(5, 1_000_005, n).astype(np.int32)
+    six = [a, a, b, a, a, b]
+    res = _frame(six, v, device).groupby([f"k{i}" for i in range(6)], agg=_agg())
+    _check(six, v, res, sort_result=True)
+
+
+def test_groupby_then_agg_takes_the_same_routes(monkeypatch):
+    """``df.groupby(by).agg(actions)`` (the h2o benchmark's form) == ``df.groupby(by,
+    agg=actions)``, through the GPU combine, with the grouper-built GroupBy still reachable."""
+    rng = np.random.default_rng(45)
+    n = 30_000
+    keys = [rng.integers(0, 300, n).astype(np.int32) * 1000, rng.integers(-50, 50, n).astype(np.int16)]
+    v = rng.normal(size=n)
+    df = _frame(keys, v, True)
+    calls = _spy(monkeypatch)
+    res = df.groupby(["k0", "k1"], sort=True).agg(_agg())
+    assert "vh_combine_keys" in calls
+    _check(keys, v, res)
+    g = df.groupby(["k0", "k1"])
+    assert g.groupby_expression == ["k0", "k1"]

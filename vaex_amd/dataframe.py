@@ -533,7 +533,9 @@ class DataFrame:
     def groupby(self, by=None, agg=None, sort=False, assume_sparse="auto", row_limit=None, copy=True,
                 progress=None, delay=False):
         """dataframe.py:6622-6683."""
-        from .groupby import GroupBy, _dense_range, groupby_multikey, parse_actions
+        from .groupby import GroupBy, GroupByDeferred, _dense_range, groupby_multikey, parse_actions
+        if agg is None:  # df.groupby(by).agg(...): the same routes as groupby(by, agg=...)
+            return GroupByDeferred(self, by, sort=sort, assume_sparse=assume_sparse, row_limit=row_limit)
         dense_ranges = {}
         if agg is not None and assume_sparse != True and isinstance(by, (list, tuple)) and len(by) > 1:  # noqa: E712
             res = groupby_multikey(self, by, agg, sort=sort, row_limit=row_limit)
@@ -556,8 +558,6 @@ class DataFrame:
                         return res
         groupby = GroupBy(self, by=by, sort=sort, row_limit=row_limit, dense=assume_sparse != True,  # noqa: E712
                           dense_ranges=dense_ranges)
-        if agg is None:
-            return groupby
         return groupby.agg(agg)
 
     def export_hdf5(self, path, **kwargs):
