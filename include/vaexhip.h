@@ -213,6 +213,18 @@ int vh_expr_eval(const uint32_t *code, int ncode, const uint64_t *consts, int nc
 int vh_combine_keys(uint64_t n, int nkeys, const void *const *cols, const int *dtypes, const int64_t *mins,
                     const int64_t *mults, int64_t *out);
 
+/* dense rank of an int64 HBM column: rank[i] = number of distinct keys below keys[i], the
+ * distinct keys ascending in distinct[0..*m) (capacity n); n < 2^31.  Replaces the
+ * GrouperCombined set of a combined key (groupby.py:248-288, ordered_set::create +
+ * map_ordinal, hash_primitives.hpp:468-516,543-583) with sorted ordinals. */
+int vh_dense_rank_i64(uint64_t n, const int64_t *keys, int32_t *rank, int64_t *distinct, uint64_t *m);
+
+/* group labels of combined keys (the inverse of vh_combine_keys; groupby.py:248-288 decodes
+ * the GrouperCombined bins back to per-key labels): v = table ? table[ck[i]] : ck[i],
+ * outs[j][i] = (v / mults[j]) % spans[j] + mins[j] stored in itemsizes[j] bytes; HBM buffers */
+int vh_decode_keys(uint64_t n, const int64_t *ck, const int64_t *table, int nkeys, const int64_t *mins,
+                   const int64_t *mults, const int64_t *spans, const int *itemsizes, void *const *outs);
+
 #ifdef __cplusplus
 }
 #endif

@@ -195,3 +195,24 @@ def test_groupby_then_agg_takes_the_same_routes(monkeypatch):
     _check(keys, v, res)
     g = df.groupby(["k0", "k1"])
     assert g.groupby_expression == ["k0", "k1"]
+
+
+@pytest.mark.parametrize("n", [1, 2, 1000, 300_001])
+def test_dense_rank_i64(n):
+    """vh_dense_rank_i64 == np.unique(return_inverse): ranks bit-exact, distinct keys sorted
+    (signed order across negative keys and the int64 extremes)."""
+    import ctypes
+    from vaex_amd import _lib
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(n)
+    pool = np.concatenate([rng.integers(-2 ** 62, 2 ** 62, 50), [np.iinfo(np.int64).min, np.iinfo(np.int64).max, 0, -1]])
+    keys = pool[rng.integers(0, len(pool), n)].astype(np.int64)
+    d_keys = DeviceArray.from_numpy(keys)
+    rank = DeviceArray.empty(n, np.int32)
+    distinct = DeviceArray.empty(n, np.int64)
+    m = ctypes.c_uint64()
+    _lib.call("vh_dense_rank_i64", n, d_keys.ptr, rank.ptr, distinct.ptr, ctypes.byref(m))
+    uniq, inv = np.unique(keys, return_inverse=True)
+    assert m.value == len(uniq)
+    np.testing.assert_array_equal(rank.to_numpy(), inv.ravel())
+    np.testing.assert_array_equal(distinct[:m.value].to_numpy(), uniq)

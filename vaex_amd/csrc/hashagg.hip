@@ -42,6 +42,7 @@
 // (VH_ERR_RUNTIME) and the caller falls back to the ordered_set path.
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -1424,6 +1425,128 @@ int vh_combine_keys(uint64_t n, int nkeys, const void *const *cols, const int *d
         hipLaunchKernelGGL(k_combine_keys, dim3(blocks_for(n, 256, 8)), dim3(256), 0, stream(), p, n, out);
         VH_HIP(hipGetLastError());
     }
+    VH_API_END
+}
+
+}  // extern "C"
+
+namespace vh {
+// ---- dense rank of int64 keys: (key, row) pairs radix-sorted, run heads flagged, an
+// inclusive scan of the flags numbers the runs, each sorted row scatters its run number
+// to its original row and every run head writes its key to the distinct list.
+__global__ void k_dr_iota(uint32_t *idx, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        idx[i] = (uint32_t)i;
+}
+
+__global__ void k_dr_heads(const int64_t *sk, uint32_t *flag, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        flag[i] = (i == 0 || sk[i] != sk[i - 1]) ? 1u : 0u;
+}
+
+__global__ void k_dr_scatter(const int64_t *sk, const uint32_t *sidx, const uint32_t *flag, const uint32_t *scan,
+                             int32_t *rank, int64_t *distinct, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t r = scan[i] - 1u;
+        rank[sidx[i]] = (int32_t)r;
+        if (flag[i]) distinct[r] = sk[i];
+    }
+}
+// ---- labels of combined keys: key j of group i = (v / mult_j) % span_j + min_j, with
+// v = table ? table[ck[i]] : ck[i] (the inverse of k_combine_keys, after a dense rank),
+// stored in the label's width (values fit it by construction)
+struct HdParams {
+    void *out[HC_MAX_KEYS];
+    int32_t itemsize[HC_MAX_KEYS];
+    int64_t min[HC_MAX_KEYS];
+    int64_t mult[HC_MAX_KEYS];
+    int64_t span[HC_MAX_KEYS];
+    int nkeys;
+};
+
+__global__ __launch_bounds__(256) void k_decode_keys(HdParams p, const int64_t *ck, const int64_t *table, uint64_t n) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const int64_t v = table ? table[ck[i]] : ck[i];
+        for (int j = 0; j < p.nkeys; j++) {
+            const int64_t k = (v / p.mult[j]) % p.span[j] + p.min[j];
+            switch (p.itemsize[j]) {
+            case 1: static_cast<int8_t *>(p.out[j])[i] = (int8_t)k; break;
+            case 2: static_cast<int16_t *>(p.out[j])[i] = (int16_t)k; break;
+            case 4: static_cast<int32_t *>(p.out[j])[i] = (int32_t)k; break;
+            default: static_cast<int64_t *>(p.out[j])[i] = k;
+            }
+        }
+    }
+}
+}  // namespace vh
+
+extern "C" {
+
+int vh_decode_keys(uint64_t n, const int64_t *ck, const int64_t *table, int nkeys, const int64_t *mins,
+                   const int64_t *mults, const int64_t *spans, const int *itemsizes, void *const *outs) {
+    VH_API_BEGIN
+    if (nkeys < 1 || nkeys > HC_MAX_KEYS) fail(VH_ERR_ARG, "decode_keys: 1..8 key columns");
+    HdParams p{};
+    p.nkeys = nkeys;
+    for (int j = 0; j < nkeys; j++) {
+        if (itemsizes[j] != 1 && itemsizes[j] != 2 && itemsizes[j] != 4 && itemsizes[j] != 8)
+            fail(VH_ERR_ARG, "decode_keys: label itemsize must be 1, 2, 4 or 8");
+        if (mults[j] < 1 || spans[j] < 1) fail(VH_ERR_ARG, "decode_keys: multipliers and spans must be >= 1");
+        if (n && resolve_loc(outs[j], VH_LOC_AUTO) != VH_LOC_DEVICE) fail(VH_ERR_ARG, "decode_keys: device outputs only");
+        p.out[j] = outs[j];
+        p.itemsize[j] = itemsizes[j];
+        p.min[j] = mins[j];
+        p.mult[j] = mults[j];
+        p.span[j] = spans[j];
+    }
+    if (n) {
+        if (resolve_loc(ck, VH_LOC_AUTO) != VH_LOC_DEVICE || (table && resolve_loc(table, VH_LOC_AUTO) != VH_LOC_DEVICE))
+            fail(VH_ERR_ARG, "decode_keys: device inputs only");
+        TimedScope ts("decode_keys");
+        hipLaunchKernelGGL(k_decode_keys, dim3(blocks_for(n, 256, 8)), dim3(256), 0, stream(), p, ck, table, n);
+        VH_HIP(hipGetLastError());
+    }
+    VH_API_END
+}
+
+int vh_dense_rank_i64(uint64_t n, const int64_t *keys, int32_t *rank, int64_t *distinct, uint64_t *m) {
+    VH_API_BEGIN
+    if (!m) fail(VH_ERR_ARG, "dense_rank: m is null");
+    *m = 0;
+    if (n >= (uint64_t(1) << 31)) fail(VH_ERR_ARG, "dense_rank: at most 2^31 - 1 rows");
+    if (!n) return VH_OK;
+    for (const void *p : {(const void *)keys, (const void *)rank, (const void *)distinct})
+        if (resolve_loc(p, VH_LOC_AUTO) != VH_LOC_DEVICE) fail(VH_ERR_ARG, "dense_rank: device buffers only");
+    TimedScope ts("dense_rank");
+    hipStream_t st = stream();
+    DevBuf sk, idx, sidx, flag, scan, tmp;
+    sk.ensure(n * 8);
+    idx.ensure(n * 4);
+    sidx.ensure(n * 4);
+    flag.ensure(n * 4);
+    scan.ensure(n * 4);
+    size_t t1 = 0, t2 = 0;
+    VH_HIP(rocprim::radix_sort_pairs(nullptr, t1, (int64_t *)nullptr, (int64_t *)nullptr, (uint32_t *)nullptr,
+                                     (uint32_t *)nullptr, (size_t)n, 0, 64, st));
+    VH_HIP(rocprim::inclusive_scan(nullptr, t2, (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)n,
+                                   rocprim::plus<uint32_t>(), st));
+    tmp.ensure(std::max<size_t>(std::max(t1, t2), 16));
+    const unsigned g = blocks_for(n, 256, 8);
+    hipLaunchKernelGGL(k_dr_iota, dim3(g), dim3(256), 0, st, idx.as<uint32_t>(), n);
+    size_t tb = tmp.bytes;
+    VH_HIP(rocprim::radix_sort_pairs(tmp.ptr, tb, keys, sk.as<int64_t>(), idx.as<uint32_t>(), sidx.as<uint32_t>(),
+                                     (size_t)n, 0, 64, st));
+    hipLaunchKernelGGL(k_dr_heads, dim3(g), dim3(256), 0, st, sk.as<int64_t>(), flag.as<uint32_t>(), n);
+    tb = tmp.bytes;
+    VH_HIP(rocprim::inclusive_scan(tmp.ptr, tb, flag.as<uint32_t>(), scan.as<uint32_t>(), (size_t)n,
+                                   rocprim::plus<uint32_t>(), st));
+    hipLaunchKernelGGL(k_dr_scatter, dim3(g), dim3(256), 0, st, sk.as<int64_t>(), sidx.as<uint32_t>(),
+                       flag.as<uint32_t>(), scan.as<uint32_t>(), rank, distinct, n);
+    VH_HIP(hipGetLastError());
+    uint32_t last = 0;
+    VH_HIP(hipMemcpyAsync(&last, scan.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, st));
+    VH_HIP(hipStreamSynchronize(st));
+    *m = last;
     VH_API_END
 }
 

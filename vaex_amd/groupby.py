@@ -205,12 +205,7 @@ def groupby_multikey(df, by, agg, sort=False, row_limit=None):
     tmp = df.copy()
     tmp.add_column(COMBINED_KEY, combined)
     res = tmp.groupby(COMBINED_KEY, agg=actions, sort=sort, row_limit=row_limit)
-    ck = np.asarray(res.columns[COMBINED_KEY], dtype=np.int64)
-    columns = {}
-    for (name, vmin, vmax), sp, mult in zip(ranges, spans, mults):
-        kd = np.dtype(df.columns[name].dtype)
-        labels = (ck // mult) % sp + vmin
-        columns[name] = labels.astype(label_dtype(kd, vmin, vmax) if len(labels) else kd)
+    columns = _decode_labels(df, res.columns[COMBINED_KEY], None, ranges, mults)
     for name, values in res.columns.items():
         if name != COMBINED_KEY:
             columns[name] = values
@@ -244,19 +239,45 @@ def _combine_columns(df, ranges):
     return combined, mults
 
 
+def _decode_labels(df, ck, table, ranges, mults):
+    """{key name: labels} of combined keys ``ck`` (host or HBM), decoded on the GPU
+    (``vh_decode_keys``, optionally through the dense-rank ``table``), each key in its
+    label dtype (groupby.py:131-133 down-casts)."""
+    import ctypes
+    from . import _lib
+    from .device import DeviceArray
+    ck = ck if isinstance(ck, DeviceArray) else DeviceArray.from_numpy(np.ascontiguousarray(ck, dtype=np.int64))
+    n, k = len(ck), len(ranges)
+    dtypes = []
+    for name, vmin, vmax in ranges:
+        kd = np.dtype(df.columns[name].dtype)
+        dtypes.append(np.dtype(label_dtype(kd, vmin, vmax)) if n else kd)
+    if ck.dtype != np.int64:
+        raise TypeError("combined keys must be int64")
+    outs = [DeviceArray.empty(n, dt) for dt in dtypes]
+    if n:
+        _lib.call("vh_decode_keys", n, ck.ptr, table.ptr if table is not None else None, k,
+                  (ctypes.c_int64 * k)(*[vmin for _, vmin, _ in ranges]), (ctypes.c_int64 * k)(*mults),
+                  (ctypes.c_int64 * k)(*[vmax - vmin + 1 for _, vmin, vmax in ranges]),
+                  (ctypes.c_int * k)(*[dt.itemsize for dt in dtypes]), (ctypes.c_void_p * k)(*[o.ptr for o in outs]))
+    return {name: o.to_numpy() if n else np.empty(0, dt) for (name, _, _), o, dt in zip(ranges, outs, dtypes)}
+
+
 RECOMBINED_KEY = "__vaex_amd_recombined_key_{}"
 
 
 def _groupby_recombine(df, ranges, agg, sort=False, row_limit=None):
     """Multi-key groupby whose cartesian span reaches 2**62: the reference's ``_combine``
     recursion (groupby.py:248-288).  The leading keys whose span product stays below 2**62
-    are combined on the GPU into one int64 value, that value is re-ordinalised through two
-    GPU ordered sets (the distinct combined values, then a set built from them in sorted
-    order, so ordinal order = lexicographic key order, ``ordered_set::create``
-    hash_primitives.hpp:468-516), and the ordinal column (span = number of distinct
-    combinations) replaces those keys; the remaining keys are combined with it the same way
+    are combined on the GPU into one int64 value, that value is replaced by its dense rank
+    (``vh_dense_rank_i64``: radix sort, run heads, scan; the reference builds an ordered
+    set of it instead, GrouperCombined + ``ordered_set::create`` hash_primitives.hpp:468-516;
+    sorted ranks keep the lexicographic key order), and the rank column (span = number of
+    distinct combinations) replaces those keys; the remaining keys are combined with it the same way
     (recursing while the spans still overflow).  Labels are decoded back per key."""
-    from .superutils import ordered_set_int64
+    import ctypes
+    from . import _lib
+    from .device import DeviceArray
     spans = [vmax - vmin + 1 for _, vmin, vmax in ranges]
     take, prod = 1, spans[0]
     while take < len(spans) and prod * spans[take] < 2 ** 62:
@@ -268,13 +289,12 @@ def _groupby_recombine(df, ranges, agg, sort=False, row_limit=None):
     names = [name for name, _, _ in ranges]
     actions = [(name, a) for name, a in parse_actions(df, agg, names)]
     combined, mults = _combine_columns(df, head)
-    seen = ordered_set_int64()
-    seen.update(combined)
-    distinct = np.sort(seen.key_array())
-    ranked = ordered_set_int64()
-    ranked.update(distinct)  # ordinal i = i-th smallest combined value
-    ordinal = ranked.map_ordinal(combined)
-    del combined, seen
+    n = len(combined)
+    ordinal = DeviceArray.empty(n, np.int32)
+    distinct_dev = DeviceArray.empty(max(n, 1), np.int64)
+    m = ctypes.c_uint64()
+    _lib.call("vh_dense_rank_i64", n, combined.ptr, ordinal.ptr, distinct_dev.ptr, ctypes.byref(m))
+    del combined
     depth = 0
     while RECOMBINED_KEY.format(depth) in df.columns:
         depth += 1
@@ -283,13 +303,8 @@ def _groupby_recombine(df, ranges, agg, sort=False, row_limit=None):
     tmp.add_column(key, ordinal)
     by = [key] + [name for name, _, _ in rest]
     res = tmp.groupby(by, agg=actions, sort=sort, row_limit=row_limit)
-    ck = distinct[np.asarray(res.columns[key], dtype=np.int64)]
-    columns = {}
-    for (name, vmin, vmax), mult in zip(head, mults):
-        sp = vmax - vmin + 1
-        kd = np.dtype(df.columns[name].dtype)
-        labels = (ck // mult) % sp + vmin
-        columns[name] = labels.astype(label_dtype(kd, vmin, vmax) if len(labels) else kd)
+    columns = _decode_labels(df, res.columns[key], distinct_dev, head, mults)
+    del distinct_dev
     for name, values in res.columns.items():
         if name != key:
             columns[name] = values
