@@ -24,23 +24,24 @@ namespace vh {
 
 __device__ inline bool operator<(vbool a, vbool b) { return a.v < b.v; }
 
-// BinnerScalar<T>::to_bins (superagg_binners.cpp:14-56)
-template <typename T> __device__ inline uint64_t scalar_index(const BinnerDev &b, uint64_t i) {
-    T value = load_v<T>(b.data, i, b.flip);
+// BinnerScalar<T>::to_bins (superagg_binners.cpp:14-56), on an already loaded raw value
+template <typename T> __device__ inline uint64_t scalar_cell(const BinnerDev &b, T raw, bool masked) {
+    T value = b.flip ? bswap_v(raw) : raw;
     double value_double = to_double(value);
     double scaled = (value_double - b.vmin) * b.scale;
-    bool masked = b.mask ? (b.mask[i] == 1) : false;
     if (scaled != scaled || masked) return 0;  // nan -> 0
     if (scaled < 0) return 1;                  // underflow -> 1
     if (scaled >= 1) return b.bins + 2;        // overflow (incl. vmax) -> bins+2
     return (uint64_t)(int64_t)((int)(scaled * (double)b.bins) + 2);
 }
 
+template <typename T> __device__ inline uint64_t scalar_index(const BinnerDev &b, uint64_t i) {
+    return scalar_cell<T>(b, reinterpret_cast<const T *>(b.data)[i], b.mask ? (b.mask[i] == 1) : false);
+}
+
 // BinnerOrdinal<T>::to_bins (superagg_binners.cpp:104-142): the subtraction of
 // the uint64 min_value happens before the byte swap, as in the reference.
-template <typename T> __device__ inline uint64_t ordinal_index(const BinnerDev &b, uint64_t i) {
-    const T raw = reinterpret_cast<const T *>(b.data)[i];
-    bool masked = b.mask ? (b.mask[i] == 1) : false;
+template <typename T> __device__ inline uint64_t ordinal_cell(const BinnerDev &b, T raw, bool masked) {
     if constexpr (is_float_t<T>::value) {
         T value = raw - (T)b.min_value;
         if (b.flip) value = bswap_v(value);
@@ -64,6 +65,10 @@ template <typename T> __device__ inline uint64_t ordinal_index(const BinnerDev &
         if ((uint64_t)(int64_t)value >= b.ordinal_count) return b.ordinal_count + 2;
         return (uint64_t)((int64_t)value + 2);
     }
+}
+
+template <typename T> __device__ inline uint64_t ordinal_index(const BinnerDev &b, uint64_t i) {
+    return ordinal_cell<T>(b, reinterpret_cast<const T *>(b.data)[i], b.mask ? (b.mask[i] == 1) : false);
 }
 
 // BinnerOrdinal over _ordinal_values(key, set): map_ordinal (hash_primitives.hpp:556-583)

@@ -253,6 +253,112 @@ __global__ __launch_bounds__(256) void k_agg_lds(BinPlan p, AggDev a, uint64_t n
     }
 }
 
+// Small grids, binner dispatch hoisted out of the row loop.  k_agg_lds evaluates the
+// generic plan_index per row and aggregator: a switch over kind and dtype per binner per
+// row, measured at ~75 scalar + branch instructions per wave iteration (SQ counters, h2o
+// q1), so those passes ran at ~1e11 rows/s whatever the column width.  Here one launch per
+// dimension (kind and dtype as template arguments) adds index * stride into a u16 cell
+// column (cells < 2^16 by the LDS bound), and each aggregator's pass reads that column.
+constexpr int CELL_U = 4;  // rows per thread per step, loads issued together
+
+template <int KIND_B, typename T>
+__global__ __launch_bounds__(256) void k_cells_dim(BinnerDev b, uint64_t n, uint16_t *cells, int first) {
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j0 < n; j0 += step * CELL_U) {
+        T raw[CELL_U];
+        bool m[CELL_U];
+        uint16_t prev[CELL_U];
+#pragma unroll
+        for (int u = 0; u < CELL_U; u++) {
+            const uint64_t j = j0 + (uint64_t)u * step;
+            const bool in = j < n;
+            raw[u] = in ? reinterpret_cast<const T *>(b.data)[j] : T{};
+            m[u] = (in && b.mask) ? b.mask[j] == 1 : false;
+            prev[u] = (in && !first) ? cells[j] : (uint16_t)0;
+        }
+#pragma unroll
+        for (int u = 0; u < CELL_U; u++) {
+            const uint64_t j = j0 + (uint64_t)u * step;
+            if (j >= n) continue;
+            const uint64_t c = KIND_B == 0 ? scalar_cell<T>(b, raw[u], m[u]) : ordinal_cell<T>(b, raw[u], m[u]);
+            cells[j] = (uint16_t)(prev[u] + c * b.stride);
+        }
+    }
+}
+
+template <int KIND, typename T>
+__global__ __launch_bounds__(256) void k_agg_lds_c(AggDev a, const uint16_t *cells, uint64_t n, uint64_t L, T fill) {
+    using G = typename Upcast<T>::type;
+    using C = typename LdsCell<KIND, T>::type;
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    C *g = reinterpret_cast<C *>(lds_raw);
+    for (uint64_t c = threadIdx.x; c < L; c += blockDim.x) {
+        if constexpr (KIND == VH_AGG_MIN || KIND == VH_AGG_MAX) g[c] = fill;
+        else g[c] = (C)0;
+    }
+    __syncthreads();
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j0 < n; j0 += step * CELL_U) {
+        uint16_t cell[CELL_U];
+        bool keep[CELL_U];
+        T v[CELL_U];
+#pragma unroll
+        for (int u = 0; u < CELL_U; u++) {
+            const uint64_t j = j0 + (uint64_t)u * step;
+            const bool in = j < n;
+            cell[u] = in ? cells[j] : (uint16_t)0;
+            keep[u] = in && (!a.mask || a.mask[j] == 1);
+            v[u] = (in && a.data) ? reinterpret_cast<const T *>(a.data)[j] : T{};
+        }
+#pragma unroll
+        for (int u = 0; u < CELL_U; u++) {
+            if (!keep[u]) continue;
+            const uint32_t c = cell[u];
+            if constexpr (KIND == VH_AGG_COUNT) {
+                if (a.data && is_nan_v(a.flip ? bswap_v(v[u]) : v[u])) continue;
+                atomicAdd(g + c, 1ULL);
+            } else if constexpr (KIND == VH_AGG_SUM) {
+                const T x = a.flip ? bswap_v(v[u]) : v[u];
+                if (is_nan_v(x)) continue;
+                atomic_add_grid<G>(g + c, upcast_v(x));
+            } else if constexpr (KIND == VH_AGG_MIN || KIND == VH_AGG_MAX) {
+                const T x = a.flip ? bswap_v(v[u]) : v[u];
+                if (is_nan_v(x)) continue;
+                atomic_minmax<T>(g + c, x, KIND == VH_AGG_MAX);
+            } else if constexpr (KIND == VH_AGG_SUM_MOMENT) {
+                // the reference converts to the upcast type first, then byte swaps (superagg.cpp:415-417)
+                G value = upcast_v(v[u]);
+                if (a.flip) value = bswap_v(value);
+                if (is_nan_v(value)) continue;
+                double pw;
+                if (a.moment == 0) pw = 1.0;
+                else if (a.moment == 1) pw = (double)value;
+                else if (a.moment == 2) pw = (double)value * (double)value;
+                else pw = pow((double)value, (double)a.moment);
+                atomic_add_grid<G>(g + c, (G)pw);
+            }
+        }
+    }
+    __syncthreads();
+    for (uint64_t c = threadIdx.x; c < L; c += blockDim.x) {
+        const C v = g[c];
+        if constexpr (KIND == VH_AGG_MIN || KIND == VH_AGG_MAX) {
+            using W = std::conditional_t<sizeof(T) == 8, uint64_t,
+                                         std::conditional_t<sizeof(T) == 4, uint32_t,
+                                                            std::conditional_t<sizeof(T) == 2, uint16_t, uint8_t>>>;
+            W vb, fb;
+            __builtin_memcpy(&vb, &v, sizeof(T));
+            __builtin_memcpy(&fb, &fill, sizeof(T));
+            if (vb != fb)
+                atomic_minmax<T>(reinterpret_cast<T *>(a.grid) + c, v, KIND == VH_AGG_MAX);
+        } else if constexpr (KIND == VH_AGG_COUNT) {
+            if (v) atomicAdd((unsigned long long *)a.grid + c, v);
+        } else {
+            if (v != (C)0) atomic_add_grid<G>(reinterpret_cast<G *>(a.grid) + c, v);
+        }
+    }
+}
+
 // AggFirst (superagg.cpp:481-505).  Per chunk: (A) min order key per cell,
 // (B) lowest row holding that key, (C) per cell: take it if strictly smaller
 // than the grid's order -- ties go to the earliest row, as a serial pass does.
@@ -1048,6 +1154,11 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
             // small grids: LDS sub-grid per workgroup for every kind but AggFirst / AggNUnique
             const bool small = L * 8 <= LDS_AGG_MAX_BYTES;
             auto lds_ok = [&](int kind) { return small && kind != VH_AGG_FIRST && kind != VH_AGG_NUNIQUE; };
+            // binners the cell kernels handle (scalar / ordinal); set-ordinal binners keep
+            // the per-row plan_index of k_agg_lds
+            bool cells_ok = small && L <= 65536;
+            for (int d = 0; d < plan.nb; d++) cells_ok = cells_ok && (plan.b[d].kind == 0 || plan.b[d].kind == 1);
+            uint16_t *cells = nullptr;
             uint64_t *idx = nullptr;
             for (int k = 0; k < naggs && !idx; k++) {
                 if (lds_ok(ads[k].kind)) continue;
@@ -1059,6 +1170,47 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
             }
             for (int k = 0; k < naggs; k++) {
                 AggDev &ad = ads[k];
+                if (lds_ok(ad.kind) && cells_ok) {
+                    if (!cells) {
+                        TimedScope ts("bin_cells");
+                        g->ws.cells.ensure(std::max<uint64_t>(len, 1) * 2);
+                        cells = g->ws.cells.as<uint16_t>();
+                        const dim3 cg(blocks_for(len, 256, 8)), cb(256);
+                        for (int d = 0; d < plan.nb; d++) {
+                            const BinnerDev &b = plan.b[d];
+                            const int first = d == 0 ? 1 : 0;
+                            if (b.kind == 0) {
+                                VH_DISPATCH_DTYPE(b.dtype, T, hipLaunchKernelGGL((k_cells_dim<0, T>), cg, cb, 0, stream(), b, len, cells, first));
+                            } else {
+                                VH_DISPATCH_DTYPE(b.dtype, T, hipLaunchKernelGGL((k_cells_dim<1, T>), cg, cb, 0, stream(), b, len, cells, first));
+                            }
+                            VH_HIP(hipGetLastError());
+                        }
+                    }
+                    TimedScope ts("bin_aggregate_lds");
+                    dim3 grd(blocks_for(len, 256, 8)), blk(256);
+                    const size_t shm = (size_t)((L * 8 + 15) & ~uint64_t(15));
+                    const bool mx = ad.kind == VH_AGG_MAX;
+                    switch (ad.kind) {
+                    case VH_AGG_COUNT:
+                        VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg_lds_c<VH_AGG_COUNT, T>), grd, blk, shm, stream(), ad, cells, len, L, T{}));
+                        break;
+                    case VH_AGG_SUM:
+                        VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg_lds_c<VH_AGG_SUM, T>), grd, blk, shm, stream(), ad, cells, len, L, T{}));
+                        break;
+                    case VH_AGG_MIN:
+                        VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg_lds_c<VH_AGG_MIN, T>), grd, blk, shm, stream(), ad, cells, len, L, minmax_fill<T>(false)));
+                        break;
+                    case VH_AGG_MAX:
+                        VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg_lds_c<VH_AGG_MAX, T>), grd, blk, shm, stream(), ad, cells, len, L, minmax_fill<T>(mx)));
+                        break;
+                    case VH_AGG_SUM_MOMENT:
+                        VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg_lds_c<VH_AGG_SUM_MOMENT, T>), grd, blk, shm, stream(), ad, cells, len, L, T{}));
+                        break;
+                    }
+                    VH_HIP(hipGetLastError());
+                    continue;
+                }
                 if (lds_ok(ad.kind)) {
                     TimedScope ts("bin_aggregate_lds");
                     dim3 grd(blocks_for(len, 256, 4)), blk(256);

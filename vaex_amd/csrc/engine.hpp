@@ -99,6 +99,7 @@ struct HostPipe {
 // per-grid device scratch, reused across bin() calls
 struct Workspace {
     DevBuf idx;                                   // generic path indices1d
+    DevBuf cells;                                 // small-grid path: u16 cell per row
     HostPipe pipe;                                // host-column staging
     DevBuf tile_entries, tile_values, tile_meta;  // tiled path
     ~Workspace();
