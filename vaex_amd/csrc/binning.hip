@@ -359,6 +359,86 @@ __global__ __launch_bounds__(256) void k_agg_lds_c(AggDev a, const uint16_t *cel
     }
 }
 
+// Several count / sum aggregators of one small grid in ONE pass over the u16 cells (each
+// aggregator of k_agg_lds_c re-reads the cells and pays its own loop).  Per step a thread
+// takes SF_U rows; the aggregator's dtype is dispatched once per step (not per row), its
+// values and mask loaded for all SF_U rows, then added into its LDS sub-grid.
+constexpr int SF_MAX = 8;
+constexpr int SF_U = 8;
+struct SmallAggs {
+    int na, pad;
+    uint32_t lds_off[SF_MAX];  // byte offset of each aggregator's sub-grid
+    AggDev a[SF_MAX];
+};
+
+template <typename T>
+__device__ inline void sf_rows(const AggDev &a, unsigned char *lds, const uint16_t (&cell)[SF_U], uint64_t j0,
+                               uint64_t step, uint64_t n) {
+    using G = typename Upcast<T>::type;
+    T v[SF_U];
+    bool keep[SF_U];
+#pragma unroll
+    for (int u = 0; u < SF_U; u++) {
+        const uint64_t j = j0 + (uint64_t)u * step;
+        const bool in = j < n;
+        keep[u] = in && (!a.mask || a.mask[j] == 1);
+        v[u] = (in && a.data) ? reinterpret_cast<const T *>(a.data)[j] : T{};
+    }
+#pragma unroll
+    for (int u = 0; u < SF_U; u++) {
+        if (!keep[u]) continue;
+        const T x = a.flip ? bswap_v(v[u]) : v[u];
+        if (a.kind == VH_AGG_COUNT) {
+            if (a.data && is_nan_v(x)) continue;
+            atomicAdd(reinterpret_cast<unsigned long long *>(lds) + cell[u], 1ULL);
+        } else {
+            if (is_nan_v(x)) continue;
+            atomic_add_grid<G>(reinterpret_cast<G *>(lds) + cell[u], upcast_v(x));
+        }
+    }
+}
+
+template <typename T> __device__ inline void sf_flush(const AggDev &a, const unsigned char *lds, uint64_t L) {
+    using G = typename Upcast<T>::type;
+    for (uint64_t c = threadIdx.x; c < L; c += blockDim.x) {
+        if (a.kind == VH_AGG_COUNT) {
+            const unsigned long long v = reinterpret_cast<const unsigned long long *>(lds)[c];
+            if (v) atomicAdd((unsigned long long *)a.grid + c, v);
+        } else {
+            const G v = reinterpret_cast<const G *>(lds)[c];
+            if (v != (G)0) atomic_add_grid<G>(reinterpret_cast<G *>(a.grid) + c, v);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_small_fused(SmallAggs sa, const uint16_t *cells, uint64_t n, uint64_t L,
+                                                      uint32_t lds_words) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    uint32_t *w = reinterpret_cast<uint32_t *>(lds_raw);
+    for (uint32_t i = threadIdx.x; i < lds_words; i += blockDim.x) w[i] = 0;
+    __syncthreads();
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j0 < n; j0 += step * SF_U) {
+        uint16_t cell[SF_U];
+#pragma unroll
+        for (int u = 0; u < SF_U; u++) {
+            const uint64_t j = j0 + (uint64_t)u * step;
+            cell[u] = j < n ? cells[j] : (uint16_t)0;
+        }
+        for (int k = 0; k < sa.na; k++) {
+            const AggDev &a = sa.a[k];
+            unsigned char *lds = lds_raw + sa.lds_off[k];
+            VH_DEV_DISPATCH(a.dtype, T, sf_rows<T>(a, lds, cell, j0, step, n); break)
+        }
+    }
+    __syncthreads();
+    for (int k = 0; k < sa.na; k++) {
+        const AggDev &a = sa.a[k];
+        const unsigned char *lds = lds_raw + sa.lds_off[k];
+        VH_DEV_DISPATCH(a.dtype, T, sf_flush<T>(a, lds, L); break)
+    }
+}
+
 // AggFirst (superagg.cpp:481-505).  Per chunk: (A) min order key per cell,
 // (B) lowest row holding that key, (C) per cell: take it if strictly smaller
 // than the grid's order -- ties go to the earliest row, as a serial pass does.
@@ -1168,8 +1248,55 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                 hipLaunchKernelGGL(k_indices, dim3(blocks_for(len, 256)), dim3(256), 0, stream(), plan, len, idx);
                 VH_HIP(hipGetLastError());
             }
+            auto make_cells = [&]() {
+                if (cells) return;
+                TimedScope ts("bin_cells");
+                g->ws.cells.ensure(std::max<uint64_t>(len, 1) * 2);
+                cells = g->ws.cells.as<uint16_t>();
+                const dim3 cg(blocks_for(len, 256, 8)), cb(256);
+                for (int d = 0; d < plan.nb; d++) {
+                    const BinnerDev &b = plan.b[d];
+                    const int first = d == 0 ? 1 : 0;
+                    if (b.kind == 0) {
+                        VH_DISPATCH_DTYPE(b.dtype, T, hipLaunchKernelGGL((k_cells_dim<0, T>), cg, cb, 0, stream(), b, len, cells, first));
+                    } else {
+                        VH_DISPATCH_DTYPE(b.dtype, T, hipLaunchKernelGGL((k_cells_dim<1, T>), cg, cb, 0, stream(), b, len, cells, first));
+                    }
+                    VH_HIP(hipGetLastError());
+                }
+            };
+            // count / sum aggregators share one pass over the cells, as many per launch as
+            // their sub-grids fit the LDS budget
+            std::vector<char> done(naggs, 0);
+            if (cells_ok && len) {
+                std::vector<int> pend;
+                for (int k = 0; k < naggs; k++)
+                    if (ads[k].kind == VH_AGG_COUNT || ads[k].kind == VH_AGG_SUM) pend.push_back(k);
+                size_t i = 0;
+                while (i < pend.size()) {
+                    SmallAggs sa{};
+                    uint64_t off = 0;
+                    size_t j = i;
+                    while (j < pend.size() && sa.na < SF_MAX && off + L * 8 <= LDS_AGG_MAX_BYTES) {
+                        sa.lds_off[sa.na] = (uint32_t)off;
+                        sa.a[sa.na++] = ads[pend[j]];
+                        off += (L * 8 + 15) & ~uint64_t(15);
+                        j++;
+                    }
+                    if (sa.na >= 2) {
+                        make_cells();
+                        TimedScope ts("bin_aggregate_lds");
+                        hipLaunchKernelGGL(k_small_fused, dim3(blocks_for(len, 256, 8)), dim3(256), (size_t)off, stream(), sa,
+                                           cells, len, L, (uint32_t)(off / 4));
+                        VH_HIP(hipGetLastError());
+                        for (size_t q = i; q < j; q++) done[pend[q]] = 1;
+                    }
+                    i = j;
+                }
+            }
             for (int k = 0; k < naggs; k++) {
                 AggDev &ad = ads[k];
+                if (done[k]) continue;
                 if (lds_ok(ad.kind) && cells_ok) {
                     if (!cells) {
                         TimedScope ts("bin_cells");
