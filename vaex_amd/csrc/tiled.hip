@@ -436,6 +436,77 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
     }
 }
 
+// The generic pass A's per-row work with the dtype dispatch hoisted out of the row loop:
+// one switch per binner (or aggregator) per batch, then TA_RPT rows of plain typed loads
+// and index math (per-row dispatch cost ~75 scalar + branch instructions per wave
+// iteration, see DESIGN.md, small grids).
+template <typename T> __device__ __forceinline__ void ta_dim(const BinnerDev &b, uint64_t b0, uint64_t row_end,
+                                                             uint64_t (&cell)[TA_RPT]) {
+    T raw[TA_RPT];
+    bool m[TA_RPT];
+#pragma unroll
+    for (int r = 0; r < TA_RPT; r++) {
+        const uint64_t i = b0 + (uint64_t)r * TA_THREADS + threadIdx.x;
+        const bool in = i < row_end;
+        raw[r] = in ? reinterpret_cast<const T *>(b.data)[i] : T{};
+        m[r] = (in && b.mask) ? b.mask[i] == 1 : false;
+    }
+    if (b.kind == 0) {
+#pragma unroll
+        for (int r = 0; r < TA_RPT; r++) cell[r] += scalar_cell<T>(b, raw[r], m[r]) * b.stride;
+    } else {
+#pragma unroll
+        for (int r = 0; r < TA_RPT; r++) cell[r] += ordinal_cell<T>(b, raw[r], m[r]) * b.stride;
+    }
+}
+
+// load_slot_value on a loaded raw value
+template <typename T> __device__ __forceinline__ double slot_of(T raw, bool *nan) {
+    *nan = false;
+    if constexpr (std::is_same_v<T, double> || std::is_same_v<T, float>) {
+        const double d = (double)raw;
+        *nan = d != d;
+        return d;
+    } else if constexpr (std::is_same_v<T, vbool>) {
+        return __builtin_bit_cast(double, (uint64_t)(raw.v ? 1 : 0));
+    } else if constexpr (is_signed_int_t<T>::value) {
+        return __builtin_bit_cast(double, (int64_t)raw);
+    } else {
+        return __builtin_bit_cast(double, (uint64_t)raw);
+    }
+}
+
+template <typename T, int NV>
+__device__ __forceinline__ void ta_agg(const FusedAgg &a, int k, int slot, uint64_t b0, uint64_t row_end,
+                                       uint32_t (&f)[TA_RPT], double (&vals)[TA_RPT][NV > 0 ? NV : 1]) {
+    T raw[TA_RPT];
+    bool m[TA_RPT];
+#pragma unroll
+    for (int r = 0; r < TA_RPT; r++) {
+        const uint64_t i = b0 + (uint64_t)r * TA_THREADS + threadIdx.x;
+        const bool in = i < row_end;
+        raw[r] = (in && a.data) ? reinterpret_cast<const T *>(a.data)[i] : T{};
+        m[r] = (in && a.mask) ? a.mask[i] == 1 : true;
+    }
+#pragma unroll
+    for (int r = 0; r < TA_RPT; r++) {
+        bool keep = m[r];
+        double v = 0.0;
+        if (a.data) {
+            bool nan;
+            v = slot_of<T>(raw[r], &nan);
+            keep = keep && !nan;
+        }
+        if (keep) f[r] |= 1u << k;
+        if constexpr (NV > 0) {
+            const double carried = keep ? v : (a.vint ? 0.0 : __builtin_nan(""));
+#pragma unroll
+            for (int s = 0; s < NV; s++)  // compile-time slot index: the array stays in registers
+                if (s == slot) vals[r][s] = carried;
+        }
+    }
+}
+
 // generic pass A: any binner kinds/dtypes, masks and keep flags
 template <int ND, int NV>
 __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
@@ -454,16 +525,71 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter(BinPlan p, 
         uint32_t tile[TA_RPT], ent[TA_RPT];
         int32_t rank[TA_RPT];
         double vals[TA_RPT][NV > 0 ? NV : 1];
+        if constexpr (ND == -1) {
+            // plans with a set-ordinal binner: per-row hash probe, per-row dispatch (the
+            // hoisted form's register footprint made this case slower: 21.6 -> 27.1 ms C3)
 #pragma unroll
-        for (int r = 0; r < TA_RPT; r++) {
-            const uint64_t i = b0 + (uint64_t)r * TA_THREADS + threadIdx.x;
-            rank[r] = -1;
-            if (i < row_end) {
-                const uint64_t c = cell_of<ND>(p, i);
-                const uint32_t f = row_contrib<NV>(fa, tp, i, vals[r]);
-                tile[r] = (uint32_t)(c >> tp.s_log2);
-                ent[r] = ((uint32_t)c & smask) | (f << 16);
-                if (f) rank[r] = (int32_t)atomicAdd(&l.hist[tile[r]], 1u);
+            for (int r = 0; r < TA_RPT; r++) {
+                const uint64_t i = b0 + (uint64_t)r * TA_THREADS + threadIdx.x;
+                rank[r] = -1;
+                if (i < row_end) {
+                    const uint64_t c = plan_index(p, i);
+                    const uint32_t f = row_contrib<NV>(fa, tp, i, vals[r]);
+                    tile[r] = (uint32_t)(c >> tp.s_log2);
+                    ent[r] = ((uint32_t)c & smask) | (f << 16);
+                    if (f) rank[r] = (int32_t)atomicAdd(&l.hist[tile[r]], 1u);
+                }
+            }
+        } else {
+            uint64_t cell[TA_RPT];
+            uint32_t fl[TA_RPT];
+    #pragma unroll
+            for (int r = 0; r < TA_RPT; r++) {
+                cell[r] = 0;
+                fl[r] = 0;
+            }
+            if constexpr (ND == 0) {
+                for (int d = 0; d < p.nb; d++) {
+                    const BinnerDev &b = p.b[d];
+                    if (b.kind == 2) {  // set-ordinal binner: a hash probe per row
+    #pragma unroll
+                        for (int r = 0; r < TA_RPT; r++) {
+                            const uint64_t i = b0 + (uint64_t)r * TA_THREADS + threadIdx.x;
+                            if (i < row_end) cell[r] += binner_index(b, i) * b.stride;
+                        }
+                        continue;
+                    }
+                    VH_DEV_DISPATCH(b.dtype, T, ta_dim<T>(b, b0, row_end, cell); break)
+                }
+            } else {
+    #pragma unroll
+                for (int r = 0; r < TA_RPT; r++) {
+                    const uint64_t i = b0 + (uint64_t)r * TA_THREADS + threadIdx.x;
+                    if (i < row_end) cell[r] = cell_of<ND>(p, i);
+                }
+            }
+    #pragma unroll
+            for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+                if (k >= fa.na) break;
+                const FusedAgg &a = fa.a[k];
+                const int slot = tp.val_slot[k];
+                if (!a.data) {
+                    ta_agg<uint8_t, NV>(a, k, slot, b0, row_end, fl, vals);
+                } else {
+                    VH_DEV_DISPATCH(a.dtype, T, ta_agg<T, NV>(a, k, slot, b0, row_end, fl, vals); break)
+                }
+            }
+    #pragma unroll
+            for (int r = 0; r < TA_RPT; r++) {
+                const uint64_t i = b0 + (uint64_t)r * TA_THREADS + threadIdx.x;
+                rank[r] = -1;
+                if (i < row_end) {
+                    const uint64_t c = cell[r];
+                    const uint32_t f = fl[r];
+                    tile[r] = (uint32_t)(c >> tp.s_log2);
+                    ent[r] = ((uint32_t)c & smask) | (f << 16);
+                    if (f) rank[r] = (int32_t)atomicAdd(&l.hist[tile[r]], 1u);
+                }
             }
         }
         batch_commit<NV>(l, fa, tp, T, region0, tile, ent, rank, vals, &s_total);
@@ -887,6 +1013,7 @@ static void launch_scatter_nd(int nd, int fast, unsigned grid, size_t lds, const
     case 1: launch_scatter<1, NV>(fast, grid, lds, plan, fa, tp, n); break;
     case 2: launch_scatter<2, NV>(fast, grid, lds, plan, fa, tp, n); break;
     case 3: launch_scatter<3, NV>(fast, grid, lds, plan, fa, tp, n); break;
+    case -1: launch_scatter<-1, NV>(0, grid, lds, plan, fa, tp, n); break;
     default: launch_scatter<0, NV>(0, grid, lds, plan, fa, tp, n);
     }
 }
@@ -914,6 +1041,7 @@ template <int NV> static int scatter_blocks_per_cu_nd(int nd, int fast, size_t l
     case 1: return scatter_blocks_per_cu<1, NV>(fast, lds);
     case 2: return scatter_blocks_per_cu<2, NV>(fast, lds);
     case 3: return scatter_blocks_per_cu<3, NV>(fast, lds);
+    case -1: return scatter_blocks_per_cu<-1, NV>(0, lds);
     default: return scatter_blocks_per_cu<0, NV>(0, lds);
     }
 }
@@ -1042,6 +1170,10 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     // ---- sample
     // the fast pass A: native f64 binners and sums, no masks, 16-byte aligned columns
     bool fast = nd_f64 > 0 && !flags_mode;
+    // generic pass A flavour: -1 = a set-ordinal binner (per-row form), 0 = hoisted dispatch
+    bool has_set = false;
+    for (int d = 0; d < plan.nb; d++) has_set = has_set || plan.b[d].kind == 2;
+    const int nd_k = nd_f64 > 0 ? nd_f64 : (has_set ? -1 : 0);
     for (int d = 0; d < plan.nb && fast; d++) fast = !plan.b[d].mask && aligned16(plan.b[d].data);
     for (int k = 0; k < fa.na; k++) {
         if (fa.a[k].mask) fast = false;
@@ -1065,7 +1197,7 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         static std::mutex mu;
         static std::map<std::tuple<int, int, int, int, size_t>, int> cache;
         std::lock_guard<std::mutex> lk(mu);
-        const auto key = std::make_tuple(current_device(), ord ? -1 : nd_f64, nv, fast_mode, lds_a);
+        const auto key = std::make_tuple(current_device(), ord ? -2 : nd_k, nv, fast_mode, lds_a);
         auto it = cache.find(key);
         if (it == cache.end()) {
             int v = 0;
@@ -1073,9 +1205,9 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
                 const void *kf = ord_kernel(nv, fast_mode);
                 VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kf, TA_THREADS, lds_a));
             } else {
-                v = nv == 0 ? scatter_blocks_per_cu_nd<0>(nd_f64, fast_mode, lds_a)
-                            : nv == 1 ? scatter_blocks_per_cu_nd<1>(nd_f64, fast_mode, lds_a)
-                                      : scatter_blocks_per_cu_nd<2>(nd_f64, fast_mode, lds_a);
+                v = nv == 0 ? scatter_blocks_per_cu_nd<0>(nd_k, fast_mode, lds_a)
+                            : nv == 1 ? scatter_blocks_per_cu_nd<1>(nd_k, fast_mode, lds_a)
+                                      : scatter_blocks_per_cu_nd<2>(nd_k, fast_mode, lds_a);
             }
             it = cache.emplace(key, v).first;
         }
@@ -1180,9 +1312,9 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
             }
         } else {
             switch (nv) {
-            case 0: launch_scatter_nd<0>(nd_f64, fast_mode, W, lds, plan, fa, tp, n); break;
-            case 1: launch_scatter_nd<1>(nd_f64, fast_mode, W, lds, plan, fa, tp, n); break;
-            default: launch_scatter_nd<2>(nd_f64, fast_mode, W, lds, plan, fa, tp, n);
+            case 0: launch_scatter_nd<0>(nd_k, fast_mode, W, lds, plan, fa, tp, n); break;
+            case 1: launch_scatter_nd<1>(nd_k, fast_mode, W, lds, plan, fa, tp, n); break;
+            default: launch_scatter_nd<2>(nd_k, fast_mode, W, lds, plan, fa, tp, n);
             }
         }
         VH_HIP(hipGetLastError());
