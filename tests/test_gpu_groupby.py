@@ -153,3 +153,31 @@ def test_dense_and_hash_groupers_agree(dense):
     assert gk[order].tolist() == uk.tolist()
     np.testing.assert_array_equal(dfg["n"].to_numpy()[order], c)
     np.testing.assert_allclose(dfg["v_sum"].to_numpy()[order], s, rtol=1e-6, atol=1e-9)
+
+
+def test_large_grid_mixed_aggregators_split_routes():
+    """count(*) + sum + min + max on a grid beyond the LDS sub-grid size with > 2^20 rows:
+    count / sum take the tile path, min / max the generic one (run_bin splits the mix);
+    every column equals numpy's per-key result."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(77)
+    n = 1_300_001
+    key = rng.integers(-20_000, 30_000, n).astype(np.int32)
+    v = rng.integers(-100, 100, n).astype(np.int8)
+    w = rng.normal(size=n).astype(np.float32)
+    df = vaex_amd.from_arrays(key=DeviceArray.from_numpy(key), v=DeviceArray.from_numpy(v),
+                              w=DeviceArray.from_numpy(w))
+    res = df.groupby("key", sort=True).agg({"n": "count", "vs": vaex_amd.agg.sum("v"),
+                                            "vmax": vaex_amd.agg.max("v"), "wmin": vaex_amd.agg.min("w")})
+    uk, inv = np.unique(key, return_inverse=True)
+    np.testing.assert_array_equal(res["key"].to_numpy(), uk)
+    np.testing.assert_array_equal(res["n"].to_numpy(), np.bincount(inv))
+    np.testing.assert_array_equal(res["vs"].to_numpy(),
+                                  np.bincount(inv, weights=v.astype(np.float64)).astype(np.int64))
+    vmax = np.full(len(uk), -128, np.int8)
+    np.maximum.at(vmax, inv, v)
+    np.testing.assert_array_equal(res["vmax"].to_numpy(), vmax)
+    wmin = np.full(len(uk), np.inf, np.float32)
+    np.minimum.at(wmin, inv, w)
+    np.testing.assert_array_equal(res["wmin"].to_numpy(), wmin)

@@ -359,6 +359,34 @@ __global__ __launch_bounds__(256) void k_agg_lds_c(AggDev a, const uint16_t *cel
     }
 }
 
+// indices1d of the generic path with the binner dispatch hoisted out of the row loop (one
+// launch per dimension, kind and dtype as template arguments; k_indices keeps set-ordinal
+// binners, whose per-row hash probe dominates anyway)
+template <int KIND_B, typename T>
+__global__ __launch_bounds__(256) void k_idx_dim(BinnerDev b, uint64_t n, uint64_t *idx, int first) {
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j0 < n; j0 += step * CELL_U) {
+        T raw[CELL_U];
+        bool m[CELL_U];
+        uint64_t prev[CELL_U];
+#pragma unroll
+        for (int u = 0; u < CELL_U; u++) {
+            const uint64_t j = j0 + (uint64_t)u * step;
+            const bool in = j < n;
+            raw[u] = in ? reinterpret_cast<const T *>(b.data)[j] : T{};
+            m[u] = (in && b.mask) ? b.mask[j] == 1 : false;
+            prev[u] = (in && !first) ? idx[j] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < CELL_U; u++) {
+            const uint64_t j = j0 + (uint64_t)u * step;
+            if (j >= n) continue;
+            const uint64_t c = KIND_B == 0 ? scalar_cell<T>(b, raw[u], m[u]) : ordinal_cell<T>(b, raw[u], m[u]);
+            idx[j] = prev[u] + c * b.stride;
+        }
+    }
+}
+
 // Several count / sum aggregators of one small grid in ONE pass over the u16 cells (each
 // aggregator of k_agg_lds_c re-reads the cells and pays its own loop).  Per step a thread
 // takes SF_U rows; the aggregator's dtype is dispatched once per step (not per row), its
@@ -1150,6 +1178,22 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
         const vh_agg *a = aggs[k];
         tile_generic = (a->kind == VH_AGG_COUNT || (a->kind == VH_AGG_SUM && a->data.set)) && !a->mask.set && !a->flip;
     }
+    if (!all_fusable && !tile_generic && !any_host && naggs > 1 && L * 8 > LDS_AGG_MAX_BYTES) {
+        // a mix on a large grid (e.g. groupby count(*) + min + max): the count / sum
+        // aggregators take the tile path, only the rest pays the generic path's global
+        // atomics (one scattered atomic per row each: ~2.4e10 rows/s chip-wide)
+        std::vector<vh_agg *> tiled, rest;
+        for (int k = 0; k < naggs; k++) {
+            const vh_agg *a = aggs[k];
+            const bool t = (a->kind == VH_AGG_COUNT || (a->kind == VH_AGG_SUM && a->data.set)) && !a->mask.set && !a->flip;
+            (t && tiled.size() < (size_t)MAX_FUSED_AGGS ? tiled : rest).push_back(aggs[k]);
+        }
+        if (!tiled.empty() && !rest.empty()) {
+            run_bin(g, tiled.data(), (int)tiled.size(), length);
+            run_bin(g, rest.data(), (int)rest.size(), length);
+            return;
+        }
+    }
     const uint64_t chunk_max = any_host ? (uint64_t(1) << 24) : ((all_fusable || tile_generic) ? length : (uint64_t(1) << 26));
     HostPipe &pipe = g->ws.pipe;
     if (any_host) {
@@ -1245,8 +1289,24 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                 g->ws.idx.ensure(len * 8);
                 idx = g->ws.idx.as<uint64_t>();
                 TimedScope ts("bin_indices");
-                hipLaunchKernelGGL(k_indices, dim3(blocks_for(len, 256)), dim3(256), 0, stream(), plan, len, idx);
-                VH_HIP(hipGetLastError());
+                bool hoist = plan.nb > 0;
+                for (int d = 0; d < plan.nb; d++) hoist = hoist && (plan.b[d].kind == 0 || plan.b[d].kind == 1);
+                if (hoist) {
+                    const dim3 cg(blocks_for(len, 256, 8)), cb(256);
+                    for (int d = 0; d < plan.nb; d++) {
+                        const BinnerDev &b = plan.b[d];
+                        const int first = d == 0 ? 1 : 0;
+                        if (b.kind == 0) {
+                            VH_DISPATCH_DTYPE(b.dtype, T, hipLaunchKernelGGL((k_idx_dim<0, T>), cg, cb, 0, stream(), b, len, idx, first));
+                        } else {
+                            VH_DISPATCH_DTYPE(b.dtype, T, hipLaunchKernelGGL((k_idx_dim<1, T>), cg, cb, 0, stream(), b, len, idx, first));
+                        }
+                        VH_HIP(hipGetLastError());
+                    }
+                } else {
+                    hipLaunchKernelGGL(k_indices, dim3(blocks_for(len, 256)), dim3(256), 0, stream(), plan, len, idx);
+                    VH_HIP(hipGetLastError());
+                }
             }
             auto make_cells = [&]() {
                 if (cells) return;
