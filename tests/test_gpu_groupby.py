@@ -181,3 +181,36 @@ def test_large_grid_mixed_aggregators_split_routes():
     wmin = np.full(len(uk), np.inf, np.float32)
     np.minimum.at(wmin, inv, w)
     np.testing.assert_array_equal(res["wmin"].to_numpy(), wmin)
+
+
+def test_two_small_int_keys_narrow_lds_cells():
+    """A 10^4-cell grid of two int8 keys (h2o q2 shape): counts and 8/16-bit integer sums
+    aggregate in 32-bit LDS cells (k_agg_lds_c<..., NARROW>); exact against numpy,
+    including extreme values and a float count with NaNs."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(78)
+    n = 2_000_003
+    k1 = rng.integers(5, 105, n).astype(np.int8)
+    k2 = rng.integers(-50, 50, n).astype(np.int8)
+    v8 = rng.choice(np.array([-128, 127, -1, 3], np.int8), n)
+    v16 = rng.choice(np.array([-32768, 32767, 7], np.int16), n)
+    u8 = rng.integers(0, 256, n).astype(np.uint8)
+    f = rng.normal(size=n)
+    f[::11] = np.nan
+    cols = dict(k1=k1, k2=k2, v8=v8, v16=v16, u8=u8, f=f)
+    df = vaex_amd.from_arrays(**{c: DeviceArray.from_numpy(a) for c, a in cols.items()})
+    res = df.groupby(["k1", "k2"], sort=True).agg({"n": "count", "s8": vaex_amd.agg.sum("v8"),
+                                                   "s16": vaex_amd.agg.sum("v16"), "su": vaex_amd.agg.sum("u8"),
+                                                   "nf": vaex_amd.agg.count("f")})
+    tup = np.stack([k1.astype(np.int64), k2.astype(np.int64)], axis=1)
+    uniq, inv = np.unique(tup, axis=0, return_inverse=True)
+    inv = inv.ravel()
+    np.testing.assert_array_equal(res["k1"].to_numpy(), uniq[:, 0])
+    np.testing.assert_array_equal(res["k2"].to_numpy(), uniq[:, 1])
+    np.testing.assert_array_equal(res["n"].to_numpy(), np.bincount(inv))
+    for name, col in (("s8", v8), ("s16", v16), ("su", u8)):
+        exp = np.zeros(len(uniq), np.int64)
+        np.add.at(exp, inv, col.astype(np.int64))
+        np.testing.assert_array_equal(res[name].to_numpy().astype(np.int64), exp, err_msg=name)
+    np.testing.assert_array_equal(res["nf"].to_numpy(), np.bincount(inv[~np.isnan(f)], minlength=len(uniq)))

@@ -286,10 +286,15 @@ __global__ __launch_bounds__(256) void k_cells_dim(BinnerDev b, uint64_t n, uint
     }
 }
 
-template <int KIND, typename T>
+// NARROW: 32-bit LDS cells (counts; sums of 8/16-bit integers when a workgroup's rows
+// cannot overflow them, checked on the host), half the LDS of a sub-grid, so grids of
+// ~10^4 cells keep several workgroups per CU
+template <int KIND, typename T, bool NARROW = false>
 __global__ __launch_bounds__(256) void k_agg_lds_c(AggDev a, const uint16_t *cells, uint64_t n, uint64_t L, T fill) {
     using G = typename Upcast<T>::type;
-    using C = typename LdsCell<KIND, T>::type;
+    using C = std::conditional_t<NARROW,
+                                 std::conditional_t<KIND == VH_AGG_COUNT || !is_signed_int_t<T>::value, uint32_t, int32_t>,
+                                 typename LdsCell<KIND, T>::type>;
     extern __shared__ __align__(16) unsigned char lds_raw[];
     C *g = reinterpret_cast<C *>(lds_raw);
     for (uint64_t c = threadIdx.x; c < L; c += blockDim.x) {
@@ -316,11 +321,12 @@ __global__ __launch_bounds__(256) void k_agg_lds_c(AggDev a, const uint16_t *cel
             const uint32_t c = cell[u];
             if constexpr (KIND == VH_AGG_COUNT) {
                 if (a.data && is_nan_v(a.flip ? bswap_v(v[u]) : v[u])) continue;
-                atomicAdd(g + c, 1ULL);
+                atomicAdd(g + c, (C)1);
             } else if constexpr (KIND == VH_AGG_SUM) {
                 const T x = a.flip ? bswap_v(v[u]) : v[u];
                 if (is_nan_v(x)) continue;
-                atomic_add_grid<G>(g + c, upcast_v(x));
+                if constexpr (NARROW) atomicAdd(g + c, (C)x);
+                else atomic_add_grid<G>(g + c, upcast_v(x));
             } else if constexpr (KIND == VH_AGG_MIN || KIND == VH_AGG_MAX) {
                 const T x = a.flip ? bswap_v(v[u]) : v[u];
                 if (is_nan_v(x)) continue;
@@ -352,9 +358,9 @@ __global__ __launch_bounds__(256) void k_agg_lds_c(AggDev a, const uint16_t *cel
             if (vb != fb)
                 atomic_minmax<T>(reinterpret_cast<T *>(a.grid) + c, v, KIND == VH_AGG_MAX);
         } else if constexpr (KIND == VH_AGG_COUNT) {
-            if (v) atomicAdd((unsigned long long *)a.grid + c, v);
+            if (v) atomicAdd((unsigned long long *)a.grid + c, (unsigned long long)v);
         } else {
-            if (v != (C)0) atomic_add_grid<G>(reinterpret_cast<G *>(a.grid) + c, v);
+            if (v != (C)0) atomic_add_grid<G>(reinterpret_cast<G *>(a.grid) + c, (G)v);
         }
     }
 }
@@ -1377,13 +1383,31 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                     TimedScope ts("bin_aggregate_lds");
                     dim3 grd(blocks_for(len, 256, 8)), blk(256);
                     const size_t shm = (size_t)((L * 8 + 15) & ~uint64_t(15));
+                    const size_t shm32 = (size_t)((L * 4 + 15) & ~uint64_t(15));
                     const bool mx = ad.kind == VH_AGG_MAX;
+                    // rows one workgroup adds into its sub-grid (bounds 32-bit partials)
+                    const uint64_t rows_wg = (len + (uint64_t)grd.x - 1) / grd.x + 256 * CELL_U;
+                    const bool narrow_sum = !ad.flip && (((ad.dtype == VH_I8 || ad.dtype == VH_U8) && rows_wg < (1ull << 23)) ||
+                                                         ((ad.dtype == VH_I16 || ad.dtype == VH_U16) && rows_wg < (1ull << 15)));
                     switch (ad.kind) {
                     case VH_AGG_COUNT:
-                        VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg_lds_c<VH_AGG_COUNT, T>), grd, blk, shm, stream(), ad, cells, len, L, T{}));
+                        if (rows_wg < (1ull << 32)) {
+                            VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg_lds_c<VH_AGG_COUNT, T, true>), grd, blk, shm32, stream(), ad, cells, len, L, T{}));
+                        } else {
+                            VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg_lds_c<VH_AGG_COUNT, T>), grd, blk, shm, stream(), ad, cells, len, L, T{}));
+                        }
                         break;
                     case VH_AGG_SUM:
-                        VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg_lds_c<VH_AGG_SUM, T>), grd, blk, shm, stream(), ad, cells, len, L, T{}));
+                        if (narrow_sum) {
+                            switch (ad.dtype) {
+                            case VH_I8: hipLaunchKernelGGL((k_agg_lds_c<VH_AGG_SUM, int8_t, true>), grd, blk, shm32, stream(), ad, cells, len, L, (int8_t)0); break;
+                            case VH_U8: hipLaunchKernelGGL((k_agg_lds_c<VH_AGG_SUM, uint8_t, true>), grd, blk, shm32, stream(), ad, cells, len, L, (uint8_t)0); break;
+                            case VH_I16: hipLaunchKernelGGL((k_agg_lds_c<VH_AGG_SUM, int16_t, true>), grd, blk, shm32, stream(), ad, cells, len, L, (int16_t)0); break;
+                            default: hipLaunchKernelGGL((k_agg_lds_c<VH_AGG_SUM, uint16_t, true>), grd, blk, shm32, stream(), ad, cells, len, L, (uint16_t)0);
+                            }
+                        } else {
+                            VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg_lds_c<VH_AGG_SUM, T>), grd, blk, shm, stream(), ad, cells, len, L, T{}));
+                        }
                         break;
                     case VH_AGG_MIN:
                         VH_DISPATCH_DTYPE(ad.dtype, T, hipLaunchKernelGGL((k_agg_lds_c<VH_AGG_MIN, T>), grd, blk, shm, stream(), ad, cells, len, L, minmax_fill<T>(false)));
