@@ -269,3 +269,42 @@ def test_hash_partition_merge_uint64_keys():
         np.add.at(es, inv, keys >> np.uint64(40))
         np.testing.assert_array_equal(got["s"], es)
         assert bool(got["nn_none"][0])
+
+
+def _empty_rank_worker(rank, world, path):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from vaex_amd.distributed import combine_groups
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if rank == 1:  # an empty shard: no groups at all
+        local = (np.empty(0, np.int64), np.empty(0, np.int64), [np.empty(0, np.float64)], [np.empty(0, np.int64)])
+    else:
+        keys = np.array([-7, 3, 10 ** 12], np.int64) + rank
+        local = (keys, np.array([1, 2, 3], np.int64), [np.array([0.5, 1.5, 2.5])], [np.array([1, 1, 3], np.int64)])
+    gk, gc, gs, gn = combine_groups(local)
+    if rank == 1:
+        np.savez(path, keys=gk, counts=gc, s=gs[0], nn=gn[0])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_hash_partition_merge_with_an_empty_rank():
+    """A rank with no groups (empty row shard) still takes part in both exchanges and ends
+    with the whole merged, key-sorted result."""
+    pytest.importorskip("torch")
+    import torch.multiprocessing as mp
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(34700 + os.getpid() % 1000)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "e.npz")
+        mp.spawn(_empty_rank_worker, args=(3, path), nprocs=3, join=True)
+        got = np.load(path)
+    base = np.array([-7, 3, 10 ** 12], np.int64)
+    keys = np.concatenate([base, base + 2])
+    order = np.argsort(keys)
+    np.testing.assert_array_equal(got["keys"], keys[order])
+    np.testing.assert_array_equal(got["counts"], np.array([1, 2, 3, 1, 2, 3])[order])
+    np.testing.assert_array_equal(got["s"], np.array([0.5, 1.5, 2.5, 0.5, 1.5, 2.5])[order])
+    np.testing.assert_array_equal(got["nn"], np.array([1, 1, 3, 1, 1, 3])[order])
