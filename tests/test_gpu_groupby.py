@@ -214,3 +214,34 @@ def test_two_small_int_keys_narrow_lds_cells():
         np.add.at(exp, inv, col.astype(np.int64))
         np.testing.assert_array_equal(res[name].to_numpy().astype(np.int64), exp, err_msg=name)
     np.testing.assert_array_equal(res["nf"].to_numpy(), np.bincount(inv[~np.isnan(f)], minlength=len(uniq)))
+
+
+def test_small_grid_shared_plain_counts():
+    """h2o q4 shape: count(*) and counts of integer columns (never NaN) share one LDS
+    sub-grid in the fused small-grid pass; a float count with NaNs and the means stay
+    separate.  Exact against numpy."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(79)
+    n = 1_500_007
+    key = rng.integers(5, 105, n).astype(np.int8)
+    v1 = rng.integers(5, 15, n).astype(np.int8)
+    v2 = rng.integers(-300, 300, n).astype(np.int16)
+    v3 = rng.normal(size=n).astype(np.float32)
+    v3[::7] = np.nan
+    df = vaex_amd.from_arrays(**{c: DeviceArray.from_numpy(a) for c, a in dict(key=key, v1=v1, v2=v2, v3=v3).items()})
+    res = df.groupby(["key"], sort=True).agg({"n": "count", "c1": vaex_amd.agg.count("v1"), "c2": vaex_amd.agg.count("v2"),
+                                              "c3": vaex_amd.agg.count("v3"), "m1": vaex_amd.agg.mean("v1"),
+                                              "m2": vaex_amd.agg.mean("v2")})
+    uk, inv = np.unique(key, return_inverse=True)
+    cnt = np.bincount(inv)
+    np.testing.assert_array_equal(res["key"].to_numpy(), uk)
+    for c in ("n", "c1", "c2"):
+        np.testing.assert_array_equal(res[c].to_numpy(), cnt, err_msg=c)
+    np.testing.assert_array_equal(res["c3"].to_numpy(), np.bincount(inv[~np.isnan(v3)], minlength=len(uk)))
+    s1 = np.zeros(len(uk), np.int64)
+    np.add.at(s1, inv, v1.astype(np.int64))
+    s2 = np.zeros(len(uk), np.int64)
+    np.add.at(s2, inv, v2.astype(np.int64))
+    np.testing.assert_allclose(res["m1"].to_numpy(), s1 / cnt, rtol=1e-12)
+    np.testing.assert_allclose(res["m2"].to_numpy(), s2 / cnt, rtol=1e-12)

@@ -402,6 +402,9 @@ constexpr int SF_U = 8;
 struct SmallAggs {
     int na, pad;
     uint32_t lds_off[SF_MAX];  // byte offset of each aggregator's sub-grid
+    uint32_t shared;           // bit k: aggregator k is a row count equal to an earlier one
+                               // (count(*) / count of an unmasked integer column): it adds
+                               // nothing itself and flushes that one's sub-grid
     AggDev a[SF_MAX];
 };
 
@@ -460,6 +463,7 @@ __global__ __launch_bounds__(256) void k_small_fused(SmallAggs sa, const uint16_
             cell[u] = j < n ? cells[j] : (uint16_t)0;
         }
         for (int k = 0; k < sa.na; k++) {
+            if ((sa.shared >> k) & 1) continue;
             const AggDev &a = sa.a[k];
             unsigned char *lds = lds_raw + sa.lds_off[k];
             VH_DEV_DISPATCH(a.dtype, T, sf_rows<T>(a, lds, cell, j0, step, n); break)
@@ -1343,9 +1347,25 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                     SmallAggs sa{};
                     uint64_t off = 0;
                     size_t j = i;
-                    while (j < pend.size() && sa.na < SF_MAX && off + L * 8 <= LDS_AGG_MAX_BYTES) {
+                    // a count that sees every row (no mask; no data, or integer data that
+                    // is never NaN) equals any other such count of the same chunk
+                    auto plain_count = [](const AggDev &a) {
+                        return a.kind == VH_AGG_COUNT && !a.mask && (!a.data || (a.dtype != VH_F64 && a.dtype != VH_F32));
+                    };
+                    int first_plain = -1;
+                    while (j < pend.size() && sa.na < SF_MAX) {
+                        const AggDev &a = ads[pend[j]];
+                        if (plain_count(a) && first_plain >= 0) {
+                            sa.lds_off[sa.na] = sa.lds_off[first_plain];
+                            sa.shared |= 1u << sa.na;
+                            sa.a[sa.na++] = a;
+                            j++;
+                            continue;
+                        }
+                        if (off + L * 8 > LDS_AGG_MAX_BYTES) break;
+                        if (plain_count(a)) first_plain = sa.na;
                         sa.lds_off[sa.na] = (uint32_t)off;
-                        sa.a[sa.na++] = ads[pend[j]];
+                        sa.a[sa.na++] = a;
                         off += (L * 8 + 15) & ~uint64_t(15);
                         j++;
                     }
