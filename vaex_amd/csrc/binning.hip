@@ -399,18 +399,23 @@ __global__ __launch_bounds__(256) void k_idx_dim(BinnerDev b, uint64_t n, uint64
 // values and mask loaded for all SF_U rows, then added into its LDS sub-grid.
 constexpr int SF_MAX = 8;
 constexpr int SF_U = 8;
+// one fused launch's sub-grids: at most 48 KB, so three workgroups stay resident per CU
+// (a 2 x 42 KB fused launch of h2o q2 ran at one per CU: 8.7 -> 10.8 ms)
+constexpr uint64_t SF_LDS_BUDGET = 48 * 1024;
 struct SmallAggs {
     int na, pad;
     uint32_t lds_off[SF_MAX];  // byte offset of each aggregator's sub-grid
     uint32_t shared;           // bit k: aggregator k is a row count equal to an earlier one
                                // (count(*) / count of an unmasked integer column): it adds
                                // nothing itself and flushes that one's sub-grid
+    uint32_t narrow;           // bit k: 32-bit LDS cells (counts; 8/16-bit integer sums whose
+                               // per-workgroup partials fit, checked on the host)
     AggDev a[SF_MAX];
 };
 
 template <typename T>
 __device__ inline void sf_rows(const AggDev &a, unsigned char *lds, const uint16_t (&cell)[SF_U], uint64_t j0,
-                               uint64_t step, uint64_t n) {
+                               uint64_t step, uint64_t n, bool narrow) {
     using G = typename Upcast<T>::type;
     T v[SF_U];
     bool keep[SF_U];
@@ -427,22 +432,32 @@ __device__ inline void sf_rows(const AggDev &a, unsigned char *lds, const uint16
         const T x = a.flip ? bswap_v(v[u]) : v[u];
         if (a.kind == VH_AGG_COUNT) {
             if (a.data && is_nan_v(x)) continue;
-            atomicAdd(reinterpret_cast<unsigned long long *>(lds) + cell[u], 1ULL);
+            if (narrow) atomicAdd(reinterpret_cast<uint32_t *>(lds) + cell[u], 1u);
+            else atomicAdd(reinterpret_cast<unsigned long long *>(lds) + cell[u], 1ULL);
         } else {
             if (is_nan_v(x)) continue;
+            if constexpr (std::is_integral_v<T> && sizeof(T) <= 2) {
+                if (narrow) {
+                    atomicAdd(reinterpret_cast<int32_t *>(lds) + cell[u], (int32_t)x);
+                    continue;
+                }
+            }
             atomic_add_grid<G>(reinterpret_cast<G *>(lds) + cell[u], upcast_v(x));
         }
     }
 }
 
-template <typename T> __device__ inline void sf_flush(const AggDev &a, const unsigned char *lds, uint64_t L) {
+template <typename T>
+__device__ inline void sf_flush(const AggDev &a, const unsigned char *lds, uint64_t L, bool narrow) {
     using G = typename Upcast<T>::type;
     for (uint64_t c = threadIdx.x; c < L; c += blockDim.x) {
         if (a.kind == VH_AGG_COUNT) {
-            const unsigned long long v = reinterpret_cast<const unsigned long long *>(lds)[c];
+            const unsigned long long v = narrow ? (unsigned long long)reinterpret_cast<const uint32_t *>(lds)[c]
+                                                : reinterpret_cast<const unsigned long long *>(lds)[c];
             if (v) atomicAdd((unsigned long long *)a.grid + c, v);
         } else {
-            const G v = reinterpret_cast<const G *>(lds)[c];
+            // a narrow partial is an int32 (two's complement of the exact sum, which fits)
+            const G v = narrow ? (G)(int64_t)reinterpret_cast<const int32_t *>(lds)[c] : reinterpret_cast<const G *>(lds)[c];
             if (v != (G)0) atomic_add_grid<G>(reinterpret_cast<G *>(a.grid) + c, v);
         }
     }
@@ -466,14 +481,16 @@ __global__ __launch_bounds__(256) void k_small_fused(SmallAggs sa, const uint16_
             if ((sa.shared >> k) & 1) continue;
             const AggDev &a = sa.a[k];
             unsigned char *lds = lds_raw + sa.lds_off[k];
-            VH_DEV_DISPATCH(a.dtype, T, sf_rows<T>(a, lds, cell, j0, step, n); break)
+            const bool nw = (sa.narrow >> k) & 1;
+            VH_DEV_DISPATCH(a.dtype, T, sf_rows<T>(a, lds, cell, j0, step, n, nw); break)
         }
     }
     __syncthreads();
     for (int k = 0; k < sa.na; k++) {
         const AggDev &a = sa.a[k];
         const unsigned char *lds = lds_raw + sa.lds_off[k];
-        VH_DEV_DISPATCH(a.dtype, T, sf_flush<T>(a, lds, L); break)
+        const bool nw = (sa.narrow >> k) & 1;
+        VH_DEV_DISPATCH(a.dtype, T, sf_flush<T>(a, lds, L, nw); break)
     }
 }
 
@@ -1353,20 +1370,33 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                         return a.kind == VH_AGG_COUNT && !a.mask && (!a.data || (a.dtype != VH_F64 && a.dtype != VH_F32));
                     };
                     int first_plain = -1;
+                    // rows one workgroup adds into its sub-grids (bounds 32-bit partials)
+                    const uint64_t rows_wg = (len + (uint64_t)blocks_for(len, 256, 8) - 1) / blocks_for(len, 256, 8) + 256 * SF_U;
+                    auto narrow_ok = [&](const AggDev &a) {
+                        if (a.kind == VH_AGG_COUNT) return rows_wg < (1ull << 32);
+                        if (a.flip) return false;
+                        if (a.dtype == VH_I8 || a.dtype == VH_U8) return rows_wg < (1ull << 23);
+                        if (a.dtype == VH_I16 || a.dtype == VH_U16) return rows_wg < (1ull << 15);
+                        return false;
+                    };
                     while (j < pend.size() && sa.na < SF_MAX) {
                         const AggDev &a = ads[pend[j]];
                         if (plain_count(a) && first_plain >= 0) {
                             sa.lds_off[sa.na] = sa.lds_off[first_plain];
                             sa.shared |= 1u << sa.na;
+                            if ((sa.narrow >> first_plain) & 1) sa.narrow |= 1u << sa.na;
                             sa.a[sa.na++] = a;
                             j++;
                             continue;
                         }
-                        if (off + L * 8 > LDS_AGG_MAX_BYTES) break;
+                        const bool nw = narrow_ok(a);
+                        const uint64_t bytes = L * (nw ? 4 : 8);
+                        if (off + bytes > SF_LDS_BUDGET) break;
                         if (plain_count(a)) first_plain = sa.na;
+                        if (nw) sa.narrow |= 1u << sa.na;
                         sa.lds_off[sa.na] = (uint32_t)off;
                         sa.a[sa.na++] = a;
-                        off += (L * 8 + 15) & ~uint64_t(15);
+                        off += (bytes + 15) & ~uint64_t(15);
                         j++;
                     }
                     if (sa.na >= 2) {
