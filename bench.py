@@ -54,19 +54,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    # BENCH_FORCE_DIST=1: the N>1 code path (RCCL init, grid all-reduce, max-over-ranks
-    # timing) on a single rank, to exercise it on a one-GPU box
-    if world > 1 or os.environ.get("BENCH_FORCE_DIST"):
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
     import vaex_amd
     from vaex_amd import _lib, superagg
     from vaex_amd.device import DeviceArray
     from vaex_amd import distributed as vdist
 
     _lib.call("vh_set_device", local_rank)
+    # BENCH_FORCE_DIST=1: the N>1 code path (RCCL communicator, grid all-reduce,
+    # max-over-ranks timing) on a single rank, to exercise it on a one-GPU box
+    if world > 1 or os.environ.get("BENCH_FORCE_DIST"):
+        from vaex_amd import comm as vcomm
+        dist = vcomm.init("rccl")
     n = int(args.rows)
     bins = args.bins
     # resident synthetic columns (each rank its own shard: seeds offset by rank)
@@ -86,11 +84,12 @@ def main():
         grid.bin([count, total])
         if dist is not None:
             vdist.allreduce_aggs([count, total])
-        return count, total
+        # the grids read back to host numpy arrays, as get_result does (cpu.py:592-605)
+        return np.asarray(count), np.asarray(total)
 
     def barrier():
         if dist is not None:
-            dist.barrier()
+            vdist.barrier()
         _lib.synchronize()
 
     for _ in range(args.warmup):
@@ -110,30 +109,33 @@ def main():
         t.append(time.perf_counter())
         grid.bin([count, total])
         t.append(time.perf_counter())
-        grid.bin([count, total])
+        np.asarray(count), np.asarray(total)
         t.append(time.perf_counter())
         del count, total, grid
         t.append(time.perf_counter())
         print("breakdown_ms", {k: round((b - a) * 1e3, 3) for k, a, b in
-                               zip(["grid", "aggs", "bin1", "bin2_same_grid", "free"], t, t[1:])}, flush=True)
-    _lib.timing_reset()
-    _lib.timing_enable(True)
+                               zip(["grid", "aggs", "bin", "read_back", "free"], t, t[1:])}, flush=True)
+    # timed region: no HIP-event timers inside it
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = step()
     barrier()
     t1 = time.perf_counter()
-    _lib.timing_enable(False)
     elapsed = t1 - t0
     if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = vdist.allreduce_scalar(elapsed, "max")
     ms_per_step = elapsed / args.steps * 1e3
     total_rows = n * world * args.steps
     value = total_rows / elapsed
+
+    # per-kernel HIP-event durations from a separate instrumented run of the same steps
+    _lib.timing_reset()
+    _lib.timing_enable(True)
+    for _ in range(args.steps):
+        step()
+    _lib.synchronize()
+    _lib.timing_enable(False)
 
     # roofline of the dominant kernel (pass A of the tiled path): algorithmic bytes = 24 B/row
     # (x, y, w read once) x rows per launch / its average HIP-event duration
@@ -168,11 +170,19 @@ def main():
         roofline["traffic"] = traffic["bytes"]
         roofline["traffic_source"] = traffic["source"]
 
-    check = None
-    if args.check and rank == 0:
-        count, total = res
-        c = np.asarray(count)
-        check = {"count_total": int(c.sum()), "rows": n * world, "count_equal": int(c.sum()) == n * world}
+    # full-size properties of the last timed step's result (every run): every row lands in
+    # one cell (the synthetic columns hold no NaN, NaN rows would sit in cell 0), and the
+    # grid's sum equals an independent reduction of w (a 0-d sum: the small-grid LDS path,
+    # not the tile path) within 1e-6 relative
+    count, total = res
+    local_w = float(vaex_amd.from_arrays(w=w).sum("w"))
+    ref_sum = vdist.allreduce_scalar(local_w, "sum") if dist is not None else local_w
+    c_tot = int(np.asarray(count).sum())
+    s_tot = float(np.asarray(total).sum())
+    check = {"count_total": c_tot, "rows": n * world, "count_equal": c_tot == n * world,
+             "sum_total": s_tot, "sum_reference": ref_sum,
+             "sum_rel_err": abs(s_tot - ref_sum) / abs(ref_sum) if ref_sum else None}
+    check["ok"] = bool(check["count_equal"] and check["sum_rel_err"] is not None and check["sum_rel_err"] < 1e-6)
 
     extra = {}
     if rank == 0 and world == 1 and not args.no_groupby:
@@ -184,6 +194,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(x, y, w, n, bins, args.cpu_seconds)
+        extra["c1"] = bench_c1(args)
 
     if rank == 0:
         line = {
@@ -209,12 +220,11 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
-        if check:
-            line["check"] = check
+        line["check"] = check
         line.update(extra)
         print(json.dumps(line), flush=True)
     if dist is not None:
-        dist.destroy_process_group()
+        vdist.shutdown()
 
 
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_c2.json")
@@ -381,9 +391,10 @@ def bench_groupby(n, args):
     return out
 
 
-def cpu_baseline(x, y, w, n, bins, target_seconds):
+def cpu_baseline(x, y, w, n, bins, target_seconds, repeats=5):
     """oracle/superagg_oracle.c or_bench_grid2d: reference threading model (1 Mi-row chunks,
-    max(2, T//8) private grids for a >=1e7-byte part, serial reduce) on a bounded sample."""
+    max(2, T//8) private grids for a >=1e7-byte part, serial reduce) on a bounded sample;
+    the median of `repeats` runs."""
     from oracle import oracle
     L = oracle.lib()
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
@@ -403,13 +414,12 @@ def cpu_baseline(x, y, w, n, bins, target_seconds):
                                  parts, threads, 1 << 20, cnt.ctypes.data, sm.ctypes.data)
         return time.perf_counter() - t0, used
 
-    def run(m):
-        return run_parts(m, nparts)
-
     probe = min(n, 1 << 24)
-    t, _ = run(probe)
-    m = int(min(n, 1 << 28, max(probe, probe * target_seconds / max(t, 1e-6))))
-    t, used = run(m)
+    t, _ = run_parts(probe, nparts)
+    m = int(min(n, 1 << 28, max(probe, probe * (target_seconds / repeats) / max(t, 1e-6))))
+    runs = [run_parts(m, nparts) for _ in range(repeats)]
+    t = float(np.median([r[0] for r in runs]))
+    used = runs[0][1]
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -420,12 +430,57 @@ def cpu_baseline(x, y, w, n, bins, target_seconds):
     except OSError:
         pass
     # the same sample without the ideal_splits cap (one private grid per thread)
-    t_unc, used_unc = run_parts(m, threads)
+    unc = [run_parts(m, threads) for _ in range(repeats)]
+    t_unc = float(np.median([r[0] for r in unc]))
     return {"value": m / t, "unit": "rows/s", "cores": used, "kind": "port",
-            "uncapped": {"value": m / t_unc, "cores": used_unc, "nparts": threads},
-            "sample": f"first {m} rows of the same x,y,w columns, count+sum 1027x1027 grid, {t:.2f} s",
+            "uncapped": {"value": m / t_unc, "cores": unc[0][1], "nparts": threads},
+            "sample": f"first {m} rows of the same x,y,w columns, count+sum 1027x1027 grid, median of {repeats} "
+                      f"runs ({t:.2f} s each)",
+            "runs_s": [round(r[0], 4) for r in runs],
             "threads_available": threads, "nparts_rule": "max(2, T//8) (cpu.py:487-499)",
             "cpu_model": cpu_model, "host": platform.node()}
+
+
+def bench_c1(args, repeats=5, gpu_repeats=20):
+    """C1 (BASELINE configs[0]): df.count(binby='x', shape=256) on 1e7 float64 rows with no
+    limits -- the minmax limits pre-pass, then the bin pass -- end to end
+    through the DataFrame API on an HBM column (median of `gpu_repeats`), next to the C
+    port of the reference's ExecutorLocal (T threads, private per-thread grids, median of
+    `repeats`); also the bin pass alone with limits=[-5, 5]."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    from oracle import oracle
+    n, bins = 10_000_000, 256
+    x = DeviceArray.random(n, "normal", seed=1)
+    df = vaex_amd.from_arrays(x=x)
+    out = {"rows": n, "bins": bins, "algorithmic_bytes_per_row": {"minmax+bin": 16, "bin": 8}}
+    for name, lim in (("minmax+bin", None), ("bin", [-5.0, 5.0])):
+        df.count(binby="x", shape=bins, limits=lim)
+        ts = []
+        for _ in range(gpu_repeats):
+            t0 = time.perf_counter()
+            c = df.count(binby="x", shape=bins, limits=lim)
+            ts.append(time.perf_counter() - t0)
+        t = float(np.median(ts))
+        out[name] = {"gpu_ms": round(t * 1e3, 4), "gpu_rows_per_s": n / t, "count_total": int(np.asarray(c).sum())}
+    L = oracle.lib()
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    hx = x.to_numpy()
+    lim = np.zeros(2)
+    g = np.zeros(bins + 3, np.int64)
+    for name, do_mm in (("minmax+bin", 1), ("bin", 0)):
+        if not do_mm:
+            lim[:] = (-5.0, 5.0)
+        ts = []
+        for _ in range(repeats):
+            t0 = time.perf_counter()
+            L.or_bench_count1d(hx.ctypes.data, n, threads, bins, do_mm, lim.ctypes.data, g.ctypes.data)
+            ts.append(time.perf_counter() - t0)
+        t = float(np.median(ts))
+        out[name].update(cpu_ms=round(t * 1e3, 3), cpu_rows_per_s=n / t, cpu_threads=threads,
+                         cpu_equal=bool(int(g.sum()) == n))
+        out[name]["gpu_over_cpu"] = round(out[name]["gpu_rows_per_s"] / out[name]["cpu_rows_per_s"], 2)
+    return out
 
 
 if __name__ == "__main__":

@@ -57,6 +57,9 @@ enum vh_agg_kind {
                               dropmissing, bit 1 dropnan */
 };
 
+/* reductions of the multi-GPU collectives */
+enum vh_op { VH_OP_SUM = 0, VH_OP_MIN = 1, VH_OP_MAX = 2 };
+
 typedef struct vh_binner vh_binner;
 typedef struct vh_grid vh_grid;
 typedef struct vh_agg vh_agg;
@@ -199,6 +202,32 @@ int vh_hashagg_finish(vh_hashagg *h, uint64_t *ngroups);
 /* host outputs, ngroups items each: keys as int64, count(*) int64, per value column its sum
  * (8 bytes: double for float columns, int64/uint64 for integers) and non-NaN count int64 */
 int vh_hashagg_read(vh_hashagg *h, int64_t *keys, int64_t *counts, void *const *sums, int64_t *const *nonnull);
+/* ---- multi-GPU (comm.hip): RCCL bound by the library, one process per GPU ----------
+ * The reference has no multi-process path; its ExecutorLocal reduces per-thread task
+ * parts serially (execution.py:285, Aggregator::reduce superagg.cpp:160-167,205-212,
+ * 252-259,354-361,470-480).  Across GPUs the same reductions run as collectives on the
+ * library stream.  The caller distributes rank 0's unique id (128 bytes)
+ * to every rank before vh_comm_init (vaex_amd/comm.py does it over its host channel). */
+typedef struct vh_comm vh_comm;
+int vh_comm_unique_id(void *out128);
+int vh_comm_init(const void *id128, int world, int rank, vh_comm **out); /* on the current device */
+int vh_comm_destroy(vh_comm *comm);
+/* in-place all-reduce of `count` items of `dtype` (host or HBM buffer) with vh_op */
+int vh_comm_allreduce(vh_comm *comm, void *buf, uint64_t count, int dtype, int op, int loc);
+/* recv = every rank's `bytes` of send, rank-major */
+int vh_comm_allgather(vh_comm *comm, const void *send, void *recv, uint64_t bytes, int loc);
+/* send / recv hold per-rank segments back to back in rank order (sizes in bytes) */
+int vh_comm_alltoallv(vh_comm *comm, const void *send, const uint64_t *send_bytes, void *recv,
+                      const uint64_t *recv_bytes, int loc);
+int vh_comm_barrier(vh_comm *comm);
+/* an aggregator's HBM grid combined across ranks in place: SUM for count / sum / moment,
+ * MIN / MAX for min / max, AggFirst by (order, rank) on the device (superagg.cpp:470-480) */
+int vh_comm_agg_allreduce(vh_comm *comm, vh_agg *agg);
+/* groupby results across ranks (after vh_hashagg_finish): every group row to its owner
+ * rank splitmix64(key bits) % world over RCCL, owners fold equal keys in rank order; with
+ * `gather` every rank then holds the whole key-sorted result (read with vh_hashagg_read) */
+int vh_hashagg_exchange(vh_hashagg *h, vh_comm *comm, int gather);
+
 /* ---- expressions on HBM columns (expr.hip) ----------------------------------
  * out[i] = program(cols[.][i]) for i < n: the device evaluation of a virtual column,
  * selection or filter (the reference evaluates them with numpy per chunk, cpu.py:542-581,

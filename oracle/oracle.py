@@ -74,6 +74,8 @@ def lib():
         L.or_minmax_f64.argtypes = [vp, u64, vp, vp]
         L.or_bench_grid2d.argtypes = [vp, vp, vp, u64, dbl, dbl, dbl, dbl, u64, i32, i32, u64, vp, vp]
         L.or_bench_grid2d.restype = i32
+        L.or_bench_count1d.argtypes = [vp, u64, i32, u64, i32, vp, vp]
+        L.or_bench_count1d.restype = i32
         L.or_bench_groupby_i32.argtypes = [vp, vp, u64, i32, i32, u64, ctypes.c_int64, vp, vp, vp]
         L.or_bench_groupby_i32.restype = ctypes.c_int64
         _lib = L
@@ -295,6 +297,20 @@ def nunique_grid(binners, data, mask=None, selection=False, dropmissing=False, d
     if dropnan:
         out = out - nans
     return _fortran_view(out.astype(np.int64), shape)
+
+
+def var_grid(binners, data, mask=None, n=None):
+    """AggregatorDescriptorVar (agg.py:196-224): the expression is cast to float64
+    (``expression.astype('float64')``, :197-198), then _sum_moment(2), sum and count of
+    the cast values on the same binners; finish = sum_moment/count - (sum/count)**2
+    (0/0 -> nan, divide and invalid ignored)."""
+    x = np.asarray(data).astype(np.float64)
+    sm = compute_grid(binners, "sum_moment", data=x, mask=mask, n=n, moment=2)
+    s = compute_grid(binners, "sum", data=x, mask=mask, n=n)
+    c = compute_grid(binners, "count", data=x, mask=mask, n=n)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        mean = s / c
+        return np.asarray(sm, dtype=np.float64) / c - mean ** 2
 
 
 def extract_central_part(ar):

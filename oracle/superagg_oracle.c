@@ -729,6 +729,88 @@ int or_bench_grid2d(const double *x, const double *y, const double *w, uint64_t 
     return used;
 }
 
+/* C1 (BASELINE configs[0]): df.count(binby='x', shape=bins) on float64 rows with
+ * limits=None, as ExecutorLocal runs it: the limits pre-pass (DataFrame.minmax ->
+ * TaskStatistic OP_MIN_MAX, per-chunk vaexfast statisticNd<op_min_max> on T threads,
+ * nanmin/nanmax reduce; dataframe.py:1276-1333, vaexfast.cpp:1043-1055, tasks.py:173-185),
+ * then the count pass into one private 1-d grid per thread (a 259-cell part is < 1e5
+ * bytes, so ideal_splits = T, cpu.py:487-499), chunk = min(1 Mi, max(1024, ceil(n/T)))
+ * (execution.py:149-156), serial reduce.  do_minmax = 0 takes lim[] as given. */
+int or_bench_count1d(const double *x, uint64_t n, int nthreads, uint64_t bins, int do_minmax, double *lim,
+                     int64_t *count_out) {
+    uint64_t chunk = (n + nthreads - 1) / nthreads;
+    if (chunk < 1024) chunk = 1024;
+    if (chunk > (1u << 20)) chunk = 1u << 20;
+    const uint64_t nchunks = (n + chunk - 1) / chunk;
+    if (do_minmax) {
+        double *los = (double *)malloc(sizeof(double) * nthreads), *his = (double *)malloc(sizeof(double) * nthreads);
+        for (int t = 0; t < nthreads; t++) {
+            los[t] = INFINITY;
+            his[t] = -INFINITY;
+        }
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+        for (uint64_t c = 0; c < nchunks; c++) {
+#ifdef _OPENMP
+            int t = omp_get_thread_num();
+#else
+            int t = 0;
+#endif
+            uint64_t i1 = c * chunk, i2 = i1 + chunk < n ? i1 + chunk : n;
+            double lo = los[t], hi = his[t];
+            for (uint64_t i = i1; i < i2; i++) {
+                double v = x[i];
+                if (v < lo) lo = v;  /* NaN fails both compares */
+                if (v > hi) hi = v;
+            }
+            los[t] = lo;
+            his[t] = hi;
+        }
+        double lo = INFINITY, hi = -INFINITY;
+        for (int t = 0; t < nthreads; t++) {
+            if (los[t] < lo) lo = los[t];
+            if (his[t] > hi) hi = his[t];
+        }
+        lim[0] = lo;
+        lim[1] = hi;
+        free(los);
+        free(his);
+    }
+    const uint64_t shape = bins + 3;
+    int64_t *grids = (int64_t *)calloc(shape * (uint64_t)nthreads, sizeof(int64_t));
+    const double vmin = lim[0], scale = 1. / (lim[1] - lim[0]);
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+    for (uint64_t c = 0; c < nchunks; c++) {
+#ifdef _OPENMP
+        int t = omp_get_thread_num();
+#else
+        int t = 0;
+#endif
+        int64_t *g = grids + shape * (uint64_t)t;
+        uint64_t i1 = c * chunk, i2 = i1 + chunk < n ? i1 + chunk : n;
+        uint64_t idx[1024];
+        for (uint64_t b = i1; b < i2; b += 1024) {
+            uint64_t len = i2 - b < 1024 ? i2 - b : 1024;
+            for (uint64_t i = 0; i < len; i++) {
+                double s = (x[b + i] - vmin) * scale;
+                uint64_t ix;
+                if (s != s) ix = 0;
+                else if (s < 0) ix = 1;
+                else if (s >= 1) ix = bins + 2;
+                else ix = (uint64_t)((int)(s * (double)bins) + 2);
+                idx[i] = ix;
+            }
+            for (uint64_t i = 0; i < len; i++) g[idx[i]] += 1;
+        }
+    }
+    for (uint64_t i = 0; i < shape; i++) {
+        int64_t c = 0;
+        for (int t = 0; t < nthreads; t++) c += grids[shape * (uint64_t)t + i];
+        count_out[i] = c;
+    }
+    free(grids);
+    return nthreads;
+}
+
 /* groupby(int32 key).agg({v: [sum, count]}) as the reference runs it
  * (groupby.py:97-168, cpu.py:147-195): pass 1 builds ordered_set with
  * nmaps = 7*T maps under per-map locks (hash_primitives.hpp:96-247), pass 2

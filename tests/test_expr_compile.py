@@ -38,6 +38,8 @@ def _run(prog, df):
                 st.append(g(c.astype(np.float64)) if c.dtype.kind == "f" else h(c.astype(np.int64)))
             elif op == "CONST":
                 st.append(np.full(n, prog.consts[arg], np.uint64))
+            elif op == "F2I":
+                st.append(h(f(st.pop()).astype(np.int64)))
             elif op in ("I2F", "U2F"):
                 st.append(g(i(st.pop()).astype(np.float64) if op == "I2F" else st.pop().astype(np.float64)))
             elif op == "ROUND_F32":
@@ -90,6 +92,8 @@ EXPRESSIONS = [
     "where(x > 0, x, -x)", "i8 + i8", "i8 * 3", "f * 2.5 + f", "i32 / 2", "x // 0.7", "x % -1.3",
     "minimum(x, y)", "u8 + 1", "i << 2", "x ** 3 - x ** 0.5", "b & (i > 3)", "f + i8", "f + i32", "i32 + i8",
     "np.floor(x) + 1", "isnan(log(x))", "u8 > 200", "i == 3", "b | ~b", "x + 1 - 1", "where(b, i8, i32)",
+    "astype(i32, 'float64')", "astype(i, 'float64') ** 2", "astype(x * 100, 'int32')", "astype(i32, 'int8')",
+    "astype(f, 'float64') + x", "astype(x, 'float32')", "astype(u8, 'int16') - 300", "astype(x, 'float64')",
 ]
 
 
@@ -97,7 +101,8 @@ EXPRESSIONS = [
 def test_program_matches_numpy(e):
     df = _frame()
     prog = expr.compile_expression(df, e)
-    ns = dict(np=np, sqrt=np.sqrt, abs=np.abs, where=np.where, minimum=np.minimum, isnan=np.isnan, log=np.log)
+    ns = dict(np=np, sqrt=np.sqrt, abs=np.abs, where=np.where, minimum=np.minimum, isnan=np.isnan, log=np.log,
+              astype=lambda a, d: np.asarray(a).astype(d))
     ns.update({k: np.asarray(v) for k, v in df.columns.items()})
     with np.errstate(all="ignore"):
         expected = np.asarray(eval(e, {"__builtins__": {}}, ns))  # noqa: S307

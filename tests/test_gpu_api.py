@@ -180,3 +180,32 @@ def test_categorical_groupby():
     dfg = df.groupby(by="g", agg="count")
     assert dfg.g.tolist() == ["cat", "dog", "snake"]
     assert dfg["count"].tolist() == [4, 4, 2]
+
+
+@pytest.mark.parametrize("dtype,lo,hi", [("int64", 3_500_000_000, 5_000_000_000),
+                                         ("int32", -2 ** 31, 2 ** 31 - 1),
+                                         ("int8", -128, 127), ("float32", -1e3, 1e3)])
+@pytest.mark.parametrize("hbm", [False, True])
+def test_var_std_cast_to_float64(dtype, lo, hi, hbm):
+    """agg.py:196-224: var/std take the moments of astype(x, 'float64').  Integer squares
+    here overflow int64 (int64 >= 3.04e9, int32 near 2^31), so an integer moment grid would
+    wrap; the result must equal the oracle's float64 restatement within 1e-6."""
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(11)
+    n = 200_000
+    g = rng.normal(size=n)
+    if dtype.startswith("float"):
+        v = rng.uniform(lo, hi, n).astype(dtype)
+    else:
+        v = rng.integers(lo, hi, n, endpoint=True, dtype=np.int64).astype(dtype)
+    cols = dict(g=g, v=v)
+    df = vx().from_arrays(**({k: DeviceArray.from_numpy(a) for k, a in cols.items()} if hbm else cols))
+    spec = oracle.Binner("scalar", g, vmin=-3, vmax=3, bins=16)
+    exp = oracle.extract_central_part(oracle.var_grid([spec], v))
+    got = df.var("v", binby="g", limits=[-3, 3], shape=16)
+    assert got.dtype == np.float64
+    np.testing.assert_allclose(got, exp, rtol=1e-6)
+    np.testing.assert_allclose(df.std("v", binby="g", limits=[-3, 3], shape=16), exp ** 0.5, rtol=1e-6)
+    # no binby: one cell (the whole column)
+    whole = oracle.var_grid([], v, n=n)
+    np.testing.assert_allclose(df.var("v"), whole, rtol=1e-6)

@@ -245,3 +245,40 @@ def test_small_grid_shared_plain_counts():
     np.add.at(s2, inv, v2.astype(np.int64))
     np.testing.assert_allclose(res["m1"].to_numpy(), s1 / cnt, rtol=1e-12)
     np.testing.assert_allclose(res["m2"].to_numpy(), s2 / cnt, rtol=1e-12)
+
+
+def test_small_grid_wide_cells_beyond_fused_budget():
+    """grids of 6145..12288 cells whose count / sum need 8-byte LDS cells
+    exceed the fused pass's 48 KB budget on their own; they must take the per-aggregator
+    LDS path (the host loop once stopped advancing there).  Two int8 keys (~10^4 cells) with
+    sums of int32 / float32 / float64 and a count of an int column, and a 100x100 binby
+    sum of float32; exact (integers) / 1e-6 (floats) against numpy."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(80)
+    n = 1_200_011
+    k1 = rng.integers(5, 105, n).astype(np.int8)
+    k2 = rng.integers(-50, 50, n).astype(np.int8)
+    i32 = rng.integers(-2 ** 31, 2 ** 31 - 1, n, dtype=np.int64).astype(np.int32)
+    f32 = rng.normal(size=n).astype(np.float32)
+    f64 = rng.normal(size=n)
+    cols = dict(k1=k1, k2=k2, i32=i32, f32=f32, f64=f64)
+    df = vaex_amd.from_arrays(**{c: DeviceArray.from_numpy(a) for c, a in cols.items()})
+    res = df.groupby(["k1", "k2"], sort=True).agg({"si": vaex_amd.agg.sum("i32"), "sf": vaex_amd.agg.sum("f32"),
+                                                   "sd": vaex_amd.agg.sum("f64"), "ci": vaex_amd.agg.count("i32")})
+    tup = np.stack([k1.astype(np.int64), k2.astype(np.int64)], axis=1)
+    uniq, inv = np.unique(tup, axis=0, return_inverse=True)
+    inv = inv.ravel()
+    si = np.zeros(len(uniq), np.int64)
+    np.add.at(si, inv, i32.astype(np.int64))
+    np.testing.assert_array_equal(res["si"].to_numpy(), si)
+    np.testing.assert_array_equal(res["ci"].to_numpy(), np.bincount(inv))
+    np.testing.assert_allclose(res["sf"].to_numpy(), np.bincount(inv, weights=f32.astype(np.float64)), rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(res["sd"].to_numpy(), np.bincount(inv, weights=f64), rtol=1e-6, atol=1e-9)
+    x, y = rng.normal(size=n), rng.normal(size=n)
+    df2 = vaex_amd.from_arrays(x=DeviceArray.from_numpy(x), y=DeviceArray.from_numpy(y), f32=DeviceArray.from_numpy(f32))
+    got = df2.sum("f32", binby=["x", "y"], limits=[[-3, 3], [-3, 3]], shape=100)
+    bx = oracle.Binner("scalar", x, vmin=-3, vmax=3, bins=100)
+    by = oracle.Binner("scalar", y, vmin=-3, vmax=3, bins=100)
+    exp = oracle.extract_central_part(oracle.compute_grid([bx, by], "sum", data=f32))
+    np.testing.assert_allclose(got, exp, rtol=1e-6, atol=1e-6)

@@ -42,3 +42,33 @@ def test_groupby_from_mapped_file(tmp_path):
     np.testing.assert_array_equal(g["key"].to_numpy()[order], uk)
     np.testing.assert_array_equal(g["n"].to_numpy()[order], c)
     np.testing.assert_allclose(g["s"].to_numpy()[order], s, rtol=1e-6, atol=1e-9)
+
+
+def test_c4_mean_1024_from_mapped_file(tmp_path, monkeypatch):
+    """C4's query shape (BASELINE configs[3]) on one GPU: mean(w, binby=[x, y], shape=1024)
+    over a memory-mapped vaex HDF5 file, streamed through three 16 Mi-row staging chunks of
+    the double-buffered pipeline in one bin() call (so buffer reuse is exercised), equal to
+    the oracle's sum / count (agg.py:158-188)."""
+    import vaex_amd
+    from vaex_amd import execution
+    monkeypatch.setattr(execution, "CHUNK_SIZE_HOST", 1 << 26)  # one host chunk -> 3 pipe chunks
+    rng = np.random.default_rng(13)
+    n = (1 << 25) + 12345
+    cols = {"x": rng.normal(size=n), "y": rng.normal(size=n), "w": rng.random(n)}
+    cols["w"][::1009] = np.nan
+    path = tmp_path / "c4.hdf5"
+    vaex_amd.from_arrays(**cols).export_hdf5(path)
+    del cols
+    df = vaex_amd.open(path)
+    x, y, w = (np.asarray(df.columns[c]) for c in ("x", "y", "w"))
+    lim = [[-4, 4], [-4, 4]]
+    got = df.mean("w", binby=["x", "y"], limits=lim, shape=1024)
+    bx = oracle.Binner("scalar", x, vmin=-4, vmax=4, bins=1024)
+    by = oracle.Binner("scalar", y, vmin=-4, vmax=4, bins=1024)
+    s = oracle.extract_central_part(oracle.compute_grid([bx, by], "sum", data=w))
+    c = oracle.extract_central_part(oracle.compute_grid([bx, by], "count", data=w))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        exp = s / c
+    assert got.shape == (1024, 1024)
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(exp))
+    np.testing.assert_allclose(got, exp, rtol=1e-6, atol=1e-12)

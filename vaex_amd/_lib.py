@@ -86,6 +86,15 @@ SIGNATURES = {
     "vh_combine_keys": (_i32, [_u64, _i32, _p(_vp), _p(_i32), _p(_i64), _p(_i64), _vp]),
     "vh_dense_rank_i64": (_i32, [_u64, _vp, _vp, _vp, _p(_u64)]),
     "vh_decode_keys": (_i32, [_u64, _vp, _vp, _i32, _p(_i64), _p(_i64), _p(_i64), _p(_i32), _p(_vp)]),
+    "vh_comm_unique_id": (_i32, [_vp]),
+    "vh_comm_init": (_i32, [_vp, _i32, _i32, _p(_vp)]),
+    "vh_comm_destroy": (_i32, [_vp]),
+    "vh_comm_allreduce": (_i32, [_vp, _vp, _u64, _i32, _i32, _i32]),
+    "vh_comm_allgather": (_i32, [_vp, _vp, _vp, _u64, _i32]),
+    "vh_comm_alltoallv": (_i32, [_vp, _vp, _p(_u64), _vp, _p(_u64), _i32]),
+    "vh_comm_barrier": (_i32, [_vp]),
+    "vh_comm_agg_allreduce": (_i32, [_vp, _vp]),
+    "vh_hashagg_exchange": (_i32, [_vp, _vp, _i32]),
     "vh_expr_eval": (_i32, [_p(ctypes.c_uint32), _i32, _p(_u64), _i32, _p(_vp), _p(_i32), _i32, _u64, _i32, _vp]),
 }
 

@@ -188,9 +188,15 @@ class AggregatorDescriptorVar(AggregatorDescriptorMulti):
 
     def add_tasks(self, df, binners):
         from .promise import delayed
-        sum_moment = _sum_moment(self.expression, 2, selection=self.selection, edges=self.edges)
-        sum_ = sum(self.expression, selection=self.selection, edges=self.edges)
-        count_ = count(self.expression, selection=self.selection, edges=self.edges)
+        # agg.py:196-201: the moments are taken of the expression cast to float64, so
+        # integer squares neither wrap nor accumulate in an int64 grid (a float64 column
+        # is its own cast: the same values, no extra device pass)
+        expression = str(self.expression)
+        if df.data_type(expression) != np.dtype("float64"):
+            expression = str(df[expression].astype("float64"))
+        sum_moment = _sum_moment(expression, 2, selection=self.selection, edges=self.edges)
+        sum_ = sum(expression, selection=self.selection, edges=self.edges)
+        count_ = count(expression, selection=self.selection, edges=self.edges)
         task_sum_moment = sum_moment.add_tasks(df, binners)[0][0]
         task_sum = sum_.add_tasks(df, binners)[0][0]
         task_count = count_.add_tasks(df, binners)[0][0]

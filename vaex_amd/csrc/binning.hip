@@ -15,6 +15,7 @@
 // in place.
 #include <limits>
 #include <memory>
+#include <mutex>
 
 #include "common.hpp"
 #include "engine.hpp"
@@ -39,12 +40,6 @@ struct vh_binner {
     uint64_t shape() const { return (kind == 0 ? bins : ordinal_count) + 3; }
 };
 
-struct vh_grid {
-    std::vector<vh_binner *> binners;
-    std::vector<uint64_t> shapes, strides;
-    uint64_t length1d = 1;
-    Workspace ws;
-};
 
 
 namespace vh {
@@ -1021,6 +1016,7 @@ int vh_agg_info(const vh_agg *a, uint64_t *bytes, int *grid_dtype, uint64_t *ite
 
 int vh_agg_download(vh_agg *a, void *host, uint64_t bytes) {
     VH_API_BEGIN
+    std::lock_guard<std::mutex> lk(a->grid->mu);
     if (bytes != a->grid->length1d * a->grid_isz) fail(VH_ERR_ARG, "download size mismatch");
     nunique_finalize(a);
     VH_HIP(hipMemcpyAsync(host, a->g.ptr, bytes, hipMemcpyDeviceToHost, stream()));
@@ -1030,6 +1026,7 @@ int vh_agg_download(vh_agg *a, void *host, uint64_t bytes) {
 
 int vh_agg_download_order(vh_agg *a, void *host, uint64_t bytes) {
     VH_API_BEGIN
+    std::lock_guard<std::mutex> lk(a->grid->mu);
     if (a->kind != VH_AGG_FIRST) fail(VH_ERR_ARG, "not an AggFirst");
     if (bytes != a->grid->length1d * a->grid_isz) fail(VH_ERR_ARG, "download size mismatch");
     VH_HIP(hipMemcpyAsync(host, a->g2.ptr, bytes, hipMemcpyDeviceToHost, stream()));
@@ -1039,6 +1036,7 @@ int vh_agg_download_order(vh_agg *a, void *host, uint64_t bytes) {
 
 int vh_agg_upload_order(vh_agg *a, const void *host, uint64_t bytes) {
     VH_API_BEGIN
+    std::lock_guard<std::mutex> lk(a->grid->mu);
     if (a->kind != VH_AGG_FIRST) fail(VH_ERR_ARG, "not an AggFirst");
     if (bytes != a->grid->length1d * a->grid_isz) fail(VH_ERR_ARG, "upload size mismatch");
     VH_HIP(hipMemcpyAsync(a->g2.ptr, host, bytes, hipMemcpyHostToDevice, stream()));
@@ -1048,6 +1046,7 @@ int vh_agg_upload_order(vh_agg *a, const void *host, uint64_t bytes) {
 
 int vh_agg_upload(vh_agg *a, const void *host, uint64_t bytes) {
     VH_API_BEGIN
+    std::lock_guard<std::mutex> lk(a->grid->mu);
     if (bytes != a->grid->length1d * a->grid_isz) fail(VH_ERR_ARG, "upload size mismatch");
     if (a->kind == VH_AGG_NUNIQUE) return VH_OK;  // a derived grid (recomputed when read)
     VH_HIP(hipMemcpyAsync(a->g.ptr, host, bytes, hipMemcpyHostToDevice, stream()));
@@ -1057,6 +1056,7 @@ int vh_agg_upload(vh_agg *a, const void *host, uint64_t bytes) {
 
 int vh_agg_device_ptr(vh_agg *a, void **grid_dptr, void **grid2_dptr) {
     VH_API_BEGIN
+    std::lock_guard<std::mutex> lk(a->grid->mu);
     nunique_finalize(a);
     if (grid_dptr) *grid_dptr = a->g.ptr;
     if (grid2_dptr) *grid2_dptr = a->g2.ptr;
@@ -1065,6 +1065,7 @@ int vh_agg_device_ptr(vh_agg *a, void **grid_dptr, void **grid2_dptr) {
 
 int vh_agg_reduce(vh_agg *a, vh_agg *const *others, int nothers) {
     VH_API_BEGIN
+    std::lock_guard<std::mutex> lk(a->grid->mu);
     const uint64_t L = a->grid->length1d;
     for (int k = 0; k < nothers; k++) {
         vh_agg *o = others[k];
@@ -1106,6 +1107,7 @@ int vh_agg_reduce(vh_agg *a, vh_agg *const *others, int nothers) {
 
 int vh_grid_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length, int has_length) {
     VH_API_BEGIN
+    std::lock_guard<std::mutex> lk(g->mu);
     if (!has_length) {
         if (g->binners.empty()) fail(VH_ERR_RUNTIME, "no binners set and no length given");
         if (!g->binners[0]->data.set) fail(VH_ERR_RUNTIME, "data not set");
@@ -1371,7 +1373,8 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                     };
                     int first_plain = -1;
                     // rows one workgroup adds into its sub-grids (bounds 32-bit partials)
-                    const uint64_t rows_wg = (len + (uint64_t)blocks_for(len, 256, 8) - 1) / blocks_for(len, 256, 8) + 256 * SF_U;
+                    const dim3 sf_grid(blocks_for(len, 256, 8)), sf_block(256);
+                    const uint64_t rows_wg = rows_per_wg(len, sf_grid.x, sf_block.x, SF_U);
                     auto narrow_ok = [&](const AggDev &a) {
                         if (a.kind == VH_AGG_COUNT) return rows_wg < (1ull << 32);
                         if (a.flip) return false;
@@ -1399,10 +1402,16 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                         off += (bytes + 15) & ~uint64_t(15);
                         j++;
                     }
+                    if (j == i) {
+                        // the first candidate alone exceeds the fused pass's budget: it takes
+                        // the per-aggregator LDS path below
+                        i++;
+                        continue;
+                    }
                     if (sa.na >= 2) {
                         make_cells();
                         TimedScope ts("bin_aggregate_lds");
-                        hipLaunchKernelGGL(k_small_fused, dim3(blocks_for(len, 256, 8)), dim3(256), (size_t)off, stream(), sa,
+                        hipLaunchKernelGGL(k_small_fused, sf_grid, sf_block, (size_t)off, stream(), sa,
                                            cells, len, L, (uint32_t)(off / 4));
                         VH_HIP(hipGetLastError());
                         for (size_t q = i; q < j; q++) done[pend[q]] = 1;
@@ -1414,29 +1423,14 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                 AggDev &ad = ads[k];
                 if (done[k]) continue;
                 if (lds_ok(ad.kind) && cells_ok) {
-                    if (!cells) {
-                        TimedScope ts("bin_cells");
-                        g->ws.cells.ensure(std::max<uint64_t>(len, 1) * 2);
-                        cells = g->ws.cells.as<uint16_t>();
-                        const dim3 cg(blocks_for(len, 256, 8)), cb(256);
-                        for (int d = 0; d < plan.nb; d++) {
-                            const BinnerDev &b = plan.b[d];
-                            const int first = d == 0 ? 1 : 0;
-                            if (b.kind == 0) {
-                                VH_DISPATCH_DTYPE(b.dtype, T, hipLaunchKernelGGL((k_cells_dim<0, T>), cg, cb, 0, stream(), b, len, cells, first));
-                            } else {
-                                VH_DISPATCH_DTYPE(b.dtype, T, hipLaunchKernelGGL((k_cells_dim<1, T>), cg, cb, 0, stream(), b, len, cells, first));
-                            }
-                            VH_HIP(hipGetLastError());
-                        }
-                    }
+                    make_cells();
                     TimedScope ts("bin_aggregate_lds");
                     dim3 grd(blocks_for(len, 256, 8)), blk(256);
                     const size_t shm = (size_t)((L * 8 + 15) & ~uint64_t(15));
                     const size_t shm32 = (size_t)((L * 4 + 15) & ~uint64_t(15));
                     const bool mx = ad.kind == VH_AGG_MAX;
                     // rows one workgroup adds into its sub-grid (bounds 32-bit partials)
-                    const uint64_t rows_wg = (len + (uint64_t)grd.x - 1) / grd.x + 256 * CELL_U;
+                    const uint64_t rows_wg = rows_per_wg(len, grd.x, blk.x, CELL_U);
                     const bool narrow_sum = !ad.flip && (((ad.dtype == VH_I8 || ad.dtype == VH_U8) && rows_wg < (1ull << 23)) ||
                                                          ((ad.dtype == VH_I16 || ad.dtype == VH_U16) && rows_wg < (1ull << 15)));
                     switch (ad.kind) {

@@ -159,6 +159,13 @@ inline unsigned blocks_for(uint64_t n, unsigned threads, unsigned per_cu = 8) {
     return (unsigned)b;
 }
 
+// upper bound on the rows one workgroup of a grid-stride kernel visits: launched with
+// `blocks` workgroups of `threads` lanes, each lane taking `unroll` rows per step (bounds
+// narrow per-workgroup partial sums; derive `blocks` from the launch's own dim3)
+inline uint64_t rows_per_wg(uint64_t n, unsigned blocks, unsigned threads, unsigned unroll) {
+    return (n + blocks - 1) / blocks + (uint64_t)threads * unroll;
+}
+
 // kernel timing (hipEvents around named launches on the library stream)
 struct TimedScope {
     const char *name;

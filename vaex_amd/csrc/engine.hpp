@@ -1,6 +1,7 @@
 // Internal structures of the binning engine shared by binning.hip and tiled.hip.
 #pragma once
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "common.hpp"
@@ -112,6 +113,17 @@ void launch_fused(const BinPlan &plan, FusedAggs &fa, uint64_t n, uint64_t cells
 bool try_tiled(const BinPlan &plan, const FusedAggs &fa, uint64_t n, uint64_t cells, int nd_f64, Workspace &ws);
 
 }  // namespace vh
+
+struct vh_grid {
+    // one TaskPart uses a grid at a time (execution.py:358-375), but a C caller may bin
+    // different grids -- or, by mistake, the same one -- from several threads: bin and
+    // reduce hold the grid's lock (grids of different parts run concurrently)
+    std::mutex mu;
+    std::vector<vh_binner *> binners;
+    std::vector<uint64_t> shapes, strides;
+    uint64_t length1d = 1;
+    vh::Workspace ws;
+};
 
 struct vh_agg {
     vh_grid *grid = nullptr;

@@ -51,6 +51,7 @@
 #include <mutex>
 #include <type_traits>
 
+#include "comm.hpp"
 #include "common.hpp"
 #include "hashset.hpp"
 
@@ -920,6 +921,8 @@ struct vh_hashagg {
     uint64_t slots = 0;  // HBM table slots (power of two), 0 = not allocated
     DevBuf tab;          // keys | cnt | sum[nv] | nn[nv] (slots + 1 each) | used, err
     DevBuf out;
+    DevBuf xres;            // groups after a cross-rank exchange (vh_hashagg_exchange)
+    const char *res = nullptr;  // result columns: key | count | sum[nv] | nonnull[nv], ngroups each
     uint64_t ngroups = 0;
     bool finished = false;
     uint64_t rows = 0;
@@ -1374,6 +1377,7 @@ int vh_hashagg_finish(vh_hashagg *h, uint64_t *ngroups) {
                     });
                 });
                 VH_HIP(hipGetLastError());
+                h->res = outp;
             }
         }
     }
@@ -1388,8 +1392,7 @@ int vh_hashagg_read(vh_hashagg *h, int64_t *keys, int64_t *counts, void *const *
     if (!h->finished) fail(VH_ERR_RUNTIME, "hashagg: read before finish");
     const uint64_t m = h->ngroups;
     if (!m) return VH_OK;
-    const char *outp = out_results(h, m, sort_tmp_bytes(key_bits_size(h->key_dtype), m));
-    const int64_t *okey = reinterpret_cast<const int64_t *>(outp);
+    const int64_t *okey = reinterpret_cast<const int64_t *>(h->res);
     const int64_t *ocnt = okey + m;
     const uint64_t *osum = reinterpret_cast<const uint64_t *>(ocnt + m);
     const int64_t *onn = reinterpret_cast<const int64_t *>(osum + m * h->nv);
@@ -1547,6 +1550,244 @@ int vh_dense_rank_i64(uint64_t n, const int64_t *keys, int32_t *rank, int64_t *d
     VH_HIP(hipMemcpyAsync(&last, scan.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, st));
     VH_HIP(hipStreamSynchronize(st));
     *m = last;
+    VH_API_END
+}
+
+}  // extern "C"
+
+// ---- groupby results across ranks: hash-partition exchange on the device ------------------
+// Every rank holds its shard's groups (key-sorted, vh_hashagg_finish).  Each group row
+// [key, count, sum_v.., nonnull_v..] goes to owner splitmix64(key bits) % world
+// (vaex_amd/distributed.py group_owner) in one RCCL all-to-all; the owner sorts what it
+// received by key (stable: senders stay in rank order) and folds each run of equal keys
+// in that order, so float sums add exactly as a merge of the ranks' parts in rank order
+// would (superagg.cpp:354-361 reduce in part order).  With `gather` the owners' disjoint
+// results are all-gathered and sorted again, so every rank holds the whole result.
+namespace vh {
+
+__host__ __device__ inline uint64_t xo_mix(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+constexpr int XO_MAX_WORLD = 64;
+
+__global__ __launch_bounds__(256) void k_xo_owner(const int64_t *okey, uint64_t m, int world, uint32_t *owner,
+                                                  uint32_t *idx, unsigned long long *hist) {
+    __shared__ uint32_t h[XO_MAX_WORLD];
+    if (threadIdx.x < XO_MAX_WORLD) h[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) {
+        const uint32_t o = (uint32_t)(xo_mix((uint64_t)okey[j]) % (uint64_t)world);
+        owner[j] = o;
+        idx[j] = (uint32_t)j;
+        atomicAdd(&h[o], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)world && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+}
+
+// row j of the send buffer <- group sidx[j] (rows of one destination keep key order)
+__global__ __launch_bounds__(256) void k_xo_pack(const char *res, uint64_t m, int nv, const uint32_t *sidx, uint64_t *rows) {
+    const int R = 2 + 2 * nv;
+    const uint64_t *col = reinterpret_cast<const uint64_t *>(res);
+    for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) {
+        const uint64_t i = sidx[j];
+        for (int c = 0; c < R; c++) rows[j * R + c] = col[(uint64_t)c * m + i];
+    }
+}
+
+// sortable key bits of received row j (signed keys: sign bit flipped) + its index
+__global__ __launch_bounds__(256) void k_xo_keys(const uint64_t *rows, uint64_t M, int R, int is_signed, uint64_t *skey,
+                                                 uint32_t *idx) {
+    for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < M; j += (uint64_t)gridDim.x * 256) {
+        const uint64_t k = rows[j * R];
+        skey[j] = is_signed ? (k ^ 0x8000000000000000ULL) : k;
+        idx[j] = (uint32_t)j;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_xo_heads(const uint64_t *skey, uint64_t M, uint32_t *flag) {
+    for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < M; j += (uint64_t)gridDim.x * 256)
+        flag[j] = (j == 0 || skey[j] != skey[j - 1]) ? 1u : 0u;
+}
+
+// one output group per run of equal keys, folded in sorted (= rank) order
+__global__ __launch_bounds__(256) void k_xo_runs(const uint64_t *rows, const uint32_t *sidx, const uint32_t *flag,
+                                                 const uint32_t *scan, uint64_t M, int nv, uint32_t vfloat,
+                                                 uint64_t m_out, uint64_t *out) {
+    const int R = 2 + 2 * nv;
+    for (uint64_t p = blockIdx.x * 256ull + threadIdx.x; p < M; p += (uint64_t)gridDim.x * 256) {
+        if (!flag[p]) continue;
+        const uint64_t g = scan[p] - 1u;
+        const uint64_t *r0 = rows + (uint64_t)sidx[p] * R;
+        uint64_t acc[2 + 2 * HA_MAX_V];
+        for (int c = 0; c < R; c++) acc[c] = r0[c];
+        for (uint64_t q = p + 1; q < M && !flag[q]; q++) {
+            const uint64_t *r = rows + (uint64_t)sidx[q] * R;
+            acc[1] += r[1];
+            for (int v = 0; v < nv; v++) {
+                if ((vfloat >> v) & 1)
+                    acc[2 + v] = __builtin_bit_cast(uint64_t, __builtin_bit_cast(double, acc[2 + v]) +
+                                                                  __builtin_bit_cast(double, r[2 + v]));
+                else
+                    acc[2 + v] += r[2 + v];
+                acc[2 + nv + v] += r[2 + nv + v];
+            }
+        }
+        for (int c = 0; c < R; c++) out[(uint64_t)c * m_out + g] = acc[c];
+    }
+}
+
+// fold M packed rows (any order within a key: stable sort keeps the given order) into
+// key-sorted result columns in h->xres; returns the number of groups
+static uint64_t xo_fold(vh_hashagg *h, const uint64_t *rows, uint64_t M) {
+    hipStream_t st = stream();
+    const int R = 2 + 2 * h->nv;
+    if (!M) {
+        h->xres.ensure(8);
+        h->res = h->xres.as<char>();
+        return 0;
+    }
+    if (M >= (1ull << 32)) fail(VH_ERR_RUNTIME, "hashagg exchange: too many group rows");
+    DevBuf skey, skey2, idx, sidx, flag, scan, tmp;
+    skey.ensure(8 * M);
+    skey2.ensure(8 * M);
+    idx.ensure(4 * M);
+    sidx.ensure(4 * M);
+    flag.ensure(4 * M);
+    scan.ensure(4 * M);
+    size_t t1 = 0, t2 = 0;
+    VH_HIP(rocprim::radix_sort_pairs(nullptr, t1, (uint64_t *)nullptr, (uint64_t *)nullptr, (uint32_t *)nullptr,
+                                     (uint32_t *)nullptr, (size_t)M, 0, 64, st));
+    VH_HIP(rocprim::inclusive_scan(nullptr, t2, (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)M,
+                                   rocprim::plus<uint32_t>(), st));
+    tmp.ensure(std::max<size_t>(std::max(t1, t2), 16));
+    const unsigned g = blocks_for(M, 256, 8);
+    hipLaunchKernelGGL(k_xo_keys, dim3(g), dim3(256), 0, st, rows, M, R, key_signed(h->key_dtype), skey.as<uint64_t>(),
+                       idx.as<uint32_t>());
+    size_t tb = tmp.bytes;
+    VH_HIP(rocprim::radix_sort_pairs(tmp.ptr, tb, skey.as<uint64_t>(), skey2.as<uint64_t>(), idx.as<uint32_t>(),
+                                     sidx.as<uint32_t>(), (size_t)M, 0, 64, st));
+    hipLaunchKernelGGL(k_xo_heads, dim3(g), dim3(256), 0, st, skey2.as<uint64_t>(), M, flag.as<uint32_t>());
+    tb = tmp.bytes;
+    VH_HIP(rocprim::inclusive_scan(tmp.ptr, tb, flag.as<uint32_t>(), scan.as<uint32_t>(), (size_t)M,
+                                   rocprim::plus<uint32_t>(), st));
+    uint32_t mo = 0;
+    VH_HIP(hipMemcpyAsync(&mo, scan.as<uint32_t>() + (M - 1), 4, hipMemcpyDeviceToHost, st));
+    VH_HIP(hipStreamSynchronize(st));
+    DevBuf out;
+    out.ensure(8 * (uint64_t)mo * R + 8);
+    hipLaunchKernelGGL(k_xo_runs, dim3(g), dim3(256), 0, st, rows, sidx.as<uint32_t>(), flag.as<uint32_t>(),
+                       scan.as<uint32_t>(), M, h->nv, h->vfloat, (uint64_t)mo, out.as<uint64_t>());
+    VH_HIP(hipGetLastError());
+    VH_HIP(hipStreamSynchronize(st));
+    std::swap(h->xres.ptr, out.ptr);
+    std::swap(h->xres.bytes, out.bytes);
+    h->res = h->xres.as<char>();
+    return mo;
+}
+
+}  // namespace vh
+
+extern "C" {
+
+int vh_hashagg_exchange(vh_hashagg *h, vh_comm *c, int gather) {
+    VH_API_BEGIN
+    if (!h->finished) fail(VH_ERR_RUNTIME, "hashagg: exchange before finish");
+    std::lock_guard<std::mutex> lk(comm_mutex(c));
+    hipStream_t st = stream();
+    const int world = comm_world(c), me = comm_rank(c);
+    if (world > XO_MAX_WORLD) fail(VH_ERR_ARG, "hashagg exchange: at most 64 ranks");
+    const int R = 2 + 2 * h->nv;
+    const uint64_t m = h->ngroups;
+    // ---- owners, rows packed by destination
+    DevBuf owner, idx, sowner, sidx, tmp, hist, rows;
+    owner.ensure(4 * std::max<uint64_t>(m, 1));
+    idx.ensure(4 * std::max<uint64_t>(m, 1));
+    sowner.ensure(4 * std::max<uint64_t>(m, 1));
+    sidx.ensure(4 * std::max<uint64_t>(m, 1));
+    hist.ensure(8 * (uint64_t)world * world + 8);
+    rows.ensure(8 * (uint64_t)R * std::max<uint64_t>(m, 1));
+    unsigned long long *d_hist = hist.as<unsigned long long>();  // [world] mine | [world][world] all
+    VH_HIP(hipMemsetAsync(d_hist, 0, 8 * (uint64_t)world, st));
+    if (m) {
+        const unsigned g = blocks_for(m, 256, 8);
+        hipLaunchKernelGGL(k_xo_owner, dim3(g), dim3(256), 0, st, reinterpret_cast<const int64_t *>(h->res), m, world,
+                           owner.as<uint32_t>(), idx.as<uint32_t>(), d_hist);
+        int bits = 1;
+        while ((1 << bits) < world) bits++;
+        size_t tb = 0;
+        VH_HIP(rocprim::radix_sort_pairs(nullptr, tb, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                         (uint32_t *)nullptr, (size_t)m, 0, bits, st));
+        tmp.ensure(std::max<size_t>(tb, 16));
+        tb = tmp.bytes;
+        VH_HIP(rocprim::radix_sort_pairs(tmp.ptr, tb, owner.as<uint32_t>(), sowner.as<uint32_t>(), idx.as<uint32_t>(),
+                                         sidx.as<uint32_t>(), (size_t)m, 0, bits, st));
+        hipLaunchKernelGGL(k_xo_pack, dim3(g), dim3(256), 0, st, h->res, m, h->nv, sidx.as<uint32_t>(),
+                           rows.as<uint64_t>());
+        VH_HIP(hipGetLastError());
+    }
+    // ---- every rank's send counts, then the rows
+    comm_allgather_dev(c, d_hist, d_hist + world, 8 * (uint64_t)world);
+    std::vector<uint64_t> all((uint64_t)world * world);
+    VH_HIP(hipMemcpyAsync(all.data(), d_hist + world, 8 * all.size(), hipMemcpyDeviceToHost, st));
+    VH_HIP(hipStreamSynchronize(st));
+    std::vector<uint64_t> sb(world), rb(world);
+    uint64_t M = 0;
+    for (int r = 0; r < world; r++) {
+        sb[r] = all[(uint64_t)me * world + r] * 8 * R;
+        rb[r] = all[(uint64_t)r * world + me] * 8 * R;
+        M += all[(uint64_t)r * world + me];
+    }
+    DevBuf recv;
+    recv.ensure(8 * (uint64_t)R * std::max<uint64_t>(M, 1));
+    {
+        TimedScope ts("ha_exchange");
+        comm_alltoallv_dev(c, rows.ptr, sb.data(), recv.ptr, rb.data());
+    }
+    uint64_t mine = xo_fold(h, recv.as<uint64_t>(), M);
+    if (gather) {
+        // owners' disjoint results to every rank (padded all-gather), sorted once more
+        DevBuf cnt;
+        cnt.ensure(8 * (uint64_t)(world + 1));
+        VH_HIP(hipMemcpyAsync(cnt.as<uint64_t>(), &mine, 8, hipMemcpyHostToDevice, st));
+        comm_allgather_dev(c, cnt.as<uint64_t>(), cnt.as<uint64_t>() + 1, 8);
+        std::vector<uint64_t> sizes(world);
+        VH_HIP(hipMemcpyAsync(sizes.data(), cnt.as<uint64_t>() + 1, 8 * (uint64_t)world, hipMemcpyDeviceToHost, st));
+        VH_HIP(hipStreamSynchronize(st));
+        uint64_t top = 0, tot = 0;
+        for (auto v : sizes) {
+            top = std::max(top, v);
+            tot += v;
+        }
+        // my result as rows, padded to `top`
+        DevBuf mrows, allrows, packed;
+        mrows.ensure(8 * (uint64_t)R * std::max<uint64_t>(top, 1));
+        if (mine) {
+            DevBuf iota;
+            iota.ensure(4 * mine);
+            hipLaunchKernelGGL(k_dr_iota, dim3(blocks_for(mine, 256, 8)), dim3(256), 0, st, iota.as<uint32_t>(), mine);
+            hipLaunchKernelGGL(k_xo_pack, dim3(blocks_for(mine, 256, 8)), dim3(256), 0, st, h->res, mine, h->nv,
+                               iota.as<uint32_t>(), mrows.as<uint64_t>());
+            VH_HIP(hipStreamSynchronize(st));
+        }
+        allrows.ensure(8 * (uint64_t)R * std::max<uint64_t>(top, 1) * world);
+        comm_allgather_dev(c, mrows.ptr, allrows.ptr, 8 * (uint64_t)R * top);
+        packed.ensure(8 * (uint64_t)R * std::max<uint64_t>(tot, 1));
+        uint64_t at = 0;
+        for (int r = 0; r < world; r++) {
+            if (sizes[r])
+                VH_HIP(hipMemcpyAsync(packed.as<uint64_t>() + at * R, allrows.as<uint64_t>() + (uint64_t)r * top * R,
+                                      8 * (uint64_t)R * sizes[r], hipMemcpyDeviceToDevice, st));
+            at += sizes[r];
+        }
+        mine = xo_fold(h, packed.as<uint64_t>(), tot);
+    }
+    h->ngroups = mine;
+    VH_HIP(hipStreamSynchronize(st));
     VH_API_END
 }
 

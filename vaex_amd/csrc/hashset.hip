@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <limits>
 #include <memory>
+#include <mutex>
 #include <numeric>
 
 #include "common.hpp"
@@ -29,6 +30,12 @@ using namespace vh;
 enum { C_DISTINCT = 0, C_OVERFLOW, C_NAN_FIRST, C_NULL_FIRST, C_SPECIAL_FIRST, C_NAN_COUNT, C_NULL_COUNT, C_CURSOR, C_N };
 
 struct vh_set {
+    // ordered_set.update is called concurrently on ONE set by every worker thread of the
+    // reference (cpu.py:147-195; per-map mutexes, hash_primitives.hpp:242-247): every entry
+    // point holds this lock, so concurrent updates serialise whole (row numbering, staging
+    // buffers, counters and the table stay consistent; ordinals follow the order in which
+    // the calls ran, as the reference's follow its thread interleaving)
+    std::recursive_mutex mu;
     int dtype = VH_I64;
     uint64_t cap = 0;
     DevBuf tab, lut, ctr;
@@ -383,6 +390,7 @@ static void set_seal(vh_set *s) {
 }
 
 SetDev set_device_view(vh_set *s) {
+    std::lock_guard<std::recursive_mutex> lk(s->mu);
     set_seal(s);
     SetDev d{};
     d.lut = s->lut.as<uint64_t>();
@@ -506,6 +514,7 @@ static void set_update(vh_set *s, const void *keys, const uint8_t *mask, const u
 
 int vh_set_update(vh_set *s, const void *keys, const uint8_t *mask, uint64_t n, int loc) {
     VH_API_BEGIN
+    std::lock_guard<std::recursive_mutex> lk(s->mu);
     set_update(s, keys, mask, nullptr, n, loc);
     VH_API_END
 }
@@ -513,12 +522,14 @@ int vh_set_update(vh_set *s, const void *keys, const uint8_t *mask, uint64_t n, 
 int vh_set_update_selected(vh_set *s, const void *keys, const uint8_t *mask, const uint8_t *select, uint64_t n,
                            int loc) {
     VH_API_BEGIN
+    std::lock_guard<std::recursive_mutex> lk(s->mu);
     set_update(s, keys, mask, select, n, loc);
     VH_API_END
 }
 
 int vh_set_seal(vh_set *s) {
     VH_API_BEGIN
+    std::lock_guard<std::recursive_mutex> lk(s->mu);
     set_seal(s);
     VH_API_END
 }
@@ -526,6 +537,7 @@ int vh_set_seal(vh_set *s) {
 int vh_set_info(vh_set *s, int64_t *length, int64_t *nan_count, int64_t *null_count, int64_t *nan_value,
                 int64_t *null_value) {
     VH_API_BEGIN
+    std::lock_guard<std::recursive_mutex> lk(s->mu);
     set_seal(s);
     if (length) *length = s->length;
     if (nan_count) *nan_count = s->nan_count;
@@ -537,6 +549,7 @@ int vh_set_info(vh_set *s, int64_t *length, int64_t *nan_count, int64_t *null_co
 
 int vh_set_key_array(vh_set *s, void *out) {
     VH_API_BEGIN
+    std::lock_guard<std::recursive_mutex> lk(s->mu);
     set_seal(s);
     VH_DISPATCH_DTYPE(s->dtype, T, write_keys<T>(s, reinterpret_cast<T *>(out)));
     VH_API_END
@@ -544,6 +557,7 @@ int vh_set_key_array(vh_set *s, void *out) {
 
 int vh_set_map_ordinal(vh_set *s, const void *keys, uint64_t n, int loc, void *out, int out_itemsize, int out_loc) {
     VH_API_BEGIN
+    std::lock_guard<std::recursive_mutex> lk(s->mu);
     set_seal(s);
     if (out_itemsize != 1 && out_itemsize != 2 && out_itemsize != 4 && out_itemsize != 8)
         fail(VH_ERR_ARG, "out_itemsize must be 1, 2, 4 or 8");

@@ -113,6 +113,10 @@ class Expression:
     def __invert__(self): return Expression(self.df, f"(~{self.expression})")
     __hash__ = object.__hash__
 
+    def astype(self, data_type):
+        """expression.py ``Expression.astype``: the expression ``astype(x, 'dtype')``."""
+        return Expression(self.df, f"astype({self.expression}, {str(np.dtype(data_type))!r})")
+
     @property
     def dtype(self):
         return self.df.data_type(self.expression)
@@ -141,6 +145,11 @@ class Expression:
 def _ordinal_values(x, ordered_set):
     """functions.py:2441-2448 (host evaluation; the bin kernel fuses it instead)."""
     return ordered_set.map_ordinal(x)
+
+
+def _astype(x, data_type):
+    """functions.py ``astype`` on host chunks (numpy ``ndarray.astype``)."""
+    return np.asarray(x).astype(data_type) if not np.ma.isMaskedArray(x) else x.astype(data_type)
 
 
 class DataFrame:
@@ -252,7 +261,7 @@ class DataFrame:
 
     # ---- evaluation --------------------------------------------------------------
     def _namespace(self, i1, i2, filter_mask=None):
-        ns = {"np": np, "_ordinal_values": _ordinal_values}
+        ns = {"np": np, "_ordinal_values": _ordinal_values, "astype": _astype}
         for name, col in self.columns.items():
             ns[name] = col
         ns.update(self.variables)
@@ -275,7 +284,7 @@ class DataFrame:
             return self._eval_device(expression, i1, i2)
         if expression in self.virtual_columns:
             return self._eval_host(self.virtual_columns[expression], i1, i2, filter_mask)
-        ns = {"np": np, "_ordinal_values": _ordinal_values}
+        ns = {"np": np, "_ordinal_values": _ordinal_values, "astype": _astype}
         ns.update(self.variables)
         for name, col in self.columns.items():
             if name in expression:

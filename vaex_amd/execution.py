@@ -62,6 +62,11 @@ class ExecutorLocal:
         self.passes = 0
         self.local = threading.local()
         self.lock = threading.Lock()
+        # passes run one at a time: a thread whose task another thread's pass took waits
+        # here until that pass has fulfilled it (execution_test.py:79-101); the library
+        # itself is safe for concurrent callers (per-grid / per-set locks), but one device
+        # stream serialises the work anyway
+        self.run_lock = threading.Lock()
 
     def schedule(self, task):
         with self.lock:
@@ -103,15 +108,16 @@ class ExecutorLocal:
             raise RuntimeError("nested execute call")
         self.local.executing = True
         try:
-            while True:
-                tasks = self._pop_tasks()
-                if not tasks:
-                    break
-                per_df = {}
-                for t in tasks:
-                    per_df.setdefault(id(t.df), (t.df, []))[1].append(t)
-                for df, df_tasks in per_df.values():
-                    self._run(df, _merge(df_tasks, df))
+            with self.run_lock:
+                while True:
+                    tasks = self._pop_tasks()
+                    if not tasks:
+                        break
+                    per_df = {}
+                    for t in tasks:
+                        per_df.setdefault(id(t.df), (t.df, []))[1].append(t)
+                    for df, df_tasks in per_df.values():
+                        self._run(df, _merge(df_tasks, df))
         finally:
             self.local.executing = False
 

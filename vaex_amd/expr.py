@@ -290,6 +290,8 @@ class Compiler:
             raise UnsupportedExpression("call")
         if node.keywords:
             raise UnsupportedExpression("keyword arguments")
+        if name == "astype" and len(node.args) == 2:
+            return self._astype(node.args[0], node.args[1])
         args = [self.visit(a) for a in node.args]
         if name in FUNCTIONS and len(args) == 1:
             ufunc, op = FUNCTIONS[name]
@@ -331,6 +333,35 @@ class Compiler:
                 code = c.code + a.code + b.code + [OP["WHERE"]]
             return _Typed(self._finish(code, dt), dt)
         raise UnsupportedExpression(f"function {name}")
+
+    def _astype(self, value_node, dtype_node):
+        """``astype(x, 'dtype')`` (the reference's ``Expression.astype``, expression.py;
+        ``agg.py:197-201`` casts var/std inputs this way): numpy ``ndarray.astype``
+        semantics -- float -> int truncates toward zero, integers wrap."""
+        if not (isinstance(dtype_node, ast.Constant) and isinstance(dtype_node.value, str)):
+            raise UnsupportedExpression("astype needs a constant dtype string")
+        try:
+            dt = np.dtype(dtype_node.value)
+        except TypeError as e:
+            raise UnsupportedExpression(str(e))
+        if dt.kind not in "biuf" or dt.itemsize > 8:
+            raise UnsupportedExpression(f"astype to {dt}")
+        a = self.visit(value_node)
+        if a.dtype == dt and a.scalar is None:
+            return a
+        if a.scalar is not None:
+            with np.errstate(all="ignore"):
+                return self._const(np.array(a.scalar).astype(dt).item())
+        if dt.kind == "f":
+            return _Typed(self._finish(self._to_float(a), dt), dt)
+        if dt.kind == "b":
+            if a.dtype.kind == "f":
+                code = self._to_float(a) + self._const(0.0).code + [OP["NE_F"]]
+            else:
+                code = a.code + self._const(0).code + [OP["NE_I"]]
+            return _Typed(code, dt)
+        code = list(a.code) + ([OP["F2I"]] if a.dtype.kind == "f" else [])
+        return _Typed(self._finish(code, dt), dt)
 
 
 def _stack_depth(code):

@@ -74,10 +74,21 @@ class HashAgg:
                 raise HashAggOverflow(msg)
             _lib.check(rc)
 
-    def finish(self):
+    def finish(self, comm=None, gather=True):
+        """The groups, key-sorted: (keys, counts, sums, nonnull).  With an RCCL communicator
+        (``comm.device``) the ranks' groups are first exchanged by hash partition on the
+        device (vh_hashagg_exchange): each rank keeps the groups it owns, or with ``gather``
+        the whole result."""
         m = ctypes.c_uint64()
         _lib.call("vh_hashagg_finish", self._h, ctypes.byref(m))
-        m = m.value
+        if comm is not None and comm.world > 1:
+            if not comm.device:
+                raise ValueError("the device exchange needs an RCCL communicator")
+            _lib.call("vh_hashagg_exchange", self._h, comm.handle, int(bool(gather)))
+            _lib.call("vh_hashagg_finish", self._h, ctypes.byref(m))
+        return self._read(m.value)
+
+    def _read(self, m):
         # page-locked result columns: the read-back is one fast DMA per column
         keys = _lib.pinned_empty(m, np.int64)
         counts = _lib.pinned_empty(m, np.int64)
@@ -176,13 +187,16 @@ def try_groupby(df, by, actions, parse, sort=False, row_limit=None):
     distributed = getattr(executor, "world", 1) > 1
     if distributed:  # every rank takes the same route, or the collectives below would hang
         from .distributed import all_ranks_true
-        ok = all_ranks_true(ok, group=executor.group)
+        ok = all_ranks_true(ok, executor.comm)
     if not ok:
         return None
-    keys, counts, sums, nonnull = ha.finish()
-    if distributed:  # ExecutorDistributed: merge the ranks' groups
-        from .distributed import combine_groups
-        keys, counts, sums, nonnull = combine_groups((keys, counts, sums, nonnull), group=executor.group)
+    if distributed and executor.comm.device:  # RCCL: hash-partition exchange on the device
+        keys, counts, sums, nonnull = ha.finish(executor.comm, gather=True)
+    else:
+        keys, counts, sums, nonnull = ha.finish()
+        if distributed:  # CPU exchange: the same partition, merged on the host
+            from .distributed import combine_groups
+            keys, counts, sums, nonnull = combine_groups((keys, counts, sums, nonnull), executor.comm)
     if row_limit is not None and len(keys) > row_limit:
         raise RowLimitException(f"Resulting grouper has {len(keys):,} unique combinations, which is larger "
                                 f"than the allowed row limit of {row_limit:,}")

@@ -1,6 +1,13 @@
 """Minimal promises + ``@delayed`` (the role of ``vaex/promise.py`` / ``vaex/delayed.py``):
 tasks are promises fulfilled by the executor; ``delayed`` functions run once all their
-promise arguments are fulfilled."""
+promise arguments are fulfilled.
+
+Thread-safe: a task scheduled by one thread may be fulfilled by another thread's executor
+pass (execution_test.py:79-101 counts from a thread pool), so the state change and the
+callback list are guarded by one lock; callbacks run outside it."""
+import threading
+
+_LOCK = threading.RLock()
 
 
 class Promise:
@@ -28,18 +35,20 @@ class Promise:
         if isinstance(value, Promise):
             value.then(self.fulfill, self.reject)
             return
-        if self._done:
-            return
-        self._done, self._value = True, value
-        cbs, self._callbacks = self._callbacks, []
+        with _LOCK:
+            if self._done:
+                return
+            self._done, self._value = True, value
+            cbs, self._callbacks = self._callbacks, []
         for ok, _ in cbs:
             ok(value)
 
     def reject(self, error):
-        if self._done:
-            return
-        self._done, self._error = True, error
-        cbs, self._callbacks = self._callbacks, []
+        with _LOCK:
+            if self._done:
+                return
+            self._done, self._error = True, error
+            cbs, self._callbacks = self._callbacks, []
         for _, bad in cbs:
             bad(error)
 
@@ -61,10 +70,12 @@ class Promise:
             else:
                 out.reject(e)
 
-        if self._done:
+        with _LOCK:
+            done = self._done
+            if not done:
+                self._callbacks.append((ok, bad))
+        if done:
             (ok(self._value) if self._error is None else bad(self._error))
-        else:
-            self._callbacks.append((ok, bad))
         return out
 
     def get(self):
@@ -82,11 +93,13 @@ def delayed(f):
         promises = [a for a in list(args) + list(kwargs.values()) if isinstance(a, Promise)]
         result = Promise()
 
+        fired = []
+
         def run(_=None):
-            if not all(p._done for p in promises):
-                return
-            if result._done:
-                return
+            with _LOCK:
+                if not all(p._done for p in promises) or fired:
+                    return
+                fired.append(True)
             for p in promises:
                 if p._error is not None:
                     result.reject(p._error)
