@@ -248,6 +248,11 @@ int vh_combine_keys(uint64_t n, int nkeys, const void *const *cols, const int *d
  * map_ordinal, hash_primitives.hpp:468-516,543-583) with sorted ordinals. */
 int vh_dense_rank_i64(uint64_t n, const int64_t *keys, int32_t *rank, int64_t *distinct, uint64_t *m);
 
+/* stable ascending argsort of an HBM key column of `dtype` (order: int64, HBM): the Grouper
+ * sort=True order (groupby.py:137-156 sorts the set's keys; NaN after every number, -0.0 ==
+ * 0.0 keep their order); n < 2^32 */
+int vh_argsort(uint64_t n, const void *keys, int dtype, int64_t *order);
+
 /* group labels of combined keys (the inverse of vh_combine_keys; groupby.py:248-288 decodes
  * the GrouperCombined bins back to per-key labels): v = table ? table[ck[i]] : ck[i],
  * outs[j][i] = (v / mults[j]) % spans[j] + mins[j] stored in itemsizes[j] bytes; HBM buffers */

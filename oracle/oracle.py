@@ -349,6 +349,16 @@ class OrderedSet:
             return hash64(int(bits.view(np.uint64)[0]))
         return hash64(int(key))  # int32/int64 sign-extend, unsigned zero-extend
 
+    @staticmethod
+    def _ident(key, dtype):
+        """Map identity of a key: floats by bit pattern (hash<double> hashes the bits,
+        hash.hpp:69-85, so -0.0 and 0.0 land in different buckets and stay distinct keys;
+        a Python dict would merge them), integers by value."""
+        if np.dtype(dtype).kind == "f":
+            return ("f", int(np.array([key], dtype=dtype).view(np.uint64 if np.dtype(dtype).itemsize == 8
+                                                              else np.uint32)[0]), float(key))
+        return key.item()
+
     def update(self, keys, mask=None, return_values=False):
         """``_update`` (hash_primitives.hpp:96-281).  With ``return_values`` (the offsets path)
         null rows are flushed before NaN rows, otherwise NaN before null (:248-274)."""
@@ -361,7 +371,7 @@ class OrderedSet:
             elif keys.dtype.kind == "f" and k != k:
                 nans.append(i)
             else:
-                buckets[self._hash_key(k, keys.dtype) % self.nmaps].append(k.item())
+                buckets[self._hash_key(k, keys.dtype) % self.nmaps].append(self._ident(k, keys.dtype))
         for m, bucket in enumerate(buckets):
             for k in bucket:
                 mp = self.maps[m]
@@ -406,7 +416,7 @@ class OrderedSet:
         out = np.zeros(len(self), dtype=dtype)
         for m, off in zip(self.maps, self.offsets()):
             for k, v in m.items():
-                out[v + off] = k
+                out[v + off] = k[2] if isinstance(k, tuple) else k
         if self.nan_count:
             out[self.nan_value] = np.nan
         if self.null_count:
@@ -424,7 +434,7 @@ class OrderedSet:
                 out[i] = self.nan_value
                 continue
             m = self._hash_key(k, keys.dtype) % self.nmaps
-            v = self.maps[m].get(k.item())
+            v = self.maps[m].get(self._ident(k, keys.dtype))
             out[i] = -1 if v is None else v + offs[m]
         return out
 

@@ -209,3 +209,18 @@ def test_var_std_cast_to_float64(dtype, lo, hi, hbm):
     # no binby: one cell (the whole column)
     whole = oracle.var_grid([], v, n=n)
     np.testing.assert_allclose(df.var("v"), whole, rtol=1e-6)
+
+
+def test_zero_d_grid_after_binned_query():
+    """Aggregations without binby (one cell) right after binned ones on the same frame: the
+    small-grid pass's cell scratch must be cell 0 for every row, not what a previous query
+    left there."""
+    rng = np.random.default_rng(12)
+    n = 300_000
+    x = rng.normal(size=n)
+    v = rng.integers(-1000, 1000, n)
+    df = vx().from_arrays(x=x, v=v)
+    df.count(binby="x", limits=[-3, 3], shape=100)
+    assert int(df.sum("v")) == int(v.sum())
+    assert int(df.count("v")) == n
+    assert int(df.min("v")) == int(v.min()) and int(df.max("v")) == int(v.max())

@@ -221,8 +221,10 @@ def test_rccl_hashagg_exchange_roundtrip():
         p.join(300)
         assert p.exitcode == 0
         got = np.load(path)
-    for a, b in (("k1", "k2"), ("c1", "c2"), ("s1a", "s2a"), ("s1b", "s2b"), ("n1", "n2")):
+    for a, b in (("k1", "k2"), ("c1", "c2"), ("s1b", "s2b"), ("n1", "n2")):
         np.testing.assert_array_equal(got[a], got[b], err_msg=a)
+    # two independent updates: float sums in different atomic orders
+    np.testing.assert_allclose(got["s1a"], got["s2a"], rtol=1e-12, atol=1e-15)
     uk, s, cnt = oracle.groupby_reference(got["keys"], got["v"])
     np.testing.assert_array_equal(got["k2"], uk)
     np.testing.assert_array_equal(got["n2"], cnt)

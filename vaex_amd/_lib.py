@@ -95,6 +95,7 @@ SIGNATURES = {
     "vh_comm_barrier": (_i32, [_vp]),
     "vh_comm_agg_allreduce": (_i32, [_vp, _vp]),
     "vh_hashagg_exchange": (_i32, [_vp, _vp, _i32]),
+    "vh_argsort": (_i32, [_u64, _vp, _i32, _vp]),
     "vh_expr_eval": (_i32, [_p(ctypes.c_uint32), _i32, _p(_u64), _i32, _p(_vp), _p(_i32), _i32, _u64, _i32, _vp]),
 }
 

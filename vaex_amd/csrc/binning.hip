@@ -1342,6 +1342,8 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                 TimedScope ts("bin_cells");
                 g->ws.cells.ensure(std::max<uint64_t>(len, 1) * 2);
                 cells = g->ws.cells.as<uint16_t>();
+                // no binners (a 0-d grid, df.sum('x')): every row is cell 0
+                if (plan.nb == 0) VH_HIP(hipMemsetAsync(cells, 0, std::max<uint64_t>(len, 1) * 2, stream()));
                 const dim3 cg(blocks_for(len, 256, 8)), cb(256);
                 for (int d = 0; d < plan.nb; d++) {
                     const BinnerDev &b = plan.b[d];

@@ -1792,3 +1792,65 @@ int vh_hashagg_exchange(vh_hashagg *h, vh_comm *c, int gather) {
 }
 
 }  // extern "C"
+
+// ---- stable argsort of a key column on the device (Grouper sort=True, groupby.py:137-156:
+// ascending, NaN after every number; -0.0 and 0.0 compare equal, so they keep their order)
+namespace vh {
+template <typename T> __device__ inline uint64_t sortable_bits(T v) {
+    if constexpr (std::is_same_v<T, double> || std::is_same_v<T, float>) {
+        if (v != v) return ~0ULL;                        // NaN last
+        const double d = (double)v == 0.0 ? 0.0 : (double)v;  // -0.0 == 0.0
+        const uint64_t u = __builtin_bit_cast(uint64_t, d);
+        return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
+    } else if constexpr (std::is_same_v<T, vbool>) {
+        return v.v ? 1 : 0;
+    } else if constexpr (std::is_signed_v<T>) {
+        return (uint64_t)(int64_t)v ^ 0x8000000000000000ULL;
+    } else {
+        return (uint64_t)v;
+    }
+}
+
+template <typename T> __global__ __launch_bounds__(256) void k_sortkeys(const T *keys, uint64_t n, uint64_t *sk, uint32_t *idx) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        sk[i] = sortable_bits<T>(keys[i]);
+        idx[i] = (uint32_t)i;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_widen_idx(const uint32_t *idx, uint64_t n, int64_t *out) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) out[i] = idx[i];
+}
+}  // namespace vh
+
+extern "C" {
+
+int vh_argsort(uint64_t n, const void *keys, int dtype, int64_t *order) {
+    VH_API_BEGIN
+    if (n >= (uint64_t(1) << 32)) fail(VH_ERR_ARG, "argsort: at most 2^32 - 1 keys");
+    if (!n) return VH_OK;
+    if (resolve_loc(keys, VH_LOC_AUTO) != VH_LOC_DEVICE || resolve_loc(order, VH_LOC_AUTO) != VH_LOC_DEVICE)
+        fail(VH_ERR_ARG, "argsort: device buffers only");
+    hipStream_t st = stream();
+    DevBuf sk, sk2, idx, idx2, tmp;
+    sk.ensure(8 * n);
+    sk2.ensure(8 * n);
+    idx.ensure(4 * n);
+    idx2.ensure(4 * n);
+    const unsigned g = blocks_for(n, 256, 8);
+    VH_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(k_sortkeys<T>, dim3(g), dim3(256), 0, st, static_cast<const T *>(keys), n,
+                                                   sk.as<uint64_t>(), idx.as<uint32_t>()));
+    size_t tb = 0;
+    VH_HIP(rocprim::radix_sort_pairs(nullptr, tb, (uint64_t *)nullptr, (uint64_t *)nullptr, (uint32_t *)nullptr,
+                                     (uint32_t *)nullptr, (size_t)n, 0, 64, st));
+    tmp.ensure(std::max<size_t>(tb, 16));
+    tb = tmp.bytes;
+    VH_HIP(rocprim::radix_sort_pairs(tmp.ptr, tb, sk.as<uint64_t>(), sk2.as<uint64_t>(), idx.as<uint32_t>(),
+                                     idx2.as<uint32_t>(), (size_t)n, 0, 64, st));
+    hipLaunchKernelGGL(k_widen_idx, dim3(g), dim3(256), 0, st, idx2.as<uint32_t>(), n, order);
+    VH_HIP(hipGetLastError());
+    VH_HIP(hipStreamSynchronize(st));
+    VH_API_END
+}
+
+}  // extern "C"

@@ -17,10 +17,13 @@
 // 3/4 full, or a probe sequence longer than SET_MAX_PROBE, is refused and flags overflow:
 // the table then grows x4 and the chunk is re-run (inserts are idempotent).
 #include <algorithm>
+#include <cmath>
 #include <limits>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <numeric>
+#include <type_traits>
 
 #include "common.hpp"
 #include "hashset.hpp"
@@ -42,6 +45,7 @@ struct vh_set {
     DevBuf stage_keys, stage_mask, stage_select;
     DevBuf c_slot, c_first, c_ord, c_bits;
     uint64_t rows_seen = 0;
+    uint64_t nan_count_before = 0, null_count_before = 0;  // counters before the current chunk
     // the reference flushes NaN/null rows after the regular keys of the update call that
     // saw them first (hash_primitives.hpp:248-274): their ordinal position is the end of
     // that call, ties broken NaN before null
@@ -55,60 +59,518 @@ struct vh_set {
 
 namespace vh {
 
-template <typename T>
-__global__ __launch_bounds__(256) void k_set_insert(const T *keys, const uint8_t *mask, const uint8_t *select, uint64_t n,
-                                                    uint64_t row0, uint64_t *tab, uint64_t cap_mask, uint64_t limit,
-                                                    uint64_t *ctr) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t row = row0 + i;
-        if (select && !select[i]) continue;  // filtered out / not selected
-        if (mask && mask[i]) {
-            atomicMin((unsigned long long *)&ctr[C_NULL_FIRST], (unsigned long long)row);
-            atomicAdd((unsigned long long *)&ctr[C_NULL_COUNT], 1ULL);
-            continue;
-        }
-        const T v = keys[i];
-        if (is_nan_v(v)) {
-            atomicMin((unsigned long long *)&ctr[C_NAN_FIRST], (unsigned long long)row);
-            atomicAdd((unsigned long long *)&ctr[C_NAN_COUNT], 1ULL);
-            continue;
-        }
-        const uint64_t kb = key_bits(v);
-        if (kb == SET_EMPTY) {
-            atomicMin((unsigned long long *)&ctr[C_SPECIAL_FIRST], (unsigned long long)row);
-            continue;
-        }
-        uint64_t pos = hash64(kb) & cap_mask;
-        int p = 0;
-        bool refused = false;
-        for (; p <= SET_MAX_PROBE; p++) {
-            uint64_t k = __hip_atomic_load(&tab[2 * pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (k == kb) break;
-            if (k == SET_EMPTY) {
-                // a new key: refuse it once the table holds `limit` keys (the host grows the
-                // table and re-runs the chunk)
-                if (__hip_atomic_load(&ctr[C_DISTINCT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= limit) {
-                    refused = true;
-                    break;
-                }
-                uint64_t old = atomicCAS((unsigned long long *)&tab[2 * pos], (unsigned long long)SET_EMPTY,
-                                         (unsigned long long)kb);
-                if (old == SET_EMPTY) {
-                    atomicAdd((unsigned long long *)&ctr[C_DISTINCT], 1ULL);
-                    break;
-                }
-                if (old == kb) break;
+// ---- update: hash-partitioned insert ------------------------------------------------------
+// Per update chunk (hash_primitives.hpp:96-281 `_update` over one chunk of keys):
+//   sample -- ~1 M evenly spaced rows: fine bucket histogram (top 12 bits of the key hash)
+//             and a distinct-key estimate (Chao1) -> the HBM table is grown before the
+//             pass, and P = 2^p buckets of <= ~SI_TARGET_KEYS keys are chosen;
+//   pass A -- workgroup w owns a row range; per 4096-row batch it classifies the rows
+//             (unselected / null / NaN / the EMPTY-bits key are counted in LDS, their
+//             first rows kept), ranks the regular rows per bucket in LDS, counting-sorts
+//             (key bits, row) by bucket and streams the runs to per-(w, bucket) regions;
+//   pass B -- work unit = (bucket, range of pass-A workgroups): the unit's entries are
+//             deduplicated in an LDS table keeping each key's smallest row (ds_min), then
+//             each distinct key is inserted into the HBM table ONCE per unit (CAS on an
+//             EMPTY slot, atomicMin of the first row) -- not once per row;
+//   direct -- (P == 1, few keys) each workgroup dedups its raw rows in LDS, then merges.
+// A key that finds its LDS table closed (full: a sampling miss), or a row whose pass-A
+// region is full, goes straight to the HBM table.  An HBM insert past `limit` keys is
+// refused and raises the overflow counter; the host then grows the table and re-runs the
+// chunk (inserts are idempotent).  Two host round trips per chunk: the sample and the end.
+constexpr int SI_THREADS = 512;
+constexpr int SI_RPT = 8;
+constexpr int SI_BATCH = SI_THREADS * SI_RPT;
+constexpr int SB_THREADS = 1024;
+constexpr int SB_M = 8;                   // entries per lane per pass-B step
+constexpr uint32_t SI_LT_LOG2 = 13;
+constexpr uint32_t SI_LT = 1u << SI_LT_LOG2;  // LDS table slots (+2 side records)
+constexpr uint32_t SI_LT_MAX = 5120;          // close at 62.5 % (+ <= 1024 racing inserts)
+constexpr uint32_t SI_TARGET_KEYS = 4096;     // P: a bucket holds about this many keys
+constexpr uint32_t SI_FINE_LOG2 = 12;
+constexpr uint32_t SI_MAX_P_LOG2 = 11;
+constexpr int SI_SAMPLE_BLOCKS = 256;
+constexpr uint32_t SI_DEST_OVER = 0x80000000u;
+constexpr uint32_t SI_ROW_NONE = 0xffffffffu;
+
+template <typename T> using si_kb_t = std::conditional_t<sizeof(T) == 8, uint64_t, uint32_t>;
+
+struct SiParams {
+    const void *keys;
+    const uint8_t *mask, *select;
+    uint64_t n, row0;  // rows of the chunk; set row number of its first row
+    uint32_t p_log2, P, W, pad;
+    uint64_t rows_per_wg, wg_stride;
+    const uint32_t *cap;   // [P]
+    const uint64_t *toff;  // [P]
+    uint32_t *fills;       // [P][W]
+    void *ent;             // <= 4-byte keys: u64 (row << 32 | key bits); else u64 key bits
+    uint32_t *ent_row;     // 8-byte keys: the rows
+};
+
+struct SiTable {
+    uint64_t *tab;
+    uint64_t cap_mask, limit;
+    uint64_t *ctr;
+};
+
+struct SiUnit {
+    uint32_t bucket, w_begin, w_end, pad;
+};
+
+// top p_log2 bits of the key hash's high word (fine histogram: top SI_FINE_LOG2 bits)
+__device__ inline uint32_t si_h32(uint64_t kb) { return (uint32_t)(hash64(kb) >> 32); }
+__device__ inline uint32_t si_bucket(uint64_t kb, uint32_t p_log2) {
+    return (uint32_t)(((uint64_t)si_h32(kb) << p_log2) >> 32);
+}
+
+// one distinct key (and the smallest row it was seen at) into the HBM table
+__device__ inline void si_global(const SiTable &g, uint64_t kb, uint64_t row) {
+    uint64_t pos = hash64(kb) & g.cap_mask;
+    for (int p = 0; p <= SET_MAX_PROBE; p++) {
+        const uint64_t k = __hip_atomic_load(&g.tab[2 * pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool mine = k == kb;
+        if (!mine && k == SET_EMPTY) {
+            if (__hip_atomic_load(&g.ctr[C_DISTINCT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= g.limit) {
+                atomicOr((unsigned long long *)&g.ctr[C_OVERFLOW], 1ULL);  // grow + re-run
+                return;
             }
-            pos = (pos + 1) & cap_mask;
+            const uint64_t old = atomicCAS((unsigned long long *)&g.tab[2 * pos], (unsigned long long)SET_EMPTY,
+                                           (unsigned long long)kb);
+            if (old == SET_EMPTY) atomicAdd((unsigned long long *)&g.ctr[C_DISTINCT], 1ULL);
+            mine = old == SET_EMPTY || old == kb;
         }
-        if (refused || p > SET_MAX_PROBE) {
-            ctr[C_OVERFLOW] = 1;
+        if (mine) {
+            if (__hip_atomic_load(&g.tab[2 * pos + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > row)
+                atomicMin((unsigned long long *)&g.tab[2 * pos + 1], (unsigned long long)row);
+            return;
+        }
+        pos = (pos + 1) & g.cap_mask;
+    }
+    atomicOr((unsigned long long *)&g.ctr[C_OVERFLOW], 1ULL);
+}
+
+// ---- LDS dedup table: key bits -> smallest row (chunk-relative) ---------------------------
+template <typename KB> __host__ __device__ constexpr KB si_empty() { return ~KB(0); }
+template <typename KB> __host__ __device__ constexpr KB si_closed() { return ~KB(0) - 1; }
+
+template <typename KB> struct SiLds {
+    KB *keys;        // [SI_LT]
+    uint32_t *rows;  // [SI_LT + 2]: +2 side records for the keys equal to CLOSED / EMPTY
+    uint32_t *used;
+};
+
+__host__ __device__ constexpr size_t si_lt_bytes(int kbsize) { return (size_t)kbsize * SI_LT + 4 * (SI_LT + 2) + 16; }
+
+template <typename KB> __device__ inline SiLds<KB> si_lt_layout(unsigned char *raw) {
+    SiLds<KB> t;
+    t.keys = reinterpret_cast<KB *>(raw);
+    t.rows = reinterpret_cast<uint32_t *>(raw + sizeof(KB) * SI_LT);
+    t.used = t.rows + SI_LT + 2;
+    return t;
+}
+
+template <typename KB> __device__ inline void si_lt_init(const SiLds<KB> &t, int nthreads) {
+    for (uint32_t i = threadIdx.x; i < SI_LT + 2; i += nthreads) {
+        if (i < SI_LT) t.keys[i] = si_empty<KB>();
+        t.rows[i] = SI_ROW_NONE;
+    }
+    if (threadIdx.x == 0) *t.used = 0;
+}
+
+template <typename KB> struct alignas(16) SiKB4 {
+    KB v[4];
+};
+
+__device__ inline uint32_t si_cas(uint32_t *p, uint32_t cmp, uint32_t val) { return atomicCAS(p, cmp, val); }
+__device__ inline uint64_t si_cas(uint64_t *p, uint64_t cmp, uint64_t val) {
+    return atomicCAS(reinterpret_cast<unsigned long long *>(p), (unsigned long long)cmp, (unsigned long long)val);
+}
+
+// Bucketised linear probing over groups of 4 slots (one ds_read_b128 for 4-byte keys): a
+// key lives at the first free slot of its group sequence, so a probe ends at a hit or at
+// the first EMPTY (CAS) / CLOSED slot.  Past SI_LT_MAX keys the table closes: EMPTY slots a
+// new key reaches become CLOSED and the key goes to the HBM table (every key is wholly in
+// the LDS table or wholly in the HBM path; the min over both is the same).
+template <typename KB>
+__device__ inline void si_lt_add(const SiLds<KB> &t, const SiTable &g, uint64_t row0, KB kb, uint32_t row) {
+    constexpr KB EMPTY = si_empty<KB>(), CLOSED = si_closed<KB>();
+    if (kb >= CLOSED) {
+        atomicMin(&t.rows[SI_LT + (uint32_t)(kb - CLOSED)], row);
+        return;
+    }
+    uint32_t grp = ((uint32_t)hash64((uint64_t)kb) & (SI_LT - 1)) >> 2;
+    for (;;) {
+        const SiKB4<KB> q = *reinterpret_cast<const SiKB4<KB> *>(t.keys + 4 * grp);
+        int hit = -1, fr = -1;
+#pragma unroll
+        for (int j = 3; j >= 0; j--) {
+            if (q.v[j] == kb) hit = j;
+            if (q.v[j] >= CLOSED) fr = j;
+        }
+        if (hit >= 0 && (fr < 0 || hit < fr)) {
+            atomicMin(&t.rows[4 * grp + hit], row);
+            return;
+        }
+        if (fr < 0) {
+            grp = (grp + 1) & (SI_LT / 4 - 1);
             continue;
         }
-        if (__hip_atomic_load(&tab[2 * pos + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > row)
-            atomicMin((unsigned long long *)&tab[2 * pos + 1], (unsigned long long)row);
+        if (q.v[fr] == CLOSED) {
+            si_global(g, (uint64_t)kb, row0 + row);
+            return;
+        }
+        const uint32_t pos = 4 * grp + fr;
+        const bool open = *reinterpret_cast<volatile uint32_t *>(t.used) < SI_LT_MAX;
+        const KB cur = si_cas(&t.keys[pos], EMPTY, open ? kb : CLOSED);
+        if (cur == EMPTY) {
+            if (!open) {
+                si_global(g, (uint64_t)kb, row0 + row);
+                return;
+            }
+            atomicAdd(t.used, 1u);
+            atomicMin(&t.rows[pos], row);
+            return;
+        }
+        if (cur == kb) {
+            atomicMin(&t.rows[pos], row);
+            return;
+        }
     }
+}
+
+// every key the LDS table holds, with its smallest row, into the HBM table (after a barrier)
+template <typename KB> __device__ inline void si_lt_merge(const SiLds<KB> &t, const SiTable &g, uint64_t row0, int nthreads) {
+    for (uint32_t i = threadIdx.x; i < SI_LT + 2; i += nthreads) {
+        const uint32_t r = t.rows[i];
+        if (r == SI_ROW_NONE) continue;
+        const KB kb = i < SI_LT ? t.keys[i] : (KB)(si_closed<KB>() + (i - SI_LT));
+        si_global(g, (uint64_t)kb, row0 + r);
+    }
+}
+
+// ---- per-workgroup counters of the rows that never enter the table -----------------------
+struct SiSpecial {
+    uint32_t nan_first, null_first, spec_first, pad;
+    uint32_t nan_cnt, null_cnt;
+};
+
+__device__ inline void si_special_init(SiSpecial *sp) {
+    if (threadIdx.x == 0) {
+        sp->nan_first = sp->null_first = sp->spec_first = SI_ROW_NONE;
+        sp->nan_cnt = sp->null_cnt = 0;
+    }
+}
+
+__device__ inline void si_special_flush(const SiSpecial *sp, uint64_t row0, uint64_t *ctr) {
+    if (threadIdx.x != 0) return;
+    if (sp->nan_cnt) {
+        atomicMin((unsigned long long *)&ctr[C_NAN_FIRST], (unsigned long long)(row0 + sp->nan_first));
+        atomicAdd((unsigned long long *)&ctr[C_NAN_COUNT], (unsigned long long)sp->nan_cnt);
+    }
+    if (sp->null_cnt) {
+        atomicMin((unsigned long long *)&ctr[C_NULL_FIRST], (unsigned long long)(row0 + sp->null_first));
+        atomicAdd((unsigned long long *)&ctr[C_NULL_COUNT], (unsigned long long)sp->null_cnt);
+    }
+    if (sp->spec_first != SI_ROW_NONE)
+        atomicMin((unsigned long long *)&ctr[C_SPECIAL_FIRST], (unsigned long long)(row0 + sp->spec_first));
+}
+
+// classify row i (chunk-relative): returns true with its key bits when it is a regular key
+template <typename T>
+__device__ inline bool si_row(const SiParams &sp, uint64_t i, SiSpecial *spec, si_kb_t<T> *kb) {
+    if (sp.select && !sp.select[i]) return false;  // filtered out / not selected
+    if (sp.mask && sp.mask[i]) {
+        atomicMin(&spec->null_first, (uint32_t)i);
+        atomicAdd(&spec->null_cnt, 1u);
+        return false;
+    }
+    const T v = static_cast<const T *>(sp.keys)[i];
+    if (is_nan_v(v)) {
+        atomicMin(&spec->nan_first, (uint32_t)i);
+        atomicAdd(&spec->nan_cnt, 1u);
+        return false;
+    }
+    const uint64_t b = key_bits(v);
+    if (b == SET_EMPTY) {  // 8-byte keys only: the side slot ("special")
+        atomicMin(&spec->spec_first, (uint32_t)i);
+        return false;
+    }
+    *kb = (si_kb_t<T>)b;
+    return true;
+}
+
+// ---- sample -------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(SI_THREADS) void k_si_sample(SiParams sp, uint64_t block_stride,
+                                                          unsigned long long *fine_hist, uint64_t *skeys, uint32_t *scnt,
+                                                          uint64_t smask) {
+    __shared__ uint32_t h[1u << SI_FINE_LOG2];
+    __shared__ SiSpecial spec;  // discarded: the pass counts these rows
+    for (uint32_t t = threadIdx.x; t < (1u << SI_FINE_LOG2); t += SI_THREADS) h[t] = 0;
+    si_special_init(&spec);
+    __syncthreads();
+    const uint64_t r0 = blockIdx.x * block_stride;
+    for (uint64_t r = threadIdx.x; r < SI_BATCH; r += SI_THREADS) {
+        const uint64_t i = r0 + r;
+        if (i >= sp.n) break;
+        si_kb_t<T> kb;
+        if (!si_row<T>(sp, i, &spec, &kb)) continue;
+        atomicAdd(&h[si_h32(kb) >> (32 - SI_FINE_LOG2)], 1u);
+        uint64_t pos = hash64(kb) & smask;
+        for (int p = 0; p < 1 << 14; p++) {
+            uint64_t cur = __hip_atomic_load(&skeys[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cur == SET_EMPTY)
+                cur = atomicCAS((unsigned long long *)&skeys[pos], (unsigned long long)SET_EMPTY, (unsigned long long)kb);
+            if (cur == SET_EMPTY || cur == (uint64_t)kb) {
+                atomicAdd(&scnt[pos], 1u);
+                break;
+            }
+            pos = (pos + 1) & smask;
+        }
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < (1u << SI_FINE_LOG2); t += SI_THREADS)
+        if (h[t]) atomicAdd(&fine_hist[t], (unsigned long long)h[t]);
+}
+
+// distinct keys of the sample, and how many were seen once / twice (Chao1 inputs)
+__global__ __launch_bounds__(256) void k_si_sample_stats(const uint32_t *scnt, uint64_t slots, unsigned long long *stats) {
+    uint64_t d = 0, f1 = 0, f2 = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < slots; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t c = scnt[i];
+        d += c != 0;
+        f1 += c == 1;
+        f2 += c == 2;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        d += __shfl_down(d, off, 64);
+        f1 += __shfl_down(f1, off, 64);
+        f2 += __shfl_down(f2, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&stats[0], (unsigned long long)d);
+        atomicAdd(&stats[1], (unsigned long long)f1);
+        atomicAdd(&stats[2], (unsigned long long)f2);
+    }
+}
+
+// ---- pass A -------------------------------------------------------------------------------
+__host__ __device__ constexpr size_t si_scatter_lds_bytes(uint32_t P) {
+    return (size_t)(8 + 4 + 4) * (SI_BATCH + 1) + 16 * ((size_t)P + 1) + 64;
+}
+
+__device__ inline void si_lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <typename T>
+__global__ __launch_bounds__(SI_THREADS) void k_si_scatter(SiParams sp, SiTable g) {
+    using KB = si_kb_t<T>;
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    __shared__ SiSpecial spec;
+    __shared__ uint32_t s_total, s_over;
+    uint64_t *skb = reinterpret_cast<uint64_t *>(lds_raw);           // [SI_BATCH + 1]
+    uint32_t *srow = reinterpret_cast<uint32_t *>(skb + SI_BATCH + 1);  // [SI_BATCH + 1]
+    uint32_t *sdst = srow + SI_BATCH + 1;                               // [SI_BATCH + 1]
+    uint32_t *hist = sdst + SI_BATCH + 1;                               // [P + 1]: [P] = sink
+    uint32_t *boff = hist + sp.P + 1, *base = boff + sp.P, *lim = base + sp.P, *wave_sums = lim + sp.P;
+    for (uint32_t t = threadIdx.x; t <= sp.P; t += SI_THREADS) hist[t] = 0;
+    for (uint32_t t = threadIdx.x; t < sp.P; t += SI_THREADS) {
+        base[t] = (uint32_t)sp.toff[t];
+        lim[t] = (uint32_t)sp.toff[t] + sp.cap[t];
+    }
+    si_special_init(&spec);
+    __syncthreads();
+    const uint32_t w = blockIdx.x, P = sp.P;
+    const uint64_t row_begin = (uint64_t)w * sp.rows_per_wg;
+    const uint64_t row_end = min(sp.n, row_begin + sp.rows_per_wg);
+    const uint64_t region0 = (uint64_t)w * sp.wg_stride;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint64_t b0 = row_begin; b0 < row_end; b0 += SI_BATCH) {
+        KB kb[SI_RPT];
+        uint32_t bkt[SI_RPT];
+        int32_t rank[SI_RPT];
+#pragma unroll
+        for (int r = 0; r < SI_RPT; r++) {
+            const uint64_t i = b0 + (uint64_t)r * SI_THREADS + threadIdx.x;
+            rank[r] = -1;
+            bkt[r] = 0;
+            kb[r] = 0;
+            if (i < row_end && si_row<T>(sp, i, &spec, &kb[r])) {
+                bkt[r] = si_bucket((uint64_t)kb[r], sp.p_log2);
+                rank[r] = (int32_t)atomicAdd(&hist[bkt[r]], 1u);
+            }
+        }
+        // exclusive scan of the bucket histogram
+        si_lds_barrier();
+        {
+            const uint32_t per = (P + SI_THREADS - 1) / SI_THREADS;
+            const uint32_t t0 = threadIdx.x * per;
+            uint32_t sum = 0;
+            for (uint32_t t = t0; t < t0 + per && t < P; t++) sum += hist[t];
+            uint32_t inc = sum;
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(inc, off, 64);
+                if (lane >= off) inc += y;
+            }
+            if (lane == 63) wave_sums[wave] = inc;
+            si_lds_barrier();
+            uint32_t wave_base = 0, total = 0;
+            for (int k = 0; k < SI_THREADS / 64; k++) {
+                if (k < wave) wave_base += wave_sums[k];
+                total += wave_sums[k];
+            }
+            uint32_t acc = wave_base + inc - sum;
+            for (uint32_t t = t0; t < t0 + per && t < P; t++) {
+                boff[t] = acc;
+                acc += hist[t];
+            }
+            if (threadIdx.x == 0) {
+                s_total = total;
+                s_over = 0;
+            }
+        }
+        si_lds_barrier();
+        bool over = false;
+#pragma unroll
+        for (int r = 0; r < SI_RPT; r++) {
+            if (rank[r] < 0) continue;
+            const uint32_t t = bkt[r];
+            const uint32_t pos = boff[t] + (uint32_t)rank[r];
+            const uint32_t d = base[t] + (uint32_t)rank[r];
+            const bool fits = d < lim[t];
+            over |= !fits;
+            sdst[pos] = fits ? d : SI_DEST_OVER;
+            skb[pos] = (uint64_t)kb[r];
+            srow[pos] = (uint32_t)(b0 + (uint64_t)r * SI_THREADS + threadIdx.x);
+        }
+        if (over) s_over = 1;
+        si_lds_barrier();
+        const uint32_t tot = s_total;
+        for (uint32_t k = threadIdx.x; k < tot; k += SI_THREADS) {
+            const uint32_t dst = sdst[k];
+            if (dst & SI_DEST_OVER) continue;
+            const uint64_t e = region0 + dst;
+            if constexpr (sizeof(KB) == 4) {
+                reinterpret_cast<uint64_t *>(sp.ent)[e] = ((uint64_t)srow[k] << 32) | (uint32_t)skb[k];
+            } else {
+                reinterpret_cast<uint64_t *>(sp.ent)[e] = skb[k];
+                sp.ent_row[e] = srow[k];
+            }
+        }
+        if (s_over) {  // a full region (sampling miss): those rows go to the HBM table
+            for (uint32_t k = threadIdx.x; k < tot; k += SI_THREADS)
+                if (sdst[k] & SI_DEST_OVER) si_global(g, skb[k], sp.row0 + srow[k]);
+        }
+        si_lds_barrier();
+        for (uint32_t t = threadIdx.x; t < P; t += SI_THREADS) {
+            base[t] += hist[t];
+            hist[t] = 0;
+        }
+        si_lds_barrier();
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < P; t += SI_THREADS) sp.fills[(uint64_t)t * sp.W + w] = base[t] - (uint32_t)sp.toff[t];
+    si_special_flush(&spec, sp.row0, g.ctr);
+}
+
+// ---- pass B -------------------------------------------------------------------------------
+template <typename KB>
+__global__ __launch_bounds__(SB_THREADS) void k_si_reduce(SiParams sp, SiTable g, const SiUnit *units) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    __shared__ uint32_t s_fill[1024];
+    __shared__ uint32_t s_pre[1025];
+    const SiUnit u = units[blockIdx.x];
+    const uint32_t b = u.bucket;
+    const uint32_t cap = sp.cap[b];
+    const uint32_t nw = u.w_end - u.w_begin;  // <= 1024 (host checks)
+    bool any = false;
+    for (uint32_t k = threadIdx.x; k < nw; k += SB_THREADS) {
+        const uint32_t f = min(sp.fills[(uint64_t)b * sp.W + u.w_begin + k], cap);
+        s_fill[k] = f;
+        any |= f != 0;
+    }
+    if (!__syncthreads_or(any)) return;
+    const SiLds<KB> t = si_lt_layout<KB>(lds_raw);
+    si_lt_init<KB>(t, SB_THREADS);
+    if (threadIdx.x < 64) {  // exclusive scan of the region fills (16 regions per lane)
+        const uint32_t lane = threadIdx.x, k0 = lane * 16;
+        uint32_t sum = 0;
+        for (uint32_t k = k0; k < k0 + 16 && k < nw; k++) sum += s_fill[k];
+        uint32_t inc = sum;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(inc, off, 64);
+            if ((int)lane >= off) inc += y;
+        }
+        uint32_t acc = inc - sum;
+        for (uint32_t k = k0; k < k0 + 16 && k < nw; k++) {
+            s_pre[k] = acc;
+            acc += s_fill[k];
+        }
+        if (lane == 63) s_pre[nw] = inc;
+    }
+    __syncthreads();
+    const uint32_t E = s_pre[nw];
+    const uint64_t toff_b = sp.toff[b];
+    uint32_t kr = 0;  // region of this lane's current entry (entry indices of a lane only grow)
+    for (uint32_t c0 = 0; c0 < E; c0 += SB_THREADS * SB_M) {
+        KB kb[SB_M];
+        uint32_t row[SB_M];
+        bool valid[SB_M];
+#pragma unroll
+        for (int j = 0; j < SB_M; j++) {
+            const uint32_t c = c0 + j * SB_THREADS + threadIdx.x;
+            const uint32_t cc = c < E ? c : E - 1;
+            while (s_pre[kr + 1] <= cc) kr++;
+            const uint64_t e = (uint64_t)(u.w_begin + kr) * sp.wg_stride + toff_b + (cc - s_pre[kr]);
+            valid[j] = c < E;
+            if constexpr (sizeof(KB) == 4) {
+                const uint64_t q = reinterpret_cast<const uint64_t *>(sp.ent)[e];
+                kb[j] = (KB)(uint32_t)q;
+                row[j] = (uint32_t)(q >> 32);
+            } else {
+                kb[j] = reinterpret_cast<const uint64_t *>(sp.ent)[e];
+                row[j] = sp.ent_row[e];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < SB_M; j++)
+            if (valid[j]) si_lt_add<KB>(t, g, sp.row0, kb[j], row[j]);
+    }
+    __syncthreads();
+    si_lt_merge<KB>(t, g, sp.row0, SB_THREADS);
+}
+
+// ---- direct (P == 1): each workgroup dedups its row range of the raw keys -----------------
+template <typename T>
+__global__ __launch_bounds__(SB_THREADS) void k_si_direct(SiParams sp, SiTable g) {
+    using KB = si_kb_t<T>;
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    __shared__ SiSpecial spec;
+    const SiLds<KB> t = si_lt_layout<KB>(lds_raw);
+    si_lt_init<KB>(t, SB_THREADS);
+    si_special_init(&spec);
+    __syncthreads();
+    const uint64_t row_begin = (uint64_t)blockIdx.x * sp.rows_per_wg;
+    const uint64_t row_end = min(sp.n, row_begin + sp.rows_per_wg);
+    constexpr int U = 4;
+    for (uint64_t b0 = row_begin; b0 < row_end; b0 += (uint64_t)U * SB_THREADS) {
+        KB kb[U];
+        bool valid[U];
+#pragma unroll
+        for (int r = 0; r < U; r++) {
+            const uint64_t i = b0 + (uint64_t)r * SB_THREADS + threadIdx.x;
+            valid[r] = i < row_end && si_row<T>(sp, i, &spec, &kb[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < U; r++)
+            if (valid[r]) si_lt_add<KB>(t, g, sp.row0, kb[r], (uint32_t)(b0 + (uint64_t)r * SB_THREADS + threadIdx.x));
+    }
+    __syncthreads();
+    si_lt_merge<KB>(t, g, sp.row0, SB_THREADS);
+    si_special_flush(&spec, sp.row0, g.ctr);
 }
 
 __global__ void k_set_rehash(const uint64_t *otab, uint64_t ocap, uint64_t *ntab, uint64_t ncap_mask) {
@@ -446,20 +908,212 @@ int vh_set_destroy(vh_set *s) {
     VH_API_END
 }
 
+namespace vh {
+
+// partition scratch shared by the sets of a device (regions of a 2^28-row chunk are ~2 GB)
+struct SiScratch {
+    std::mutex mu;
+    DevBuf sample, meta, ent, ent_row;
+};
+static SiScratch &si_scratch() {
+    static std::mutex g;
+    static std::map<int, std::unique_ptr<SiScratch>> m;
+    std::lock_guard<std::mutex> lk(g);
+    auto &p = m[current_device()];
+    if (!p) p = std::make_unique<SiScratch>();
+    return *p;
+}
+
+static uint64_t si_next_pow2(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+static int si_blocks_per_cu(const void *kernel, int threads, size_t lds) {
+    int nb = 0;
+    VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, threads, lds));
+    return std::max(1, nb);
+}
+
+// one chunk of rows (device-resident, < 2^32) into the set; rows numbered from row0
+static void si_chunk(vh_set *s, SiScratch &S, const void *keys, const uint8_t *mask, const uint8_t *select, uint64_t n,
+                     uint64_t row0) {
+    hipStream_t st = stream();
+    const int isz = dtype_itemsize(s->dtype);
+    const int kbs = isz == 8 ? 8 : 4;
+    SiParams sp{};
+    sp.keys = keys;
+    sp.mask = mask;
+    sp.select = select;
+    sp.n = n;
+    sp.row0 = row0;
+    // ---- sample: fine bucket histogram + distinct estimate, read back with the counters
+    const uint64_t sslots = 1ull << 21;
+    const uint64_t nbatch = (n + SI_BATCH - 1) / SI_BATCH;
+    const uint64_t sblocks = std::min<uint64_t>(nbatch, SI_SAMPLE_BLOCKS);
+    const uint64_t bstride = std::max<uint64_t>(SI_BATCH, n / sblocks);
+    const uint32_t FINE = 1u << SI_FINE_LOG2;
+    S.sample.ensure(sslots * 12 + 8 * FINE + 64);
+    uint64_t *skeys = S.sample.as<uint64_t>();
+    uint32_t *scnt = reinterpret_cast<uint32_t *>(skeys + sslots);
+    unsigned long long *fine = reinterpret_cast<unsigned long long *>(scnt + sslots);
+    unsigned long long *stats = fine + FINE;
+    VH_HIP(hipMemsetAsync(skeys, 0xff, 8 * sslots, st));
+    VH_HIP(hipMemsetAsync(scnt, 0, 4 * sslots + 8 * FINE + 64, st));
+    {
+        TimedScope ts("set_sample");
+        VH_DISPATCH_DTYPE(s->dtype, T,
+                          hipLaunchKernelGGL(k_si_sample<T>, dim3(sblocks), dim3(SI_THREADS), 0, st, sp, bstride, fine,
+                                             skeys, scnt, sslots - 1));
+        hipLaunchKernelGGL(k_si_sample_stats, dim3(blocks_for(sslots, 256, 4)), dim3(256), 0, st, scnt, sslots, stats);
+        VH_HIP(hipGetLastError());
+    }
+    std::vector<uint64_t> fh(FINE + 3), c(C_N);
+    VH_HIP(hipMemcpyAsync(fh.data(), fine, 8 * (FINE + 3), hipMemcpyDeviceToHost, st));
+    VH_HIP(hipMemcpyAsync(c.data(), s->ctr.ptr, 8 * C_N, hipMemcpyDeviceToHost, st));
+    VH_HIP(hipStreamSynchronize(st));
+    uint64_t sampled = 0;
+    for (uint32_t i = 0; i < FINE; i++) sampled += fh[i];
+    const double ds = (double)fh[FINE], f1 = (double)fh[FINE + 1], f2 = (double)fh[FINE + 2];
+    double dest;
+    if (sampled >= n || sblocks == nbatch) dest = ds;  // every row sampled: exact
+    else dest = f2 > 0 ? ds + f1 * f1 / (2 * f2) : ds + f1 * (f1 - 1) / 2;  // Chao1
+    dest = std::min<double>(std::max(dest, 1.0), (double)n);
+    // the HBM table at <= 1/2 load for what it holds plus the estimate
+    const uint64_t need = c[C_DISTINCT] + (uint64_t)dest;
+    if (2 * need > s->cap) set_grow(s, si_next_pow2(2 * need));
+    uint32_t p_log2 = 0;
+    while (p_log2 < SI_MAX_P_LOG2 && dest / (double)(1u << p_log2) > SI_TARGET_KEYS) p_log2++;
+    sp.p_log2 = p_log2;
+    sp.P = 1u << p_log2;
+    const uint32_t P = sp.P;
+    const size_t lt_lds = si_lt_bytes(kbs);
+
+    std::vector<SiUnit> units;
+    std::vector<uint32_t> cap;
+    std::vector<uint64_t> toff;
+    uint32_t W = 0;
+    if (P > 1) {
+        std::vector<uint64_t> bh(P, 0);
+        for (uint32_t i = 0; i < FINE; i++) bh[i >> (SI_FINE_LOG2 - p_log2)] += fh[i];
+        const size_t lds_a = si_scatter_lds_bytes(P);
+        int bpc = 1;
+        VH_DISPATCH_DTYPE(s->dtype, T,
+                          bpc = si_blocks_per_cu(reinterpret_cast<const void *>(k_si_scatter<T>), SI_THREADS, lds_a));
+        bpc = std::min(bpc, 4);
+        W = std::min<uint32_t>(1024, (uint32_t)cu_count() * bpc);
+        const uint64_t rows_per_wg = ((n + W - 1) / W + SI_BATCH - 1) / SI_BATCH * SI_BATCH;
+        cap.resize(P);
+        toff.resize(P);
+        uint64_t stride = 0;
+        for (uint32_t t = 0; t < P; t++) {
+            const double e = (double)rows_per_wg * (double)bh[t] / (double)std::max<uint64_t>(sampled, 1);
+            uint64_t cc = (uint64_t)(e * 1.04 + 6.0 * std::sqrt(e + 1.0)) + 32;
+            cc = std::min<uint64_t>((cc + 7) & ~uint64_t(7), rows_per_wg + 8);
+            cap[t] = (uint32_t)cc;
+            toff[t] = stride;
+            stride += cc;
+        }
+        if (stride + rows_per_wg >= (uint64_t)SI_DEST_OVER) fail(VH_ERR_RUNTIME, "ordered_set: region table too large");
+        const uint64_t total = stride * W;
+        S.ent.ensure(8 * total + 64);
+        if (kbs == 8) S.ent_row.ensure(4 * total + 64);
+        const double target = std::max(1.0, (double)n / ((double)cu_count() * 2));
+        for (uint32_t t = 0; t < P; t++) {
+            const double e = (double)n * (double)bh[t] / (double)std::max<uint64_t>(sampled, 1);
+            const uint32_t gq = (uint32_t)std::min<double>(W, std::max(1.0, std::ceil(e / target)));
+            for (uint32_t k = 0; k < gq; k++)
+                units.push_back({t, (uint32_t)((uint64_t)W * k / gq), (uint32_t)((uint64_t)W * (k + 1) / gq), 0});
+        }
+        const uint64_t meta_bytes = 8 * (uint64_t)P + sizeof(SiUnit) * units.size() + 4 * (uint64_t)P +
+                                    4 * (uint64_t)P * W + 256;
+        S.meta.ensure(meta_bytes);
+        unsigned char *mb = S.meta.as<unsigned char>();
+        uint64_t *d_toff = reinterpret_cast<uint64_t *>(mb);
+        SiUnit *d_units = reinterpret_cast<SiUnit *>(d_toff + P);
+        uint32_t *d_cap = reinterpret_cast<uint32_t *>(d_units + units.size());
+        uint32_t *d_fills = d_cap + P;
+        VH_HIP(hipMemcpyAsync(d_toff, toff.data(), 8 * (uint64_t)P, hipMemcpyHostToDevice, st));
+        VH_HIP(hipMemcpyAsync(d_units, units.data(), sizeof(SiUnit) * units.size(), hipMemcpyHostToDevice, st));
+        VH_HIP(hipMemcpyAsync(d_cap, cap.data(), 4 * (uint64_t)P, hipMemcpyHostToDevice, st));
+        sp.W = W;
+        sp.rows_per_wg = rows_per_wg;
+        sp.wg_stride = stride;
+        sp.cap = d_cap;
+        sp.toff = d_toff;
+        sp.fills = d_fills;
+        sp.ent = S.ent.ptr;
+        sp.ent_row = S.ent_row.as<uint32_t>();
+    }
+    for (int attempt = 0;; attempt++) {
+        SiTable g{s->tab.as<uint64_t>(), s->cap - 1, s->cap / 4 * 3, s->ctr.as<uint64_t>()};
+        if (P == 1) {
+            TimedScope ts("set_insert");
+            int bpc = 1;
+            VH_DISPATCH_DTYPE(s->dtype, T,
+                              bpc = si_blocks_per_cu(reinterpret_cast<const void *>(k_si_direct<T>), SB_THREADS, lt_lds));
+            const uint64_t Wd = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cu_count() * bpc,
+                                                                          (n + 4 * SB_THREADS - 1) / (4 * SB_THREADS)));
+            sp.rows_per_wg = (n + Wd - 1) / Wd;
+            VH_DISPATCH_DTYPE(s->dtype, T,
+                              hipLaunchKernelGGL(k_si_direct<T>, dim3((unsigned)Wd), dim3(SB_THREADS), lt_lds, st, sp, g));
+            VH_HIP(hipGetLastError());
+        } else {
+            {
+                TimedScope ts("set_insert");
+                VH_DISPATCH_DTYPE(s->dtype, T,
+                                  hipLaunchKernelGGL(k_si_scatter<T>, dim3(W), dim3(SI_THREADS), si_scatter_lds_bytes(P),
+                                                     st, sp, g));
+                VH_HIP(hipGetLastError());
+            }
+            {
+                TimedScope ts("set_reduce");
+                const SiUnit *d_units = reinterpret_cast<const SiUnit *>(S.meta.as<uint64_t>() + P);
+                if (kbs == 8)
+                    hipLaunchKernelGGL(k_si_reduce<uint64_t>, dim3((unsigned)units.size()), dim3(SB_THREADS), lt_lds, st,
+                                       sp, g, d_units);
+                else
+                    hipLaunchKernelGGL(k_si_reduce<uint32_t>, dim3((unsigned)units.size()), dim3(SB_THREADS), lt_lds, st,
+                                       sp, g, d_units);
+                VH_HIP(hipGetLastError());
+            }
+        }
+        VH_HIP(hipMemcpyAsync(c.data(), s->ctr.ptr, 8 * C_N, hipMemcpyDeviceToHost, st));
+        VH_HIP(hipStreamSynchronize(st));
+        if (!c[C_OVERFLOW]) {
+            if (c[C_DISTINCT] * 2 > s->cap) set_grow(s, si_next_pow2(c[C_DISTINCT] * 2));
+            break;
+        }
+        // the estimate missed: grow x4 and re-run the chunk (inserts are idempotent; the
+        // special rows' counts of this chunk are taken back first)
+        if (attempt > 16) fail(VH_ERR_RUNTIME, "hash set could not grow enough");
+        set_grow(s, s->cap * 4);
+        uint64_t reset[C_N];
+        memcpy(reset, c.data(), sizeof(reset));
+        reset[C_OVERFLOW] = 0;
+        reset[C_NAN_COUNT] = s->nan_count_before;
+        reset[C_NULL_COUNT] = s->null_count_before;
+        VH_HIP(hipMemcpyAsync(s->ctr.ptr, reset, 8 * C_N, hipMemcpyHostToDevice, st));
+        VH_HIP(hipStreamSynchronize(st));
+    }
+}
+
+}  // namespace vh
+
 static void set_update(vh_set *s, const void *keys, const uint8_t *mask, const uint8_t *select, uint64_t n, int loc) {
     loc = resolve_loc(keys, loc);
     const int isz = dtype_itemsize(s->dtype);
-    // Chunks start at cap/4 rows and double after every chunk that did not need the table
-    // to grow, so a too-small table is found after a cheap chunk and a settled one is
-    // streamed in a few large launches.  Inside a launch, new keys past `limit` (3/4 of the
-    // capacity) are refused and flag overflow; the table then grows and the chunk re-runs.
-    const uint64_t stage_max = loc == VH_LOC_HOST ? (uint64_t(1) << 24) : ~0ULL;
-    uint64_t want = std::max<uint64_t>(s->cap / 4, 1 << 16);
-    for (uint64_t row0 = 0, len = 0; row0 < n; row0 += len) {
-        len = std::min({want, stage_max, n - row0});
-        const void *dk = reinterpret_cast<const char *>(keys) + row0 * isz;
-        const uint8_t *dm = mask ? mask + row0 : nullptr;
-        const uint8_t *ds = select ? select + row0 : nullptr;
+    // host keys are staged per 16 Mi rows; device keys are taken 2^28 rows at a time (the
+    // pass-A regions of a chunk are ~8 B per row)
+    const uint64_t CH = loc == VH_LOC_HOST ? (uint64_t(1) << 24) : (uint64_t(1) << 28);
+    SiScratch &S = si_scratch();
+    std::lock_guard<std::mutex> lk(S.mu);
+    for (uint64_t r0 = 0; r0 < n; r0 += CH) {
+        const uint64_t len = std::min(CH, n - r0);
+        const void *dk = reinterpret_cast<const char *>(keys) + r0 * isz;
+        const uint8_t *dm = mask ? mask + r0 : nullptr;
+        const uint8_t *ds = select ? select + r0 : nullptr;
         if (loc == VH_LOC_HOST) {
             s->stage_keys.ensure(len * isz);
             VH_HIP(hipMemcpyAsync(s->stage_keys.ptr, dk, len * isz, hipMemcpyHostToDevice, stream()));
@@ -475,32 +1129,15 @@ static void set_update(vh_set *s, const void *keys, const uint8_t *mask, const u
                 ds = s->stage_select.as<uint8_t>();
             }
         }
-        bool grew = false;
-        for (int attempt = 0;; attempt++) {
-            {
-                TimedScope ts("set_insert");
-                const uint64_t limit = s->cap / 4 * 3;
-                VH_DISPATCH_DTYPE(s->dtype, T,
-                                  hipLaunchKernelGGL(k_set_insert<T>, dim3(std::min<uint64_t>(blocks_for(len, 256), 1 << 16)),
-                                                     dim3(256), 0, stream(), reinterpret_cast<const T *>(dk), dm, ds, len,
-                                                     s->rows_seen + row0, s->tab.as<uint64_t>(), s->cap - 1, limit,
-                                                     s->ctr.as<uint64_t>()));
-                VH_HIP(hipGetLastError());
-            }
-            auto c = read_ctr(s);
-            const bool overflow = c[C_OVERFLOW] != 0;
-            if (overflow || c[C_DISTINCT] * 2 > s->cap) {
-                uint64_t nc = s->cap * 4;
-                while (c[C_DISTINCT] * 2 > nc) nc *= 2;
-                set_grow(s, nc);
-                grew = true;
-                uint64_t zero = 0;
-                VH_HIP(hipMemcpyAsync(s->ctr.as<uint64_t>() + C_OVERFLOW, &zero, 8, hipMemcpyHostToDevice, stream()));
-            }
-            if (!overflow) break;
-            if (attempt > 16) fail(VH_ERR_RUNTIME, "hash set could not grow enough");
+        // the chunk's NaN / null counts, restored if the chunk must be re-run
+        {
+            std::vector<uint64_t> c(C_N);
+            VH_HIP(hipMemcpyAsync(c.data(), s->ctr.ptr, 8 * C_N, hipMemcpyDeviceToHost, stream()));
+            VH_HIP(hipStreamSynchronize(stream()));
+            s->nan_count_before = c[C_NAN_COUNT];
+            s->null_count_before = c[C_NULL_COUNT];
         }
-        want = grew ? std::max<uint64_t>(want, s->cap / 4) : want * 2;
+        si_chunk(s, S, dk, dm, ds, len, s->rows_seen + r0);
     }
     s->rows_seen += n;
     {
@@ -509,7 +1146,6 @@ static void set_update(vh_set *s, const void *keys, const uint8_t *mask, const u
         if (c[C_NULL_FIRST] != ~0ULL && s->null_pos == ~0ULL) s->null_pos = s->rows_seen;
     }
     s->sealed = false;
-    VH_HIP(hipStreamSynchronize(stream()));
 }
 
 int vh_set_update(vh_set *s, const void *keys, const uint8_t *mask, uint64_t n, int loc) {

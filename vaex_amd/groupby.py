@@ -40,9 +40,11 @@ class Grouper(BinnerBase):
             nulls = np.zeros(len(values), bool)
             if oset.has_null:
                 nulls[oset.null_value] = True
-            # arrow-style sort: nulls last, NaN after numbers (groupby.py:137-156)
-            order = sorted(range(len(values)), key=lambda i: (bool(nulls[i]), _nan_key(values[i])))
-            order = np.asarray(order, dtype=np.int64)
+            # arrow-style sort: nulls last, NaN after numbers (groupby.py:137-156), as a
+            # stable radix argsort on the GPU; the null slot is moved to the end
+            order = _device_argsort(values)
+            if oset.has_null:
+                order = np.concatenate([order[order != oset.null_value], [oset.null_value]]).astype(np.int64)
             sorted_values = values[order]
             null_value = int(np.nonzero(nulls[order])[0][0]) if oset.has_null else -1
             oset = type(oset)(sorted_values.astype(oset._dtype), null_value, oset.nan_count, oset.null_count,
@@ -63,11 +65,17 @@ class Grouper(BinnerBase):
         return vals
 
 
-def _nan_key(v):
-    try:
-        return (1, 0) if v != v else (0, v)
-    except TypeError:
-        return (0, v)
+def _device_argsort(values):
+    """Stable ascending order of a key array (NaN last), computed on the GPU (vh_argsort)."""
+    from . import _lib
+    from .device import DeviceArray
+    values = np.ascontiguousarray(values)
+    if not len(values):
+        return np.empty(0, np.int64)
+    keys = DeviceArray.from_numpy(values)
+    out = DeviceArray(len(values), np.int64)
+    _lib.call("vh_argsort", len(values), keys.ptr, _lib.dtype_code(values.dtype)[0], out.ptr)
+    return out.to_numpy()
 
 
 # integer keys whose value range is at most this many cells are binned densely
