@@ -419,7 +419,8 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_sample(const K *keys, uint64_
 // distinct keys of the sample, and how many were seen once / twice (Chao1 inputs)
 __global__ __launch_bounds__(256) void k_ha_sample_stats(const uint32_t *scnt, uint64_t slots,
                                                          unsigned long long *stats) {
-    uint64_t d = 0, f1 = 0, f2 = 0;
+    __shared__ uint32_t part[3][4];
+    uint32_t d = 0, f1 = 0, f2 = 0;
     for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < slots; i += (uint64_t)gridDim.x * 256) {
         const uint32_t c = scnt[i];
         d += c != 0;
@@ -431,10 +432,15 @@ __global__ __launch_bounds__(256) void k_ha_sample_stats(const uint32_t *scnt, u
         f1 += __shfl_down(f1, off, 64);
         f2 += __shfl_down(f2, off, 64);
     }
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&stats[0], (unsigned long long)d);
-        atomicAdd(&stats[1], (unsigned long long)f1);
-        atomicAdd(&stats[2], (unsigned long long)f2);
+    if ((threadIdx.x & 63) == 0) {  // one atomic per block and counter, not per wave
+        part[0][threadIdx.x >> 6] = d;
+        part[1][threadIdx.x >> 6] = f1;
+        part[2][threadIdx.x >> 6] = f2;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const uint32_t v = part[threadIdx.x][0] + part[threadIdx.x][1] + part[threadIdx.x][2] + part[threadIdx.x][3];
+        if (v) atomicAdd(&stats[threadIdx.x], (unsigned long long)v);
     }
 }
 

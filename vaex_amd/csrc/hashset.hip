@@ -88,7 +88,7 @@ constexpr uint32_t SI_LT_MAX = 5120;          // close at 62.5 % (+ <= 1024 raci
 constexpr uint32_t SI_TARGET_KEYS = 4096;     // P: a bucket holds about this many keys
 constexpr uint32_t SI_FINE_LOG2 = 12;
 constexpr uint32_t SI_MAX_P_LOG2 = 11;
-constexpr int SI_SAMPLE_BLOCKS = 256;
+constexpr int SI_SAMPLE_BLOCKS = 128;
 constexpr uint32_t SI_DEST_OVER = 0x80000000u;
 constexpr uint32_t SI_ROW_NONE = 0xffffffffu;
 
@@ -105,12 +105,14 @@ struct SiParams {
     uint32_t *fills;       // [P][W]
     void *ent;             // <= 4-byte keys: u64 (row << 32 | key bits); else u64 key bits
     uint32_t *ent_row;     // 8-byte keys: the rows
+    uint32_t debug;        // experiment switches (VH_SI_DEBUG), 0 in production
 };
 
 struct SiTable {
     uint64_t *tab;
     uint64_t cap_mask, limit;
     uint64_t *ctr;
+    uint32_t *wg_new;  // the workgroup's LDS count of keys it inserted (added to C_DISTINCT once)
 };
 
 struct SiUnit {
@@ -123,20 +125,20 @@ __device__ inline uint32_t si_bucket(uint64_t kb, uint32_t p_log2) {
     return (uint32_t)(((uint64_t)si_h32(kb) << p_log2) >> 32);
 }
 
-// one distinct key (and the smallest row it was seen at) into the HBM table
+// One distinct key (and the smallest row it was seen at) into the HBM table.  The table was
+// sized for the sampled estimate at <= 1/2 load; a probe sequence longer than SET_MAX_PROBE
+// (the estimate missed and the table filled up) raises the overflow counter instead, and
+// the host grows the table and re-runs the chunk.  New keys are counted per workgroup in
+// LDS (one global add per workgroup: one counter bumped by every new key serialises).
 __device__ inline void si_global(const SiTable &g, uint64_t kb, uint64_t row) {
     uint64_t pos = hash64(kb) & g.cap_mask;
     for (int p = 0; p <= SET_MAX_PROBE; p++) {
         const uint64_t k = __hip_atomic_load(&g.tab[2 * pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         bool mine = k == kb;
         if (!mine && k == SET_EMPTY) {
-            if (__hip_atomic_load(&g.ctr[C_DISTINCT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= g.limit) {
-                atomicOr((unsigned long long *)&g.ctr[C_OVERFLOW], 1ULL);  // grow + re-run
-                return;
-            }
             const uint64_t old = atomicCAS((unsigned long long *)&g.tab[2 * pos], (unsigned long long)SET_EMPTY,
                                            (unsigned long long)kb);
-            if (old == SET_EMPTY) atomicAdd((unsigned long long *)&g.ctr[C_DISTINCT], 1ULL);
+            if (old == SET_EMPTY) atomicAdd(g.wg_new, 1u);
             mine = old == SET_EMPTY || old == kb;
         }
         if (mine) {
@@ -150,6 +152,18 @@ __device__ inline void si_global(const SiTable &g, uint64_t kb, uint64_t row) {
 }
 
 // ---- LDS dedup table: key bits -> smallest row (chunk-relative) ---------------------------
+// LDS slot hash: a 32-bit mixer (murmur3 fmix32), cheaper than hash64's 64-bit multiplies;
+// independent of the bucket bits (which come from hash64)
+__device__ inline uint32_t si_lds_hash(uint64_t kb) {
+    uint32_t h = (uint32_t)kb ^ (uint32_t)(kb >> 32) * 0x9e3779b9u;
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
+
 template <typename KB> __host__ __device__ constexpr KB si_empty() { return ~KB(0); }
 template <typename KB> __host__ __device__ constexpr KB si_closed() { return ~KB(0) - 1; }
 
@@ -198,7 +212,7 @@ __device__ inline void si_lt_add(const SiLds<KB> &t, const SiTable &g, uint64_t 
         atomicMin(&t.rows[SI_LT + (uint32_t)(kb - CLOSED)], row);
         return;
     }
-    uint32_t grp = ((uint32_t)hash64((uint64_t)kb) & (SI_LT - 1)) >> 2;
+    uint32_t grp = (si_lds_hash((uint64_t)kb) & (SI_LT - 1)) >> 2;
     for (;;) {
         const SiKB4<KB> q = *reinterpret_cast<const SiKB4<KB> *>(t.keys + 4 * grp);
         int hit = -1, fr = -1;
@@ -236,6 +250,36 @@ __device__ inline void si_lt_add(const SiLds<KB> &t, const SiTable &g, uint64_t 
             return;
         }
     }
+}
+
+// M entries at once: every home-group read is issued before any is used, hits take their
+// ds_min right away (no return value to wait for), and only entries whose key is not in
+// its home group (new keys, displaced keys, marker-valued keys) take si_lt_add's probe
+// loop -- one entry at a time a lane would wait an LDS round trip per entry.
+template <typename KB, int M>
+__device__ inline void si_lt_add_many(const SiLds<KB> &t, const SiTable &g, uint64_t row0, const KB *kb,
+                                      const uint32_t *row, const bool *valid) {
+    SiKB4<KB> q[M];
+    uint32_t base[M];
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+        base[i] = (si_lds_hash((uint64_t)kb[i]) & (SI_LT - 1)) & ~3u;
+        q[i] = *reinterpret_cast<const SiKB4<KB> *>(t.keys + base[i]);
+    }
+    bool slow[M];
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+        uint32_t slot = ~0u;
+#pragma unroll
+        for (int j = 3; j >= 0; j--)
+            if (q[i].v[j] == kb[i]) slot = base[i] + j;
+        if (kb[i] >= si_closed<KB>()) slot = ~0u;
+        slow[i] = valid[i] && slot == ~0u;
+        if (valid[i] && slot != ~0u) atomicMin(&t.rows[slot], row[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < M; i++)
+        if (slow[i]) si_lt_add<KB>(t, g, row0, kb[i], row[i]);
 }
 
 // every key the LDS table holds, with its smallest row, into the HBM table (after a barrier)
@@ -335,7 +379,8 @@ __global__ __launch_bounds__(SI_THREADS) void k_si_sample(SiParams sp, uint64_t 
 
 // distinct keys of the sample, and how many were seen once / twice (Chao1 inputs)
 __global__ __launch_bounds__(256) void k_si_sample_stats(const uint32_t *scnt, uint64_t slots, unsigned long long *stats) {
-    uint64_t d = 0, f1 = 0, f2 = 0;
+    __shared__ uint32_t part[3][4];
+    uint32_t d = 0, f1 = 0, f2 = 0;
     for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < slots; i += (uint64_t)gridDim.x * 256) {
         const uint32_t c = scnt[i];
         d += c != 0;
@@ -347,10 +392,15 @@ __global__ __launch_bounds__(256) void k_si_sample_stats(const uint32_t *scnt, u
         f1 += __shfl_down(f1, off, 64);
         f2 += __shfl_down(f2, off, 64);
     }
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&stats[0], (unsigned long long)d);
-        atomicAdd(&stats[1], (unsigned long long)f1);
-        atomicAdd(&stats[2], (unsigned long long)f2);
+    if ((threadIdx.x & 63) == 0) {  // one atomic per block and counter, not per wave
+        part[0][threadIdx.x >> 6] = d;
+        part[1][threadIdx.x >> 6] = f1;
+        part[2][threadIdx.x >> 6] = f2;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const uint32_t v = part[threadIdx.x][0] + part[threadIdx.x][1] + part[threadIdx.x][2] + part[threadIdx.x][3];
+        if (v) atomicAdd(&stats[threadIdx.x], (unsigned long long)v);
     }
 }
 
@@ -365,12 +415,22 @@ __device__ inline void si_lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
+__device__ inline void si_new_init(uint32_t *s_new) {
+    if (threadIdx.x == 0) *s_new = 0;
+}
+// after a workgroup barrier
+__device__ inline void si_new_flush(const uint32_t *s_new, uint64_t *ctr) {
+    if (threadIdx.x == 0 && *s_new) atomicAdd((unsigned long long *)&ctr[C_DISTINCT], (unsigned long long)*s_new);
+}
+
 template <typename T>
 __global__ __launch_bounds__(SI_THREADS) void k_si_scatter(SiParams sp, SiTable g) {
     using KB = si_kb_t<T>;
     extern __shared__ __align__(16) unsigned char lds_raw[];
     __shared__ SiSpecial spec;
-    __shared__ uint32_t s_total, s_over;
+    __shared__ uint32_t s_total, s_over, s_new;
+    g.wg_new = &s_new;
+    si_new_init(&s_new);
     uint64_t *skb = reinterpret_cast<uint64_t *>(lds_raw);           // [SI_BATCH + 1]
     uint32_t *srow = reinterpret_cast<uint32_t *>(skb + SI_BATCH + 1);  // [SI_BATCH + 1]
     uint32_t *sdst = srow + SI_BATCH + 1;                               // [SI_BATCH + 1]
@@ -474,6 +534,7 @@ __global__ __launch_bounds__(SI_THREADS) void k_si_scatter(SiParams sp, SiTable 
     __syncthreads();
     for (uint32_t t = threadIdx.x; t < P; t += SI_THREADS) sp.fills[(uint64_t)t * sp.W + w] = base[t] - (uint32_t)sp.toff[t];
     si_special_flush(&spec, sp.row0, g.ctr);
+    si_new_flush(&s_new, g.ctr);
 }
 
 // ---- pass B -------------------------------------------------------------------------------
@@ -482,6 +543,9 @@ __global__ __launch_bounds__(SB_THREADS) void k_si_reduce(SiParams sp, SiTable g
     extern __shared__ __align__(16) unsigned char lds_raw[];
     __shared__ uint32_t s_fill[1024];
     __shared__ uint32_t s_pre[1025];
+    __shared__ uint32_t s_new;
+    g.wg_new = &s_new;
+    si_new_init(&s_new);
     const SiUnit u = units[blockIdx.x];
     const uint32_t b = u.bucket;
     const uint32_t cap = sp.cap[b];
@@ -535,12 +599,17 @@ __global__ __launch_bounds__(SB_THREADS) void k_si_reduce(SiParams sp, SiTable g
                 row[j] = sp.ent_row[e];
             }
         }
+        if (sp.debug & 2) {
 #pragma unroll
-        for (int j = 0; j < SB_M; j++)
-            if (valid[j]) si_lt_add<KB>(t, g, sp.row0, kb[j], row[j]);
+            for (int j = 0; j < SB_M; j++) asm volatile("" ::"v"(kb[j]), "v"(row[j]));
+        } else {
+            si_lt_add_many<KB, SB_M>(t, g, sp.row0, kb, row, valid);
+        }
     }
     __syncthreads();
-    si_lt_merge<KB>(t, g, sp.row0, SB_THREADS);
+    if (!(sp.debug & 1)) si_lt_merge<KB>(t, g, sp.row0, SB_THREADS);
+    __syncthreads();
+    si_new_flush(&s_new, g.ctr);
 }
 
 // ---- direct (P == 1): each workgroup dedups its row range of the raw keys -----------------
@@ -549,6 +618,9 @@ __global__ __launch_bounds__(SB_THREADS) void k_si_direct(SiParams sp, SiTable g
     using KB = si_kb_t<T>;
     extern __shared__ __align__(16) unsigned char lds_raw[];
     __shared__ SiSpecial spec;
+    __shared__ uint32_t s_new;
+    g.wg_new = &s_new;
+    si_new_init(&s_new);
     const SiLds<KB> t = si_lt_layout<KB>(lds_raw);
     si_lt_init<KB>(t, SB_THREADS);
     si_special_init(&spec);
@@ -558,19 +630,22 @@ __global__ __launch_bounds__(SB_THREADS) void k_si_direct(SiParams sp, SiTable g
     constexpr int U = 4;
     for (uint64_t b0 = row_begin; b0 < row_end; b0 += (uint64_t)U * SB_THREADS) {
         KB kb[U];
+        uint32_t row[U];
         bool valid[U];
 #pragma unroll
         for (int r = 0; r < U; r++) {
             const uint64_t i = b0 + (uint64_t)r * SB_THREADS + threadIdx.x;
+            kb[r] = 0;
+            row[r] = (uint32_t)i;
             valid[r] = i < row_end && si_row<T>(sp, i, &spec, &kb[r]);
         }
-#pragma unroll
-        for (int r = 0; r < U; r++)
-            if (valid[r]) si_lt_add<KB>(t, g, sp.row0, kb[r], (uint32_t)(b0 + (uint64_t)r * SB_THREADS + threadIdx.x));
+        si_lt_add_many<KB, U>(t, g, sp.row0, kb, row, valid);
     }
     __syncthreads();
     si_lt_merge<KB>(t, g, sp.row0, SB_THREADS);
+    __syncthreads();
     si_special_flush(&spec, sp.row0, g.ctr);
+    si_new_flush(&s_new, g.ctr);
 }
 
 __global__ void k_set_rehash(const uint64_t *otab, uint64_t ocap, uint64_t *ntab, uint64_t ncap_mask) {
@@ -589,16 +664,25 @@ __global__ void k_set_rehash(const uint64_t *otab, uint64_t ocap, uint64_t *ntab
     }
 }
 
-__global__ void k_set_compact(const uint64_t *tab, uint64_t cap, uint64_t *slot, uint64_t *first, uint64_t *bits,
-                              uint64_t *ctr) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t kb = tab[2 * i];
-        if (kb == SET_EMPTY) continue;
-        const uint64_t j = atomicAdd((unsigned long long *)&ctr[C_CURSOR], 1ULL);
-        slot[j] = i;
-        first[j] = tab[2 * i + 1];
-        bits[j] = kb;
+__global__ __launch_bounds__(256) void k_set_compact(const uint64_t *tab, uint64_t cap, uint64_t *slot, uint64_t *first,
+                                                     uint64_t *bits, uint64_t *ctr) {
+    // one cursor add per wave (ballot + popcount), not per occupied slot
+    const int lane = threadIdx.x & 63;
+    const uint64_t step = (uint64_t)gridDim.x * 256;
+    for (uint64_t i0 = blockIdx.x * 256ull; i0 < cap; i0 += step) {
+        const uint64_t i = i0 + threadIdx.x;
+        const uint64_t kb = i < cap ? tab[2 * i] : SET_EMPTY;
+        const bool occ = kb != SET_EMPTY;
+        const uint64_t m = __ballot(occ);
+        uint64_t base = 0;
+        if (lane == 0 && m) base = atomicAdd((unsigned long long *)&ctr[C_CURSOR], (unsigned long long)__popcll(m));
+        base = __shfl(base, 0, 64);
+        if (occ) {
+            const uint64_t j = base + (uint64_t)__popcll(m & ((1ull << lane) - 1));
+            slot[j] = i;
+            first[j] = tab[2 * i + 1];
+            bits[j] = kb;
+        }
     }
 }
 
@@ -948,6 +1032,7 @@ static void si_chunk(vh_set *s, SiScratch &S, const void *keys, const uint8_t *m
     sp.select = select;
     sp.n = n;
     sp.row0 = row0;
+    if (const char *dbg = getenv("VH_SI_DEBUG")) sp.debug = (uint32_t)atoi(dbg);
     // ---- sample: fine bucket histogram + distinct estimate, read back with the counters
     const uint64_t sslots = 1ull << 21;
     const uint64_t nbatch = (n + SI_BATCH - 1) / SI_BATCH;
@@ -1019,6 +1104,8 @@ static void si_chunk(vh_set *s, SiScratch &S, const void *keys, const uint8_t *m
         const uint64_t total = stride * W;
         S.ent.ensure(8 * total + 64);
         if (kbs == 8) S.ent_row.ensure(4 * total + 64);
+        // pass-B units: a unit merges each of its keys into the HBM table once, so split a
+        // bucket over ranges of workgroups only as far as the CUs need work
         const double target = std::max(1.0, (double)n / ((double)cu_count() * 2));
         for (uint32_t t = 0; t < P; t++) {
             const double e = (double)n * (double)bh[t] / (double)std::max<uint64_t>(sampled, 1);
@@ -1047,7 +1134,7 @@ static void si_chunk(vh_set *s, SiScratch &S, const void *keys, const uint8_t *m
         sp.ent_row = S.ent_row.as<uint32_t>();
     }
     for (int attempt = 0;; attempt++) {
-        SiTable g{s->tab.as<uint64_t>(), s->cap - 1, s->cap / 4 * 3, s->ctr.as<uint64_t>()};
+        SiTable g{s->tab.as<uint64_t>(), s->cap - 1, s->cap / 4 * 3, s->ctr.as<uint64_t>(), nullptr};
         if (P == 1) {
             TimedScope ts("set_insert");
             int bpc = 1;
@@ -1104,9 +1191,9 @@ static void si_chunk(vh_set *s, SiScratch &S, const void *keys, const uint8_t *m
 static void set_update(vh_set *s, const void *keys, const uint8_t *mask, const uint8_t *select, uint64_t n, int loc) {
     loc = resolve_loc(keys, loc);
     const int isz = dtype_itemsize(s->dtype);
-    // host keys are staged per 16 Mi rows; device keys are taken 2^28 rows at a time (the
-    // pass-A regions of a chunk are ~8 B per row)
-    const uint64_t CH = loc == VH_LOC_HOST ? (uint64_t(1) << 24) : (uint64_t(1) << 28);
+    // host keys are staged per 16 Mi rows; device keys are taken 2^30 rows at a time (the
+    // pass-A regions of a chunk are ~8 B per row; each chunk merges every key once per unit)
+    const uint64_t CH = loc == VH_LOC_HOST ? (uint64_t(1) << 24) : (uint64_t(1) << 30);
     SiScratch &S = si_scratch();
     std::lock_guard<std::mutex> lk(S.mu);
     for (uint64_t r0 = 0; r0 < n; r0 += CH) {
