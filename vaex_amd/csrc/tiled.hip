@@ -407,7 +407,9 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
         const uint32_t kk = sk[k];
         const uint32_t t = kk >> 16;
         const uint32_t dest = l.dbase[t] + k;
-        if (dest < l.lim[t]) {
+        if (tp.debug & 128) {  // experiment: no region stores
+            asm volatile("" ::"v"(kk), "v"(dest));
+        } else if (dest < l.lim[t]) {
             const uint64_t e = region0 + dest;
             reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)kk;
 #pragma unroll
@@ -693,7 +695,11 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan
             const uint32_t t = c >> s_log2;
             key[r] = (t << 16) | (c & smask);
             rank[r] = -1;
-            if (f) rank[r] = (int32_t)atomicAdd(&l.hist[t], 1u);
+            if (tp.debug & 64) {  // experiment: no ranking
+                asm volatile("" ::"v"(key[r]), "v"(f));
+            } else if (f) {
+                rank[r] = (int32_t)atomicAdd(&l.hist[t], 1u);
+            }
         }
     };
     double2 cur[PAIRS][NC], nxt[PAIRS][NC];
@@ -714,7 +720,12 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan
 #pragma unroll
                     for (int c = 0; c < NC; c++) cur[q][c] = nxt[q][c];
         }
-        batch_commit_fast<NV, SB * TA_RPT>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
+        if (tp.debug & 32) {  // experiment: no commit (loads, cell math, ranking only)
+#pragma unroll
+            for (int r = 0; r < SB * TA_RPT; r++) asm volatile("" ::"v"(key[r]), "v"(rank[r]));
+        } else {
+            batch_commit_fast<NV, SB * TA_RPT>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
+        }
         if (!VH_TA_DRAIN)
 #pragma unroll
             for (int q = 0; q < PAIRS; q++)
