@@ -14,7 +14,8 @@ sys.path.insert(0, ROOT)
 from vaex_amd import _lib, superagg  # noqa: E402
 from vaex_amd.device import DeviceArray  # noqa: E402
 
-KERNELS = ["tile_sample", "tile_scatter_f64", "tile_scatter_ord", "tile_reduce", "minmax"]
+KERNELS = ["tile_sample", "tile_scatter_f64", "tile_scatter_ord", "tile_reduce", "minmax", "ha_sample",
+           "ha_scatter_f64", "ha_reduce", "ha_finish", "set_sample", "set_insert", "set_reduce"]
 
 
 def main():
@@ -31,7 +32,7 @@ def main():
     y = DeviceArray.random(n, "normal", seed=3)
     w = DeviceArray.random(n, "uniform", seed=4)
     workloads = a.workloads.split(",")
-    if "c3" in workloads:
+    if "c3" in workloads or "c3fused" in workloads or "c3set" in workloads:
         import vaex_amd
         keys = DeviceArray.random(n, "randint", seed=5, a=5, b=5 + 10 ** 6, dtype="int32")
         df3 = vaex_amd.from_arrays(key=keys, v=x)
@@ -39,6 +40,16 @@ def main():
     def step(wl):
         if wl == "c3":
             df3.groupby("key", agg={"v_sum": vaex_amd.agg.sum("v"), "v_count": vaex_amd.agg.count("v")})
+            return
+        if wl == "c3fused":
+            from vaex_amd.hashagg import HashAgg
+            ha = HashAgg(keys.dtype, [x.dtype], [True])
+            ha.update(keys, [x])
+            ha.finish()
+            return
+        if wl == "c3set":
+            from vaex_amd import superutils
+            superutils.ordered_set_int32().update(keys)
             return
         with_sum = wl == "c2sum"
         bx = superagg.BinnerScalar_float64("x", -4.0, 4.0, 1024)

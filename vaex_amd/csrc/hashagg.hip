@@ -58,6 +58,15 @@
 namespace vh {
 
 constexpr int HA_MAX_V = 2;
+// one value column with 8-byte keys: packed 16-byte {key, value} entries (one store / load);
+// with <= 4-byte keys the key and value arrays are separate, 12 bytes per entry instead of 16
+// (pass A and pass B run at the HBM read/write ceiling, so bytes are time)
+#ifndef VH_HA_PACK4
+#define VH_HA_PACK4 0
+#endif
+template <typename KB, int NV> __host__ __device__ constexpr bool ha_packed() {
+    return NV == 1 && (sizeof(KB) == 8 || VH_HA_PACK4);
+}
 constexpr int HA_THREADS = 512;            // pass A
 constexpr int HA_RPT = 8;
 constexpr int HA_BATCH = HA_THREADS * HA_RPT;
@@ -545,7 +554,7 @@ __device__ inline void ha_commit(const HaScatterLds<KB> &l, const HaParams &hp, 
         const uint64_t key = (uint64_t)l.sk[k];
         const bool ok = k < tot && !(dest & HA_DEST_OVERFLOW);
         const uint64_t e = ok ? region0 + dest : dummy;
-        if constexpr (NV == 1) {  // packed {key, value}: one 16-byte store per row
+        if constexpr (ha_packed<KB, NV>()) {  // packed {key, value}: one 16-byte store per row
             const uint64_t vbits = l.sv[k];
             reinterpret_cast<uint4 *>(hp.ent)[e] =
                 make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)vbits, (uint32_t)(vbits >> 32));
@@ -757,7 +766,7 @@ __global__ __launch_bounds__(HB_THREADS) void k_ha_reduce(HaParams hp, HaTable g
             while (s_pre[kr + 1] <= cc) kr++;
             const uint64_t e = (uint64_t)(u.w_begin + kr) * hp.wg_stride + toff_b + (cc - s_pre[kr]);
             valid[j] = c < E;
-            if constexpr (NV == 1) {
+            if constexpr (ha_packed<KB, NV>()) {
                 const uint4 q = reinterpret_cast<const uint4 *>(hp.ent)[e];
                 kb[j] = (KB)(((uint64_t)q.y << 32) | q.x);
                 vb[j][0] = ((uint64_t)q.w << 32) | q.z;
@@ -1164,7 +1173,7 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     }
     if (stride + rows_per_wg >= (uint64_t)HA_DEST_OVERFLOW) fail(VH_ERR_RUNTIME, "hashagg: region table too large");
     const uint64_t total = stride * W + (uint64_t)W * HA_THREADS;  // regions + dummy slots
-    if (nv == 1) {
+    if (nv == 1 && (kbs == 8 || VH_HA_PACK4)) {
         S.entries.ensure(16 * total + 64);  // packed {key, value} entries
     } else {
         S.entries.ensure((uint64_t)kbs * total + 16);
@@ -1197,7 +1206,7 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     hp.fills = d_fills;
     hp.ent = S.entries.ptr;
     hp.dummy0 = stride * W;
-    if (nv != 1)
+    if (!(nv == 1 && (kbs == 8 || VH_HA_PACK4)))
         for (int v = 0; v < nv; v++) hp.vbits[v] = S.vbits.as<uint64_t>() + (uint64_t)v * total;
     // the fast pass A: 4- or 8-byte keys, float64 values, 16-byte aligned columns; rows past
     // the last multiple of 8 go straight to the HBM table
