@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--host-rows", type=float, default=2e8,
                    help="rows of the PCIe-inclusive measurement (host numpy columns); 0 = skip")
     p.add_argument("--groupby-rows", type=float, default=1e9)
+    p.add_argument("--c4-rows", type=float, default=2e9,
+                   help="rows of the C4 leg (2D mean streamed from a memory-mapped HDF5 file); 0 = skip")
     p.add_argument("--check", action="store_true", help="verify size-independent properties")
     p.add_argument("--breakdown", action="store_true", help="print host-side timing of one step")
     return p.parse_args()
@@ -191,6 +193,8 @@ def main():
         extra["count_only"] = bench_count_only(x, y, n, bins, args)
     if rank == 0 and world == 1 and args.host_rows > 0:
         extra["host_columns"] = bench_host_columns(x, y, w, int(min(args.host_rows, n)), bins)
+    if rank == 0 and world == 1 and args.c4_rows > 0:
+        extra["c4"] = bench_c4(int(args.c4_rows), bins)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(x, y, w, n, bins, args.cpu_seconds)
@@ -322,6 +326,123 @@ def bench_host_columns(x, y, w, m, bins):
     t = min(times)
     ok = int(np.asarray(c).sum()) == m
     return {"rows": m, "seconds": t, "rows_per_s": m / t, "host_GBps": 24 * m / t / 1e9, "count_equal": ok}
+
+
+def h2d_peak(nbytes=1 << 30, reps=4):
+    """Host -> HBM copy rate of this box, the C4 leg's roofline: hipHostMalloc'd sources
+    copied to one HBM block as one 1 GiB copy, and as 4 back-to-back 256 MiB copies on 1, 2
+    and 4 streams (best of `reps` each); `pinned_GBps` is the best of those.  Measured with
+    the HIP runtime directly (ctypes), outside the library under test."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    hip.hipHostMalloc.argtypes = [ctypes.POINTER(vp), sz, ctypes.c_uint]
+    hip.hipMalloc.argtypes = [ctypes.POINTER(vp), sz]
+    hip.hipMemcpyAsync.argtypes = [vp, vp, sz, ctypes.c_int, vp]
+    hip.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(vp), ctypes.c_uint]
+    hip.hipStreamSynchronize.argtypes = [vp]
+    hip.hipFree.argtypes = [vp]
+    hip.hipHostFree.argtypes = [vp]
+    hip.hipStreamDestroy.argtypes = [vp]
+    src, dst = vp(), vp()
+    if hip.hipHostMalloc(ctypes.byref(src), nbytes, 0) or hip.hipMalloc(ctypes.byref(dst), nbytes):
+        return {"error": "allocation failed"}
+    ctypes.memset(src, 1, nbytes)
+    streams = [vp() for _ in range(4)]
+    for st in streams:
+        hip.hipStreamCreateWithFlags(ctypes.byref(st), 1)
+    out = {}
+    try:
+        for name, pieces, ns in (("1x1GiB", 1, 1), ("4x256MiB_1stream", 4, 1), ("4x256MiB_2streams", 4, 2),
+                                 ("4x256MiB_4streams", 4, 4)):
+            part = nbytes // pieces
+            best = float("inf")
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                for i in range(pieces):
+                    hip.hipMemcpyAsync(vp(dst.value + i * part), vp(src.value + i * part), part, 1, streams[i % ns])
+                for st in streams[:ns]:
+                    hip.hipStreamSynchronize(st)
+                best = min(best, time.perf_counter() - t0)
+            out[name] = round(nbytes / best / 1e9, 2)
+    finally:
+        for st in streams:
+            hip.hipStreamDestroy(st)
+        hip.hipFree(dst)
+        hip.hipHostFree(src)
+    out["pinned_GBps"] = max(out.values())
+    return out
+
+
+def bench_c4(rows, bins, repeats=2):
+    """C4's query on one GPU (BASELINE configs[3] per rank): mean(w, binby=[x, y], shape=1024)
+    over x, y, w float64 columns of `rows` rows in a vaex HDF5 file written by export_hdf5 and
+    opened with vaex_amd.open (memory-mapped; page cache warm), so every row crosses the host
+    link through the library's double-buffered pipeline.  Roofline: the box's measured pinned
+    host -> HBM rate.  Host-pipeline modes: 'bounce' (host threads copy each chunk into a
+    pinned bounce buffer, DMA from there), 'register_per_chunk' (each chunk's pages are
+    registered for its copy), 'pageable' (the runtime's pageable copy path) and
+    'registered_mapping' (the default: the file mapping is registered once, on first use,
+    and every chunk is DMA'd in place)."""
+    import shutil
+    import tempfile
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    nbytes = 24 * rows
+    out = {"rows": rows, "bytes": nbytes, "algorithmic_bytes_per_row": 24}
+    try:
+        with open("/proc/meminfo") as f:
+            avail = {l.split(":")[0]: int(l.split()[1]) * 1024 for l in f}.get("MemAvailable", 0)
+    except OSError:
+        avail = 0
+    cands = [d for d in ("/dev/shm", tempfile.gettempdir()) if os.path.isdir(d)]
+    where = next((d for d in cands if shutil.disk_usage(d).free > 1.15 * nbytes), None)
+    if where is None or avail < 2.2 * nbytes:
+        out["skipped"] = f"needs {2.2 * nbytes / 1e9:.0f} GB host memory and {1.15 * nbytes / 1e9:.0f} GB of file space"
+        return out
+    out["h2d"] = h2d_peak()
+    path = os.path.join(where, f"vaex_amd_c4_{os.getpid()}.hdf5")
+    try:
+        t0 = time.perf_counter()
+        cols = {"x": DeviceArray.random(rows, "normal", seed=12), "y": DeviceArray.random(rows, "normal", seed=13),
+                "w": DeviceArray.random(rows, "uniform", seed=14)}
+        vaex_amd.from_arrays(**cols).export_hdf5(path)
+        del cols
+        out["write_seconds"] = round(time.perf_counter() - t0, 2)
+        out["file_dir"] = where
+        df = vaex_amd.open(path)
+        lim = [[-4.0, 4.0], [-4.0, 4.0]]
+        modes = (("bounce", "0", "0"), ("register_per_chunk", "0", "1"), ("pageable", "0", "2"),
+                 ("registered_mapping", "1", "0"))
+        for mode, reg, pipe in modes:
+            os.environ["VH_HOST_REGISTER"], os.environ["VH_HOST_PIPE"] = reg, pipe
+            t0 = time.perf_counter()
+            df.mean("w", binby=["x", "y"], limits=lim, shape=bins)  # warm (page cache, pinned buffers)
+            first = time.perf_counter() - t0
+            ts = []
+            for _ in range(repeats):
+                t0 = time.perf_counter()
+                m = df.mean("w", binby=["x", "y"], limits=lim, shape=bins)
+                ts.append(time.perf_counter() - t0)
+            t = float(np.median(ts))
+            gbps = nbytes / t / 1e9
+            out[mode] = {"seconds": round(t, 4), "first_call_seconds": round(first, 4), "rows_per_s": rows / t,
+                         "host_GBps": round(gbps, 2), "frac_of_pinned_h2d": round(gbps / out["h2d"]["pinned_GBps"], 3),
+                         "finite_cells": int(np.isfinite(m).sum())}
+        os.environ.pop("VH_HOST_REGISTER", None)
+        os.environ.pop("VH_HOST_PIPE", None)
+        c = df.count(binby=["x", "y"], limits=lim, shape=bins, edges=True)
+        out["count_equal"] = int(np.asarray(c).sum()) == rows
+        best = max((m[0] for m in modes), key=lambda k: out[k]["host_GBps"])
+        out["best_mode"] = best
+        out["frac_of_pinned_h2d"] = out[best]["frac_of_pinned_h2d"]
+    finally:
+        os.environ.pop("VH_HOST_REGISTER", None)
+        os.environ.pop("VH_HOST_PIPE", None)
+        df = None
+        if os.path.exists(path):
+            os.remove(path)
+    return out
 
 
 def bench_groupby(n, args):

@@ -77,6 +77,11 @@ int vh_free(void *dptr);
 /* page-locked host blocks (cached; result arrays are read back through them) */
 int vh_host_alloc(void **ptr, uint64_t bytes);
 int vh_host_free(void *ptr, uint64_t bytes);
+/* Register a page-aligned host range (typically a column memory-mapped from a file) for
+ * direct DMA: host columns whose chunks lie inside it stream to HBM with no bounce copy.
+ * The range must stay mapped until vh_host_unregister(ptr) (which drains the device). */
+int vh_host_register(void *ptr, uint64_t bytes);
+int vh_host_unregister(void *ptr);
 int vh_memcpy_htod(void *dst, const void *src, uint64_t bytes);
 int vh_memcpy_dtoh(void *dst, const void *src, uint64_t bytes);
 int vh_memcpy_dtod(void *dst, const void *src, uint64_t bytes);

@@ -72,3 +72,35 @@ def test_c4_mean_1024_from_mapped_file(tmp_path, monkeypatch):
     assert got.shape == (1024, 1024)
     np.testing.assert_array_equal(np.isnan(got), np.isnan(exp))
     np.testing.assert_allclose(got, exp, rtol=1e-6, atol=1e-12)
+
+
+@pytest.mark.parametrize("reg,pipe", [("1", "0"), ("0", "0"), ("0", "1"), ("0", "2")])
+def test_host_pipe_modes(tmp_path, monkeypatch, reg, pipe):
+    """Every way a mapped column chunk reaches the DMA engine gives the oracle's answer:
+    the file mapping registered once (default), the pinned bounce buffer, per-chunk
+    registration, the runtime's pageable path.  The registration is dropped with the
+    last column array over the mapping."""
+    import gc
+    import vaex_amd
+    from vaex_amd import _lib, execution
+    monkeypatch.setattr(execution, "CHUNK_SIZE_HOST", 1 << 26)
+    monkeypatch.setenv("VH_HOST_REGISTER", reg)
+    monkeypatch.setenv("VH_HOST_PIPE", pipe)
+    rng = np.random.default_rng(14)
+    n = 9_000_017  # > 64 MiB per column, one partial pipe chunk
+    cols = {"x": rng.normal(size=n), "y": rng.normal(size=n), "w": rng.random(n)}
+    path = tmp_path / "modes.hdf5"
+    vaex_amd.from_arrays(**cols).export_hdf5(path)
+    df = vaex_amd.open(path)
+    lim = [[-4, 4], [-4, 4]]
+    got_s = df.sum("w", binby=["x", "y"], limits=lim, shape=300)
+    got_c = df.count(binby=["x", "y"], limits=lim, shape=300)
+    assert (len(_lib._MAPS) == 1) == (reg == "1")
+    bx = oracle.Binner("scalar", cols["x"], vmin=-4, vmax=4, bins=300)
+    by = oracle.Binner("scalar", cols["y"], vmin=-4, vmax=4, bins=300)
+    np.testing.assert_array_equal(got_c, oracle.extract_central_part(oracle.compute_grid([bx, by], "count")))
+    np.testing.assert_allclose(got_s, oracle.extract_central_part(oracle.compute_grid([bx, by], "sum", data=cols["w"])),
+                               rtol=1e-9, atol=1e-12)
+    del df
+    gc.collect()
+    assert not _lib._MAPS and not _lib._ROOTS

@@ -4,7 +4,10 @@ The product path has no fallback: if the HIP library is missing this module rais
 ``ImportError`` and every GPU entry point fails loudly.
 """
 import ctypes
+import mmap
 import os
+import threading
+import weakref
 
 import numpy as np
 
@@ -31,6 +34,8 @@ SIGNATURES = {
     "vh_free": (_i32, [_vp]),
     "vh_host_alloc": (_i32, [_p(_vp), _u64]),
     "vh_host_free": (_i32, [_vp, _u64]),
+    "vh_host_register": (_i32, [_vp, _u64]),
+    "vh_host_unregister": (_i32, [_vp]),
     "vh_memcpy_htod": (_i32, [_vp, _vp, _u64]),
     "vh_memcpy_dtoh": (_i32, [_vp, _vp, _u64]),
     "vh_memcpy_dtod": (_i32, [_vp, _vp, _u64]),
@@ -216,6 +221,59 @@ class _PinnedBlock:
         if getattr(self, "ptr", None):
             lib().vh_host_free(self.ptr, self.nbytes)
             self.ptr = None
+
+
+# ---- file mappings registered for direct DMA (vh_host_register) ------------------------
+_REG_LOCK = threading.RLock()  # re-entrant: a finalizer may run from GC inside the lock
+_MAPS = {}   # id(mmap) -> [address, live column count]
+_ROOTS = {}  # id(root column array) -> id(mmap), or None when registration failed
+
+
+def _release(key, mk):
+    with _REG_LOCK:
+        _ROOTS.pop(key, None)
+        ent = _MAPS.get(mk)
+        if ent is None:
+            return
+        ent[1] -= 1
+        if ent[1] == 0:
+            del _MAPS[mk]
+            lib().vh_host_unregister(ent[0])
+
+
+def host_register(a):
+    """Register the file mapping under a host column (vaex_amd.open maps HDF5 columns
+    with mmap) once, so the binning pipeline DMAs its chunks in place instead of copying
+    them into pinned bounce buffers.  The registration lives while any column array over
+    the mapping does (finalizers run before the arrays release the mapping).
+    VH_HOST_REGISTER=0 turns this off.  Returns True when `a` lies in a registered mapping."""
+    if os.environ.get("VH_HOST_REGISTER", "1") == "0" or not isinstance(a, np.ndarray) or a.nbytes < (64 << 20):
+        return False
+    root = a
+    while isinstance(root.base, np.ndarray):
+        root = root.base
+    mv = root.base
+    if not (isinstance(mv, memoryview) and isinstance(mv.obj, mmap.mmap)):
+        return False
+    key = id(root)
+    with _REG_LOCK:
+        if key in _ROOTS:
+            return _ROOTS[key] is not None
+        mm = mv.obj
+        mk = id(mm)
+        ent = _MAPS.get(mk)
+        if ent is None:
+            addr = np.frombuffer(mm, np.uint8).ctypes.data
+            if lib().vh_host_register(addr, len(mm)) != 0:
+                # e.g. more than the host can pin: the bounce-buffer pipeline streams it
+                _ROOTS[key] = None
+                weakref.finalize(root, _ROOTS.pop, key, None).atexit = False
+                return False
+            ent = _MAPS[mk] = [addr, 0]
+        ent[1] += 1
+        _ROOTS[key] = mk
+        weakref.finalize(root, _release, key, mk).atexit = False
+        return True
 
 
 def pinned_empty(n, dtype):

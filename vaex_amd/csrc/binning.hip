@@ -740,9 +740,28 @@ Workspace::~Workspace() = default;
 
 HostPipe::~HostPipe() {
     for (int b = 0; b < 2; b++) {
-        if (copied[b]) (void)hipEventDestroy(copied[b]);
+        if (copied[b]) {
+            (void)hipEventSynchronize(copied[b]);
+            release_registered(b);
+            (void)hipEventDestroy(copied[b]);
+        }
         if (consumed[b]) (void)hipEventDestroy(consumed[b]);
     }
+}
+
+void HostPipe::release_registered(int b) {
+    for (void *p : registered[b]) (void)hipHostUnregister(p);
+    registered[b].clear();
+}
+
+// How chunks of host columns outside a vh_host_register range reach the DMA engine
+// (VH_HOST_PIPE, read per chunk so a caller may switch it):
+//   0 (default) host threads copy the chunk into the pinned bounce buffer, DMA from there
+//   1 page-aligned chunks >= 1 MiB are registered for the copy and DMA'd in place
+//   2 the runtime's own pageable copy path
+static int host_pipe_mode() {
+    const char *e = getenv("VH_HOST_PIPE");
+    return e ? atoi(e) : 0;
 }
 
 void HostPipe::add(const ColumnRef &c) {
@@ -769,8 +788,8 @@ void HostPipe::plan(uint64_t chunk_rows) {
     for (int b = 0; b < 2; b++) {
         // the previous bin() call's copies and kernels are done (run_bin syncs at its end)
         pending_copy[b] = pending_use[b] = false;
-        pinned[b].ensure(bytes);
-        dev[b].ensure(bytes);
+        release_registered(b);
+        dev[b].ensure(bytes);  // the pinned bounce buffer is taken when a chunk needs it
         if (!copied[b]) VH_HIP(hipEventCreateWithFlags(&copied[b], hipEventDisableTiming));
         if (!consumed[b]) VH_HIP(hipEventCreateWithFlags(&consumed[b], hipEventDisableTiming));
     }
@@ -779,18 +798,43 @@ void HostPipe::plan(uint64_t chunk_rows) {
 void HostPipe::issue(uint64_t ci, uint64_t row0, uint64_t len) {
     static const int threads = [] {
         const char *e = getenv("VH_COPY_THREADS");
-        return e ? std::max(1, atoi(e)) : 8;
+        return e ? std::max(1, atoi(e)) : 16;
     }();
     const int b = (int)(ci & 1);
     hipStream_t cs = copy_stream();
-    if (pending_copy[b]) VH_HIP(hipEventSynchronize(copied[b]));  // bounce buffer b drained
-    for (size_t i = 0; i < cols.size(); i++)
-        parallel_memcpy(pinned[b].as<char>() + off[i], reinterpret_cast<const char *>(cols[i]) + row0 * isz[i],
-                        len * isz[i], threads);
+    if (pending_copy[b]) {
+        VH_HIP(hipEventSynchronize(copied[b]));  // bounce buffer b drained
+        release_registered(b);
+    }
+    // the DMA source of each column: its registered pages, or the pinned bounce buffer
+    std::vector<const char *> src(cols.size());
+    const uint64_t page = 4096;
+    for (size_t i = 0; i < cols.size(); i++) {
+        const char *p = reinterpret_cast<const char *>(cols[i]) + row0 * isz[i];
+        const uint64_t bytes = len * isz[i];
+        src[i] = nullptr;
+        const int mode = host_pipe_mode();
+        if (host_registered(p, bytes) || mode == 2) {
+            src[i] = p;
+        } else if (mode == 1 && (reinterpret_cast<uintptr_t>(p) % page) == 0 && bytes >= (1u << 20)) {
+            const uint64_t rb = (bytes + page - 1) / page * page;
+            hipError_t e = hipHostRegister(const_cast<char *>(p), rb, hipHostRegisterReadOnly);
+            if (e == hipSuccess) {
+                registered[b].push_back(const_cast<char *>(p));
+                src[i] = p;
+            } else {
+                (void)hipGetLastError();
+            }
+        }
+        if (!src[i]) {
+            pinned[b].ensure(this->bytes);
+            parallel_memcpy(pinned[b].as<char>() + off[i], p, bytes, threads);
+            src[i] = pinned[b].as<char>() + off[i];
+        }
+    }
     if (pending_use[b]) VH_HIP(hipStreamWaitEvent(cs, consumed[b], 0));  // chunk ci-2 binned
     for (size_t i = 0; i < cols.size(); i++)
-        VH_HIP(hipMemcpyAsync(dev[b].as<char>() + off[i], pinned[b].as<char>() + off[i], len * isz[i],
-                              hipMemcpyHostToDevice, cs));
+        VH_HIP(hipMemcpyAsync(dev[b].as<char>() + off[i], src[i], len * isz[i], hipMemcpyHostToDevice, cs));
     VH_HIP(hipEventRecord(copied[b], cs));
     pending_copy[b] = true;
 }

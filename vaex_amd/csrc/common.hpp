@@ -147,6 +147,7 @@ template <typename T> __device__ inline bool is_nan_v(T v) {
 hipStream_t stream();
 hipStream_t copy_stream();  // H2D staging copies (overlap the compute stream)
 void parallel_memcpy(void *dst, const void *src, uint64_t bytes, int threads);
+bool host_registered(const void *p, uint64_t bytes);  // inside a vh_host_register range
 int current_device();
 int cu_count();
 
@@ -205,6 +206,9 @@ struct DevBuf {
     template <typename T> T *as() const { return reinterpret_cast<T *>(ptr); }
 };
 
+void *host_block_alloc(uint64_t bytes);  // page-locked, from the library's block cache
+void host_block_free(void *ptr, uint64_t bytes);
+
 // page-locked host buffer (DMA source of the H2D staging pipeline)
 struct PinnedBuf {
     void *ptr = nullptr;
@@ -214,19 +218,14 @@ struct PinnedBuf {
     PinnedBuf &operator=(const PinnedBuf &) = delete;
     ~PinnedBuf() { release(); }
     void release() {
-        if (ptr) (void)hipHostFree(ptr);
+        if (ptr) host_block_free(ptr, bytes);
         ptr = nullptr;
         bytes = 0;
     }
     void ensure(uint64_t b) {
         if (b <= bytes) return;
         release();
-        hipError_t e = hipHostMalloc(&ptr, b, hipHostMallocDefault);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            ptr = nullptr;
-            fail(VH_ERR_NOMEM, "hipHostMalloc of " + std::to_string(b) + " bytes failed: " + hipGetErrorString(e));
-        }
+        ptr = host_block_alloc(b);
         bytes = b;
     }
     template <typename T> T *as() const { return reinterpret_cast<T *>(ptr); }

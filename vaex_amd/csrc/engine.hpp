@@ -88,7 +88,11 @@ struct HostPipe {
     DevBuf dev[2];
     hipEvent_t copied[2] = {nullptr, nullptr}, consumed[2] = {nullptr, nullptr};
     bool pending_copy[2] = {false, false}, pending_use[2] = {false, false};
+    // page-aligned column ranges registered with the runtime for a direct DMA (memory-mapped
+    // files: the page cache is the DMA source, no bounce copy), per buffer until its copy ends
+    std::vector<void *> registered[2];
     ~HostPipe();
+    void release_registered(int b);
     void add(const ColumnRef &c);
     void plan(uint64_t chunk_rows);
     void issue(uint64_t ci, uint64_t row0, uint64_t len);  // stage chunk ci into buffer ci & 1

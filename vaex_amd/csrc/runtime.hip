@@ -35,8 +35,8 @@ int current_device() {
 
 // ---- device block cache (common.hpp) ---------------------------------------------------
 namespace {
-constexpr uint64_t CACHE_MAX_BLOCK = 256ull << 20;
-constexpr uint64_t CACHE_MAX_BYTES = 2ull << 30;
+constexpr uint64_t CACHE_MAX_BLOCK = 1ull << 30;
+constexpr uint64_t CACHE_MAX_BYTES = 4ull << 30;
 struct BlockCache {
     std::multimap<uint64_t, void *> free;
     uint64_t cached = 0;
@@ -97,15 +97,51 @@ void dev_free(void *ptr, uint64_t bytes) {
 // ---- pinned host block cache (vh_host_alloc / vh_host_free) ---------------------------
 // Result arrays (grids, groupby columns) are read back through page-locked blocks: a
 // pageable D2H runs at ~5-10 GB/s, page-locked at PCIe/xGMI rate, and hipHostMalloc itself
-// is slow, so freed blocks are kept (sizes rounded to 64 KiB, <= 1 GiB cached).
+// (and hipHostFree) are slow, so freed blocks are kept (sizes rounded to 64 KiB, <= 2 GiB
+// cached); the host pipeline's bounce buffers come from the same cache.
 namespace {
-constexpr uint64_t HCACHE_MAX_BYTES = 1ull << 30;
+constexpr uint64_t HCACHE_MAX_BYTES = 2ull << 30;
 std::mutex g_hcache_mu;
 std::multimap<uint64_t, void *> g_hcache;
 uint64_t g_hcached = 0;
 }  // namespace
 
 static uint64_t host_round(uint64_t bytes) { return (std::max<uint64_t>(bytes, 1) + 65535) & ~uint64_t(65535); }
+
+void *host_block_alloc(uint64_t bytes) {
+    const uint64_t b = host_round(bytes);
+    {
+        std::lock_guard<std::mutex> lk(g_hcache_mu);
+        auto it = g_hcache.find(b);
+        if (it != g_hcache.end()) {
+            void *p = it->second;
+            g_hcache.erase(it);
+            g_hcached -= b;
+            return p;
+        }
+    }
+    void *p = nullptr;
+    hipError_t e = hipHostMalloc(&p, b, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        fail(VH_ERR_NOMEM, "hipHostMalloc of " + std::to_string(b) + " bytes failed: " + hipGetErrorString(e));
+    }
+    return p;
+}
+
+void host_block_free(void *ptr, uint64_t bytes) {
+    if (!ptr) return;
+    const uint64_t b = host_round(bytes);
+    {
+        std::lock_guard<std::mutex> lk(g_hcache_mu);
+        if (g_hcached + b <= HCACHE_MAX_BYTES) {
+            g_hcache.emplace(b, ptr);
+            g_hcached += b;
+            return;
+        }
+    }
+    (void)hipHostFree(ptr);
+}
 
 hipStream_t stream() {
     int d = current_device();
@@ -116,6 +152,20 @@ hipStream_t stream() {
     VH_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     g_streams[d] = s;
     return s;
+}
+
+// ---- registered host ranges (vh_host_register): the host pipeline DMAs column chunks that
+// lie inside one in place, with no bounce copy and no per-chunk registration
+static std::mutex g_reg_mu;
+static std::map<uintptr_t, uintptr_t> g_reg;  // start -> end
+
+bool host_registered(const void *p, uint64_t bytes) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg.upper_bound(a);
+    if (it == g_reg.begin()) return false;
+    --it;
+    return a >= it->first && a + bytes <= it->second;
 }
 
 static std::map<int, hipStream_t> g_copy_streams;
@@ -390,40 +440,43 @@ int vh_free(void *dptr) {
 
 int vh_host_alloc(void **ptr, uint64_t bytes) {
     VH_API_BEGIN
-    const uint64_t b = host_round(bytes);
-    {
-        std::lock_guard<std::mutex> lk(g_hcache_mu);
-        auto it = g_hcache.find(b);
-        if (it != g_hcache.end()) {
-            *ptr = it->second;
-            g_hcache.erase(it);
-            g_hcached -= b;
-            return VH_OK;
-        }
-    }
-    void *p = nullptr;
-    hipError_t e = hipHostMalloc(&p, b, hipHostMallocDefault);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        fail(VH_ERR_NOMEM, "hipHostMalloc of " + std::to_string(b) + " bytes failed");
-    }
-    *ptr = p;
+    *ptr = host_block_alloc(bytes);
     VH_API_END
 }
 
 int vh_host_free(void *ptr, uint64_t bytes) {
     VH_API_BEGIN
-    if (!ptr) return VH_OK;
-    const uint64_t b = host_round(bytes);
-    {
-        std::lock_guard<std::mutex> lk(g_hcache_mu);
-        if (g_hcached + b <= HCACHE_MAX_BYTES) {
-            g_hcache.emplace(b, ptr);
-            g_hcached += b;
-            return VH_OK;
-        }
+    host_block_free(ptr, bytes);
+    VH_API_END
+}
+
+int vh_host_register(void *ptr, uint64_t bytes) {
+    VH_API_BEGIN
+    if (!ptr || !bytes) fail(VH_ERR_ARG, "vh_host_register: empty range");
+    const uintptr_t page = 4096, a = reinterpret_cast<uintptr_t>(ptr);
+    if (a % page) fail(VH_ERR_ARG, "vh_host_register: start must be page aligned");
+    const uint64_t len = (bytes + page - 1) / page * page;
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg.upper_bound(a + len - 1);
+    if (it != g_reg.begin() && std::prev(it)->second > a) fail(VH_ERR_ARG, "vh_host_register: range overlaps a registered one");
+    hipError_t e = hipHostRegister(ptr, len, hipHostRegisterReadOnly);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        fail(VH_ERR_NOMEM, std::string("hipHostRegister failed: ") + hipGetErrorString(e));
     }
-    VH_HIP(hipHostFree(ptr));
+    g_reg[a] = a + len;
+    VH_API_END
+}
+
+int vh_host_unregister(void *ptr) {
+    VH_API_BEGIN
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == g_reg.end()) fail(VH_ERR_ARG, "vh_host_unregister: not a registered range");
+    // copies from the range were issued on the library's streams; drain them first
+    VH_HIP(hipDeviceSynchronize());
+    g_reg.erase(it);
+    VH_HIP(hipHostUnregister(ptr));
     VH_API_END
 }
 

@@ -22,7 +22,10 @@ from .device import DeviceArray
 from .tasks import TaskAggregation, TaskAggregations, TaskMinMax, TaskSetCreate
 from .taskparts import TaskPartAggregation, TaskPartMinMax, TaskPartSetCreate
 
-CHUNK_SIZE_HOST = int(os.environ.get("VAEX_AMD_CHUNK_SIZE", 16 * 1024 * 1024))
+# rows per task pass over host (memory-mapped / numpy) columns: each pass is one bin() call,
+# inside which the library double-buffers 16 Mi-row pipe chunks (copy of chunk i+1 under the
+# kernels of chunk i); a pass of 16 pipe chunks leaves only its first copy exposed
+CHUNK_SIZE_HOST = int(os.environ.get("VAEX_AMD_CHUNK_SIZE", 256 * 1024 * 1024))
 
 
 def _env_chunk_size():

@@ -455,6 +455,12 @@ class _Writer:
         self.parts.append(("array", arr))
         return at
 
+    def put_device(self, col):
+        """an HBM column, read back in pieces when the file is written (never whole in RAM)"""
+        at = self.alloc(len(col) * col.dtype.itemsize, _ALIGN)
+        self.parts.append(("device", col))
+        return at
+
 
 def _object_header(messages):
     body = b"".join(messages)
@@ -501,16 +507,23 @@ def export_hdf5(df, path):
         col = df.columns.get(name)
         if col is None:
             col = df.evaluate(name)
-        if isinstance(col, DeviceArray):
-            col = col.to_numpy()
-        col = np.asarray(col)
-        if col.ndim != 1 or col.dtype.kind not in "biuf":
-            raise HDF5Error(f"column {name!r} of dtype {col.dtype} cannot be exported")
-        store = col.view(np.uint8) if col.dtype.kind == "b" else col
-        data_at = w.put_array(np.ascontiguousarray(store))
-        dmsgs = [_msg(0x01, _dataspace(len(col))), _msg(0x03, _datatype(col.dtype), flags=1),
+        if isinstance(col, DeviceArray) and np.dtype(col.dtype).kind in "iuf":
+            store = col
+            data_at = w.put_device(col)
+            col = np.empty(0, col.dtype)  # dtype / kind for the header below
+            nbytes, length = len(store) * store.dtype.itemsize, len(store)
+        else:
+            if isinstance(col, DeviceArray):
+                col = col.to_numpy()
+            col = np.asarray(col)
+            if col.ndim != 1 or col.dtype.kind not in "biuf":
+                raise HDF5Error(f"column {name!r} of dtype {col.dtype} cannot be exported")
+            store = col.view(np.uint8) if col.dtype.kind == "b" else col
+            data_at = w.put_array(np.ascontiguousarray(store))
+            nbytes, length = store.nbytes, len(col)
+        dmsgs = [_msg(0x01, _dataspace(length)), _msg(0x03, _datatype(col.dtype), flags=1),
                  _msg(0x05, struct.pack("<BBBB", 2, 2, 0, 0), flags=1),
-                 _msg(0x08, struct.pack("<BBQQ", 3, 1, data_at, store.nbytes))]
+                 _msg(0x08, struct.pack("<BBQQ", 3, 1, data_at, nbytes))]
         if col.dtype.kind == "b":
             dmsgs.append(_msg(0x0C, _string_attr("dtype", "bool")))
         data_hdr = w.put(_object_header(dmsgs))
@@ -538,6 +551,10 @@ def export_hdf5(df, path):
                 f.write(b"\x00" * item)
             elif kind == "bytes":
                 f.write(item)
+            elif kind == "device":
+                step = max(1, (256 << 20) // item.dtype.itemsize)
+                for i in range(0, len(item), step):
+                    item[i:i + step].to_numpy().tofile(f)
             else:
                 item.tofile(f)
         f.truncate(w.size)

@@ -37,6 +37,7 @@ def _column(ar):
     if a.ndim == 1 and not a.flags.c_contiguous:
         a = np.ascontiguousarray(a)
     length = len(a) if a.ndim >= 1 else a.size
+    _lib.host_register(a)
     return a.ctypes.data, length, a.itemsize, a.ndim, _lib.LOC_HOST, a
 
 
