@@ -471,10 +471,13 @@ def bench_groupby(n, args):
         if mode == "fused":
             ha = HashAgg(keys.dtype, [v.dtype], [False])
             ha.update(keys, [v])
-            return len(ha.finish()[0])
+            k, c, s, _ = ha.finish()
+            return k, c, s[0]
         dfg = df.groupby("key", agg={"v": ["sum", "count"]}, assume_sparse="auto" if mode == "auto" else True)
-        return len(dfg["key"].to_numpy())
+        return dfg["key"].to_numpy(), dfg["v_count"].to_numpy(), dfg["v_sum"].to_numpy()
 
+    v_total = float(vaex_amd.from_arrays(v=v).sum("v"))  # independent 0-d reduction
+    ref_groups = None
     for mode in ("auto", "fused", "hash"):
         run(mode)  # warm-up
         _lib.trace_report()
@@ -490,7 +493,7 @@ def bench_groupby(n, args):
             if prof:
                 prof.enable()
             t0 = time.perf_counter()
-            groups = run(mode)
+            res = run(mode)
             _lib.synchronize()
             times.append(time.perf_counter() - t0)
             if prof:
@@ -507,7 +510,20 @@ def bench_groupby(n, args):
             c, ms = _lib.timing_read(k)
             if c:
                 per[k] = round(ms, 3)
-        out[mode] = {"groups": groups, "seconds": t, "rows_per_s": n / t, "algorithmic_GBps": 12 * n / t / 1e9,
+        # outside the timed region: full-size properties of the last result -- every row
+        # counted once, the sum total against an independent reduction, routes agree
+        gk, gc, gs = (np.asarray(a) for a in res)
+        order = np.argsort(gk, kind="stable")
+        check = {"count_total": int(gc.sum()), "count_equal": int(gc.sum()) == n,
+                 "sum_rel_err": abs(float(gs.sum(dtype=np.float64)) - v_total) / abs(v_total)}
+        if ref_groups is None:
+            ref_groups = (gk[order], gc[order])
+        else:
+            check["same_groups_as_auto"] = bool(np.array_equal(gk[order], ref_groups[0])
+                                                and np.array_equal(gc[order], ref_groups[1]))
+        check["ok"] = check["count_equal"] and check["sum_rel_err"] < 1e-6 and check.get("same_groups_as_auto", True)
+        groups = len(gk)
+        out[mode] = {"groups": groups, "check": check, "seconds": t, "rows_per_s": n / t, "algorithmic_GBps": 12 * n / t / 1e9,
                      "kernel_ms_last": per}
     del keys, v, df
     return out

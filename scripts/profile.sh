@@ -6,7 +6,7 @@ TAG=${1:-r01}
 ROWS=${2:-1e9}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-ARGS="--rows $ROWS --steps 3 --warmup 1 --no-cpu-baseline --host-rows 0 --groupby-rows $ROWS"
+ARGS="--rows $ROWS --steps 3 --warmup 1 --no-cpu-baseline --host-rows 0 --c4-rows 0 --groupby-rows $ROWS"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
 rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/fetch -o run -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1
