@@ -18,7 +18,7 @@
 //             to per-(w, bucket) regions (the tile-partition scheme of tiled.hip with
 //             buckets for tiles).
 //   pass B -- work unit = (bucket, range of pass-A workgroups): the unit's entries are
-//             aggregated in an LDS open-address table (4-slot groups, CAS insert,
+//             aggregated in an LDS table (two-choice 4-slot groups, CAS insert,
 //             ds_add_u64 / ds_add_f64), then merged into one HBM open-address table with
 //             global atomics (one merge per distinct key per unit, not per row).
 //   finish -- occupied HBM slots are compacted, radix-sorted by key (rocPRIM) and
@@ -29,14 +29,14 @@
 // the raw columns straight into its LDS table ("direct").
 //
 // Key bits KB: uint32_t for keys of <= 4 bytes (the value as int32 / uint32), uint64_t for
-// 8-byte keys.  The two all-ones patterns of KB mark EMPTY / CLOSED LDS slots; keys with
-// those bits (e.g. -1, -2) live in two side records.  The HBM table stores keys as uint64
+// 8-byte keys.  The all-ones pattern of KB marks an EMPTY LDS slot; keys with the top two
+// patterns (e.g. -1, -2) live in two side records.  The HBM table stores keys as uint64
 // (EMPTY = all ones); an 8-byte key with that pattern lives in a side slot after the table.
 //
-// Overflow, never wrong results: an LDS table that reaches max_used distinct keys is
-// closed -- a key not yet in it is aggregated straight into the HBM table.  The decision
-// is made by a CAS on the key's first empty probe slot (key or CLOSED), so every key is
-// either wholly in the LDS table or wholly in the HBM path.  A pass-A region that is full
+// Overflow, never wrong results: a row whose key finds both of its LDS groups full is
+// aggregated straight into the HBM table (a key may so be split between an LDS record and
+// the HBM table, or between two LDS records: every record merges into the key's one HBM
+// slot with atomics).  A pass-A region that is full
 // (a sampling miss) also adds its rows to the HBM table directly.  An HBM table that grows
 // past 3/4 full is rehashed x4 after the update; one that fills up fails the update
 // (VH_ERR_RUNTIME) and the caller falls back to the ordered_set path.
@@ -74,7 +74,6 @@ constexpr int HB_THREADS = 1024;           // pass B / direct
 constexpr int HB_M = 8;                    // entries per lane per pass-B step
 constexpr uint32_t LT_SLOTS_LOG2 = 12;     // LDS table: 4096 slots (+2 special records)
 constexpr uint32_t LT_SLOTS = 1u << LT_SLOTS_LOG2;
-constexpr uint32_t LT_MAX_USED = 2560;     // close the LDS table at 62.5 % (+ <= 1024 racing inserts)
 constexpr uint32_t LT_TARGET_KEYS = 2300;  // P is chosen so a bucket holds about this many keys
 constexpr uint32_t HA_FINE_LOG2 = 12;      // sample histogram: top 12 hash bits
 constexpr uint32_t HA_MAX_P_LOG2 = 11;
@@ -184,7 +183,7 @@ template <int NV> __device__ inline void ha_global_row(const HaTable &g, uint64_
 // Per slot: key bits; one 64-bit counter word holding count(*) << 32 | non-NaN count of
 // value 0 (one ds_add_u64 updates both: a unit holds < 2^32 rows); the value sums; the
 // non-NaN count of value 1.  Records LT_SLOTS and LT_SLOTS + 1 hold the keys whose bits
-// are the CLOSED and EMPTY markers.
+// are the two top patterns (kb_closed, kb_empty).
 template <typename KB> struct LdsTable {
     KB *keys;                           // [LT_SLOTS]
     unsigned long long *cn;             // [LT_SLOTS + 2]
@@ -256,90 +255,94 @@ __device__ inline uint64_t lt_cas(uint64_t *p, uint64_t cmp, uint64_t val) {
     return atomicCAS(reinterpret_cast<unsigned long long *>(p), (unsigned long long)cmp, (unsigned long long)val);
 }
 
-// aggregate one entry into the LDS table (or, when its table is closed to it, the HBM table).
-// Bucketised linear probing: the key hashes to a group of 4 slots, read at once; a key
-// lives at the first free slot of its group sequence at insert time, so a probe ends at a
-// hit, or at the first EMPTY (CAS: insert, or CLOSED once the table is full) / CLOSED slot.
-// At ~50 % load a wave of 64 lanes needs ~2 group reads, where one-slot linear probing
-// waits on the longest of 64 chains.
-template <typename KB, int NV>
-__device__ inline void lt_add(const LdsTable<KB> &t, const HaTable &g, KB kb, const uint64_t *vb) {
-    constexpr KB EMPTY = kb_empty<KB>(), CLOSED = kb_closed<KB>();
-    uint32_t slot;
-    if (kb >= CLOSED) {
-        slot = LT_SLOTS + (uint32_t)(kb - CLOSED);
-    } else {
-        uint32_t grp = (ha_h(kb) & (LT_SLOTS - 1)) >> 2;
-        for (;;) {
-            const KB4<KB> q = *reinterpret_cast<const KB4<KB> *>(t.keys + 4 * grp);
-            int hit = -1, fr = -1;
-#pragma unroll
-            for (int j = 3; j >= 0; j--) {
-                if (q.v[j] == kb) hit = j;
-                if (q.v[j] >= CLOSED) fr = j;
-            }
-            if (hit >= 0 && (fr < 0 || hit < fr)) {
-                slot = 4 * grp + hit;
-                break;
-            }
-            if (fr < 0) {
-                grp = (grp + 1) & (LT_SLOTS / 4 - 1);
-                continue;
-            }
-            if (q.v[fr] == CLOSED) {
-                ha_global_row<NV>(g, (uint64_t)kb, vb);
-                return;
-            }
-            const uint32_t pos = 4 * grp + fr;
-            const bool open = *reinterpret_cast<volatile uint32_t *>(t.used) < LT_MAX_USED;
-            const KB cur = lt_cas(&t.keys[pos], EMPTY, open ? kb : CLOSED);
-            if (cur == EMPTY) {
-                if (!open) {
-                    ha_global_row<NV>(g, (uint64_t)kb, vb);
-                    return;
-                }
-                atomicAdd(t.used, 1u);
-                slot = pos;
-                break;
-            }
-            if (cur == kb) {
-                slot = pos;
-                break;
-            }
-            // another key took the slot: re-read the same group
-        }
-    }
-    lt_bump<KB, NV>(t, g, slot, vb);
+// Two-choice LDS table: a key lives in one of two 4-slot groups (g1 from its hash, g2 from a
+// second mix of it), so a lookup reads both groups at once and almost never needs more:
+// with ~2300 keys in 1024 groups the less loaded of two groups is rarely full (one-group
+// linear probing displaced ~5 % of keys, and the lanes holding them serialised every wave:
+// 4.6 of pass B's 7.3 ms, VH_HA_DEBUG ablation).  Insertion CASes the first EMPTY slot of
+// the group with more room; two lanes inserting one new key at once may place it in both
+// groups -- harmless, both records merge into the same HBM slot.  A key whose two groups are
+// full aggregates straight into the HBM table.  Keys whose bits are EMPTY / CLOSED live in
+// the two side records.
+template <typename KB> __device__ inline void lt2_groups(KB kb, uint32_t &g1, uint32_t &g2) {
+    const uint32_t h = ha_h(kb);
+    g1 = (h & (LT_SLOTS - 1)) >> 2;
+    g2 = (fmix32(h ^ 0x9e3779b9u) & (LT_SLOTS - 1)) >> 2;
 }
 
-// M entries at once: all home-group reads are issued together and the hits aggregated
-// with fire-and-forget LDS atomics; only entries whose key is not in its home group
-// (new keys, displaced keys, specials) take lt_add's probe loop.  One entry at a time, a
-// lane would wait an LDS round trip per entry.
+template <typename KB> __device__ inline uint32_t lt2_find(const KB4<KB> &q1, const KB4<KB> &q2, uint32_t g1, uint32_t g2,
+                                                         KB kb) {
+    uint32_t slot = ~0u;
+#pragma unroll
+    for (int j = 3; j >= 0; j--) {
+        if (q2.v[j] == kb) slot = 4 * g2 + j;
+        if (q1.v[j] == kb) slot = 4 * g1 + j;
+    }
+    return slot;
+}
+
+// a key not found in either group: insert it (or find it, if another lane just did)
+template <typename KB, int NV>
+__device__ inline void lt2_insert(const LdsTable<KB> &t, const HaTable &g, KB kb, const uint64_t *vb) {
+    constexpr KB EMPTY = kb_empty<KB>();
+    uint32_t g1, g2;
+    lt2_groups(kb, g1, g2);
+    for (int it = 0; it < 64; it++) {
+        const KB4<KB> q1 = *reinterpret_cast<const KB4<KB> *>(t.keys + 4 * g1);
+        const KB4<KB> q2 = *reinterpret_cast<const KB4<KB> *>(t.keys + 4 * g2);
+        const uint32_t hit = lt2_find(q1, q2, g1, g2, kb);
+        if (hit != ~0u) {
+            lt_bump<KB, NV>(t, g, hit, vb);
+            return;
+        }
+        int e1 = 0, e2 = 0, f1 = -1, f2 = -1;
+#pragma unroll
+        for (int j = 3; j >= 0; j--) {
+            if (q1.v[j] == EMPTY) {
+                e1++;
+                f1 = j;
+            }
+            if (q2.v[j] == EMPTY) {
+                e2++;
+                f2 = j;
+            }
+        }
+        if (e1 == 0 && e2 == 0) break;
+        const uint32_t pos = e1 >= e2 ? 4 * g1 + f1 : 4 * g2 + f2;
+        const KB cur = lt_cas(&t.keys[pos], EMPTY, kb);
+        if (cur == EMPTY || cur == kb) {
+            lt_bump<KB, NV>(t, g, pos, vb);
+            return;
+        }
+        // another key took the slot: read the groups again
+    }
+    ha_global_row<NV>(g, (uint64_t)kb, vb);
+}
+
+// M entries at once: both group reads of every entry are issued together and the hits
+// aggregated with fire-and-forget LDS atomics; only keys new to the table take lt2_insert.
 template <typename KB, int NV, int M>
-__device__ inline void lt_add_many(const LdsTable<KB> &t, const HaTable &g, const KB *kb,
-                                   const uint64_t (*vb)[NV > 0 ? NV : 1], const bool *valid) {
-    KB4<KB> q[M];
+__device__ inline void lt2_add_many(const LdsTable<KB> &t, const HaTable &g, const KB *kb,
+                                    const uint64_t (*vb)[NV > 0 ? NV : 1], const bool *valid) {
+    KB4<KB> q1[M], q2[M];
+    uint32_t g1[M], g2[M];
 #pragma unroll
     for (int i = 0; i < M; i++) {
-        const uint32_t grp = (ha_h(kb[i]) & (LT_SLOTS - 1)) >> 2;
-        q[i] = *reinterpret_cast<const KB4<KB> *>(t.keys + 4 * grp);
+        lt2_groups(kb[i], g1[i], g2[i]);
+        q1[i] = *reinterpret_cast<const KB4<KB> *>(t.keys + 4 * g1[i]);
+        q2[i] = *reinterpret_cast<const KB4<KB> *>(t.keys + 4 * g2[i]);
     }
     bool slow[M];
 #pragma unroll
     for (int i = 0; i < M; i++) {
-        const uint32_t base = (ha_h(kb[i]) & (LT_SLOTS - 1)) & ~3u;
-        uint32_t slot = ~0u;
-#pragma unroll
-        for (int j = 3; j >= 0; j--)
-            if (q[i].v[j] == kb[i]) slot = base + j;
-        if (kb[i] >= kb_closed<KB>()) slot = ~0u;
+        uint32_t slot = lt2_find(q1[i], q2[i], g1[i], g2[i], kb[i]);
+        if (kb[i] >= kb_closed<KB>()) slot = LT_SLOTS + (uint32_t)(kb[i] - kb_closed<KB>());
         slow[i] = valid[i] && slot == ~0u;
         if (valid[i] && slot != ~0u) lt_bump<KB, NV>(t, g, slot, vb[i]);
     }
 #pragma unroll
     for (int i = 0; i < M; i++)
-        if (slow[i]) lt_add<KB, NV>(t, g, kb[i], vb[i]);
+        if (slow[i]) lt2_insert<KB, NV>(t, g, kb[i], vb[i]);
 }
 
 // merge the LDS table into the HBM table (after a workgroup barrier)
@@ -370,7 +373,7 @@ struct HaParams {
     const void *keys;
     const void *vals[HA_MAX_V];
     int32_t vdtype[HA_MAX_V];
-    uint32_t p_log2, P, W, pad;
+    uint32_t p_log2, P, W, debug;  // debug: VH_HA_DEBUG experiment switches, 0 in production
     uint64_t n, rows_per_wg, wg_stride;
     const uint32_t *cap;   // [P]
     const uint64_t *toff;  // [P]
@@ -700,6 +703,142 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_f64(HaParams hp, HaTa
         hp.fills[(uint64_t)t * hp.W + w] = l.base[t] - (uint32_t)hp.toff[t];
 }
 
+// Pass A for 4-byte keys and NV <= 1 float64 values (the C3 shape), after the tile path's
+// fast scatter (tiled.hip k_tile_scatter_ord): SB batches of 4096 rows are ranked before
+// one commit, so a bucket's run per commit is SB times longer -- with P = 512 buckets a
+// 4096-row commit leaves ~8 rows per bucket, and such short runs are partial cache lines
+// that HBM receives twice (PMC: 18.7 GB written for 12 GB of entries).  LDS holds only the
+// staged key bits and values (12 B per row); a staged row's bucket is recomputed from its
+// key at stream-out, and one wave's scan turns the histogram into sorted offsets, the
+// destination bases and the advanced region bases (three LDS barriers per commit).
+__host__ __device__ constexpr size_t ha_fast_lds_bytes(int nv, int sb, uint32_t P) {
+    return (size_t)(8 * nv + 4) * sb * HA_BATCH + 20 * ((size_t)P + 1) + 64;
+}
+
+template <typename K, int NV, int SB>
+__global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTable g) {
+    static_assert(sizeof(K) == 4 && NV <= 1, "4-byte keys, at most one float64 value");
+    constexpr int PAIRS = HA_RPT / 2;
+    constexpr uint32_t CAP = SB * HA_BATCH;
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const uint32_t P = hp.P;
+    double *sv = reinterpret_cast<double *>(lds_raw);
+    uint32_t *sk = reinterpret_cast<uint32_t *>(lds_raw + (size_t)8 * NV * CAP);
+    uint32_t *hist = sk + CAP;  // [P + 1]: hist[P] takes the ranks of rows past the range
+    uint32_t *boff = hist + P + 1, *dbase = boff + P, *base = dbase + P, *lim = base + P;
+    uint32_t *wave_sums = lim + P;
+    for (uint32_t t = threadIdx.x; t <= P; t += HA_THREADS) hist[t] = 0;
+    for (uint32_t t = threadIdx.x; t < P; t += HA_THREADS) {
+        base[t] = (uint32_t)hp.toff[t];
+        lim[t] = (uint32_t)hp.toff[t] + hp.cap[t];
+    }
+    __syncthreads();
+    const uint32_t w = blockIdx.x;
+    const uint64_t n = hp.n;
+    const uint64_t row_begin = (uint64_t)w * hp.rows_per_wg;
+    const uint64_t row_end = min(n, row_begin + hp.rows_per_wg);
+    const uint64_t region0 = (uint64_t)w * hp.wg_stride;
+    const K *keys = static_cast<const K *>(hp.keys);
+    const double *vcol = static_cast<const double *>(hp.vals[0]);
+    uint32_t *ekeys = static_cast<uint32_t *>(hp.ent);
+    uint64_t *evals = hp.vbits[0];
+    struct Regs {
+        uint2 k[PAIRS];
+        double2 v[PAIRS][NV > 0 ? NV : 1];
+    };
+    // branch-free pair loads: n is a multiple of 8 here and workgroup ranges are multiples
+    // of HA_BATCH, so a pair is wholly inside the range or past it (clamped, then dropped)
+    auto load = [&](uint64_t b0, Regs &R) {
+#pragma unroll
+        for (int q = 0; q < PAIRS; q++) {
+            const uint64_t i = b0 + 2 * ((uint64_t)q * HA_THREADS + threadIdx.x);
+            const uint64_t is = i < n - 2 ? i : n - 2;
+            R.k[q] = *reinterpret_cast<const uint2 *>(keys + is);
+            if constexpr (NV > 0) R.v[q][0] = *reinterpret_cast<const double2 *>(vcol + is);
+        }
+    };
+    auto rows = [&](uint64_t b0, const Regs &cur, uint32_t *kb, int32_t *rank, double *vals) {
+#pragma unroll
+        for (int r = 0; r < HA_RPT; r++) {
+            const int q = r >> 1, h = r & 1;
+            const uint64_t i = b0 + 2 * ((uint64_t)q * HA_THREADS + threadIdx.x) + h;
+            kb[r] = ha_kb(__builtin_bit_cast(K, h ? cur.k[q].y : cur.k[q].x));
+            if constexpr (NV > 0) vals[r] = h ? cur.v[q][0].y : cur.v[q][0].x;
+            const uint32_t t = ha_bucket(hp, kb[r]);
+            const uint32_t rk = atomicAdd(&hist[i < row_end ? t : P], 1u);
+            rank[r] = i < row_end ? (int32_t)rk : -1;
+        }
+    };
+    Regs cur, nxt;
+    load(row_begin, cur);
+    for (uint64_t b0 = row_begin; b0 < row_end; b0 += CAP) {
+        uint32_t kb[SB * HA_RPT];
+        int32_t rank[SB * HA_RPT];
+        double vals[SB * HA_RPT];
+#pragma unroll
+        for (int sb = 0; sb < SB; sb++) {
+            load(b0 + (uint64_t)(sb + 1) * HA_BATCH, nxt);
+            rows(b0 + (uint64_t)sb * HA_BATCH, cur, kb + sb * HA_RPT, rank + sb * HA_RPT, vals + sb * HA_RPT);
+            cur = nxt;
+        }
+        // B1: every rank taken -> wave 0 scans the histogram
+        ha_lds_barrier();
+        if (threadIdx.x < 64) {
+            const uint32_t lane = threadIdx.x;
+            const uint32_t per = (P + 63) / 64;
+            const uint32_t t0 = lane * per;
+            uint32_t s = 0;
+            for (uint32_t t = t0; t < t0 + per && t < P; t++) s += hist[t];
+            uint32_t inc = s;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(inc, off, 64);
+                if ((int)lane >= off) inc += y;
+            }
+            uint32_t acc = inc - s;
+            for (uint32_t t = t0; t < t0 + per && t < P; t++) {
+                const uint32_t hh = hist[t], b = base[t];
+                boff[t] = acc;
+                dbase[t] = b - acc;
+                base[t] = b + hh;
+                hist[t] = 0;
+                acc += hh;
+            }
+            if (lane == 0) hist[P] = 0;
+            if (lane == 63) wave_sums[0] = inc;
+        }
+        // B2: rows stage their key bits and values at their sorted positions
+        ha_lds_barrier();
+        const uint32_t tot = wave_sums[0];
+#pragma unroll
+        for (int r = 0; r < SB * HA_RPT; r++) {
+            if (rank[r] < 0) continue;
+            const uint32_t pos = boff[ha_bucket(hp, kb[r])] + (uint32_t)rank[r];
+            sk[pos] = kb[r];
+            if constexpr (NV > 0) sv[pos] = vals[r];
+        }
+        // B3: the sorted runs stream to the regions; a full region (sampling miss) sends
+        // its rows to the HBM table
+        ha_lds_barrier();
+        for (uint32_t k = threadIdx.x; k < tot; k += HA_THREADS) {
+            const uint32_t key = sk[k];
+            const uint32_t t = ha_bucket(hp, key);
+            const uint32_t dest = dbase[t] + k;
+            if (dest < lim[t]) {
+                const uint64_t e = region0 + dest;
+                ekeys[e] = key;
+                if constexpr (NV > 0) evals[e] = __builtin_bit_cast(uint64_t, sv[k]);
+            } else {
+                uint64_t vb[NV > 0 ? NV : 1];
+                if constexpr (NV > 0) vb[0] = __builtin_bit_cast(uint64_t, sv[k]);
+                ha_global_row<NV>(g, (uint64_t)key, vb);
+            }
+        }
+    }
+    ha_lds_barrier();
+    for (uint32_t t = threadIdx.x; t < P; t += HA_THREADS) hp.fills[(uint64_t)t * hp.W + w] = base[t] - (uint32_t)hp.toff[t];
+}
+
 // rows [row0, n) straight into the HBM table (the < 8-row tail of the fast pass A)
 template <typename K, int NV>
 __global__ __launch_bounds__(64) void k_ha_tail(HaParams hp, HaTable g, uint64_t row0) {
@@ -753,32 +892,62 @@ __global__ __launch_bounds__(HB_THREADS) void k_ha_reduce(HaParams hp, HaTable g
     }
     __syncthreads();
     const uint32_t E = s_pre[nw];
+    if (E == 0) return;  // uniform: the fetch below clamps to entry E - 1
     const uint64_t toff_b = hp.toff[b];
     uint32_t kr = 0;  // region of this lane's current entry (entry indices of a lane only grow)
-    for (uint32_t c0 = 0; c0 < E; c0 += HB_THREADS * HB_M) {
+    struct Batch {
         KB kb[HB_M];
         uint64_t vb[HB_M][NV > 0 ? NV : 1];
         bool valid[HB_M];
+    };
+    auto fetch = [&](uint32_t c0, Batch &B) {
 #pragma unroll
         for (int j = 0; j < HB_M; j++) {
             const uint32_t c = c0 + j * HB_THREADS + threadIdx.x;
             const uint32_t cc = c < E ? c : E - 1;
             while (s_pre[kr + 1] <= cc) kr++;
             const uint64_t e = (uint64_t)(u.w_begin + kr) * hp.wg_stride + toff_b + (cc - s_pre[kr]);
-            valid[j] = c < E;
+            B.valid[j] = c < E;
             if constexpr (ha_packed<KB, NV>()) {
                 const uint4 q = reinterpret_cast<const uint4 *>(hp.ent)[e];
-                kb[j] = (KB)(((uint64_t)q.y << 32) | q.x);
-                vb[j][0] = ((uint64_t)q.w << 32) | q.z;
+                B.kb[j] = (KB)(((uint64_t)q.y << 32) | q.x);
+                B.vb[j][0] = ((uint64_t)q.w << 32) | q.z;
             } else {
-                kb[j] = reinterpret_cast<const KB *>(hp.ent)[e];
+                B.kb[j] = reinterpret_cast<const KB *>(hp.ent)[e];
 #pragma unroll
-                for (int v = 0; v < NV; v++) vb[j][v] = hp.vbits[v][e];
+                for (int v = 0; v < NV; v++) B.vb[j][v] = hp.vbits[v][e];
             }
         }
-        lt_add_many<KB, NV, HB_M>(t, g, kb, vb, valid);
+    };
+    auto process = [&](const Batch &B) {
+        if (hp.debug & 1) {  // experiment: entry stream only (wrong results)
+#pragma unroll
+            for (int j = 0; j < HB_M; j++) asm volatile("" ::"v"(B.kb[j]), "v"(B.vb[j][0]));
+        } else {
+            constexpr int MM = sizeof(KB) == 4 ? HB_M / 2 : HB_M / 4;  // 128 VGPRs at 1024 threads
+#pragma unroll
+            for (int h0 = 0; h0 < HB_M; h0 += MM) lt2_add_many<KB, NV, MM>(t, g, B.kb + h0, B.vb + h0, B.valid + h0);
+        }
+    };
+    constexpr uint32_t STEP = HB_THREADS * HB_M;
+    if constexpr (sizeof(KB) == 4 && NV <= 1) {
+        // 4-byte keys: the next batch's entries load while this one is aggregated
+        Batch cur, nxt;
+        fetch(0, cur);
+        for (uint32_t c0 = 0; c0 < E; c0 += STEP) {
+            fetch(c0 + STEP, nxt);
+            process(cur);
+            cur = nxt;
+        }
+    } else {
+        for (uint32_t c0 = 0; c0 < E; c0 += STEP) {
+            Batch cur;
+            fetch(c0, cur);
+            process(cur);
+        }
     }
     __syncthreads();
+    if (hp.debug & 1) return;
     lt_merge<KB, NV>(t, g, HB_THREADS);
 }
 
@@ -809,7 +978,7 @@ __global__ __launch_bounds__(HB_THREADS) void k_ha_direct(HaParams hp, HaTable g
                 for (int v = 0; v < NV; v++) vb[r][v] = ha_load_val(hp.vals[v], hp.vdtype[v], i);
             }
         }
-        lt_add_many<KB, NV, U>(t, g, kb, vb, valid);
+        lt2_add_many<KB, NV, U>(t, g, kb, vb, valid);
     }
     __syncthreads();
     lt_merge<KB, NV>(t, g, HB_THREADS);
@@ -1125,6 +1294,7 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
         hp.vdtype[v] = h->vdtype[v];
     }
     hp.n = n;
+    if (const char *dbg = getenv("VH_HA_DEBUG")) hp.debug = (uint32_t)atoi(dbg);
     hp.p_log2 = p_log2;
     hp.P = 1u << p_log2;
     const size_t lt_lds = lt_bytes(nv, kbs);
@@ -1151,12 +1321,53 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     for (uint32_t i = 0; i < FINE; i++) bh[i >> (HA_FINE_LOG2 - p_log2)] += fh[i];
 
     // ---- pass A geometry
-    const size_t lds_a = ha_scatter_lds_bytes(nv, kbs, P);
+    // the fast pass A: 4- or 8-byte keys, float64 values, 16-byte aligned columns; rows past
+    // the last multiple of 8 go straight to the HBM table.  4-byte keys with at most one
+    // value take the multi-batch commit (k_ha_scatter_k4) with as many batches per commit
+    // as the LDS holds (VH_HA_K4=0: the one-batch kernel, for A/B runs).
+    const int kisz = dtype_itemsize(h->key_dtype);
+    bool fast = (kisz == 4 || kisz == 8) && aligned16(keys) && n >= 8;
+    for (int v = 0; v < nv; v++) fast = fast && h->vdtype[v] == VH_F64 && aligned16(vals[v]);
+#ifndef VH_HA_K4_DEFAULT
+#define VH_HA_K4_DEFAULT 1
+#endif
+    static const bool k4_on = [] {
+        const char *e = getenv("VH_HA_K4");
+        return e ? atoi(e) != 0 : VH_HA_K4_DEFAULT != 0;
+    }();
+    const bool k4 = fast && k4_on && kisz == 4 && nv <= 1;
+    int sb = 0;
+    if (k4)
+        for (sb = 3; sb > 1 && ha_fast_lds_bytes(nv, sb, P) > 160 * 1024; sb--) {
+        }
+    const size_t lds_a = k4 ? ha_fast_lds_bytes(nv, sb, P) : ha_scatter_lds_bytes(nv, kbs, P);
     int bpc = 1;
-    VH_DISPATCH_KEY(h->key_dtype, K, dispatch_nv(nv, [&](auto nvc) {
-        constexpr int NV = decltype(nvc)::value;
-        bpc = blocks_per_cu(reinterpret_cast<const void *>(k_ha_scatter<K, NV>), HA_THREADS, lds_a);
-    }));
+    auto k4_kernel = [&](auto kc, auto nvc, auto sbc) {
+        using K = decltype(kc);
+        constexpr int NV = decltype(nvc)::value, SB = decltype(sbc)::value;
+        return reinterpret_cast<const void *>(k_ha_scatter_k4<K, NV, SB>);
+    };
+    auto with_k4 = [&](auto &&f) {  // f(kernel instance) for this key type / NV / SB
+        auto by_sb = [&](auto kc, auto nvc) {
+            if (sb == 3) f(kc, nvc, std::integral_constant<int, 3>());
+            else if (sb == 2) f(kc, nvc, std::integral_constant<int, 2>());
+            else f(kc, nvc, std::integral_constant<int, 1>());
+        };
+        auto by_nv = [&](auto kc) {
+            if (nv == 1) by_sb(kc, std::integral_constant<int, 1>());
+            else by_sb(kc, std::integral_constant<int, 0>());
+        };
+        if (h->key_dtype == VH_I32) by_nv(int32_t());
+        else by_nv(uint32_t());
+    };
+    if (k4) {
+        with_k4([&](auto kc, auto nvc, auto sbc) { bpc = blocks_per_cu(k4_kernel(kc, nvc, sbc), HA_THREADS, lds_a); });
+    } else {
+        VH_DISPATCH_KEY(h->key_dtype, K, dispatch_nv(nv, [&](auto nvc) {
+            constexpr int NV = decltype(nvc)::value;
+            bpc = blocks_per_cu(reinterpret_cast<const void *>(k_ha_scatter<K, NV>), HA_THREADS, lds_a);
+        }));
+    }
     bpc = std::min(bpc, 4);
     const uint32_t W = std::min<uint32_t>(1024, (uint32_t)cu_count() * bpc);
     const uint64_t rows_per_wg = ((n + W - 1) / W + HA_BATCH - 1) / HA_BATCH * HA_BATCH;
@@ -1208,16 +1419,23 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     hp.dummy0 = stride * W;
     if (!(nv == 1 && (kbs == 8 || VH_HA_PACK4)))
         for (int v = 0; v < nv; v++) hp.vbits[v] = S.vbits.as<uint64_t>() + (uint64_t)v * total;
-    // the fast pass A: 4- or 8-byte keys, float64 values, 16-byte aligned columns; rows past
-    // the last multiple of 8 go straight to the HBM table
-    const int kisz = dtype_itemsize(h->key_dtype);
-    bool fast = (kisz == 4 || kisz == 8) && aligned16(keys) && n >= 8;
-    for (int v = 0; v < nv; v++) fast = fast && h->vdtype[v] == VH_F64 && aligned16(vals[v]);
     {
         TimedScope ts(fast ? "ha_scatter_f64" : "ha_scatter");
         if (fast) {
             const uint64_t n8 = n & ~uint64_t(7);
             hp.n = n8;
+            if (k4) {
+                with_k4([&](auto kc, auto nvc, auto sbc) {
+                    using K = decltype(kc);
+                    constexpr int NV = decltype(nvc)::value, SB = decltype(sbc)::value;
+                    hipLaunchKernelGGL((k_ha_scatter_k4<K, NV, SB>), dim3(W), dim3(HA_THREADS), lds_a, st, hp, g);
+                    if (n8 < n) {
+                        HaParams ht = hp;
+                        ht.n = n;
+                        hipLaunchKernelGGL((k_ha_tail<K, NV>), dim3(1), dim3(64), 0, st, ht, g, n8);
+                    }
+                });
+            }
             auto launch = [&](auto kc) {
                 using K = decltype(kc);
                 dispatch_nv(nv, [&](auto nvc) {
@@ -1230,7 +1448,7 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
                     }
                 });
             };
-            switch (h->key_dtype) {
+            if (!k4) switch (h->key_dtype) {
             case VH_I32: launch(int32_t()); break;
             case VH_U32: launch(uint32_t()); break;
             case VH_I64: launch(int64_t()); break;
