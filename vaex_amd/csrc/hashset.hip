@@ -84,7 +84,6 @@ constexpr int SB_THREADS = 1024;
 constexpr int SB_M = 8;                   // entries per lane per pass-B step
 constexpr uint32_t SI_LT_LOG2 = 13;
 constexpr uint32_t SI_LT = 1u << SI_LT_LOG2;  // LDS table slots (+2 side records)
-constexpr uint32_t SI_LT_MAX = 5120;          // close at 62.5 % (+ <= 1024 racing inserts)
 constexpr uint32_t SI_TARGET_KEYS = 4096;     // P: a bucket holds about this many keys
 constexpr uint32_t SI_FINE_LOG2 = 12;
 constexpr uint32_t SI_MAX_P_LOG2 = 11;
@@ -200,86 +199,91 @@ __device__ inline uint64_t si_cas(uint64_t *p, uint64_t cmp, uint64_t val) {
     return atomicCAS(reinterpret_cast<unsigned long long *>(p), (unsigned long long)cmp, (unsigned long long)val);
 }
 
-// Bucketised linear probing over groups of 4 slots (one ds_read_b128 for 4-byte keys): a
-// key lives at the first free slot of its group sequence, so a probe ends at a hit or at
-// the first EMPTY (CAS) / CLOSED slot.  Past SI_LT_MAX keys the table closes: EMPTY slots a
-// new key reaches become CLOSED and the key goes to the HBM table (every key is wholly in
-// the LDS table or wholly in the HBM path; the min over both is the same).
-template <typename KB>
-__device__ inline void si_lt_add(const SiLds<KB> &t, const SiTable &g, uint64_t row0, KB kb, uint32_t row) {
-    constexpr KB EMPTY = si_empty<KB>(), CLOSED = si_closed<KB>();
-    if (kb >= CLOSED) {
-        atomicMin(&t.rows[SI_LT + (uint32_t)(kb - CLOSED)], row);
-        return;
-    }
-    uint32_t grp = (si_lds_hash((uint64_t)kb) & (SI_LT - 1)) >> 2;
-    for (;;) {
-        const SiKB4<KB> q = *reinterpret_cast<const SiKB4<KB> *>(t.keys + 4 * grp);
-        int hit = -1, fr = -1;
-#pragma unroll
-        for (int j = 3; j >= 0; j--) {
-            if (q.v[j] == kb) hit = j;
-            if (q.v[j] >= CLOSED) fr = j;
-        }
-        if (hit >= 0 && (fr < 0 || hit < fr)) {
-            atomicMin(&t.rows[4 * grp + hit], row);
-            return;
-        }
-        if (fr < 0) {
-            grp = (grp + 1) & (SI_LT / 4 - 1);
-            continue;
-        }
-        if (q.v[fr] == CLOSED) {
-            si_global(g, (uint64_t)kb, row0 + row);
-            return;
-        }
-        const uint32_t pos = 4 * grp + fr;
-        const bool open = *reinterpret_cast<volatile uint32_t *>(t.used) < SI_LT_MAX;
-        const KB cur = si_cas(&t.keys[pos], EMPTY, open ? kb : CLOSED);
-        if (cur == EMPTY) {
-            if (!open) {
-                si_global(g, (uint64_t)kb, row0 + row);
-                return;
-            }
-            atomicAdd(t.used, 1u);
-            atomicMin(&t.rows[pos], row);
-            return;
-        }
-        if (cur == kb) {
-            atomicMin(&t.rows[pos], row);
-            return;
-        }
-    }
+// Two-choice LDS table (as hashagg.hip's pass B): a key lives in one of two 4-slot groups,
+// g1 from its LDS hash and g2 from a second mix, both read at once (one ds_read_b128 each
+// for 4-byte keys), so a hit almost never needs a second round trip; one-group linear
+// probing displaced a few per cent of the keys, whose probe chains serialised every wave.
+// A new key is CASed into the first EMPTY slot of the group with more room.  Two lanes that
+// insert one key at once may place it in both groups: harmless, both records merge into the
+// key's one HBM slot with atomicMin of the row.  A key whose groups are both full goes to
+// the HBM table directly; keys whose bits are the top two patterns use the side records.
+template <typename KB> __device__ inline void si_lt2_groups(KB kb, uint32_t &g1, uint32_t &g2) {
+    const uint32_t h = si_lds_hash((uint64_t)kb);
+    g1 = (h & (SI_LT - 1)) >> 2;
+    g2 = ((h ^ 0x9e3779b9u) * 0x2545f491u) >> (32 - (SI_LT_LOG2 - 2));  // multiply-shift: top bits
 }
 
-// M entries at once: every home-group read is issued before any is used, hits take their
-// ds_min right away (no return value to wait for), and only entries whose key is not in
-// its home group (new keys, displaced keys, marker-valued keys) take si_lt_add's probe
-// loop -- one entry at a time a lane would wait an LDS round trip per entry.
+template <typename KB>
+__device__ inline uint32_t si_lt2_find(const SiKB4<KB> &q1, const SiKB4<KB> &q2, uint32_t g1, uint32_t g2, KB kb) {
+    uint32_t slot = ~0u;
+#pragma unroll
+    for (int j = 3; j >= 0; j--) {
+        if (q2.v[j] == kb) slot = 4 * g2 + j;
+        if (q1.v[j] == kb) slot = 4 * g1 + j;
+    }
+    return slot;
+}
+
+template <typename KB>
+__device__ inline void si_lt2_insert(const SiLds<KB> &t, const SiTable &g, uint64_t row0, KB kb, uint32_t row) {
+    constexpr KB EMPTY = si_empty<KB>();
+    uint32_t g1, g2;
+    si_lt2_groups(kb, g1, g2);
+    for (int it = 0; it < 64; it++) {
+        const SiKB4<KB> q1 = *reinterpret_cast<const SiKB4<KB> *>(t.keys + 4 * g1);
+        const SiKB4<KB> q2 = *reinterpret_cast<const SiKB4<KB> *>(t.keys + 4 * g2);
+        const uint32_t hit = si_lt2_find(q1, q2, g1, g2, kb);
+        if (hit != ~0u) {
+            atomicMin(&t.rows[hit], row);
+            return;
+        }
+        int e1 = 0, e2 = 0, f1 = -1, f2 = -1;
+#pragma unroll
+        for (int j = 3; j >= 0; j--) {
+            if (q1.v[j] == EMPTY) {
+                e1++;
+                f1 = j;
+            }
+            if (q2.v[j] == EMPTY) {
+                e2++;
+                f2 = j;
+            }
+        }
+        if (e1 == 0 && e2 == 0) break;
+        const uint32_t pos = e1 >= e2 ? 4 * g1 + f1 : 4 * g2 + f2;
+        const KB cur = si_cas(&t.keys[pos], EMPTY, kb);
+        if (cur == EMPTY || cur == kb) {
+            atomicMin(&t.rows[pos], row);
+            return;
+        }
+    }
+    si_global(g, (uint64_t)kb, row0 + row);
+}
+
+// M entries at once: both group reads of every entry issued before any is used, hits take
+// their ds_min right away, only keys new to the table take si_lt2_insert
 template <typename KB, int M>
 __device__ inline void si_lt_add_many(const SiLds<KB> &t, const SiTable &g, uint64_t row0, const KB *kb,
                                       const uint32_t *row, const bool *valid) {
-    SiKB4<KB> q[M];
-    uint32_t base[M];
+    SiKB4<KB> q1[M], q2[M];
+    uint32_t g1[M], g2[M];
 #pragma unroll
     for (int i = 0; i < M; i++) {
-        base[i] = (si_lds_hash((uint64_t)kb[i]) & (SI_LT - 1)) & ~3u;
-        q[i] = *reinterpret_cast<const SiKB4<KB> *>(t.keys + base[i]);
+        si_lt2_groups(kb[i], g1[i], g2[i]);
+        q1[i] = *reinterpret_cast<const SiKB4<KB> *>(t.keys + 4 * g1[i]);
+        q2[i] = *reinterpret_cast<const SiKB4<KB> *>(t.keys + 4 * g2[i]);
     }
     bool slow[M];
 #pragma unroll
     for (int i = 0; i < M; i++) {
-        uint32_t slot = ~0u;
-#pragma unroll
-        for (int j = 3; j >= 0; j--)
-            if (q[i].v[j] == kb[i]) slot = base[i] + j;
-        if (kb[i] >= si_closed<KB>()) slot = ~0u;
+        uint32_t slot = si_lt2_find(q1[i], q2[i], g1[i], g2[i], kb[i]);
+        if (kb[i] >= si_closed<KB>()) slot = SI_LT + (uint32_t)(kb[i] - si_closed<KB>());
         slow[i] = valid[i] && slot == ~0u;
         if (valid[i] && slot != ~0u) atomicMin(&t.rows[slot], row[i]);
     }
 #pragma unroll
     for (int i = 0; i < M; i++)
-        if (slow[i]) si_lt_add<KB>(t, g, row0, kb[i], row[i]);
+        if (slow[i]) si_lt2_insert<KB>(t, g, row0, kb[i], row[i]);
 }
 
 // every key the LDS table holds, with its smallest row, into the HBM table (after a barrier)
@@ -537,6 +541,145 @@ __global__ __launch_bounds__(SI_THREADS) void k_si_scatter(SiParams sp, SiTable 
     si_new_flush(&s_new, g.ctr);
 }
 
+// Pass A for keys of <= 4 bytes, after the tile path's fast scatter: SB batches of 4096 rows
+// are ranked before one commit, so a partition's run per commit is SB times longer (short
+// runs are partial lines HBM receives twice: 9.9 GB written for 8 GB of entries with one
+// batch per commit).  LDS holds the staged key bits and rows (8 B per row); a staged row's
+// partition is recomputed from its key at stream-out; one wave's scan turns the histogram
+// into sorted offsets, destination bases and advanced region bases (three LDS barriers).
+__host__ __device__ constexpr size_t si_fast_lds_bytes(int sb, uint32_t P) {
+    return (size_t)8 * sb * SI_BATCH + 20 * ((size_t)P + 1) + 64;
+}
+
+// PLAIN: 4-byte integer keys without mask / select, 16-byte aligned, n a multiple of 4 -- the
+// keys are read as 16-byte quads and the next batch is prefetched in registers while this
+// one is ranked (a quad is wholly inside a workgroup's range or wholly past it)
+template <typename T, int SB, bool PLAIN>
+__global__ __launch_bounds__(SI_THREADS) void k_si_scatter4(SiParams sp, SiTable g) {
+    static_assert(sizeof(T) <= 4, "keys of at most 4 bytes");
+    static_assert(!PLAIN || sizeof(T) == 4, "quad loads take 4-byte keys");
+    constexpr uint32_t CAP = SB * SI_BATCH;
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    __shared__ SiSpecial spec;
+    __shared__ uint32_t s_new;
+    g.wg_new = &s_new;
+    si_new_init(&s_new);
+    const uint32_t P = sp.P;
+    uint32_t *sk = reinterpret_cast<uint32_t *>(lds_raw);
+    uint32_t *srow = sk + CAP;
+    uint32_t *hist = srow + CAP;  // [P + 1]: hist[P] takes the ranks of rows that are dropped
+    uint32_t *boff = hist + P + 1, *dbase = boff + P, *base = dbase + P, *lim = base + P;
+    uint32_t *wave_sums = lim + P;
+    for (uint32_t t = threadIdx.x; t <= P; t += SI_THREADS) hist[t] = 0;
+    for (uint32_t t = threadIdx.x; t < P; t += SI_THREADS) {
+        base[t] = (uint32_t)sp.toff[t];
+        lim[t] = (uint32_t)sp.toff[t] + sp.cap[t];
+    }
+    si_special_init(&spec);
+    __syncthreads();
+    const uint32_t w = blockIdx.x;
+    const uint64_t row_begin = (uint64_t)w * sp.rows_per_wg;
+    const uint64_t row_end = min(sp.n, row_begin + sp.rows_per_wg);
+    const uint64_t region0 = (uint64_t)w * sp.wg_stride;
+    uint64_t *ent = static_cast<uint64_t *>(sp.ent);
+    constexpr int QUADS = SI_RPT / 4;
+    // row of slot r of a batch: plain -- lane-owned quads; else -- one row per lane per step
+    auto row_of = [&](uint64_t b0, int r) -> uint64_t {
+        if constexpr (PLAIN) {
+            const int sb = r / SI_RPT, rr = r % SI_RPT;
+            return b0 + (uint64_t)sb * SI_BATCH + 4 * ((uint64_t)(rr >> 2) * SI_THREADS + threadIdx.x) + (rr & 3);
+        } else {
+            return b0 + (uint64_t)r * SI_THREADS + threadIdx.x;
+        }
+    };
+    uint4 cur[QUADS], nxt[QUADS];
+    auto load = [&](uint64_t b0, uint4 (&R)[QUADS]) {
+#pragma unroll
+        for (int q = 0; q < QUADS; q++) {
+            const uint64_t i = b0 + 4 * ((uint64_t)q * SI_THREADS + threadIdx.x);
+            const uint64_t is = i < sp.n - 4 ? i : sp.n - 4;
+            R[q] = *reinterpret_cast<const uint4 *>(static_cast<const T *>(sp.keys) + is);
+        }
+    };
+    if constexpr (PLAIN) load(row_begin, cur);
+    for (uint64_t b0 = row_begin; b0 < row_end; b0 += CAP) {
+        uint32_t kb[SB * SI_RPT];
+        int32_t rank[SB * SI_RPT];
+        if constexpr (PLAIN) {
+#pragma unroll
+            for (int sb = 0; sb < SB; sb++) {
+                load(b0 + (uint64_t)(sb + 1) * SI_BATCH, nxt);
+#pragma unroll
+                for (int rr = 0; rr < SI_RPT; rr++) {
+                    const int r = sb * SI_RPT + rr;
+                    const uint32_t w4[4] = {cur[rr >> 2].x, cur[rr >> 2].y, cur[rr >> 2].z, cur[rr >> 2].w};
+                    kb[r] = w4[rr & 3];
+                    const bool ok = row_of(b0, r) < row_end;
+                    const uint32_t rk = atomicAdd(&hist[ok ? si_bucket((uint64_t)kb[r], sp.p_log2) : P], 1u);
+                    rank[r] = ok ? (int32_t)rk : -1;
+                }
+#pragma unroll
+                for (int q = 0; q < QUADS; q++) cur[q] = nxt[q];
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < SB * SI_RPT; r++) {
+                const uint64_t i = row_of(b0, r);
+                kb[r] = 0;
+                const bool ok = i < row_end && si_row<T>(sp, i, &spec, &kb[r]);
+                const uint32_t rk = atomicAdd(&hist[ok ? si_bucket((uint64_t)kb[r], sp.p_log2) : P], 1u);
+                rank[r] = ok ? (int32_t)rk : -1;
+            }
+        }
+        si_lds_barrier();
+        if (threadIdx.x < 64) {
+            const uint32_t lane = threadIdx.x;
+            const uint32_t per = (P + 63) / 64;
+            const uint32_t t0 = lane * per;
+            uint32_t sum = 0;
+            for (uint32_t t = t0; t < t0 + per && t < P; t++) sum += hist[t];
+            uint32_t inc = sum;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(inc, off, 64);
+                if ((int)lane >= off) inc += y;
+            }
+            uint32_t acc = inc - sum;
+            for (uint32_t t = t0; t < t0 + per && t < P; t++) {
+                const uint32_t hh = hist[t], bb = base[t];
+                boff[t] = acc;
+                dbase[t] = bb - acc;
+                base[t] = bb + hh;
+                hist[t] = 0;
+                acc += hh;
+            }
+            if (lane == 0) hist[P] = 0;
+            if (lane == 63) wave_sums[0] = inc;
+        }
+        si_lds_barrier();
+        const uint32_t tot = wave_sums[0];
+#pragma unroll
+        for (int r = 0; r < SB * SI_RPT; r++) {
+            if (rank[r] < 0) continue;
+            const uint32_t pos = boff[si_bucket((uint64_t)kb[r], sp.p_log2)] + (uint32_t)rank[r];
+            sk[pos] = kb[r];
+            srow[pos] = (uint32_t)row_of(b0, r);
+        }
+        si_lds_barrier();
+        for (uint32_t k = threadIdx.x; k < tot; k += SI_THREADS) {
+            const uint32_t key = sk[k], row = srow[k];
+            const uint32_t t = si_bucket((uint64_t)key, sp.p_log2);
+            const uint32_t dest = dbase[t] + k;
+            if (dest < lim[t]) ent[region0 + dest] = ((uint64_t)row << 32) | key;
+            else si_global(g, (uint64_t)key, sp.row0 + row);  // a full region (sampling miss)
+        }
+    }
+    si_lds_barrier();
+    for (uint32_t t = threadIdx.x; t < P; t += SI_THREADS) sp.fills[(uint64_t)t * sp.W + w] = base[t] - (uint32_t)sp.toff[t];
+    si_special_flush(&spec, sp.row0, g.ctr);
+    si_new_flush(&s_new, g.ctr);
+}
+
 // ---- pass B -------------------------------------------------------------------------------
 template <typename KB>
 __global__ __launch_bounds__(SB_THREADS) void k_si_reduce(SiParams sp, SiTable g, const SiUnit *units) {
@@ -603,7 +746,9 @@ __global__ __launch_bounds__(SB_THREADS) void k_si_reduce(SiParams sp, SiTable g
 #pragma unroll
             for (int j = 0; j < SB_M; j++) asm volatile("" ::"v"(kb[j]), "v"(row[j]));
         } else {
-            si_lt_add_many<KB, SB_M>(t, g, sp.row0, kb, row, valid);
+            constexpr int MM = sizeof(KB) == 4 ? SB_M / 2 : SB_M / 4;  // 128 VGPRs at 1024 threads
+#pragma unroll
+            for (int h0 = 0; h0 < SB_M; h0 += MM) si_lt_add_many<KB, MM>(t, g, sp.row0, kb + h0, row + h0, valid + h0);
         }
     }
     __syncthreads();
@@ -1075,17 +1220,76 @@ static void si_chunk(vh_set *s, SiScratch &S, const void *keys, const uint8_t *m
     const uint32_t P = sp.P;
     const size_t lt_lds = si_lt_bytes(kbs);
 
+    const bool plain = (s->dtype == VH_I32 || s->dtype == VH_U32) && !mask && !select && n % 4 == 0 &&
+                       (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
     std::vector<SiUnit> units;
     std::vector<uint32_t> cap;
     std::vector<uint64_t> toff;
     uint32_t W = 0;
+    int fast_sb = 0;
+    size_t lds_scatter = 0;
+    // f(kernel instance) of the multi-batch pass A for this key dtype and fast_sb
+    auto with_fast = [&](auto &&f) {
+        auto by_sb = [&](auto tc) {
+            using T = decltype(tc);
+            if (fast_sb == 4) f(k_si_scatter4<T, 4, false>);
+            else if (fast_sb == 3) f(k_si_scatter4<T, 3, false>);
+            else if (fast_sb == 2) f(k_si_scatter4<T, 2, false>);
+            else f(k_si_scatter4<T, 1, false>);
+        };
+        auto by_sb_plain = [&](auto tc) {
+            using T = decltype(tc);
+            if (fast_sb == 4) f(k_si_scatter4<T, 4, true>);
+            else if (fast_sb == 3) f(k_si_scatter4<T, 3, true>);
+            else if (fast_sb == 2) f(k_si_scatter4<T, 2, true>);
+            else f(k_si_scatter4<T, 1, true>);
+        };
+        if (plain) {
+            if (s->dtype == VH_I32) by_sb_plain(int32_t());
+            else by_sb_plain(uint32_t());
+            return;
+        }
+        switch (s->dtype) {
+        case VH_I32: by_sb(int32_t()); break;
+        case VH_U32: by_sb(uint32_t()); break;
+        case VH_F32: by_sb(float()); break;
+        case VH_I16: by_sb(int16_t()); break;
+        case VH_U16: by_sb(uint16_t()); break;
+        case VH_I8: by_sb(int8_t()); break;
+        case VH_U8: by_sb(uint8_t()); break;
+        case VH_BOOL: by_sb(vbool()); break;
+        default: fail(VH_ERR_RUNTIME, "internal: multi-batch set pass A takes keys of <= 4 bytes");
+        }
+    };
     if (P > 1) {
         std::vector<uint64_t> bh(P, 0);
         for (uint32_t i = 0; i < FINE; i++) bh[i >> (SI_FINE_LOG2 - p_log2)] += fh[i];
-        const size_t lds_a = si_scatter_lds_bytes(P);
+        // keys of <= 4 bytes take the multi-batch pass A (k_si_scatter4) with as many
+        // batches per commit as the LDS holds (VH_SI_FAST=0: the one-batch kernel, A/B runs)
+        static const bool fast_on = [] {
+            const char *e = getenv("VH_SI_FAST");
+            return !e || atoi(e) != 0;
+        }();
+        fast_sb = 0;
+        // quad loads with a register prefetch hide the load latency at one workgroup per CU
+        // (4 batches per commit: 3.9 ms vs 5.0 at one batch, C3 set); per-row loads need the
+        // occupancy of one batch per commit (4 workgroups per CU)
+        static const int sb_env = [] {
+            const char *e = getenv("VH_SI_SB");
+            return e ? std::min(4, std::max(1, atoi(e))) : 0;
+        }();
+        const int sb_max = sb_env ? sb_env : plain ? 4 : 1;
+        if (fast_on && isz <= 4)
+            for (fast_sb = sb_max; fast_sb > 1 && si_fast_lds_bytes(fast_sb, P) > 160 * 1024; fast_sb--) {
+            }
+        const size_t lds_a = fast_sb ? si_fast_lds_bytes(fast_sb, P) : si_scatter_lds_bytes(P);
+        lds_scatter = lds_a;
         int bpc = 1;
-        VH_DISPATCH_DTYPE(s->dtype, T,
-                          bpc = si_blocks_per_cu(reinterpret_cast<const void *>(k_si_scatter<T>), SI_THREADS, lds_a));
+        if (fast_sb)
+            with_fast([&](auto kernel) { bpc = si_blocks_per_cu(reinterpret_cast<const void *>(kernel), SI_THREADS, lds_a); });
+        else
+            VH_DISPATCH_DTYPE(s->dtype, T,
+                              bpc = si_blocks_per_cu(reinterpret_cast<const void *>(k_si_scatter<T>), SI_THREADS, lds_a));
         bpc = std::min(bpc, 4);
         W = std::min<uint32_t>(1024, (uint32_t)cu_count() * bpc);
         const uint64_t rows_per_wg = ((n + W - 1) / W + SI_BATCH - 1) / SI_BATCH * SI_BATCH;
@@ -1149,9 +1353,14 @@ static void si_chunk(vh_set *s, SiScratch &S, const void *keys, const uint8_t *m
         } else {
             {
                 TimedScope ts("set_insert");
-                VH_DISPATCH_DTYPE(s->dtype, T,
-                                  hipLaunchKernelGGL(k_si_scatter<T>, dim3(W), dim3(SI_THREADS), si_scatter_lds_bytes(P),
-                                                     st, sp, g));
+                if (fast_sb)
+                    with_fast([&](auto kernel) {
+                        hipLaunchKernelGGL(kernel, dim3(W), dim3(SI_THREADS), lds_scatter, st, sp, g);
+                    });
+                else
+                    VH_DISPATCH_DTYPE(s->dtype, T,
+                                      hipLaunchKernelGGL(k_si_scatter<T>, dim3(W), dim3(SI_THREADS), lds_scatter, st, sp,
+                                                         g));
                 VH_HIP(hipGetLastError());
             }
             {
