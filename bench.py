@@ -474,7 +474,8 @@ def bench_groupby(n, args):
             k, c, s, _ = ha.finish()
             return k, c, s[0]
         dfg = df.groupby("key", agg={"v": ["sum", "count"]}, assume_sparse="auto" if mode == "auto" else True)
-        return dfg["key"].to_numpy(), dfg["v_count"].to_numpy(), dfg["v_sum"].to_numpy()
+        # {"v": ["sum", "count"]} names the count(*) column "v" (groupby.py:345-402)
+        return dfg["key"].to_numpy(), dfg["v"].to_numpy(), dfg["v_sum"].to_numpy()
 
     v_total = float(vaex_amd.from_arrays(v=v).sum("v"))  # independent 0-d reduction
     ref_groups = None
