@@ -26,7 +26,7 @@ sys.path.insert(0, ROOT)
 
 BASELINE_METRIC = "rows/sec 2D count grid 1e9×f64 + groupby-sum 1e6 keys; HBM GB/s %peak"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-TILE_KERNELS = ["tile_sample", "tile_scatter", "tile_scatter_f64", "tile_scatter_ord", "tile_reduce"]
+TILE_KERNELS = ["tile_sample", "tile_scatter", "tile_scatter_f64", "tile_scatter_ord", "tile_scatter_set", "tile_reduce"]
 
 
 def parse():
@@ -463,7 +463,7 @@ def bench_groupby(n, args):
     v = DeviceArray.random(n, "normal", seed=6)
     df = vaex_amd.from_arrays(key=keys, v=v)
     out = {"rows": n, "algorithmic_bytes_per_row": 12}
-    names = ["minmax", "tile_sample", "tile_scatter", "tile_scatter_ord", "tile_reduce", "ha_sample",
+    names = ["minmax", "tile_sample", "tile_scatter", "tile_scatter_ord", "tile_scatter_set", "tile_reduce", "ha_sample",
              "ha_scatter", "ha_scatter_f64", "ha_reduce", "ha_finish", "set_sample", "set_insert", "set_reduce", "set_rank",
              "bin_fused_global"]
 

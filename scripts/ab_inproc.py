@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT)
 from vaex_amd import _lib, superagg  # noqa: E402
 from vaex_amd.device import DeviceArray  # noqa: E402
 
-KERNELS = ["tile_sample", "tile_scatter_f64", "tile_scatter_ord", "tile_reduce", "minmax", "ha_sample",
+KERNELS = ["tile_sample", "tile_scatter_f64", "tile_scatter_ord", "tile_scatter_set", "tile_scatter", "tile_reduce", "minmax", "ha_sample",
            "ha_scatter_f64", "ha_reduce", "ha_finish", "set_sample", "set_insert", "set_reduce"]
 
 

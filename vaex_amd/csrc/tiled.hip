@@ -749,7 +749,20 @@ __device__ inline uint64_t ordinal_i32_index(int32_t raw, uint64_t min_value, ui
 // and NV float64 sums without masks -- the C3 groupby(key).agg({sum, count}) shape.
 // Keys are read as 8-byte pairs and values as 16-byte pairs, the next batch prefetched in
 // registers (same row layout and pipelining as k_tile_scatter_f64).
-template <int NV, int SB>
+// cell of a set ordinal (set_index, binner_dev.hpp): unknown keys -> 1, past the count -> count + 2
+__device__ inline uint32_t set_ord_cell(int64_t o, uint64_t count) {
+    if (o < 0) return 1;
+    if ((uint64_t)o >= count) return (uint32_t)count + 2;
+    return (uint32_t)o + 2;
+}
+
+// SET = false: one native int32 BinnerOrdinal.  SET = true: the fused set-ordinal binner
+// (BinnerOrdinal over map_ordinal of a 4-byte integer key, no mask, packed LUT): the first
+// LUT probe of every row of a batch is issued before any is used, so a lane keeps eight
+// random lookups in flight instead of walking one probe chain at a time (the per-row form
+// fetched ~114 B per row at ~2.4 TB/s of random lines: 27 ms for C3); the rare rows whose
+// first slot holds another key continue their probe sequence afterwards.
+template <int NV, int SB, bool SET = false>
 __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
     constexpr int PAIRS = TA_RPT / 2;
     extern __shared__ __align__(16) unsigned char lds_raw[];
@@ -793,12 +806,45 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
             for (int s = 0; s < NV; s++) R.v[q][s] = *reinterpret_cast<const double2 *>(col[s] + is);
         }
     };
+    const SetDev sd = p.b[0].set;
     auto rows = [&](uint64_t b0, const Regs &cur, uint32_t *key, int32_t *rank, double (*vals)[NV > 0 ? NV : 1]) {
+        uint32_t scell[SET ? TA_RPT : 1];
+        if constexpr (SET) {
+            uint64_t e[TA_RPT], pos[TA_RPT];
+#pragma unroll
+            for (int r = 0; r < TA_RPT; r++) {
+                const uint32_t kb = (uint32_t)(r & 1 ? cur.k[r >> 1].y : cur.k[r >> 1].x);
+                pos[r] = hash64(kb) & sd.cap_mask;
+                e[r] = sd.lut[pos[r]];
+            }
+#pragma unroll
+            for (int r = 0; r < TA_RPT; r++) {
+                const uint32_t kb = (uint32_t)(r & 1 ? cur.k[r >> 1].y : cur.k[r >> 1].x);
+                int64_t o = -1;
+                if (e[r] != SET_EMPTY && (uint32_t)e[r] == kb) {
+                    o = (int64_t)(e[r] >> 32);
+                } else if (e[r] != SET_EMPTY) {
+                    uint64_t ps = pos[r];
+                    for (int k = 0; k < SET_MAX_PROBE; k++) {
+                        ps = (ps + 1) & sd.cap_mask;
+                        const uint64_t x = sd.lut[ps];
+                        if (x == SET_EMPTY) break;
+                        if ((uint32_t)x == kb) {
+                            o = (int64_t)(x >> 32);
+                            break;
+                        }
+                    }
+                }
+                scell[r] = set_ord_cell(o, count) * stride0;
+            }
+        }
 #pragma unroll
         for (int r = 0; r < TA_RPT; r++) {
             const int q = r >> 1, h = r & 1;
             const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + threadIdx.x) + h;
-            const uint32_t c = (uint32_t)ordinal_i32_index(h ? cur.k[q].y : cur.k[q].x, min_value, count) * stride0;
+            uint32_t c;
+            if constexpr (SET) c = scell[r];
+            else c = (uint32_t)ordinal_i32_index(h ? cur.k[q].y : cur.k[q].x, min_value, count) * stride0;
             uint32_t f = count_mask;
 #pragma unroll
             for (int s = 0; s < NV; s++) {
@@ -1057,13 +1103,16 @@ template <int NV> static int scatter_blocks_per_cu_nd(int nd, int fast, size_t l
     }
 }
 
-static const void *ord_kernel(int nv, int fast_mode) {
-    if (nv == 0) return reinterpret_cast<const void *>(k_tile_scatter_ord<0, 1>);
+template <bool SET> static const void *ord_kernel_t(int nv, int fast_mode) {
+    if (nv == 0) return reinterpret_cast<const void *>(k_tile_scatter_ord<0, 1, SET>);
     if (nv == 1)
-        return fast_mode == 2 ? reinterpret_cast<const void *>(k_tile_scatter_ord<1, fast_sb(1)>)
-                              : reinterpret_cast<const void *>(k_tile_scatter_ord<1, 1>);
-    return fast_mode == 2 ? reinterpret_cast<const void *>(k_tile_scatter_ord<2, fast_sb(2)>)
-                          : reinterpret_cast<const void *>(k_tile_scatter_ord<2, 1>);
+        return fast_mode == 2 ? reinterpret_cast<const void *>(k_tile_scatter_ord<1, fast_sb(1), SET>)
+                              : reinterpret_cast<const void *>(k_tile_scatter_ord<1, 1, SET>);
+    return fast_mode == 2 ? reinterpret_cast<const void *>(k_tile_scatter_ord<2, fast_sb(2), SET>)
+                          : reinterpret_cast<const void *>(k_tile_scatter_ord<2, 1, SET>);
+}
+static const void *ord_kernel(int nv, int fast_mode, bool set) {
+    return set ? ord_kernel_t<true>(nv, fast_mode) : ord_kernel_t<false>(nv, fast_mode);
 }
 
 static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64,
@@ -1074,7 +1123,9 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
 static bool ord_fast_ok(const BinPlan &plan, const FusedAggs &fa) {
     if (plan.nb != 1) return false;
     const BinnerDev &b = plan.b[0];
-    if (b.kind != 1 || b.dtype != VH_I32 || b.flip || b.mask || (reinterpret_cast<uintptr_t>(b.data) & 7)) return false;
+    const bool set_ok = b.kind == 2 && (b.dtype == VH_I32 || b.dtype == VH_U32) && !b.set.wide;
+    if (!(b.kind == 1 && b.dtype == VH_I32) && !set_ok) return false;
+    if (b.flip || b.mask || (reinterpret_cast<uintptr_t>(b.data) & 7)) return false;
     for (int k = 0; k < fa.na; k++) {
         const FusedAgg &a = fa.a[k];
         if (a.mask) return false;
@@ -1099,7 +1150,7 @@ bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t
         BinPlan p1 = plan;
         FusedAggs f1 = fa_in;
         for (int d = 0; d < p1.nb; d++) {
-            p1.b[d].data = static_cast<const char *>(p1.b[d].data) + (n - 1) * (p1.b[d].dtype == VH_I32 ? 4 : 8);
+            p1.b[d].data = static_cast<const char *>(p1.b[d].data) + (n - 1) * dtype_itemsize(p1.b[d].dtype);
             if (p1.b[d].mask) p1.b[d].mask += n - 1;
         }
         for (int k = 0; k < f1.na; k++) {
@@ -1208,12 +1259,12 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         static std::mutex mu;
         static std::map<std::tuple<int, int, int, int, size_t>, int> cache;
         std::lock_guard<std::mutex> lk(mu);
-        const auto key = std::make_tuple(current_device(), ord ? -2 : nd_k, nv, fast_mode, lds_a);
+        const auto key = std::make_tuple(current_device(), ord ? (has_set ? -3 : -2) : nd_k, nv, fast_mode, lds_a);
         auto it = cache.find(key);
         if (it == cache.end()) {
             int v = 0;
             if (ord) {
-                const void *kf = ord_kernel(nv, fast_mode);
+                const void *kf = ord_kernel(nv, fast_mode, has_set);
                 VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kf, TA_THREADS, lds_a));
             } else {
                 v = nv == 0 ? scatter_blocks_per_cu_nd<0>(nd_k, fast_mode, lds_a)
@@ -1308,19 +1359,24 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
 
     // ---- pass A
     {
-        TimedScope ts(fast ? "tile_scatter_f64" : ord ? "tile_scatter_ord" : "tile_scatter");
+        TimedScope ts(fast ? "tile_scatter_f64" : ord ? (has_set ? "tile_scatter_set" : "tile_scatter_ord") : "tile_scatter");
         const size_t lds = lds_a;
         if (ord) {
-            switch (nv) {
-            case 0: hipLaunchKernelGGL((k_tile_scatter_ord<0, 1>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n); break;
-            case 1:
-                if (fast_mode == 2) hipLaunchKernelGGL((k_tile_scatter_ord<1, fast_sb(1)>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
-                else hipLaunchKernelGGL((k_tile_scatter_ord<1, 1>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
-                break;
-            default:
-                if (fast_mode == 2) hipLaunchKernelGGL((k_tile_scatter_ord<2, fast_sb(2)>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
-                else hipLaunchKernelGGL((k_tile_scatter_ord<2, 1>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
-            }
+            auto launch_ord = [&](auto setc) {
+                constexpr bool SET = decltype(setc)::value;
+                switch (nv) {
+                case 0: hipLaunchKernelGGL((k_tile_scatter_ord<0, 1, SET>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n); break;
+                case 1:
+                    if (fast_mode == 2) hipLaunchKernelGGL((k_tile_scatter_ord<1, fast_sb(1), SET>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
+                    else hipLaunchKernelGGL((k_tile_scatter_ord<1, 1, SET>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
+                    break;
+                default:
+                    if (fast_mode == 2) hipLaunchKernelGGL((k_tile_scatter_ord<2, fast_sb(2), SET>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
+                    else hipLaunchKernelGGL((k_tile_scatter_ord<2, 1, SET>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
+                }
+            };
+            if (has_set) launch_ord(std::true_type());
+            else launch_ord(std::false_type());
         } else {
             switch (nv) {
             case 0: launch_scatter_nd<0>(nd_k, fast_mode, W, lds, plan, fa, tp, n); break;
