@@ -155,6 +155,37 @@ def test_dense_and_hash_groupers_agree(dense):
     np.testing.assert_allclose(dfg["v_sum"].to_numpy()[order], s, rtol=1e-6, atol=1e-9)
 
 
+@pytest.mark.parametrize("kdtype", ["int8", "int16", "int32", "uint32", "int64"])
+def test_set_ordinal_grid_through_hash_aggregation(kdtype):
+    """assume_sparse=True with count / sum aggregators over >= 2^22 rows: the set-ordinal
+    grid is filled by the fused hash aggregation (per-key totals added at each key's
+    ordinal cell, hashagg_bin_set_ordinal) -- groups in first-appearance order, counts
+    exact, sums within 1e-6, NaN values skipped by sum and count(v), keys of every width
+    including negative 1- and 2-byte keys (sign- vs zero-extended bits)."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(21)
+    n = (1 << 22) + 3
+    info = np.iinfo(kdtype)
+    lo, hi = max(info.min, -40_000), min(info.max, 60_000)
+    keys = rng.integers(lo, hi, n, endpoint=True).astype(kdtype)
+    v = rng.normal(size=n)
+    v[rng.random(n) < 0.01] = np.nan
+    df = vaex_amd.from_arrays(key=DeviceArray.from_numpy(keys), v=DeviceArray.from_numpy(v))
+    dfg = df.groupby("key", agg={"s": vaex_amd.agg.sum("v"), "c": vaex_amd.agg.count("v"), "n": vaex_amd.agg.count()},
+                     assume_sparse=True)
+    gk = dfg["key"].to_numpy()
+    first = np.unique(keys, return_index=True)
+    expect_order = first[0][np.argsort(first[1])]
+    np.testing.assert_array_equal(gk, expect_order)
+    uk, s, c = oracle.groupby_reference(keys, v)
+    order = np.argsort(gk, kind="stable")
+    np.testing.assert_array_equal(gk[order], uk)
+    np.testing.assert_array_equal(dfg["c"].to_numpy()[order], c)
+    np.testing.assert_array_equal(dfg["n"].to_numpy()[order], np.bincount(np.searchsorted(uk, keys), minlength=len(uk)))
+    np.testing.assert_allclose(dfg["s"].to_numpy()[order], s, rtol=1e-6, atol=1e-9)
+
+
 def test_large_grid_mixed_aggregators_split_routes():
     """count(*) + sum + min + max on a grid beyond the LDS sub-grid size with > 2^20 rows:
     count / sum take the tile path, min / max the generic one (run_bin splits the mix);

@@ -1585,6 +1585,7 @@ void launch_fused(const BinPlan &plan, FusedAggs &fa, uint64_t n, uint64_t cells
     const uint64_t lds_bytes = (off + 15) & ~uint64_t(15);
     const bool use_lds = lds_bytes <= LDS_FUSED_MAX && cells > 0;
     fa.lds_words = (uint32_t)(lds_bytes / 4);
+    if (!use_lds && hashagg_bin_set_ordinal(plan, fa, n)) return;
     if (!use_lds && try_tiled(plan, fa, n, cells, nd_f64, ws)) return;
     const int per_cu = use_lds ? (int)std::max<uint64_t>(1, std::min<uint64_t>(8, (64 * 1024) / std::max<uint64_t>(lds_bytes, 1))) : 8;
     dim3 grd(blocks_for(n, 256, per_cu)), blk(256);

@@ -115,6 +115,9 @@ void launch_fused(const BinPlan &plan, FusedAggs &fa, uint64_t n, uint64_t cells
 // tile-partitioned LDS aggregation for grids too large for one workgroup's LDS
 // (tiled.hip); returns false when the plan is not eligible
 bool try_tiled(const BinPlan &plan, const FusedAggs &fa, uint64_t n, uint64_t cells, int nd_f64, Workspace &ws);
+// a set-ordinal grid (one set-ordinal binner over an integer key) with count / float64 sum
+// aggregators through the fused hash aggregation (hashagg.hip); false when not eligible
+bool hashagg_bin_set_ordinal(const BinPlan &plan, const FusedAggs &fa, uint64_t n);
 
 }  // namespace vh
 
