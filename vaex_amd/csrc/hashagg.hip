@@ -73,9 +73,6 @@ constexpr int HA_RPT = 8;
 constexpr int HA_BATCH = HA_THREADS * HA_RPT;
 constexpr int HB_THREADS = 1024;           // pass B / direct
 constexpr int HB_M = 8;                    // entries per lane per pass-B step
-constexpr uint32_t LT_SLOTS_LOG2 = 12;     // LDS table: 4096 slots (+2 special records)
-constexpr uint32_t LT_SLOTS = 1u << LT_SLOTS_LOG2;
-constexpr uint32_t LT_TARGET_KEYS = 2300;  // P is chosen so a bucket holds about this many keys
 constexpr uint32_t HA_FINE_LOG2 = 12;      // sample histogram: top 12 hash bits
 constexpr uint32_t HA_MAX_P_LOG2 = 11;
 constexpr int HA_SAMPLE_BLOCKS = 256;
@@ -181,43 +178,60 @@ template <int NV> __device__ inline void ha_global_row(const HaTable &g, uint64_
 }
 
 // ---- LDS table --------------------------------------------------------------------------
-// Per slot: key bits; one 64-bit counter word holding count(*) << 32 | non-NaN count of
-// value 0 (one ds_add_u64 updates both: a unit holds < 2^32 rows); the value sums; the
-// non-NaN count of value 1.  Records LT_SLOTS and LT_SLOTS + 1 hold the keys whose bits
-// are the two top patterns (kb_closed, kb_empty).
+// Per slot: key bits; a counter word; the value sums; the non-NaN count of value 1.  Wide
+// table (4096 slots): the counter is count(*) << 32 | non-NaN count of value 0 (one
+// ds_add_u64 updates both: a unit holds < 2^32 rows).  Narrow table (8192 slots; 4-byte
+// keys, at most one value, no count(v)): a 32-bit count(*), 16 B per slot -- twice the keys
+// per bucket, so pass A needs half the buckets and its region runs are twice as long.
+// Records S and S + 1 (S = slots) hold the keys whose bits are the two top patterns
+// (kb_closed, kb_empty).
+template <bool N> __host__ __device__ constexpr uint32_t lt_slots() { return N ? 8192u : 4096u; }
+template <bool N> __host__ __device__ constexpr uint32_t lt_target_keys() { return N ? 4600u : 2300u; }
+
 template <typename KB> struct LdsTable {
-    KB *keys;                           // [LT_SLOTS]
-    unsigned long long *cn;             // [LT_SLOTS + 2]
-    unsigned long long *sum[HA_MAX_V];  // [LT_SLOTS + 2]
-    uint32_t *nn1;                      // [LT_SLOTS + 2]
+    KB *keys;                           // [S]
+    unsigned long long *cn;             // [S + 2] (wide)
+    uint32_t *cn32;                     // [S + 2] (narrow)
+    unsigned long long *sum[HA_MAX_V];  // [S + 2]
+    uint32_t *nn1;                      // [S + 2]
     uint32_t *used;
 };
 
-__host__ __device__ constexpr size_t lt_bytes(int nv, int kbsize) {
-    return (size_t)8 * (LT_SLOTS + 2) * (1 + nv) + (size_t)kbsize * LT_SLOTS + (nv > 1 ? (size_t)4 * (LT_SLOTS + 2) : 0) + 64;
+__host__ __device__ constexpr size_t lt_bytes(int nv, int kbsize, bool narrow) {
+    const size_t S = narrow ? 8192 : 4096;
+    return (size_t)(narrow ? 4 : 8) * (S + 2) + (size_t)8 * (S + 2) * nv + (size_t)kbsize * S +
+           (nv > 1 ? (size_t)4 * (S + 2) : 0) + 64;
 }
 
-template <typename KB, int NV> __device__ inline LdsTable<KB> lt_layout(unsigned char *raw) {
-    LdsTable<KB> t;
+template <typename KB, int NV, bool N> __device__ inline LdsTable<KB> lt_layout(unsigned char *raw) {
+    constexpr uint32_t S = lt_slots<N>();
+    LdsTable<KB> t{};
     unsigned char *p = raw;
-    t.cn = reinterpret_cast<unsigned long long *>(p);
-    p += 8 * (LT_SLOTS + 2);
+    if constexpr (N) {
+        t.cn32 = reinterpret_cast<uint32_t *>(p);
+        p += 4 * (S + 2);  // 8-byte aligned: (S + 2) is even
+    } else {
+        t.cn = reinterpret_cast<unsigned long long *>(p);
+        p += 8 * (S + 2);
+    }
     for (int v = 0; v < NV; v++) {
         t.sum[v] = reinterpret_cast<unsigned long long *>(p);
-        p += 8 * (LT_SLOTS + 2);
+        p += 8 * (S + 2);
     }
     t.keys = reinterpret_cast<KB *>(p);
-    p += sizeof(KB) * LT_SLOTS;
+    p += sizeof(KB) * S;
     t.nn1 = reinterpret_cast<uint32_t *>(p);
-    if (NV > 1) p += 4 * (LT_SLOTS + 2);
+    if (NV > 1) p += 4 * (S + 2);
     t.used = reinterpret_cast<uint32_t *>(p);
     return t;
 }
 
-template <typename KB, int NV> __device__ inline void lt_init(const LdsTable<KB> &t, int nthreads) {
-    for (uint32_t i = threadIdx.x; i < LT_SLOTS + 2; i += nthreads) {
-        if (i < LT_SLOTS) t.keys[i] = kb_empty<KB>();
-        t.cn[i] = 0;
+template <typename KB, int NV, bool N> __device__ inline void lt_init(const LdsTable<KB> &t, int nthreads) {
+    constexpr uint32_t S = lt_slots<N>();
+    for (uint32_t i = threadIdx.x; i < S + 2; i += nthreads) {
+        if (i < S) t.keys[i] = kb_empty<KB>();
+        if constexpr (N) t.cn32[i] = 0;
+        else t.cn[i] = 0;
 #pragma unroll
         for (int v = 0; v < NV; v++) t.sum[v][i] = 0;
         if constexpr (NV > 1) t.nn1[i] = 0;
@@ -225,7 +239,7 @@ template <typename KB, int NV> __device__ inline void lt_init(const LdsTable<KB>
     if (threadIdx.x == 0) *t.used = 0;
 }
 
-template <typename KB, int NV>
+template <typename KB, int NV, bool N>
 __device__ inline void lt_bump(const LdsTable<KB> &t, const HaTable &g, uint32_t slot, const uint64_t *vb) {
     unsigned long long c = 1ULL << 32;
 #pragma unroll
@@ -234,7 +248,7 @@ __device__ inline void lt_bump(const LdsTable<KB> &t, const HaTable &g, uint32_t
             const double d = __builtin_bit_cast(double, vb[v]);
             if (d == d) {
                 atomicAdd(reinterpret_cast<double *>(t.sum[v]) + slot, d);
-                if ((g.nnmask >> v) & 1) {
+                if (!N && ((g.nnmask >> v) & 1)) {
                     if (v == 0) c |= 1;
                     else atomicAdd(&t.nn1[slot], 1u);
                 }
@@ -243,7 +257,8 @@ __device__ inline void lt_bump(const LdsTable<KB> &t, const HaTable &g, uint32_t
             atomicAdd(&t.sum[v][slot], (unsigned long long)vb[v]);
         }
     }
-    atomicAdd(&t.cn[slot], c);
+    if constexpr (N) atomicAdd(&t.cn32[slot], 1u);
+    else atomicAdd(&t.cn[slot], c);
 }
 
 // four consecutive key slots: one ds_read_b128 (4-byte keys) or two (8-byte keys)
@@ -265,10 +280,11 @@ __device__ inline uint64_t lt_cas(uint64_t *p, uint64_t cmp, uint64_t val) {
 // groups -- harmless, both records merge into the same HBM slot.  A key whose two groups are
 // full aggregates straight into the HBM table.  Keys whose bits are EMPTY / CLOSED live in
 // the two side records.
-template <typename KB> __device__ inline void lt2_groups(KB kb, uint32_t &g1, uint32_t &g2) {
+template <typename KB, bool N> __device__ inline void lt2_groups(KB kb, uint32_t &g1, uint32_t &g2) {
+    constexpr uint32_t S = lt_slots<N>();
     const uint32_t h = ha_h(kb);
-    g1 = (h & (LT_SLOTS - 1)) >> 2;
-    g2 = (fmix32(h ^ 0x9e3779b9u) & (LT_SLOTS - 1)) >> 2;
+    g1 = (h & (S - 1)) >> 2;
+    g2 = (fmix32(h ^ 0x9e3779b9u) & (S - 1)) >> 2;
 }
 
 template <typename KB> __device__ inline uint32_t lt2_find(const KB4<KB> &q1, const KB4<KB> &q2, uint32_t g1, uint32_t g2,
@@ -283,17 +299,17 @@ template <typename KB> __device__ inline uint32_t lt2_find(const KB4<KB> &q1, co
 }
 
 // a key not found in either group: insert it (or find it, if another lane just did)
-template <typename KB, int NV>
+template <typename KB, int NV, bool N>
 __device__ inline void lt2_insert(const LdsTable<KB> &t, const HaTable &g, KB kb, const uint64_t *vb) {
     constexpr KB EMPTY = kb_empty<KB>();
     uint32_t g1, g2;
-    lt2_groups(kb, g1, g2);
+    lt2_groups<KB, N>(kb, g1, g2);
     for (int it = 0; it < 64; it++) {
         const KB4<KB> q1 = *reinterpret_cast<const KB4<KB> *>(t.keys + 4 * g1);
         const KB4<KB> q2 = *reinterpret_cast<const KB4<KB> *>(t.keys + 4 * g2);
         const uint32_t hit = lt2_find(q1, q2, g1, g2, kb);
         if (hit != ~0u) {
-            lt_bump<KB, NV>(t, g, hit, vb);
+            lt_bump<KB, NV, N>(t, g, hit, vb);
             return;
         }
         int e1 = 0, e2 = 0, f1 = -1, f2 = -1;
@@ -312,7 +328,7 @@ __device__ inline void lt2_insert(const LdsTable<KB> &t, const HaTable &g, KB kb
         const uint32_t pos = e1 >= e2 ? 4 * g1 + f1 : 4 * g2 + f2;
         const KB cur = lt_cas(&t.keys[pos], EMPTY, kb);
         if (cur == EMPTY || cur == kb) {
-            lt_bump<KB, NV>(t, g, pos, vb);
+            lt_bump<KB, NV, N>(t, g, pos, vb);
             return;
         }
         // another key took the slot: read the groups again
@@ -322,14 +338,15 @@ __device__ inline void lt2_insert(const LdsTable<KB> &t, const HaTable &g, KB kb
 
 // M entries at once: both group reads of every entry are issued together and the hits
 // aggregated with fire-and-forget LDS atomics; only keys new to the table take lt2_insert.
-template <typename KB, int NV, int M>
+template <typename KB, int NV, int M, bool N>
 __device__ inline void lt2_add_many(const LdsTable<KB> &t, const HaTable &g, const KB *kb,
                                     const uint64_t (*vb)[NV > 0 ? NV : 1], const bool *valid) {
+    constexpr uint32_t S = lt_slots<N>();
     KB4<KB> q1[M], q2[M];
     uint32_t g1[M], g2[M];
 #pragma unroll
     for (int i = 0; i < M; i++) {
-        lt2_groups(kb[i], g1[i], g2[i]);
+        lt2_groups<KB, N>(kb[i], g1[i], g2[i]);
         q1[i] = *reinterpret_cast<const KB4<KB> *>(t.keys + 4 * g1[i]);
         q2[i] = *reinterpret_cast<const KB4<KB> *>(t.keys + 4 * g2[i]);
     }
@@ -337,21 +354,22 @@ __device__ inline void lt2_add_many(const LdsTable<KB> &t, const HaTable &g, con
 #pragma unroll
     for (int i = 0; i < M; i++) {
         uint32_t slot = lt2_find(q1[i], q2[i], g1[i], g2[i], kb[i]);
-        if (kb[i] >= kb_closed<KB>()) slot = LT_SLOTS + (uint32_t)(kb[i] - kb_closed<KB>());
+        if (kb[i] >= kb_closed<KB>()) slot = S + (uint32_t)(kb[i] - kb_closed<KB>());
         slow[i] = valid[i] && slot == ~0u;
-        if (valid[i] && slot != ~0u) lt_bump<KB, NV>(t, g, slot, vb[i]);
+        if (valid[i] && slot != ~0u) lt_bump<KB, NV, N>(t, g, slot, vb[i]);
     }
 #pragma unroll
     for (int i = 0; i < M; i++)
-        if (slow[i]) lt2_insert<KB, NV>(t, g, kb[i], vb[i]);
+        if (slow[i]) lt2_insert<KB, NV, N>(t, g, kb[i], vb[i]);
 }
 
 // merge the LDS table into the HBM table (after a workgroup barrier)
-template <typename KB, int NV> __device__ inline void lt_merge(const LdsTable<KB> &t, const HaTable &g, int nthreads) {
-    for (uint32_t i = threadIdx.x; i < LT_SLOTS + 2; i += nthreads) {
-        const unsigned long long cn = t.cn[i];
+template <typename KB, int NV, bool N> __device__ inline void lt_merge(const LdsTable<KB> &t, const HaTable &g, int nthreads) {
+    constexpr uint32_t S = lt_slots<N>();
+    for (uint32_t i = threadIdx.x; i < S + 2; i += nthreads) {
+        const unsigned long long cn = N ? (unsigned long long)t.cn32[i] << 32 : t.cn[i];
         if (!cn) continue;
-        const KB kb = i < LT_SLOTS ? t.keys[i] : (KB)(kb_closed<KB>() + (i - LT_SLOTS));
+        const KB kb = i < S ? t.keys[i] : (KB)(kb_closed<KB>() + (i - S));
         const uint64_t s = ha_slot(g, (uint64_t)kb);
         if (s == ~0ULL) continue;
         atomicAdd(&g.cnt[s], cn >> 32);
@@ -856,7 +874,7 @@ __global__ __launch_bounds__(64) void k_ha_tail(HaParams hp, HaTable g, uint64_t
 // as one flat stream of entries (prefix sums of the region fills in LDS), one entry per
 // lane per load: consecutive lanes read consecutive entries (a wave's load is contiguous
 // unless it crosses a region end); a lane finds the region of its entry by a forward scan.
-template <typename KB, int NV>
+template <typename KB, int NV, bool N>
 __global__ __launch_bounds__(HB_THREADS) void k_ha_reduce(HaParams hp, HaTable g, const HaUnit *units) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
     __shared__ uint32_t s_fill[1024];
@@ -872,8 +890,8 @@ __global__ __launch_bounds__(HB_THREADS) void k_ha_reduce(HaParams hp, HaTable g
         any |= f != 0;
     }
     if (!__syncthreads_or(any)) return;
-    const LdsTable<KB> t = lt_layout<KB, NV>(lds_raw);
-    lt_init<KB, NV>(t, HB_THREADS);
+    const LdsTable<KB> t = lt_layout<KB, NV, N>(lds_raw);
+    lt_init<KB, NV, N>(t, HB_THREADS);
     if (threadIdx.x < 64) {
         // exclusive scan of the region fills by the first wave (16 regions per lane)
         const uint32_t lane = threadIdx.x, k0 = lane * 16;
@@ -927,7 +945,7 @@ __global__ __launch_bounds__(HB_THREADS) void k_ha_reduce(HaParams hp, HaTable g
         } else {
             constexpr int MM = sizeof(KB) == 4 ? HB_M / 2 : HB_M / 4;  // 128 VGPRs at 1024 threads
 #pragma unroll
-            for (int h0 = 0; h0 < HB_M; h0 += MM) lt2_add_many<KB, NV, MM>(t, g, B.kb + h0, B.vb + h0, B.valid + h0);
+            for (int h0 = 0; h0 < HB_M; h0 += MM) lt2_add_many<KB, NV, MM, N>(t, g, B.kb + h0, B.vb + h0, B.valid + h0);
         }
     };
     constexpr uint32_t STEP = HB_THREADS * HB_M;
@@ -949,16 +967,16 @@ __global__ __launch_bounds__(HB_THREADS) void k_ha_reduce(HaParams hp, HaTable g
     }
     __syncthreads();
     if (hp.debug & 1) return;
-    lt_merge<KB, NV>(t, g, HB_THREADS);
+    lt_merge<KB, NV, N>(t, g, HB_THREADS);
 }
 
 // ---- direct (P == 1): each workgroup aggregates a row range of the raw columns ------------
-template <typename K, int NV>
+template <typename K, int NV, bool N>
 __global__ __launch_bounds__(HB_THREADS) void k_ha_direct(HaParams hp, HaTable g) {
     using KB = kb_t<K>;
     extern __shared__ __align__(16) unsigned char lds_raw[];
-    const LdsTable<KB> t = lt_layout<KB, NV>(lds_raw);
-    lt_init<KB, NV>(t, HB_THREADS);
+    const LdsTable<KB> t = lt_layout<KB, NV, N>(lds_raw);
+    lt_init<KB, NV, N>(t, HB_THREADS);
     __syncthreads();
     const uint64_t row_begin = (uint64_t)blockIdx.x * hp.rows_per_wg;
     const uint64_t row_end = min(hp.n, row_begin + hp.rows_per_wg);
@@ -979,10 +997,10 @@ __global__ __launch_bounds__(HB_THREADS) void k_ha_direct(HaParams hp, HaTable g
                 for (int v = 0; v < NV; v++) vb[r][v] = ha_load_val(hp.vals[v], hp.vdtype[v], i);
             }
         }
-        lt2_add_many<KB, NV, U>(t, g, kb, vb, valid);
+        lt2_add_many<KB, NV, U, N>(t, g, kb, vb, valid);
     }
     __syncthreads();
-    lt_merge<KB, NV>(t, g, HB_THREADS);
+    lt_merge<KB, NV, N>(t, g, HB_THREADS);
 }
 
 // ---- table maintenance / finish -----------------------------------------------------------
@@ -1285,8 +1303,18 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     ensure_table(h, (uint64_t)dest + used_before);
     HaTable g = table_view(h->tab.ptr, h->slots, nv, h->vfloat, h->nnmask);
 
+    // the narrow LDS table (twice the slots) when no count(v) is read and keys are 4 bytes
+#ifndef VH_HA_NARROW_DEFAULT
+#define VH_HA_NARROW_DEFAULT 1
+#endif
+    static const bool narrow_on = [] {
+        const char *e = getenv("VH_HA_NARROW");
+        return e ? atoi(e) != 0 : VH_HA_NARROW_DEFAULT != 0;
+    }();
+    const bool narrow = narrow_on && kbs == 4 && nv <= 1 && h->nnmask == 0;
+    const double target_keys = narrow ? lt_target_keys<true>() : lt_target_keys<false>();
     uint32_t p_log2 = 0;
-    while (p_log2 < HA_MAX_P_LOG2 && dest / (double)(1u << p_log2) > LT_TARGET_KEYS) p_log2++;
+    while (p_log2 < HA_MAX_P_LOG2 && dest / (double)(1u << p_log2) > target_keys) p_log2++;
 
     HaParams hp{};
     hp.keys = keys;
@@ -1298,22 +1326,28 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     if (const char *dbg = getenv("VH_HA_DEBUG")) hp.debug = (uint32_t)atoi(dbg);
     hp.p_log2 = p_log2;
     hp.P = 1u << p_log2;
-    const size_t lt_lds = lt_bytes(nv, kbs);
+    const size_t lt_lds = lt_bytes(nv, kbs, narrow);
     if (p_log2 == 0) {
         // ---- direct: one LDS table per workgroup over a contiguous row range
         int bpc = 1;
-        VH_DISPATCH_KEY(h->key_dtype, K, dispatch_nv(nv, [&](auto nvc) {
-            constexpr int NV = decltype(nvc)::value;
-            bpc = blocks_per_cu(reinterpret_cast<const void *>(k_ha_direct<K, NV>), HB_THREADS, lt_lds);
-        }));
+        // f(kernel) for this key type / NV / table width
+        auto with_direct = [&](auto &&f) {
+            VH_DISPATCH_KEY(h->key_dtype, K, dispatch_nv(nv, [&](auto nvc) {
+                constexpr int NV = decltype(nvc)::value;
+                if constexpr (sizeof(kb_t<K>) == 4 && NV <= 1) {
+                    if (narrow) f(k_ha_direct<K, NV, true>);
+                    else f(k_ha_direct<K, NV, false>);
+                } else {
+                    f(k_ha_direct<K, NV, false>);
+                }
+            }));
+        };
+        with_direct([&](auto kernel) { bpc = blocks_per_cu(reinterpret_cast<const void *>(kernel), HB_THREADS, lt_lds); });
         const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cu_count() * bpc,
                                                                      (n + 4 * HB_THREADS - 1) / (4 * HB_THREADS)));
         hp.rows_per_wg = (n + W - 1) / W;
         TimedScope ts("ha_direct");
-        VH_DISPATCH_KEY(h->key_dtype, K, dispatch_nv(nv, [&](auto nvc) {
-            constexpr int NV = decltype(nvc)::value;
-            hipLaunchKernelGGL((k_ha_direct<K, NV>), dim3((unsigned)W), dim3(HB_THREADS), lt_lds, st, hp, g);
-        }));
+        with_direct([&](auto kernel) { hipLaunchKernelGGL(kernel, dim3((unsigned)W), dim3(HB_THREADS), lt_lds, st, hp, g); });
         VH_HIP(hipGetLastError());
         return;
     }
@@ -1470,8 +1504,13 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
             using KB = decltype(kbc);
             dispatch_nv(nv, [&](auto nvc) {
                 constexpr int NV = decltype(nvc)::value;
-                hipLaunchKernelGGL((k_ha_reduce<KB, NV>), dim3((unsigned)units.size()), dim3(HB_THREADS), lt_lds, st, hp,
-                                   g, d_units);
+                const dim3 grid((unsigned)units.size()), block(HB_THREADS);
+                if constexpr (sizeof(KB) == 4 && NV <= 1) {
+                    if (narrow) hipLaunchKernelGGL((k_ha_reduce<KB, NV, true>), grid, block, lt_lds, st, hp, g, d_units);
+                    else hipLaunchKernelGGL((k_ha_reduce<KB, NV, false>), grid, block, lt_lds, st, hp, g, d_units);
+                } else {
+                    hipLaunchKernelGGL((k_ha_reduce<KB, NV, false>), grid, block, lt_lds, st, hp, g, d_units);
+                }
             });
         });
         VH_HIP(hipGetLastError());
