@@ -185,8 +185,11 @@ template <int NV> __device__ inline void ha_global_row(const HaTable &g, uint64_
 // per bucket, so pass A needs half the buckets and its region runs are twice as long.
 // Records S and S + 1 (S = slots) hold the keys whose bits are the two top patterns
 // (kb_closed, kb_empty).
-template <bool N> __host__ __device__ constexpr uint32_t lt_slots() { return N ? 8192u : 4096u; }
-template <bool N> __host__ __device__ constexpr uint32_t lt_target_keys() { return N ? 4600u : 2300u; }
+#ifndef VH_LT_NARROW_SLOTS
+#define VH_LT_NARROW_SLOTS 8192
+#endif
+template <bool N> __host__ __device__ constexpr uint32_t lt_slots() { return N ? VH_LT_NARROW_SLOTS : 4096u; }
+template <bool N> __host__ __device__ constexpr uint32_t lt_target_keys() { return N ? VH_LT_NARROW_SLOTS * 9 / 16 : 2300u; }
 
 template <typename KB> struct LdsTable {
     KB *keys;                           // [S]
@@ -197,9 +200,12 @@ template <typename KB> struct LdsTable {
     uint32_t *used;
 };
 
+// every array starts 16-byte aligned: the key groups are read with ds_read_b128, which a
+// misaligned base splits (an 8-byte misalignment doubled pass B's time)
+__host__ __device__ constexpr size_t lt_a16(size_t b) { return (b + 15) & ~(size_t)15; }
 __host__ __device__ constexpr size_t lt_bytes(int nv, int kbsize, bool narrow) {
-    const size_t S = narrow ? 8192 : 4096;
-    return (size_t)(narrow ? 4 : 8) * (S + 2) + (size_t)8 * (S + 2) * nv + (size_t)kbsize * S +
+    const size_t S = narrow ? VH_LT_NARROW_SLOTS : 4096;
+    return lt_a16((size_t)(narrow ? 4 : 8) * (S + 2)) + lt_a16((size_t)8 * (S + 2)) * nv + (size_t)kbsize * S +
            (nv > 1 ? (size_t)4 * (S + 2) : 0) + 64;
 }
 
@@ -209,14 +215,14 @@ template <typename KB, int NV, bool N> __device__ inline LdsTable<KB> lt_layout(
     unsigned char *p = raw;
     if constexpr (N) {
         t.cn32 = reinterpret_cast<uint32_t *>(p);
-        p += 4 * (S + 2);  // 8-byte aligned: (S + 2) is even
+        p += lt_a16(4 * (S + 2));
     } else {
         t.cn = reinterpret_cast<unsigned long long *>(p);
-        p += 8 * (S + 2);
+        p += lt_a16(8 * (S + 2));
     }
     for (int v = 0; v < NV; v++) {
         t.sum[v] = reinterpret_cast<unsigned long long *>(p);
-        p += 8 * (S + 2);
+        p += lt_a16(8 * (S + 2));
     }
     t.keys = reinterpret_cast<KB *>(p);
     p += sizeof(KB) * S;
