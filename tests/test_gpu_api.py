@@ -224,3 +224,53 @@ def test_zero_d_grid_after_binned_query():
     assert int(df.sum("v")) == int(v.sum())
     assert int(df.count("v")) == n
     assert int(df.min("v")) == int(v.min()) and int(df.max("v")) == int(v.max())
+
+
+def test_minmax_binby_and_empty_cells():
+    """minmax(expr, binby=...) (dataframe.py:1276-1333): per cell [min, max] of the
+    expression, NaN ignored, empty cells [inf, -inf] (the OP_MIN_MAX initial values)."""
+    import vaex_amd
+    rng = np.random.default_rng(31)
+    n = 200_000
+    x = rng.normal(size=n)
+    y = rng.normal(size=n)
+    y[::17] = np.nan
+    df = vaex_amd.from_arrays(x=x, y=y)
+    got = df.minmax("y", binby="x", shape=12, limits=[-6, 6])
+    assert got.shape == (12, 2)
+    b = oracle.Binner("scalar", x, vmin=-6, vmax=6, bins=12)
+    cell = oracle.bin_indices([b], n).astype(np.int64) - 2  # central cells 0..11
+    for c in range(12):
+        sel = (cell == c) & ~np.isnan(y)
+        if sel.any():
+            assert got[c, 0] == np.min(y[sel]) and got[c, 1] == np.max(y[sel])
+        else:
+            assert got[c, 0] == np.inf and got[c, 1] == -np.inf
+    two = df.minmax(["x", "y"], binby="x", shape=4, limits=[-1, 1])
+    assert two.shape == (2, 4, 2)
+
+
+def test_limits_percentage_matches_restatement():
+    """limits('x', '90%') / limits_percentage (dataframe.py:1570-1614): the cumulative
+    16384-bin count over [min, max] interpolated at (1 -+ p) / 2 -- the same counts the
+    oracle bins (the max row falls in the overflow cell there too)."""
+    import vaex_amd
+    rng = np.random.default_rng(32)
+    x = rng.standard_t(3, size=300_000)
+    df = vaex_amd.from_arrays(x=x)
+    vmin, vmax = x.min(), x.max()
+    size = 16384
+    b = oracle.Binner("scalar", x, vmin=vmin, vmax=vmax, bins=size)
+    counts = oracle.extract_central_part(oracle.compute_grid([b], "count"))
+    cum = np.concatenate([[0], np.cumsum(counts)])
+    cum = cum / cum.max()
+    for pct in (90, 99.7):
+        f = (1 - pct / 100.) / 2
+        exp = np.interp([f, 1 - f], cum, np.linspace(vmin, vmax, size + 1))
+        np.testing.assert_allclose(df.limits("x", f"{pct}%"), exp, rtol=0, atol=0)
+        np.testing.assert_allclose(df.limits_percentage("x", pct), exp, rtol=0, atol=0)
+    # limits of a binby given as a percentage string
+    c = df.count(binby="x", limits="90%", shape=10)
+    assert int(np.asarray(c).sum()) < len(x)
+    with pytest.raises(AttributeError):
+        df.limits("x", "3sigma")

@@ -11,6 +11,9 @@ HBM per chunk) or :class:`~vaex_amd.device.DeviceArray` (HBM-resident).
 The reference's lazy expression engine is out of scope: expressions
 here are column names, or numpy expressions over host columns evaluated per chunk.
 """
+import ast
+import re
+
 import numpy as np
 
 from . import agg as vagg
@@ -427,19 +430,49 @@ class DataFrame:
 
     # ---- limits ------------------------------------------------------------------
     def limits(self, expression, value=None, square=False, selection=None, delay=False, shape=None):
-        """dataframe.py:1617+ for explicit [lo, hi] and 'minmax' (the GPU min/max pre-pass)."""
+        """dataframe.py:1617-1699 for one expression: explicit [lo, hi], 'minmax' (the GPU
+        min/max pre-pass) and percentages ('99.7%', '90percent'; the '%s' / 'percentsquare'
+        forms too, whose square flag the reference ignores).  'Nsigma' raises like the
+        reference, which calls a limits_sigma it does not define."""
         if value is None or (isinstance(value, str) and value == "minmax"):
             vmin, vmax = self.minmax(expression, selection=selection)
             return [vmin, vmax]
         if isinstance(value, str):
-            raise NotImplementedError(f"limits={value!r}: only explicit limits and 'minmax' are implemented")
+            match = re.match(r"([\d.]*)(\D*)", value)
+            number, kind = match.groups()
+            kind = kind.strip()
+            if kind in ("%", "percent", "%s", "%square", "percentsquare"):
+                return list(self.limits_percentage(expression, ast.literal_eval(number), selection=selection))
+            if kind in ("s", "sigma", "ss", "sigmasquare"):
+                raise AttributeError("'DataFrame' object has no attribute 'limits_sigma'")
+            raise ValueError("limit %r not understood" % value)
         return list(value)
+
+    def limits_percentage(self, expression, percentage=99.73, square=False, selection=False, delay=False):
+        """dataframe.py:1570-1614: the range around the median holding about `percentage` %
+        of the rows, read off the cumulative 16384-bin histogram over [min, max] (both
+        passes on the GPU)."""
+        waslist, [expressions] = listify(_ensure_strings(expression))
+        sel = None if selection in (None, False) else selection
+        out = []
+        for expr in expressions:
+            vmin, vmax = self.minmax(expr, selection=sel)
+            size = 1024 * 16
+            counts = np.asarray(self.count(binby=expr, shape=size, limits=[vmin, vmax], selection=selection))
+            cumcounts = np.concatenate([[0], np.cumsum(counts)])
+            cumcounts = cumcounts / cumcounts.max()
+            f = (1 - percentage / 100.) / 2
+            x = np.linspace(vmin, vmax, size + 1)
+            out.append(np.interp([f, 1 - f], cumcounts, x))
+        return unlistify(waslist, out)
 
     def minmax(self, expression, binby=[], limits=None, shape=default_shape, selection=False, delay=False,
                progress=None):
-        """dataframe.py:1276-1333 (no binby): NaN-ignoring min/max, cast back to the column dtype."""
+        """dataframe.py:1276-1333: NaN-ignoring min/max, cast back to the column dtype.  With
+        binby, per cell of the grid (the last dimension holds [min, max]); an empty cell reads
+        [inf, -inf], the OP_MIN_MAX initial values (tasks.py:173-185)."""
         if binby:
-            raise NotImplementedError("minmax with binby")
+            return self._minmax_binby(expression, binby, limits, shape, selection, delay)
         expression = _ensure_strings(expression)
         waslist, [expressions] = listify(expression)
         sel = selection if selection not in (None, False) else None
@@ -454,6 +487,23 @@ class DataFrame:
             return unlistify(waslist, v) if waslist else v[0]
 
         return self._delay(delay, finish(*tasks))
+
+    def _minmax_binby(self, expression, binby, limits, shape, selection, delay):
+        waslist, [expressions] = listify(_ensure_strings(expression))
+        dtypes = [self.data_type(e) for e in expressions]
+        if any(d.kind != dtypes[0].kind for d in dtypes):
+            raise TypeError("cannot mix different dtypes in 1 minmax call")
+        kw = dict(binby=binby, limits=limits, shape=shape, selection=selection, delay=True)
+        parts = [(self.min(e, **kw), self.max(e, **kw), self.count(e, **kw)) for e in expressions]
+        self.execute()
+        values = []
+        for mn, mx, cnt in parts:
+            mn, mx, cnt = (np.asarray(p.get()) for p in (mn, mx, cnt))
+            v = np.stack([mn.astype(np.float64), mx.astype(np.float64)], axis=-1)
+            v[cnt == 0] = [np.inf, -np.inf]
+            values.append(v)
+        value = unlistify(waslist, np.array(values))
+        return self._delay(delay, np.asarray(value).astype(dtypes[0]))
 
     # ---- aggregations ------------------------------------------------------------
     def _compute_agg(self, name, expression, binby=[], limits=None, shape=default_shape, selection=False,
