@@ -24,6 +24,8 @@
 // AggCount/AggSum (superagg.cpp:168-191,362-388): counts exact, float sums in a
 // different association order (within 1e-6 relative, north_star).
 #include <algorithm>
+#include <atomic>
+#include <cstdio>
 #include <cmath>
 #include <map>
 #include <memory>
@@ -82,6 +84,8 @@ struct TileParams {
     int32_t cnt_slot[MAX_FUSED_AGGS];  // count agg k -> CNT_ALWAYS / CNT_FLAG / value slot
     const double *vdata[2];    // value slot -> source column (fast kernel)
     uint32_t debug;            // experiment switches (VH_TILE_DEBUG), 0 in production
+    const uint32_t *tile_of;   // [T] region id -> grid tile (XCD-resident path), nullptr = identity
+    const uint32_t *abort_word;  // XCD-resident path's state word: pass B skips an aborted launch
 };
 
 struct WorkUnit {
@@ -926,6 +930,7 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
     extern __shared__ __align__(16) unsigned char lds_raw[];
     __shared__ uint32_t s_fill[1024];
     __shared__ uint32_t s_pre[1025];
+    if (tp.abort_word && *tp.abort_word != 1u) return;  // resident launch not committed: rerun by the host
     const WorkUnit u = units[blockIdx.x];
     const uint32_t t = u.tile;
     const uint32_t cap = tp.cap[t];
@@ -1025,7 +1030,7 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
     }
     __syncthreads();
     if (tp.debug & 16) return;
-    const uint64_t c0 = (uint64_t)t << tp.s_log2;
+    const uint64_t c0 = (uint64_t)(tp.tile_of ? tp.tile_of[t] : t) << tp.s_log2;
     const uint32_t ncell = (uint32_t)min((uint64_t)1 << tp.s_log2, tp.cells - c0);
     #pragma unroll
     for (int k = 0; k < MAX_FUSED_AGGS; k++) {
@@ -1042,6 +1047,496 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                 if (v != 0.0) atomicAdd(reinterpret_cast<double *>(fa.a[k].grid) + c0 + i, v);
             }
         }
+    }
+}
+
+// ---- XCD-resident hot tiles: one persistent launch replaces pass A + most of pass B ----
+//
+// The two-pass path moves every row through HBM twice more (pass A writes a 10-B entry,
+// pass B reads it back): 44 B of traffic per 24-B count+sum row, and HBM read/write
+// turnaround caps such a mix at ~3.6 TB/s of reads.  Here one workgroup
+// per CU (8 XCDs x P) runs the whole query.  Each XCD keeps its own replica of the H
+// densest tiles (sample histogram), spread over the LDS of its P workgroups (TPW tiles
+// each).  A workgroup reads its row range like pass A, counting-sorts each batch by
+// region id (hot tiles first, in owner order) and
+//   * hands the hot prefix to the owners on its own XCD through a batch slot (K slots per
+//     producer, plain stores that stay in the XCD's L2, read back with L1-bypassing `sc1`
+//     loads by workgroups whose HW_REG_XCC_ID is the same), and
+//   * streams the cold suffix to per-(workgroup, tile) regions for pass B, as pass A does.
+// Between batches it consumes what the producers of its XCD published for its tiles (LDS
+// atomics).  Flags: `sc1` stores / loads (ready[x][p] = batches published by p;
+// cons[x][p][c] = batches of p consumed by c; a producer reuses slot b % K once every
+// consumer acknowledged batch b - K).  No wait is unbounded: a workgroup that sees no
+// progress for `timeout` ticks (or finds more workgroups on its XCD than slots) sets the
+// state word to ABORT; the launch then writes nothing to the grids, pass B skips, and the
+// host reruns the query on the two-pass path.  Otherwise the last workgroup to finish
+// commits, every owner flushes its LDS tiles with coalesced global atomics and applies its
+// few cold-region overflows.  Results are the same sums of the same rows (counts exact,
+// float sums within 1e-6 relative).
+#ifndef VH_RES_K
+#define VH_RES_K 4
+#endif
+constexpr uint32_t RES_HDR = 64;   // run offsets per batch-slot header (P + 1 <= 64)
+constexpr uint32_t RES_OVF = 2048; // cold-region overflow entries kept per workgroup
+enum : uint32_t { RES_RUNNING = 0, RES_COMMIT = 1, RES_ABORT = 2 };
+
+struct ResidentParams {
+    uint32_t P, K, H, TPW, nb, G, wt, pad;
+    uint64_t timeout;          // wall-clock ticks without progress before ABORT
+    uint32_t *ctl;             // [0] state, [1] finished workgroups, [2 + x] slots taken on XCD x
+    uint32_t *ready;           // [8][P]
+    uint32_t *cons;            // [8][P producer][P consumer]
+    uint32_t *hdr;             // [8][P][K][RES_HDR]
+    uint32_t *skeys;           // [8][P][K][TA_BATCH] owner-local cell
+    double *svals;             // [8][P][K][TA_BATCH]
+    const uint32_t *tmap;      // [T] grid tile -> region id (hot ids 0..H-1)
+    const uint32_t *tile_of;   // [T] region id -> grid tile
+    uint32_t *ovf_key;         // [G][RES_OVF] id << 16 | cell in tile
+    double *ovf_val;           // [G][RES_OVF]
+};
+
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p) {
+    return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double *p) {
+    return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<uint64_t *>(const_cast<double *>(p)),
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double *p, double v) {
+    __hip_atomic_store(reinterpret_cast<uint64_t *>(p), __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// LDS of the resident kernel: owner tiles (fr.lds_words words) | pass-A staging | tmap[T]
+__host__ __device__ inline size_t resident_lds_bytes(uint32_t tile_words, int nv, uint32_t T) {
+    return (size_t)4 * tile_words + fast_lds_bytes(nv, T, TA_BATCH) + (size_t)4 * T;
+}
+
+// apply one staged row to the grids with global atomics (region overflow)
+template <int NV>
+__device__ inline void apply_row_global(const FusedAggs &fa, const TileParams &tp, uint64_t c, uint32_t count_mask,
+                                        const uint32_t *keyed_slot_of, const double *v) {
+    #pragma unroll
+    for (int a = 0; a < MAX_FUSED_AGGS; a++) {
+        if (a >= fa.na) break;
+        bool take = (count_mask >> a) & 1;
+        if constexpr (NV > 0) {
+            if (!take) take = v[keyed_slot_of[a]] == v[keyed_slot_of[a]];
+        }
+        if (!take) continue;
+        if (fa.a[a].kind == VH_AGG_COUNT) {
+            atomicAdd((unsigned long long *)fa.a[a].grid + c, 1ULL);
+        } else if constexpr (NV > 0) {
+            atomicAdd(reinterpret_cast<double *>(fa.a[a].grid) + c, v[tp.val_slot[a]]);
+        }
+    }
+}
+
+// Roles inside the workgroup: waves 0..RES_PW-1 produce (pass-A pipeline, synchronised by
+// an LDS counter barrier among themselves), RES_CW consumer waves poll the producers of
+// their XCD independently (no workgroup barrier), so neither side waits on the other's
+// memory latency.
+constexpr int RES_PW = TA_THREADS / 64;
+#ifndef VH_RES_CW
+#define VH_RES_CW 4
+#endif
+constexpr int RES_CW = VH_RES_CW;
+constexpr int RES_THREADS = TA_THREADS + 64 * RES_CW;
+constexpr int RES_CU = 4;  // slot entries per consumer lane in flight
+
+// barrier of the producer waves only: one lane per wave adds, then spins on the LDS counter
+__device__ __forceinline__ void prod_barrier(uint32_t *ctr, uint32_t &target) {
+    target += RES_PW;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if ((threadIdx.x & 63) == 0) {
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+            __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <int ND, int NV>
+__global__ __launch_bounds__(RES_THREADS) void k_tile_resident(BinPlan p, FusedAggs fa, FusedAggs fr, TileParams tp,
+                                                               ResidentParams rp, uint64_t n) {
+    constexpr int NC = ND + NV;
+    constexpr int PAIRS = TA_RPT / 2;
+    constexpr uint32_t CAP = TA_BATCH;
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    __shared__ uint32_t s_ctl[8], s_bar;
+    __shared__ uint32_t s_wpre[RES_CW][65], s_wbeg[RES_CW][64], s_wsb[RES_CW][64];
+    const uint32_t T = tp.ntiles;
+    unsigned char *tl = lds_raw;
+    const ScatterLds l = fast_lds<NV>(lds_raw + (size_t)4 * fr.lds_words, T, CAP);
+    uint32_t *s_tmap = reinterpret_cast<uint32_t *>(lds_raw + (size_t)4 * fr.lds_words + fast_lds_bytes(NV, T, CAP));
+    uint32_t *sk = reinterpret_cast<uint32_t *>(l.sp);
+    const uint32_t tid = threadIdx.x;
+    {
+        uint32_t *lw = reinterpret_cast<uint32_t *>(tl);
+        for (uint32_t i = tid; i < fr.lds_words; i += RES_THREADS) lw[i] = 0;
+    }
+    for (uint32_t t = tid; t < T; t += RES_THREADS) s_tmap[t] = rp.tmap[t];
+    for (uint32_t t = tid; t < T; t += RES_THREADS) {
+        l.hist[t] = 0;
+        l.base[t] = (uint32_t)tp.toff[t];
+        l.lim[t] = (uint32_t)tp.toff[t] + tp.cap[t];
+    }
+    if (tid == 0) {
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        xcc &= 0xfu;
+        const uint32_t slot = xcc < 8 ? atomicAdd(&rp.ctl[2 + xcc], 1u) : 0xffffffffu;
+        bool ab = ld_sc1(&rp.ctl[0]) == RES_ABORT;
+        if (slot >= rp.P) {  // placement the slots do not cover: the two-pass path reruns the query
+            atomicCAS(&rp.ctl[0], RES_RUNNING, RES_ABORT);
+            ab = true;
+        }
+        s_ctl[0] = xcc;
+        s_ctl[1] = slot;
+        s_ctl[3] = ab ? 1u : 0u;  // abort seen
+        s_ctl[6] = 0;             // overflow entries
+        s_ctl[7] = 0;             // overflow list full
+        s_bar = 0;
+    }
+    __syncthreads();
+    if (s_ctl[3]) return;
+    const uint32_t xcc = s_ctl[0], me = s_ctl[1];
+    const uint32_t P = rp.P, K = rp.K, H = rp.H, TPW = rp.TPW, nb = rp.nb;
+    const uint32_t smask = (1u << tp.s_log2) - 1, s_log2 = tp.s_log2;
+    const uint64_t xp0 = (uint64_t)xcc * P;
+    const uint32_t w = blockIdx.x;
+    uint32_t count_mask = 0, keyed_slot_of[MAX_FUSED_AGGS], nan_keyed[NV > 0 ? NV : 1] = {};
+    #pragma unroll
+    for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+        keyed_slot_of[k] = 0;
+        if (k >= fa.na) break;
+        keyed_slot_of[k] = fa.a[k].kind == VH_AGG_COUNT ? (uint32_t)tp.cnt_slot[k] : (uint32_t)tp.val_slot[k];
+        if (fa.a[k].kind == VH_AGG_COUNT && tp.cnt_slot[k] == CNT_ALWAYS) count_mask |= 1u << k;
+        else
+#pragma unroll
+            for (int s = 0; s < NV; s++)
+                if ((uint32_t)s == keyed_slot_of[k]) nan_keyed[s] |= 1u << k;
+    }
+    uint32_t *ovf_key = rp.ovf_key + (uint64_t)w * RES_OVF;
+    double *ovf_val = rp.ovf_val + (uint64_t)w * RES_OVF;
+
+    if (tid < TA_THREADS) {
+        // ================= producer waves =================
+        const double *col[NC];
+        double vmin[ND], scale[ND], bins_d[ND];
+        uint32_t bins2[ND], stride[ND];
+#pragma unroll
+        for (int d = 0; d < ND; d++) {
+            col[d] = reinterpret_cast<const double *>(p.b[d].data);
+            vmin[d] = p.b[d].vmin;
+            scale[d] = p.b[d].scale;
+            bins_d[d] = (double)p.b[d].bins;
+            bins2[d] = (uint32_t)p.b[d].bins + 2;
+            stride[d] = (uint32_t)p.b[d].stride;
+        }
+#pragma unroll
+        for (int s = 0; s < NV; s++) col[ND + s] = tp.vdata[s];
+        const uint64_t row_begin = (uint64_t)w * tp.rows_per_wg;
+        const uint64_t row_end = min(n, row_begin + tp.rows_per_wg);
+        const uint64_t region0 = (uint64_t)w * tp.wg_stride;
+        uint32_t bar = 0;
+        uint32_t cmin = 0;  // wave 0: least batch count every consumer acknowledged (cached)
+        uint64_t last = wall_clock64();
+        auto load = [&](uint64_t b0, double2 (&dst)[PAIRS][NC]) {
+#pragma unroll
+            for (int q = 0; q < PAIRS; q++) {
+                const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + tid);
+                const uint64_t is = i < n - 2 ? i : n - 2;
+#pragma unroll
+                for (int c = 0; c < NC; c++) dst[q][c] = *reinterpret_cast<const double2 *>(col[c] + is);
+            }
+        };
+        // one batch: `cur` holds its rows (loaded one step earlier), `nxt` receives the next
+        auto step = [&](uint32_t b, double2 (&cur)[PAIRS][NC], double2 (&nxt)[PAIRS][NC]) -> bool {
+            const uint64_t b0 = row_begin + (uint64_t)b * CAP;
+            // this batch's loads and the previous batch's stores complete; then the previous
+            // batch is published (every producer wave's stores have reached L2)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            prod_barrier(&s_bar, bar);
+            if (tid == 0 && b > 0) {
+                if (rp.wt) st_sc1(&rp.ready[xp0 + me], b);
+                else rp.ready[xp0 + me] = b;  // same XCD: the flag stays in the L2 the pollers read
+            }
+            if (b + 1 < nb) load(b0 + CAP, nxt);
+            uint32_t key[TA_RPT];
+            int32_t rank[TA_RPT];
+            double vals[TA_RPT][NV > 0 ? NV : 1];
+            if (tp.debug & 2048) {  // experiment: loads + cell math only, nothing published
+                uint32_t acc = 0;
+#pragma unroll
+                for (int r = 0; r < TA_RPT; r++) {
+                    const int q = r >> 1, h = r & 1;
+                    uint32_t c = 0;
+#pragma unroll
+                    for (int d = 0; d < ND; d++)
+                        c += scalar_f64_index32(h ? cur[q][d].y : cur[q][d].x, vmin[d], scale[d], bins_d[d], bins2[d]) * stride[d];
+                    acc += c;
+                }
+                asm volatile("" ::"v"(acc));
+                return true;
+            }
+#pragma unroll
+            for (int r = 0; r < TA_RPT; r++) {
+                const int q = r >> 1, h = r & 1;
+                const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + tid) + h;
+                uint32_t c = 0;
+#pragma unroll
+                for (int d = 0; d < ND; d++) {
+                    const double v = h ? cur[q][d].y : cur[q][d].x;
+                    c += scalar_f64_index32(v, vmin[d], scale[d], bins_d[d], bins2[d]) * stride[d];
+                }
+                uint32_t f = count_mask;
+#pragma unroll
+                for (int s = 0; s < NV; s++) {
+                    vals[r][s] = h ? cur[q][ND + s].y : cur[q][ND + s].x;
+                    f |= vals[r][s] == vals[r][s] ? nan_keyed[s] : 0u;
+                }
+                f = i < row_end ? f : 0u;
+                const uint32_t id = s_tmap[c >> s_log2];
+                key[r] = (id << 16) | (c & smask);
+                rank[r] = f ? (int32_t)atomicAdd(&l.hist[id], 1u) : -1;
+            }
+            prod_barrier(&s_bar, bar);
+            fast_scan(l, T);
+            prod_barrier(&s_bar, bar);
+            const uint32_t tot = l.wave_sums[0];
+            const uint32_t hot_n = H < T ? l.boff[H] : tot;
+#pragma unroll
+            for (int r = 0; r < TA_RPT; r++) {
+                if (rank[r] < 0) continue;
+                const uint32_t pos = l.boff[key[r] >> 16] + (uint32_t)rank[r];
+                sk[pos] = key[r];
+#pragma unroll
+                for (int s = 0; s < NV; s++) l.sv[s * CAP + pos] = vals[r][s];
+            }
+            // wave 0: slot b % K is free once every owner acknowledged batch b - K
+            if (tid < 64 && b >= K && cmin < b - K + 1) {
+                const uint32_t target = b - K + 1;
+                for (;;) {
+                    const uint32_t v = tid < P ? ld_sc1(&rp.cons[(xp0 + me) * P + tid]) : 0xffffffffu;
+                    uint32_t m = v;
+#pragma unroll
+                    for (int off = 32; off; off >>= 1) m = min(m, (uint32_t)__shfl_xor(m, off, 64));
+                    if (m >= target) {
+                        cmin = m;
+                        last = wall_clock64();
+                        break;
+                    }
+                    if (tid == 0) {
+                        const uint64_t now = wall_clock64();
+                        if (ld_sc1(&rp.ctl[0]) == RES_ABORT) s_ctl[3] = 1;
+                        else if (now - last > rp.timeout) {
+                            atomicCAS(&rp.ctl[0], RES_RUNNING, RES_ABORT);
+                            s_ctl[3] = 1;
+                        }
+                    }
+                    if (__shfl(s_ctl[3], 0, 64)) break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            // the stop decision every producer wave reads: written by lane 0 before the barrier
+            // (s_ctl[3] may change under the consumer waves at any time)
+            if (tid == 0) s_ctl[5] = s_ctl[3];
+            prod_barrier(&s_bar, bar);
+            if (s_ctl[5]) return false;
+            const uint64_t sb = (xp0 + me) * K + b % K;
+            uint32_t *dk = rp.skeys + sb * CAP;
+            double *dv = rp.svals + sb * CAP;
+            for (uint32_t k = tid; k < hot_n && !(tp.debug & 512); k += TA_THREADS) {  // 512: no slot stores
+                const uint32_t kk = sk[k];
+                const uint32_t loc = (((kk >> 16) % TPW) << s_log2) | (kk & smask);
+                if (rp.wt) st_sc1(dk + k, loc);
+                else dk[k] = loc;
+#pragma unroll
+                for (int s = 0; s < NV; s++) {
+                    if (rp.wt) st_sc1(dv + k, l.sv[s * CAP + k]);
+                    else dv[k] = l.sv[s * CAP + k];
+                }
+            }
+            for (uint32_t o = tid; o <= P; o += TA_THREADS) {
+                const uint32_t id = o * TPW;
+                const uint32_t v = id < H ? l.boff[id] : hot_n;
+                if (rp.wt) st_sc1(&rp.hdr[sb * RES_HDR + o], v);
+                else rp.hdr[sb * RES_HDR + o] = v;
+            }
+            for (uint32_t k = hot_n + tid; k < tot && !(tp.debug & 1024); k += TA_THREADS) {  // 1024: no cold stores
+                const uint32_t kk = sk[k];
+                const uint32_t t = kk >> 16;
+                const uint32_t dest = l.dbase[t] + k;
+                if (dest < l.lim[t]) {
+                    const uint64_t e = region0 + dest;
+                    reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)kk;
+#pragma unroll
+                    for (int s = 0; s < NV; s++) tp.values[s][e] = l.sv[s * CAP + k];
+                } else {  // region overflow (a sampling miss): kept until the launch commits
+                    const uint32_t pos = atomicAdd(&s_ctl[6], 1u);
+                    if (pos < RES_OVF) {
+                        ovf_key[pos] = kk;
+                        if constexpr (NV > 0) ovf_val[pos] = l.sv[k];
+                    } else {
+                        s_ctl[7] = 1;
+                    }
+                }
+            }
+            return true;
+        };
+        double2 A[PAIRS][NC], B[PAIRS][NC];
+        load(row_begin, A);
+        bool ok = true;
+        for (uint32_t b = 0; b < nb && ok; b += 2) {
+            ok = step(b, A, B);
+            if (ok && b + 1 < nb) ok = step(b + 1, B, A);
+        }
+        if (ok) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            prod_barrier(&s_bar, bar);
+            if (tid == 0) {
+                if (rp.wt) st_sc1(&rp.ready[xp0 + me], nb);
+                else rp.ready[xp0 + me] = nb;
+            }
+        }
+        for (uint32_t t = tid; t < T; t += TA_THREADS)
+            tp.fills[(uint64_t)t * tp.W + w] = t < H ? 0u : l.base[t] - (uint32_t)tp.toff[t];
+    } else {
+        // ================= consumer waves =================
+        const uint32_t cw = (tid - TA_THREADS) >> 6, lane = tid & 63;
+        const uint32_t nq = P > cw ? (P - cw + RES_CW - 1) / RES_CW : 0;  // producers of this wave
+        const uint32_t q = cw + lane * RES_CW;                             // this lane's producer
+        uint32_t *wpre = s_wpre[cw], *wbeg = s_wbeg[cw], *wsb = s_wsb[cw];
+        uint32_t nx = 0, idle = 0;
+        uint64_t last = wall_clock64();
+        for (;;) {
+            const bool mine = lane < nq && nx < nb && !(tp.debug & 4096);  // 4096: experiment, no consumers
+            if (!__any(mine)) break;
+            bool av = false;
+            uint32_t beg = 0, cnt = 0, sbq = 0;
+            if (mine && ld_sc1(&rp.ready[xp0 + q]) > nx) {
+                sbq = (uint32_t)((xp0 + q) * K + nx % K);
+                beg = ld_sc1(&rp.hdr[(uint64_t)sbq * RES_HDR + me]);
+                cnt = ld_sc1(&rp.hdr[(uint64_t)sbq * RES_HDR + me + 1]) - beg;
+                av = true;
+            }
+            uint32_t inc = cnt;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(inc, off, 64);
+                if ((int)lane >= off) inc += y;
+            }
+            const uint32_t total = __shfl(inc, 63, 64);
+            if (total) {
+                wpre[lane] = inc - cnt;
+                wbeg[lane] = beg;
+                wsb[lane] = sbq;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+                for (uint32_t i0 = 0; i0 < total; i0 += 64 * RES_CU) {
+                    uint32_t loc[RES_CU];
+                    double v[RES_CU][NV > 0 ? NV : 1];
+#pragma unroll
+                    for (int u = 0; u < RES_CU; u++) {
+                        const uint32_t i = i0 + u * 64 + lane;
+                        loc[u] = 0xffffffffu;
+                        if (i < total && !(tp.debug & 256)) {  // 256: experiment, consumers only acknowledge
+                            uint32_t k = 0;
+#pragma unroll
+                            for (uint32_t stp = 8; stp; stp >>= 1)
+                                if (k + stp < nq && wpre[k + stp] <= i) k += stp;
+                            const uint64_t e = (uint64_t)wsb[k] * CAP + wbeg[k] + (i - wpre[k]);
+                            loc[u] = ld_sc1(rp.skeys + e);
+#pragma unroll
+                            for (int s = 0; s < NV; s++) v[u][s] = ld_sc1(rp.svals + e);
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < RES_CU; u++)
+                        if (loc[u] != 0xffffffffu) reduce_entry<NV>(fr, tp, tl, loc[u], 0xfu, v[u]);
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (av) {
+                nx++;
+                if (rp.wt) st_sc1(&rp.cons[(xp0 + q) * P + me], nx);
+                else rp.cons[(xp0 + q) * P + me] = nx;
+            }
+            if (__any(av)) {
+                idle = 0;
+                if (lane == 0) last = wall_clock64();
+            } else {
+                __builtin_amdgcn_s_sleep(4);
+                if ((++idle & 15) == 0) {
+                    uint32_t stop = 0;
+                    if (lane == 0) {
+                        if (s_ctl[3] || ld_sc1(&rp.ctl[0]) == RES_ABORT) stop = 1;
+                        else if (wall_clock64() - last > rp.timeout) {
+                            atomicCAS(&rp.ctl[0], RES_RUNNING, RES_ABORT);
+                            stop = 1;
+                        }
+                        if (stop) s_ctl[3] = 1;
+                    }
+                    if (__shfl(stop, 0, 64)) break;
+                }
+            }
+        }
+    }
+    // commit when every workgroup finished; abort otherwise
+    __syncthreads();
+    if (tid == 0) {
+        if (!s_ctl[3]) {
+            if (s_ctl[7]) atomicCAS(&rp.ctl[0], RES_RUNNING, RES_ABORT);
+            atomicAdd(&rp.ctl[1], 1u);
+            const uint64_t t0 = wall_clock64();
+            for (;;) {
+                if (ld_sc1(&rp.ctl[1]) >= rp.G) {
+                    atomicCAS(&rp.ctl[0], RES_RUNNING, RES_COMMIT);
+                    break;
+                }
+                if (ld_sc1(&rp.ctl[0]) != RES_RUNNING) break;
+                if (wall_clock64() - t0 > rp.timeout) {
+                    atomicCAS(&rp.ctl[0], RES_RUNNING, RES_ABORT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(8);
+            }
+        }
+        s_ctl[2] = ld_sc1(&rp.ctl[0]) == RES_COMMIT ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!s_ctl[2]) return;
+    // flush the owner tiles
+    const uint32_t Sp = TPW << s_log2;
+    #pragma unroll
+    for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+        if (k >= fr.na) break;
+        for (uint32_t i = tid; i < Sp; i += RES_THREADS) {
+            const uint32_t id = me * TPW + (i >> s_log2);
+            if (id >= H) continue;
+            const uint64_t c = ((uint64_t)rp.tile_of[id] << s_log2) | (i & smask);
+            if (c >= tp.cells) continue;
+            if (fr.a[k].kind == VH_AGG_COUNT) {
+                const uint32_t v = reinterpret_cast<const uint32_t *>(tl + fr.a[k].lds_off)[i];
+                if (v) atomicAdd((unsigned long long *)fr.a[k].grid + c, (unsigned long long)v);
+            } else {
+                const double v = reinterpret_cast<const double *>(tl + fr.a[k].lds_off)[i];
+                if (v != 0.0) atomicAdd(reinterpret_cast<double *>(fr.a[k].grid) + c, v);
+            }
+        }
+    }
+    const uint32_t novf = min(s_ctl[6], RES_OVF);
+    for (uint32_t i = tid; i < novf; i += RES_THREADS) {
+        const uint32_t kk = ovf_key[i];
+        const uint64_t c = ((uint64_t)rp.tile_of[kk >> 16] << s_log2) | (kk & smask);
+        double v[NV > 0 ? NV : 1];
+        if constexpr (NV > 0) v[0] = ovf_val[i];
+        apply_row_global<NV>(fa, tp, c, count_mask, keyed_slot_of, v);
     }
 }
 
@@ -1115,8 +1610,16 @@ static const void *ord_kernel(int nv, int fast_mode, bool set) {
     return set ? ord_kernel_t<true>(nv, fast_mode) : ord_kernel_t<false>(nv, fast_mode);
 }
 
-static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64,
-                           Workspace &ws);
+// 0 = not tiled (caller takes another path), 1 = done, 2 = the XCD-resident launch aborted
+// (nothing written to the grids): run again on the two-pass path
+static int try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64,
+                          Workspace &ws, bool allow_res);
+static bool try_tiled_once(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64,
+                           Workspace &ws) {
+    const int r = try_tiled_impl(plan, fa_in, n, cells, nd_f64, ws, true);
+    if (r == 2) return try_tiled_impl(plan, fa_in, n, cells, nd_f64, ws, false) == 1;
+    return r == 1;
+}
 
 // the fast ordinal pass A applies: one native int32 BinnerOrdinal without mask, every
 // sum a 16-byte aligned float64 column, no aggregator masks, no counts of other columns
@@ -1146,7 +1649,7 @@ bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t
     if ((n & 1) && !fa_in.generic_vals && (nd_f64 > 0 || ord_fast_ok(plan, fa_in))) {
         // the fast pass A reads row pairs: tile all rows but the last, which takes the
         // global-atomic path
-        if (!try_tiled_impl(plan, fa_in, n - 1, cells, nd_f64, ws)) return false;
+        if (!try_tiled_once(plan, fa_in, n - 1, cells, nd_f64, ws)) return false;
         BinPlan p1 = plan;
         FusedAggs f1 = fa_in;
         for (int d = 0; d < p1.nb; d++) {
@@ -1160,7 +1663,7 @@ bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t
         launch_fused(p1, f1, 1, cells, nd_f64, ws);
         return true;
     }
-    return try_tiled_impl(plan, fa_in, n, cells, nd_f64, ws);
+    return try_tiled_once(plan, fa_in, n, cells, nd_f64, ws);
 }
 
 // Partition scratch shared by every grid of a device: a 1e9-row count+sum needs ~10 GB of
@@ -1169,8 +1672,35 @@ bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t
 // by the library stream.
 struct TileScratch {
     std::mutex mu;
-    DevBuf entries, values, meta;
+    DevBuf entries, values, meta, res;
 };
+
+// XCD-resident path switch (opt-in; measured slower than the two-pass path, DESIGN.md
+// §5.1): VH_RESIDENT=0 off (default), 1 on (slot data and flags by plain stores kept in the
+// XCD's L2), 2 on with write-through (`sc1`) stores; an aborted launch turns it off for the
+// process
+static std::atomic<bool> g_res_off{false};
+static int res_mode() {
+    if (g_res_off.load()) return 0;
+    const char *e = getenv("VH_RESIDENT");
+    return e ? atoi(e) : 0;
+}
+static uint64_t res_min_rows() {  // VH_RES_MIN_ROWS: tests run the path at small sizes
+    const char *e = getenv("VH_RES_MIN_ROWS");
+    return e ? strtoull(e, nullptr, 10) : (1ull << 24);
+}
+static uint64_t wall_clock_khz() {
+    static std::mutex mu;
+    static std::map<int, uint64_t> m;
+    std::lock_guard<std::mutex> lk(mu);
+    const int dev = current_device();
+    auto it = m.find(dev);
+    if (it != m.end()) return it->second;
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+    m[dev] = (uint64_t)khz;
+    return (uint64_t)khz;
+}
 static TileScratch &tile_scratch() {
     static std::mutex g;
     static std::map<int, std::unique_ptr<TileScratch>> m;
@@ -1180,8 +1710,8 @@ static TileScratch &tile_scratch() {
     return *p;
 }
 
-static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64,
-                           Workspace &) {
+static int try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64,
+                          Workspace &, bool allow_res) {
     TileScratch &ws = tile_scratch();
     std::lock_guard<std::mutex> ws_lock(ws.mu);
     TileParams tp{};
@@ -1276,12 +1806,25 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         bpc = it->second;
     }
     bpc = std::max(1, std::min(bpc, TA_WG_PER_CU));
-    const uint32_t W = std::min<uint32_t>(1024, (uint32_t)cu_count() * bpc);
+    // XCD-resident variant: the fast f64 pass A with <= 1 value slot, one workgroup per CU,
+    // P owners per XCD holding TPW tiles each in LDS (resident_lds_bytes + static arrays)
+    const int rmode = allow_res && fast && nv <= 1 && nd_f64 >= 1 && nd_f64 <= 3 && n >= res_min_rows() ? res_mode() : 0;
+    uint32_t rP = 0, rTPW = 0;
+    if (rmode && cu_count() % 8 == 0 && cu_count() / 8 <= (int)RES_HDR - 1) {
+        rP = (uint32_t)cu_count() / 8;
+        for (uint32_t k = 1; (S * k) <= 65536; k++) {
+            const uint64_t words = ((S * k * per_cell + 15) & ~uint64_t(15)) / 4;
+            if (resident_lds_bytes((uint32_t)words, nv, T) + 4096 > LDS_MAX_BYTES) break;
+            rTPW = k;
+        }
+    }
+    bool res = rTPW > 0;
+    const uint32_t W = res ? 8 * rP : std::min<uint32_t>(1024, (uint32_t)cu_count() * bpc);
     // pass-B work units: sum over tiles of ceil(e_t / target) <= T + 4 cu (target = n / 4 cu)
     const uint64_t max_units = (uint64_t)T + 4 * (uint64_t)cu_count() + 16;
     DevBuf &meta = ws.meta;
     const uint64_t meta_bytes = 8 * (uint64_t)T /*hist*/ + 4 * (uint64_t)T /*cap*/ + 8 * (uint64_t)T /*toff*/ +
-                                4 * (uint64_t)T * W /*fills*/ + 16 * max_units /*units*/ + 256;
+                                4 * (uint64_t)T * W /*fills*/ + 16 * max_units /*units*/ + 8 * (uint64_t)T /*tmap, tile_of*/ + 256;
     meta.ensure(meta_bytes);
     unsigned char *mb = meta.as<unsigned char>();
     uint64_t *d_hist = reinterpret_cast<uint64_t *>(mb);
@@ -1289,6 +1832,8 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     uint32_t *d_cap = reinterpret_cast<uint32_t *>(d_toff + T);
     uint32_t *d_fills = d_cap + ((T + 3) & ~3u);
     WorkUnit *d_units = reinterpret_cast<WorkUnit *>(d_fills + (uint64_t)T * W + 4 - ((uint64_t)T * W) % 4);
+    uint32_t *d_tmap = reinterpret_cast<uint32_t *>(d_units + max_units);
+    uint32_t *d_tile_of = d_tmap + T;
     const uint64_t nb = (n + TA_BATCH - 1) / TA_BATCH;
     const uint64_t sblocks = std::min<uint64_t>(nb, SAMPLE_BLOCKS);
     const uint64_t bstride = std::max<uint64_t>(TA_BATCH, (n / sblocks));
@@ -1311,17 +1856,58 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     for (auto h : hist) sampled += h;
     if (!sampled) return false;
 
-    // ---- region capacities per workgroup
+    // ---- resident plan: the H densest tiles get region ids 0..H-1 (owner o holds ids
+    // o*TPW .. o*TPW+TPW-1, dense and sparse ranks interleaved), cold tiles H..T-1
+    std::vector<uint32_t> tile_of(T), tmap(T);
+    for (uint32_t t = 0; t < T; t++) tile_of[t] = t;
+    uint32_t H = 0;
+    if (res) {
+        std::vector<uint32_t> order(T);
+        for (uint32_t t = 0; t < T; t++) order[t] = t;
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hist[a] > hist[b]; });
+        H = std::min<uint32_t>(T, rP * rTPW);
+        uint64_t hot_mass = 0;
+        for (uint32_t r = 0; r < H; r++) hot_mass += hist[order[r]];
+        if (hot_mass * 4 < sampled) res = false;  // < 25 % of the rows would stay on chip
+    }
+    if (res) {
+        std::vector<uint32_t> hot_ids(H);
+        for (uint32_t r = 0; r < H; r++) {
+            uint32_t id = r;
+            if (H == rP * rTPW) {  // every owner full: balance dense and sparse tiles
+                const uint32_t j = r / rP, q = r % rP;
+                const uint32_t o = (j & 1) ? rP - 1 - q : q;
+                id = o * rTPW + j;
+            }
+            hot_ids[r] = id;
+        }
+        std::vector<uint32_t> order(T);
+        for (uint32_t t = 0; t < T; t++) order[t] = t;
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hist[a] > hist[b]; });
+        std::vector<char> hot(T, 0);
+        for (uint32_t r = 0; r < H; r++) {
+            tile_of[hot_ids[r]] = order[r];
+            hot[order[r]] = 1;
+        }
+        uint32_t nid = H;
+        for (uint32_t t = 0; t < T; t++)
+            if (!hot[t]) tile_of[nid++] = t;
+        for (uint32_t id = 0; id < T; id++) tmap[tile_of[id]] = id;
+    }
+
+    // ---- region capacities per workgroup (by region id; hot ids have none)
     const uint64_t rows_per_wg = ((n + W - 1) / W + TA_BATCH - 1) / TA_BATCH * TA_BATCH;
     std::vector<uint32_t> cap(T);
     std::vector<uint64_t> toff(T);
     uint64_t stride = 0;
-    for (uint32_t t = 0; t < T; t++) {
+    for (uint32_t id = 0; id < T; id++) {
+        const uint32_t t = tile_of[id];
         const double e = (double)rows_per_wg * (double)hist[t] / (double)sampled;
         uint64_t c = (uint64_t)(e * 1.04 + 6.0 * std::sqrt(e + 1.0)) + 32;
         c = std::min<uint64_t>((c + 7) & ~uint64_t(7), rows_per_wg + 8);
-        cap[t] = (uint32_t)c;
-        toff[t] = stride;
+        if (res && id < H) c = 0;
+        cap[id] = (uint32_t)c;
+        toff[id] = stride;
         stride += c;
     }
     // pass A keeps region positions in u32 (destination | overflow bit)
@@ -1349,13 +1935,94 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     // ---- pass B work units: tiles split over ranges of pass-A workgroups by expected size
     std::vector<WorkUnit> units;
     const double target = std::max(1.0, (double)n / ((double)cu_count() * 4));
-    for (uint32_t t = 0; t < T; t++) {
-        const double e = (double)n * (double)hist[t] / (double)sampled;
+    for (uint32_t id = res ? H : 0; id < T; id++) {
+        const double e = (double)n * (double)hist[tile_of[id]] / (double)sampled;
         uint32_t g = (uint32_t)std::min<double>(W, std::max(1.0, std::ceil(e / target)));
-        for (uint32_t k = 0; k < g; k++) units.push_back({t, (uint32_t)((uint64_t)W * k / g), (uint32_t)((uint64_t)W * (k + 1) / g), 0});
+        for (uint32_t k = 0; k < g; k++) units.push_back({id, (uint32_t)((uint64_t)W * k / g), (uint32_t)((uint64_t)W * (k + 1) / g), 0});
     }
     if (units.size() > max_units) fail(VH_ERR_RUNTIME, "tiled binning: work-unit table overflow");
-    VH_HIP(hipMemcpyAsync(d_units, units.data(), sizeof(WorkUnit) * units.size(), hipMemcpyHostToDevice, st));
+    if (!units.empty())
+        VH_HIP(hipMemcpyAsync(d_units, units.data(), sizeof(WorkUnit) * units.size(), hipMemcpyHostToDevice, st));
+
+    if (res) {
+        // ---- XCD-resident launch (replaces pass A; pass B only for the cold tiles)
+        const uint32_t P = rP, K = VH_RES_K, G = 8 * rP;
+        FusedAggs fr = fa;  // owner tiles: TPW * S cells per aggregator
+        uint64_t roff = 0;
+        for (int k = 0; k < fr.na; k++) {
+            roff = (roff + 7) & ~uint64_t(7);
+            fr.a[k].lds_off = (uint32_t)roff;
+            roff += S * rTPW * (fr.a[k].kind == VH_AGG_COUNT ? 4 : 8);
+        }
+        fr.lds_words = (uint32_t)(((roff + 15) & ~uint64_t(15)) / 4);
+        const uint64_t ctl_b = 256, ready_b = 4ull * 8 * P, cons_b = 4ull * 8 * P * P;
+        const uint64_t hdr_b = 4ull * 8 * P * K * RES_HDR, keys_b = 4ull * 8 * P * K * TA_BATCH;
+        const uint64_t vals_b = 8ull * 8 * P * K * TA_BATCH * (nv ? 1 : 0);
+        const uint64_t okey_b = 4ull * G * RES_OVF, oval_b = 8ull * G * RES_OVF;
+        auto al = [](uint64_t b) { return (b + 255) & ~uint64_t(255); };
+        const uint64_t flags_b = al(ctl_b) + al(ready_b) + al(cons_b);
+        ws.res.ensure(flags_b + al(hdr_b) + al(keys_b) + al(vals_b) + al(okey_b) + al(oval_b));
+        unsigned char *rb = ws.res.as<unsigned char>();
+        ResidentParams rp{};
+        rp.P = P;
+        rp.K = K;
+        rp.H = H;
+        rp.TPW = rTPW;
+        rp.nb = (uint32_t)(rows_per_wg / TA_BATCH);
+        rp.G = G;
+        rp.wt = rmode == 2 ? 1u : 0u;
+        rp.timeout = 200 * wall_clock_khz();  // 200 ms without progress
+        rp.ctl = reinterpret_cast<uint32_t *>(rb);
+        rp.ready = reinterpret_cast<uint32_t *>(rb + al(ctl_b));
+        rp.cons = reinterpret_cast<uint32_t *>(rb + al(ctl_b) + al(ready_b));
+        unsigned char *q = rb + flags_b;
+        rp.hdr = reinterpret_cast<uint32_t *>(q);
+        q += al(hdr_b);
+        rp.skeys = reinterpret_cast<uint32_t *>(q);
+        q += al(keys_b);
+        rp.svals = reinterpret_cast<double *>(q);
+        q += al(vals_b);
+        rp.ovf_key = reinterpret_cast<uint32_t *>(q);
+        q += al(okey_b);
+        rp.ovf_val = reinterpret_cast<double *>(q);
+        rp.tmap = d_tmap;
+        rp.tile_of = d_tile_of;
+        tp.tile_of = d_tile_of;
+        tp.abort_word = rp.ctl;
+        VH_HIP(hipMemcpyAsync(d_tmap, tmap.data(), 4 * (uint64_t)T, hipMemcpyHostToDevice, st));
+        VH_HIP(hipMemcpyAsync(d_tile_of, tile_of.data(), 4 * (uint64_t)T, hipMemcpyHostToDevice, st));
+        VH_HIP(hipMemsetAsync(rb, 0, flags_b, st));
+        const size_t lds = resident_lds_bytes(fr.lds_words, nv, T);
+        {
+            TimedScope ts("tile_resident");
+            switch (nd_f64 * 2 + nv) {
+            case 2: hipLaunchKernelGGL((k_tile_resident<1, 0>), dim3(G), dim3(RES_THREADS), lds, st, plan, fa, fr, tp, rp, n); break;
+            case 3: hipLaunchKernelGGL((k_tile_resident<1, 1>), dim3(G), dim3(RES_THREADS), lds, st, plan, fa, fr, tp, rp, n); break;
+            case 4: hipLaunchKernelGGL((k_tile_resident<2, 0>), dim3(G), dim3(RES_THREADS), lds, st, plan, fa, fr, tp, rp, n); break;
+            case 5: hipLaunchKernelGGL((k_tile_resident<2, 1>), dim3(G), dim3(RES_THREADS), lds, st, plan, fa, fr, tp, rp, n); break;
+            case 6: hipLaunchKernelGGL((k_tile_resident<3, 0>), dim3(G), dim3(RES_THREADS), lds, st, plan, fa, fr, tp, rp, n); break;
+            default: hipLaunchKernelGGL((k_tile_resident<3, 1>), dim3(G), dim3(RES_THREADS), lds, st, plan, fa, fr, tp, rp, n);
+            }
+            VH_HIP(hipGetLastError());
+        }
+        if (!units.empty()) {
+            TimedScope ts("tile_reduce");
+            const unsigned g = (unsigned)units.size();
+            if (nv == 0) hipLaunchKernelGGL(k_tile_reduce<0>, dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
+            else hipLaunchKernelGGL(k_tile_reduce<1>, dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
+            VH_HIP(hipGetLastError());
+        }
+        uint32_t state = 0;
+        VH_HIP(hipMemcpyAsync(&state, rp.ctl, 4, hipMemcpyDeviceToHost, st));
+        VH_HIP(hipStreamSynchronize(st));
+        if (state != RES_COMMIT) {
+            g_res_off.store(true);
+            fprintf(stderr, "vaexhip: XCD-resident tile launch not committed (state %u); two-pass tile path from now on\n",
+                    state);
+            return 2;
+        }
+        return 1;
+    }
 
     // ---- pass A
     {
