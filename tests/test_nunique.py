@@ -158,3 +158,22 @@ def test_gpu_groupby_many_groups_vs_oracle():
     keys, exp = np.unique(pairs[:, 0], return_counts=True)
     np.testing.assert_array_equal(g["key"].to_numpy()[order], keys)
     np.testing.assert_array_equal(g["nu"].to_numpy()[order], exp)
+
+
+@gpu
+@pytest.mark.parametrize("lds", ["0", "1"])
+@pytest.mark.parametrize("card", [7, 300_000])
+def test_gpu_workgroup_dedup_low_and_high_cardinality(monkeypatch, card, lds):
+    """int32 / int8 values through the LDS-deduplicating collect: few distinct pairs per
+    workgroup (all rows collapse in LDS) and more distinct pairs than the LDS table holds
+    (table cleared between batches, probe misses appended as duplicates); VH_NU_LDS=0 is
+    the plain collect with block-level slot reservation."""
+    monkeypatch.setenv("VH_NU_LDS", lds)
+    rng = np.random.default_rng(card)
+    n = 3_000_000
+    x = rng.integers(0, 300, n).astype(np.int64)
+    v = rng.integers(0, card, n).astype(np.int32 if card > 127 else np.int8)
+    b = oracle.Binner("ordinal", x, ordinal_count=300, min_value=0)
+    exp = oracle.nunique_grid([b], v)
+    got = _agg_grid(v, x, parts=1, device=True)
+    np.testing.assert_array_equal(got, exp)
