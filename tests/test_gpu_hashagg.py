@@ -131,6 +131,21 @@ def test_closed_lds_tables():
     _check(keys, [v], _run(keys, [v], device=True))
 
 
+@pytest.mark.parametrize("kdtype,nvals,n,card", [("int64", 1, 16_000_000, 12_000_000),
+                                                  ("int64", 2, 16_000_000, 12_000_000),
+                                                  ("int32", 1, 24_000_000, 20_000_000)])
+def test_repartitioned_high_cardinality(kdtype, nvals, n, card):
+    """More keys per bucket than an LDS table holds with P at its cap: pass-B entries are
+    re-split into sub-buckets first (k_ha_repart); packed {key, value} and separate-array
+    entry formats, wide (8-byte keys) and narrow (int32) tables."""
+    rng = np.random.default_rng(card + nvals)
+    keys = (rng.integers(0, card, n) * 2654435761 - 77).astype(kdtype)
+    vals = [rng.normal(size=n)]
+    if nvals > 1:
+        vals.append(rng.integers(-1000, 1000, n).astype(np.int32))
+    _check(keys, vals, _run(keys, vals, device=True))
+
+
 @pytest.mark.parametrize("layout", ["sorted", "heavy", "runs"])
 def test_skewed_and_sorted_keys(layout):
     """Per-workgroup bucket fractions far from the sampled global ones: region overflow

@@ -137,7 +137,10 @@ struct HaTable {
     int nv;
 };
 
-__device__ inline uint64_t ha_slot(const HaTable &g, uint64_t key) {
+// new_keys: a workgroup-local (LDS) count of the keys this call inserted, added to g.used
+// once per workgroup by the caller; nullptr = count in g.used directly (one same-address
+// atomic per new key: ~1e8 of them for h2o q10's groups)
+__device__ inline uint64_t ha_slot(const HaTable &g, uint64_t key, uint32_t *new_keys = nullptr) {
     if (key == SET_EMPTY) return g.mask + 1;
     uint64_t pos = hash64(key) & g.mask;
     for (int p = 0; p < HA_MAX_PROBE; p++) {
@@ -147,7 +150,8 @@ __device__ inline uint64_t ha_slot(const HaTable &g, uint64_t key) {
             cur = atomicCAS((unsigned long long *)&g.keys[pos], (unsigned long long)SET_EMPTY,
                             (unsigned long long)key);
             if (cur == SET_EMPTY) {
-                if (atomicAdd(g.used, 1u) >= g.max_used) atomicOr(g.err, 1u);
+                if (new_keys) atomicAdd(new_keys, 1u);
+                else if (atomicAdd(g.used, 1u) >= g.max_used) atomicOr(g.err, 1u);
                 return pos;
             }
             if (cur == key) return pos;
@@ -369,14 +373,18 @@ __device__ inline void lt2_add_many(const LdsTable<KB> &t, const HaTable &g, con
         if (slow[i]) lt2_insert<KB, NV, N>(t, g, kb[i], vb[i]);
 }
 
-// merge the LDS table into the HBM table (after a workgroup barrier)
+// merge the LDS table into the HBM table (after a workgroup barrier, every thread); the
+// workgroup's new keys are added to g.used once
 template <typename KB, int NV, bool N> __device__ inline void lt_merge(const LdsTable<KB> &t, const HaTable &g, int nthreads) {
     constexpr uint32_t S = lt_slots<N>();
+    __shared__ uint32_t s_new;
+    if (threadIdx.x == 0) s_new = 0;
+    __syncthreads();
     for (uint32_t i = threadIdx.x; i < S + 2; i += nthreads) {
         const unsigned long long cn = N ? (unsigned long long)t.cn32[i] << 32 : t.cn[i];
         if (!cn) continue;
         const KB kb = i < S ? t.keys[i] : (KB)(kb_closed<KB>() + (i - S));
-        const uint64_t s = ha_slot(g, (uint64_t)kb);
+        const uint64_t s = ha_slot(g, (uint64_t)kb, &s_new);
         if (s == ~0ULL) continue;
         atomicAdd(&g.cnt[s], cn >> 32);
 #pragma unroll
@@ -391,6 +399,8 @@ template <typename KB, int NV, bool N> __device__ inline void lt_merge(const Lds
             }
         }
     }
+    __syncthreads();
+    if (threadIdx.x == 0 && s_new && atomicAdd(g.used, s_new) + s_new > g.max_used) atomicOr(g.err, 1u);
 }
 
 // ---- partition parameters -----------------------------------------------------------------
@@ -976,6 +986,151 @@ __global__ __launch_bounds__(HB_THREADS) void k_ha_reduce(HaParams hp, HaTable g
     lt_merge<KB, NV, N>(t, g, HB_THREADS);
 }
 
+// ---- repartition (high-cardinality keys) ------------------------------------------------
+// P is capped at 2^HA_MAX_P_LOG2 buckets by pass A's LDS; with more keys than that many LDS
+// tables hold (h2o q10: ~1e8 groups, ~5e4 keys per bucket for 2300-key tables) almost every
+// pass-B entry missed its LDS table and went to the HBM table with global atomics (q10 at
+// 1e9 rows: k_ha_reduce 229 ms).  Here every pass-B unit's entries are first split by the
+// next hash bits into S sub-buckets (sub = ((h << p) * S) >> 32, independent of the bits the
+// LDS groups use), one read and one write of each entry, into per-(unit, sub) regions; pass B
+// then runs unchanged over those regions (one region per unit) with ~1/S of the keys.
+constexpr int HR_M = 4;                      // entries per lane per step
+constexpr uint32_t HR_CH = HB_THREADS * HR_M;
+constexpr uint32_t HR_MAX_S = 64;
+
+struct RepartParams {
+    uint32_t S, p_log2;
+    const uint64_t *base;  // [units] first entry of the unit's S regions
+    const uint32_t *rcap;  // [units] entries per sub-bucket region of the unit
+    uint32_t *fills;       // [units * S] entries produced (may exceed rcap)
+    void *ent;             // output entries, same format as pass A's
+    uint64_t *vbits[HA_MAX_V];
+};
+
+template <typename KB> __device__ inline uint32_t ha_sub(KB kb, uint32_t p_log2, uint32_t S) {
+    const uint32_t rest = p_log2 ? (uint32_t)(ha_h(kb) << p_log2) : ha_h(kb);
+    return (uint32_t)(((uint64_t)rest * S) >> 32);
+}
+
+template <typename KB, int NV>
+__global__ __launch_bounds__(HB_THREADS) void k_ha_repart(HaParams hp, HaTable g, const HaUnit *units, RepartParams rq) {
+    __shared__ uint32_t s_fill[1024];
+    __shared__ uint32_t s_pre[1025];
+    __shared__ uint32_t hist[HR_MAX_S], boff[HR_MAX_S], dbase[HR_MAX_S], cursor[HR_MAX_S], s_tot;
+    __shared__ KB skb[HR_CH];
+    __shared__ uint64_t svb[NV > 0 ? NV : 1][HR_CH];
+    __shared__ uint8_t ssub[HR_CH];
+    const uint32_t ui = blockIdx.x;
+    const HaUnit u = units[ui];
+    const uint32_t b = u.bucket, S = rq.S;
+    const uint32_t cap = hp.cap[b];
+    const uint32_t nw = u.w_end - u.w_begin;
+    for (uint32_t k = threadIdx.x; k < nw; k += HB_THREADS) s_fill[k] = min(hp.fills[(uint64_t)b * hp.W + u.w_begin + k], cap);
+    if (threadIdx.x < HR_MAX_S) {
+        hist[threadIdx.x] = 0;
+        cursor[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const uint32_t lane = threadIdx.x, k0 = lane * 16;
+        uint32_t sum = 0;
+        for (uint32_t k = k0; k < k0 + 16 && k < nw; k++) sum += s_fill[k];
+        uint32_t inc = sum;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(inc, off, 64);
+            if ((int)lane >= off) inc += y;
+        }
+        uint32_t acc = inc - sum;
+        for (uint32_t k = k0; k < k0 + 16 && k < nw; k++) {
+            s_pre[k] = acc;
+            acc += s_fill[k];
+        }
+        if (lane == 63) s_pre[nw] = inc;
+    }
+    __syncthreads();
+    const uint32_t E = s_pre[nw];
+    const uint64_t toff_b = hp.toff[b];
+    const uint64_t base = rq.base[ui];
+    const uint32_t rcap = rq.rcap[ui];
+    uint32_t kr = 0;
+    for (uint32_t c0 = 0; c0 < E; c0 += HR_CH) {
+        KB kb[HR_M];
+        uint64_t vb[HR_M][NV > 0 ? NV : 1];
+        int32_t rank[HR_M];
+        uint32_t sub[HR_M];
+#pragma unroll
+        for (int j = 0; j < HR_M; j++) {
+            const uint32_t c = c0 + j * HB_THREADS + threadIdx.x;
+            const uint32_t cc = c < E ? c : E - 1;
+            while (s_pre[kr + 1] <= cc) kr++;
+            const uint64_t e = (uint64_t)(u.w_begin + kr) * hp.wg_stride + toff_b + (cc - s_pre[kr]);
+            if constexpr (ha_packed<KB, NV>()) {
+                const uint4 q = reinterpret_cast<const uint4 *>(hp.ent)[e];
+                kb[j] = (KB)(((uint64_t)q.y << 32) | q.x);
+                vb[j][0] = ((uint64_t)q.w << 32) | q.z;
+            } else {
+                kb[j] = reinterpret_cast<const KB *>(hp.ent)[e];
+#pragma unroll
+                for (int v = 0; v < NV; v++) vb[j][v] = hp.vbits[v][e];
+            }
+            sub[j] = ha_sub(kb[j], rq.p_log2, S);
+            rank[j] = c < E ? (int32_t)atomicAdd(&hist[sub[j]], 1u) : -1;
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {  // exclusive scan of the sub-bucket counts (S <= 64: one per lane)
+            const uint32_t s = threadIdx.x;
+            const uint32_t h = s < S ? hist[s] : 0u;
+            uint32_t inc = h;
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(inc, off, 64);
+                if ((int)s >= off) inc += y;
+            }
+            if (s < S) {
+                boff[s] = inc - h;
+                dbase[s] = cursor[s] - (inc - h);
+                cursor[s] += h;
+                hist[s] = 0;
+            }
+            if (s == 63) s_tot = inc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < HR_M; j++) {
+            if (rank[j] < 0) continue;
+            const uint32_t pos = boff[sub[j]] + (uint32_t)rank[j];
+            skb[pos] = kb[j];
+            ssub[pos] = (uint8_t)sub[j];
+#pragma unroll
+            for (int v = 0; v < NV; v++) svb[v][pos] = vb[j][v];
+        }
+        __syncthreads();
+        const uint32_t tot = s_tot;
+        for (uint32_t k = threadIdx.x; k < tot; k += HB_THREADS) {
+            const uint32_t s = ssub[k];
+            const uint32_t d = dbase[s] + k;
+            if (d < rcap) {
+                const uint64_t e = base + (uint64_t)s * rcap + d;
+                if constexpr (ha_packed<KB, NV>()) {
+                    const uint64_t kk = (uint64_t)skb[k], vv = svb[0][k];
+                    reinterpret_cast<uint4 *>(rq.ent)[e] = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), (uint32_t)vv,
+                                                                      (uint32_t)(vv >> 32));
+                } else {
+                    reinterpret_cast<KB *>(rq.ent)[e] = skb[k];
+#pragma unroll
+                    for (int v = 0; v < NV; v++) rq.vbits[v][e] = svb[v][k];
+                }
+            } else {  // sub-bucket region full (an unlucky split): straight into the HBM table
+                uint64_t vv[NV > 0 ? NV : 1];
+#pragma unroll
+                for (int v = 0; v < NV; v++) vv[v] = svb[v][k];
+                ha_global_row<NV>(g, (uint64_t)skb[k], vv);
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < S) rq.fills[(uint64_t)ui * S + threadIdx.x] = cursor[threadIdx.x];
+}
+
 // ---- direct (P == 1): each workgroup aggregates a row range of the raw columns ------------
 template <typename K, int NV, bool N>
 __global__ __launch_bounds__(HB_THREADS) void k_ha_direct(HaParams hp, HaTable g) {
@@ -1040,28 +1195,35 @@ template <typename KB> __device__ inline KB ha_sortable(uint64_t key, int is_sig
 template <typename KB>
 __global__ __launch_bounds__(256) void k_ha_compact(const uint64_t *keys, const unsigned long long *cnt, uint64_t slots,
                                                     int is_signed, KB *skey, uint32_t *sslot, uint32_t *counter) {
-    // one counter add per wave (ballot + popcount), not per occupied slot; i == slots is the
-    // side slot (occupied when it counted rows)
-    const int lane = threadIdx.x & 63;
-    const uint64_t step = (uint64_t)gridDim.x * 256;
-    for (uint64_t i0 = blockIdx.x * 256ull; i0 <= slots; i0 += step) {
-        const uint64_t i = i0 + threadIdx.x;
-        bool occ = false;
-        uint64_t k = SET_EMPTY;
-        if (i < slots) {
-            k = keys[i];
-            occ = k != SET_EMPTY;
-        } else if (i == slots) {
-            occ = cnt[i] != 0;
+    // 8 consecutive slots per thread, output slots reserved once per workgroup and tile (a
+    // counter add per wave was 4e6 same-address atomics for a 2^28-slot table: 47 ms);
+    // i == slots is the side slot (occupied when it counted rows)
+    __shared__ uint32_t s_w[4];
+    __shared__ unsigned long long s_base;
+    constexpr int R = 8;
+    const uint64_t tile = 256ull * R, step = (uint64_t)gridDim.x * tile;
+    for (uint64_t t0 = blockIdx.x * tile; t0 <= slots; t0 += step) {
+        const uint64_t i0 = t0 + (uint64_t)threadIdx.x * R;
+        uint64_t k[R];
+        uint32_t occ = 0;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const uint64_t i = i0 + r;
+            k[r] = SET_EMPTY;
+            if (i < slots) {
+                k[r] = keys[i];
+                if (k[r] != SET_EMPTY) occ |= 1u << r;
+            } else if (i == slots && cnt[i] != 0) {
+                occ |= 1u << r;
+            }
         }
-        const uint64_t m = __ballot(occ);
-        uint32_t base = 0;
-        if (lane == 0 && m) base = atomicAdd(counter, (uint32_t)__popcll(m));
-        base = __shfl(base, 0, 64);
-        if (occ) {
-            const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-            skey[j] = ha_sortable<KB>(k, is_signed);
-            sslot[j] = (uint32_t)i;
+        uint64_t j = block_reserve<256>((uint32_t)__popc(occ), s_w, &s_base, counter);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            if (!((occ >> r) & 1)) continue;
+            skey[j] = ha_sortable<KB>(k[r], is_signed);
+            sslot[j] = (uint32_t)(i0 + r);
+            j++;
         }
     }
 }
@@ -1144,7 +1306,7 @@ namespace vh {
 // the device's lock; they are stream-ordered on the library stream anyway.
 struct HaScratch {
     std::mutex mu;
-    DevBuf sample, meta, entries, vbits, stage;
+    DevBuf sample, meta, entries, vbits, stage, entries2, vbits2, meta2;
 };
 static HaScratch &scratch() {
     static std::mutex g;
@@ -1504,8 +1666,102 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
         }
         VH_HIP(hipGetLastError());
     }
+    // ---- repartition: more keys per bucket than an LDS table holds (P at its cap)
+    static const bool repart_on = [] {  // VH_HA_REPART=0: A/B runs without it
+        const char *e = getenv("VH_HA_REPART");
+        return !e || atoi(e) != 0;
+    }();
+    const double kpb = dest / (double)P;
+    uint32_t S_sub = 1;
+    if (repart_on && p_log2 == HA_MAX_P_LOG2 && kpb > target_keys * 1.25)
+        S_sub = std::min<uint32_t>(HR_MAX_S, (uint32_t)std::ceil(kpb / target_keys));
+    HaParams hpb = hp;
+    std::vector<HaUnit> units_b;
+    HaUnit *d_units_b = d_units;
+    if (S_sub > 1) {
+        const uint32_t U = (uint32_t)units.size();
+        std::vector<uint64_t> rbase(U);
+        std::vector<uint32_t> rcap(U);
+        uint64_t total2 = 0;
+        for (uint32_t ui = 0; ui < U; ui++) {
+            const HaUnit &un = units[ui];
+            // the unit's entries: at most its regions' capacities; expected ~ n p_b * share
+            const double e = (double)n * (double)bh[un.bucket] / (double)std::max<uint64_t>(sampled, 1) *
+                             (double)(un.w_end - un.w_begin) / (double)W;
+            const double es = e / S_sub;
+            uint64_t c = (uint64_t)(es * 1.05 + 8.0 * std::sqrt(es + 1.0)) + 64;
+            c = (c + 7) & ~uint64_t(7);
+            rcap[ui] = (uint32_t)c;
+            rbase[ui] = total2;
+            total2 += c * S_sub;
+        }
+        if (nv == 1 && (kbs == 8 || VH_HA_PACK4)) {
+            S.entries2.ensure(16 * total2 + 64);
+        } else {
+            S.entries2.ensure((uint64_t)kbs * total2 + 16);
+            if (nv) S.vbits2.ensure(8 * total2 * nv + 32);
+        }
+        const uint64_t P2 = (uint64_t)U * S_sub;
+        units_b.resize(P2);
+        std::vector<uint64_t> toff2(P2);
+        std::vector<uint32_t> cap2(P2);
+        for (uint32_t ui = 0; ui < U; ui++)
+            for (uint32_t q = 0; q < S_sub; q++) {
+                const uint64_t gi = (uint64_t)ui * S_sub + q;
+                units_b[gi] = {(uint32_t)gi, 0, 1, 0};
+                toff2[gi] = rbase[ui] + (uint64_t)q * rcap[ui];
+                cap2[gi] = rcap[ui];
+            }
+        S.meta2.ensure(8 * (uint64_t)U + 4 * (uint64_t)U + 8 * P2 + 4 * P2 + 4 * P2 + sizeof(HaUnit) * P2 + 256);
+        unsigned char *m2 = S.meta2.as<unsigned char>();
+        uint64_t *d_rbase = reinterpret_cast<uint64_t *>(m2);
+        uint64_t *d_toff2 = d_rbase + U;
+        HaUnit *d_u2 = reinterpret_cast<HaUnit *>(d_toff2 + P2);
+        uint32_t *d_rcap = reinterpret_cast<uint32_t *>(d_u2 + P2);
+        uint32_t *d_cap2 = d_rcap + U;
+        uint32_t *d_fills2 = d_cap2 + P2;
+        VH_HIP(hipMemcpyAsync(d_rbase, rbase.data(), 8 * (uint64_t)U, hipMemcpyHostToDevice, st));
+        VH_HIP(hipMemcpyAsync(d_rcap, rcap.data(), 4 * (uint64_t)U, hipMemcpyHostToDevice, st));
+        VH_HIP(hipMemcpyAsync(d_toff2, toff2.data(), 8 * P2, hipMemcpyHostToDevice, st));
+        VH_HIP(hipMemcpyAsync(d_cap2, cap2.data(), 4 * P2, hipMemcpyHostToDevice, st));
+        VH_HIP(hipMemcpyAsync(d_u2, units_b.data(), sizeof(HaUnit) * P2, hipMemcpyHostToDevice, st));
+        RepartParams rq{};
+        rq.S = S_sub;
+        rq.p_log2 = p_log2;
+        rq.base = d_rbase;
+        rq.rcap = d_rcap;
+        rq.fills = d_fills2;
+        rq.ent = S.entries2.ptr;
+        if (!(nv == 1 && (kbs == 8 || VH_HA_PACK4)))
+            for (int v = 0; v < nv; v++) rq.vbits[v] = S.vbits2.as<uint64_t>() + (uint64_t)v * total2;
+        {
+            TimedScope ts("ha_repart");
+            dispatch_kb(h->key_dtype, [&](auto kbc) {
+                using KB = decltype(kbc);
+                dispatch_nv(nv, [&](auto nvc) {
+                    constexpr int NV = decltype(nvc)::value;
+                    hipLaunchKernelGGL((k_ha_repart<KB, NV>), dim3(U), dim3(HB_THREADS), 0, st, hp, g, d_units, rq);
+                });
+            });
+            VH_HIP(hipGetLastError());
+        }
+        // pass B over the sub-bucket regions: one "workgroup" per region, units = regions
+        hpb.W = 1;
+        hpb.wg_stride = 0;
+        hpb.cap = d_cap2;
+        hpb.toff = d_toff2;
+        hpb.fills = d_fills2;
+        hpb.ent = S.entries2.ptr;
+        for (int v = 0; v < HA_MAX_V; v++) hpb.vbits[v] = rq.vbits[v];
+        d_units_b = d_u2;
+    } else {
+        units_b = units;
+    }
     {
         TimedScope ts("ha_reduce");
+        const HaParams &hp = hpb;
+        const HaUnit *d_units = d_units_b;
+        const std::vector<HaUnit> &units = units_b;
         dispatch_kb(h->key_dtype, [&](auto kbc) {
             using KB = decltype(kbc);
             dispatch_nv(nv, [&](auto nvc) {
@@ -1759,7 +2015,7 @@ int vh_hashagg_finish(vh_hashagg *h, uint64_t *ngroups) {
                 int64_t *onn = reinterpret_cast<int64_t *>(osum + m * h->nv);
                 dispatch_kb(h->key_dtype, [&](auto kbc) {
                     using KB = decltype(kbc);
-                    hipLaunchKernelGGL(k_ha_compact<KB>, dim3(blocks_for(h->slots + 1, 256, 8)), dim3(256), 0, st, g.keys,
+                    hipLaunchKernelGGL(k_ha_compact<KB>, dim3(blocks_for((h->slots + 8) / 8, 256, 8)), dim3(256), 0, st, g.keys,
                                        g.cnt, h->slots, sg, reinterpret_cast<KB *>(skey), sslot, counter);
                     VH_HIP(hipGetLastError());
                     size_t tb = tmp_bytes;

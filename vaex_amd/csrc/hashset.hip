@@ -811,22 +811,31 @@ __global__ void k_set_rehash(const uint64_t *otab, uint64_t ocap, uint64_t *ntab
 
 __global__ __launch_bounds__(256) void k_set_compact(const uint64_t *tab, uint64_t cap, uint64_t *slot, uint64_t *first,
                                                      uint64_t *bits, uint64_t *ctr) {
-    // one cursor add per wave (ballot + popcount), not per occupied slot
-    const int lane = threadIdx.x & 63;
-    const uint64_t step = (uint64_t)gridDim.x * 256;
-    for (uint64_t i0 = blockIdx.x * 256ull; i0 < cap; i0 += step) {
-        const uint64_t i = i0 + threadIdx.x;
-        const uint64_t kb = i < cap ? tab[2 * i] : SET_EMPTY;
-        const bool occ = kb != SET_EMPTY;
-        const uint64_t m = __ballot(occ);
-        uint64_t base = 0;
-        if (lane == 0 && m) base = atomicAdd((unsigned long long *)&ctr[C_CURSOR], (unsigned long long)__popcll(m));
-        base = __shfl(base, 0, 64);
-        if (occ) {
-            const uint64_t j = base + (uint64_t)__popcll(m & ((1ull << lane) - 1));
+    // 8 consecutive slots per thread; output positions reserved once per workgroup and tile
+    // (one cursor add per wave was one same-address atomic per 64 slots)
+    __shared__ uint32_t s_w[4];
+    __shared__ unsigned long long s_base;
+    constexpr int R = 8;
+    const uint64_t tile = 256ull * R, step = (uint64_t)gridDim.x * tile;
+    for (uint64_t t0 = blockIdx.x * tile; t0 < cap; t0 += step) {
+        const uint64_t i0 = t0 + (uint64_t)threadIdx.x * R;
+        uint64_t kb[R];
+        uint32_t occ = 0;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            kb[r] = i0 + r < cap ? tab[2 * (i0 + r)] : SET_EMPTY;
+            if (kb[r] != SET_EMPTY) occ |= 1u << r;
+        }
+        uint64_t j = block_reserve<256>((uint32_t)__popc(occ), s_w, &s_base,
+                                        reinterpret_cast<unsigned long long *>(&ctr[C_CURSOR]));
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            if (!((occ >> r) & 1)) continue;
+            const uint64_t i = i0 + r;
             slot[j] = i;
             first[j] = tab[2 * i + 1];
-            bits[j] = kb;
+            bits[j] = kb[r];
+            j++;
         }
     }
 }
@@ -995,7 +1004,7 @@ static void set_seal(vh_set *s) {
     s->c_ord.ensure(cap * 8);
     uint64_t zero = 0;
     VH_HIP(hipMemcpyAsync(s->ctr.as<uint64_t>() + C_CURSOR, &zero, 8, hipMemcpyHostToDevice, stream()));
-    hipLaunchKernelGGL(k_set_compact, dim3(blocks_for(cap, 256)), dim3(256), 0, stream(), s->tab.as<uint64_t>(), cap,
+    hipLaunchKernelGGL(k_set_compact, dim3(blocks_for((cap + 7) / 8, 256)), dim3(256), 0, stream(), s->tab.as<uint64_t>(), cap,
                        s->c_slot.as<uint64_t>(), s->c_first.as<uint64_t>(), s->c_bits.as<uint64_t>(),
                        s->ctr.as<uint64_t>());
     VH_HIP(hipGetLastError());

@@ -51,34 +51,6 @@ template <typename T> __device__ inline uint64_t nu_bits(T v, bool *nan) {
     }
 }
 
-// Block-level slot reservation: every thread emits `my` pairs; one atomic on the list
-// counter per workgroup and batch (a single counter bumped by every wave costs one
-// same-address atomic per 64 rows: ~9 ms per 1e8 rows).  Returns this thread's first slot.
-template <int THREADS>
-__device__ inline uint64_t block_reserve(uint32_t my, uint32_t *s_w, unsigned long long *s_base,
-                                         unsigned long long *counter) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t inc = my;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(inc, off, 64);
-        if (lane >= off) inc += y;
-    }
-    if (lane == 63) s_w[wave] = inc;
-    __syncthreads();
-    uint32_t before = 0, total = 0;
-#pragma unroll
-    for (int k = 0; k < THREADS / 64; k++) {
-        before += k < wave ? s_w[k] : 0u;
-        total += s_w[k];
-    }
-    if (threadIdx.x == 0) *s_base = total ? atomicAdd(counter, (unsigned long long)total) : 0ull;
-    __syncthreads();
-    const uint64_t base = *s_base + before + inc - my;
-    __syncthreads();  // s_w / s_base reused by the next call
-    return base;
-}
-
 // Collect with a workgroup-private LDS dedup for values of <= 4 bytes (DEDUP): (cell,
 // 32-bit value pattern) packs into one 64-bit LDS key and a pair is emitted only when its
 // CAS claims an empty slot; the table is cleared between batches once half full, a pair that
