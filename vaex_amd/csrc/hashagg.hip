@@ -2048,11 +2048,13 @@ int vh_hashagg_read(vh_hashagg *h, int64_t *keys, int64_t *counts, void *const *
     const uint64_t *osum = reinterpret_cast<const uint64_t *>(ocnt + m);
     const int64_t *onn = reinterpret_cast<const int64_t *>(osum + m * h->nv);
     hipStream_t st = stream();
-    if (keys) VH_HIP(hipMemcpyAsync(keys, okey, 8 * m, hipMemcpyDeviceToHost, st));
-    if (counts) VH_HIP(hipMemcpyAsync(counts, ocnt, 8 * m, hipMemcpyDeviceToHost, st));
+    // destinations may be host or HBM (hipMemcpyDefault: unified addressing), so a caller
+    // that decodes the keys on the device keeps them there
+    if (keys) VH_HIP(hipMemcpyAsync(keys, okey, 8 * m, hipMemcpyDefault, st));
+    if (counts) VH_HIP(hipMemcpyAsync(counts, ocnt, 8 * m, hipMemcpyDefault, st));
     for (int v = 0; v < h->nv; v++) {
-        if (sums && sums[v]) VH_HIP(hipMemcpyAsync(sums[v], osum + (uint64_t)v * m, 8 * m, hipMemcpyDeviceToHost, st));
-        if (nonnull && nonnull[v]) VH_HIP(hipMemcpyAsync(nonnull[v], onn + (uint64_t)v * m, 8 * m, hipMemcpyDeviceToHost, st));
+        if (sums && sums[v]) VH_HIP(hipMemcpyAsync(sums[v], osum + (uint64_t)v * m, 8 * m, hipMemcpyDefault, st));
+        if (nonnull && nonnull[v]) VH_HIP(hipMemcpyAsync(nonnull[v], onn + (uint64_t)v * m, 8 * m, hipMemcpyDefault, st));
     }
     VH_HIP(hipStreamSynchronize(st));
     VH_API_END

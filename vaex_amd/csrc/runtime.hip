@@ -97,10 +97,10 @@ void dev_free(void *ptr, uint64_t bytes) {
 // ---- pinned host block cache (vh_host_alloc / vh_host_free) ---------------------------
 // Result arrays (grids, groupby columns) are read back through page-locked blocks: a
 // pageable D2H runs at ~5-10 GB/s, page-locked at PCIe/xGMI rate, and hipHostMalloc itself
-// (and hipHostFree) are slow, so freed blocks are kept (sizes rounded to 64 KiB, <= 2 GiB
-// cached); the host pipeline's bounce buffers come from the same cache.
+// (and hipHostFree) are slow, so freed blocks are kept (sizes rounded to 64 KiB, <= 8 GiB
+// cached: a 1e8-group result is three 800 MB columns); the host pipeline's bounce buffers come from the same cache.
 namespace {
-constexpr uint64_t HCACHE_MAX_BYTES = 2ull << 30;
+constexpr uint64_t HCACHE_MAX_BYTES = 8ull << 30;
 std::mutex g_hcache_mu;
 std::multimap<uint64_t, void *> g_hcache;
 uint64_t g_hcached = 0;

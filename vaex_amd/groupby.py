@@ -259,7 +259,10 @@ def _decode_labels(df, ck, table, ranges, mults):
     dtypes = []
     for name, vmin, vmax in ranges:
         kd = np.dtype(df.columns[name].dtype)
-        dtypes.append(np.dtype(label_dtype(kd, vmin, vmax)) if n else kd)
+        if name.startswith("__vaex_amd_"):
+            dtypes.append(np.dtype(np.int64))  # an internal key decoded again next: int64 in HBM
+        else:
+            dtypes.append(np.dtype(label_dtype(kd, vmin, vmax)) if n else kd)
     if ck.dtype != np.int64:
         raise TypeError("combined keys must be int64")
     outs = [DeviceArray.empty(n, dt) for dt in dtypes]
@@ -268,7 +271,10 @@ def _decode_labels(df, ck, table, ranges, mults):
                   (ctypes.c_int64 * k)(*[vmin for _, vmin, _ in ranges]), (ctypes.c_int64 * k)(*mults),
                   (ctypes.c_int64 * k)(*[vmax - vmin + 1 for _, vmin, vmax in ranges]),
                   (ctypes.c_int * k)(*[dt.itemsize for dt in dtypes]), (ctypes.c_void_p * k)(*[o.ptr for o in outs]))
-    return {name: o.to_numpy() if n else np.empty(0, dt) for (name, _, _), o, dt in zip(ranges, outs, dtypes)}
+    # labels of the library's internal recombined keys stay in HBM: the next _decode_labels
+    # (_groupby_recombine) reads them there
+    return {name: (o if name.startswith("__vaex_amd_") else o.to_numpy()) if n else np.empty(0, dt)
+            for (name, _, _), o, dt in zip(ranges, outs, dtypes)}
 
 
 RECOMBINED_KEY = "__vaex_amd_recombined_key_{}"

@@ -74,7 +74,7 @@ class HashAgg:
                 raise HashAggOverflow(msg)
             _lib.check(rc)
 
-    def finish(self, comm=None, gather=True):
+    def finish(self, comm=None, gather=True, device_keys=False):
         """The groups, key-sorted: (keys, counts, sums, nonnull).  With an RCCL communicator
         (``comm.device``) the ranks' groups are first exchanged by hash partition on the
         device (vh_hashagg_exchange): each rank keeps the groups it owns, or with ``gather``
@@ -86,11 +86,12 @@ class HashAgg:
                 raise ValueError("the device exchange needs an RCCL communicator")
             _lib.call("vh_hashagg_exchange", self._h, comm.handle, int(bool(gather)))
             _lib.call("vh_hashagg_finish", self._h, ctypes.byref(m))
-        return self._read(m.value)
+        return self._read(m.value, device_keys)
 
-    def _read(self, m):
-        # page-locked result columns: the read-back is one fast DMA per column
-        keys = _lib.pinned_empty(m, np.int64)
+    def _read(self, m, device_keys=False):
+        # page-locked result columns: the read-back is one fast DMA per column; keys that are
+        # decoded on the device next (combined multi-key groupby keys) stay in HBM
+        keys = DeviceArray.empty(m, np.int64) if device_keys else _lib.pinned_empty(m, np.int64)
         counts = _lib.pinned_empty(m, np.int64)
         sums = [_lib.pinned_empty(m, np.float64 if d.kind == "f" else (np.int64 if d.kind == "i" else np.uint64))
                 for d in self.value_dtypes]
@@ -99,8 +100,9 @@ class HashAgg:
         sp = (ctypes.c_void_p * nv)(*[s.ctypes.data for s in sums])
         npp = (ctypes.c_void_p * nv)(*[c.ctypes.data if c is not None else None for c in nonnull])
         if m:
-            _lib.call("vh_hashagg_read", self._h, keys.ctypes.data, counts.ctypes.data, sp, npp)
-        if self.key_dtype == np.uint64:
+            kptr = keys.ptr if device_keys else keys.ctypes.data
+            _lib.call("vh_hashagg_read", self._h, kptr, counts.ctypes.data, sp, npp)
+        if self.key_dtype == np.uint64 and not device_keys:
             keys = keys.view(np.uint64)  # the library returns the key bits
         return keys, counts, sums, nonnull
 
@@ -190,10 +192,13 @@ def try_groupby(df, by, actions, parse, sort=False, row_limit=None):
         ok = all_ranks_true(ok, executor.comm)
     if not ok:
         return None
+    # the library's internal combined keys (groupby.py COMBINED_KEY / RECOMBINED_KEY) are
+    # decoded on the device right after: keep them in HBM (single GPU, int64 keys)
+    device_keys = by.startswith("__vaex_amd_") and np.dtype(key.dtype) == np.int64 and not distributed
     if distributed and executor.comm.device:  # RCCL: hash-partition exchange on the device
         keys, counts, sums, nonnull = ha.finish(executor.comm, gather=True)
     else:
-        keys, counts, sums, nonnull = ha.finish()
+        keys, counts, sums, nonnull = ha.finish(device_keys=device_keys)
         if distributed:  # CPU exchange: the same partition, merged on the host
             from .distributed import combine_groups
             keys, counts, sums, nonnull = combine_groups((keys, counts, sums, nonnull), executor.comm)
@@ -201,9 +206,12 @@ def try_groupby(df, by, actions, parse, sort=False, row_limit=None):
         raise RowLimitException(f"Resulting grouper has {len(keys):,} unique combinations, which is larger "
                                 f"than the allowed row limit of {row_limit:,}")
     kdt = np.dtype(key.dtype)
-    labels = keys.astype(kdt)
-    if len(labels):  # groupby.py:131-133 (keys are sorted)
-        labels = labels.astype(label_dtype(kdt, labels[0], labels[-1]))
+    if device_keys:
+        labels = keys
+    else:
+        labels = keys.astype(kdt, copy=False)
+        if len(labels):  # groupby.py:131-133 (keys are sorted)
+            labels = labels.astype(label_dtype(kdt, labels[0], labels[-1]), copy=False)
     columns = {by: labels}
     for name, op, vi in ops:
         if op == "count":
