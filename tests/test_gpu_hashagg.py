@@ -249,6 +249,60 @@ def test_dense_int32_keys_take_fast_ordinal_tile_path(n):
     np.testing.assert_allclose(fs[0], s, rtol=1e-6, atol=1e-9)
 
 
+@pytest.mark.parametrize("vdtypes", [("int8", "float32"), ("int16", "uint8"), ("int32", "uint32"), ("bool", "int64"),
+                                     ("uint16", "float64")])
+@pytest.mark.parametrize("device", [False, True])
+def test_dense_int32_keys_fast_ordinal_any_value_dtype(vdtypes, device):
+    """The fast ordinal pass A with value columns of any native dtype (the h2o q3 / q5
+    shape: int8 and float32 sums, mean of float32): exact integer sums, float sums within
+    1e-6, NaN-keyed counts; 4-byte value slots when every column is <= 4 bytes."""
+    import vaex_amd
+    from vaex_amd import _lib
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(len(vdtypes[0]) * 31 + len(vdtypes[1]))
+    n = 2_000_000
+    keys = (5 + rng.integers(0, 250_000, n)).astype(np.int32)
+    cols = {"key": keys}
+    for j, dt in enumerate(vdtypes):
+        if dt == "bool":
+            a = rng.random(n) > 0.5
+        elif dt.startswith("float"):
+            a = rng.normal(size=n).astype(dt)
+            a[::37] = np.nan
+        else:
+            info = np.iinfo(dt)
+            a = rng.integers(info.min, info.max, n, endpoint=True).astype(dt)
+        cols[f"v{j}"] = a
+    df = vaex_amd.from_arrays(**({k: DeviceArray.from_numpy(v) for k, v in cols.items()} if device else cols))
+    agg = {}  # at most 4 aggregators: one tile-path pass (sum, sum, and a mean's sum + count)
+    for j, dt in enumerate(vdtypes):
+        agg[f"s{j}"] = vaex_amd.agg.sum(f"v{j}")
+        if dt.startswith("float"):
+            agg[f"m{j}"] = vaex_amd.agg.mean(f"v{j}")
+    _lib.timing_reset()
+    _lib.timing_enable(True)
+    g = df.groupby("key", agg=agg)
+    _lib.synchronize()
+    _lib.timing_enable(False)
+    assert _lib.timing_read("tile_scatter_ord")[0] >= 1, "fast ordinal pass A not used"
+    uk, inv = np.unique(keys, return_inverse=True)
+    np.testing.assert_array_equal(g["key"].to_numpy(), uk)
+    for j, dt in enumerate(vdtypes):
+        a = cols[f"v{j}"]
+        if dt.startswith("float"):
+            ok = ~np.isnan(a)
+            es = np.bincount(inv[ok], weights=a[ok].astype(np.float64), minlength=len(uk))
+            ec = np.bincount(inv[ok], minlength=len(uk))
+            np.testing.assert_allclose(g[f"s{j}"].to_numpy(), es, rtol=1e-6, atol=1e-6)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                np.testing.assert_allclose(g[f"m{j}"].to_numpy(), es / ec, rtol=1e-6, atol=1e-6)
+        else:
+            wide = np.uint64 if dt.startswith("uint") or dt == "bool" else np.int64
+            es = np.zeros(len(uk), wide)
+            np.add.at(es, inv, a.astype(wide))
+            np.testing.assert_array_equal(g[f"s{j}"].to_numpy(), es)
+
+
 @pytest.mark.parametrize("n,card", [(3_000_000, 1_000_000), (600_000, 3)])
 @pytest.mark.parametrize("kdtype", ["int64", "uint64"])
 def test_64bit_keys_partitioned_and_chunked(kdtype, n, card):

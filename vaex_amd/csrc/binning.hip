@@ -1246,7 +1246,9 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
     }
     const uint64_t L = g->length1d;
     // count / sum of other native dtypes without masks on grids beyond the LDS sub-grid size
-    bool tile_generic = !all_fusable && naggs <= MAX_FUSED_AGGS && L * 8 > LDS_AGG_MAX_BYTES;
+    // (any number of them: run in groups of at most MAX_FUSED_AGGS with at most two sums, one
+    // tile pass per group over the same staged chunk)
+    bool tile_generic = !all_fusable && L * 8 > LDS_AGG_MAX_BYTES;
     for (int k = 0; k < naggs && tile_generic; k++) {
         const vh_agg *a = aggs[k];
         tile_generic = (a->kind == VH_AGG_COUNT || (a->kind == VH_AGG_SUM && a->data.set)) && !a->mask.set && !a->flip;
@@ -1317,7 +1319,7 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                        std::vector<std::vector<int>> groups(1);
                        int sums = 0;
                        for (int k = 0; k < naggs; k++) {
-                           if (aggs[k]->kind == VH_AGG_SUM && sums == 2) {
+                           if ((aggs[k]->kind == VH_AGG_SUM && sums == 2) || groups.back().size() == (size_t)MAX_FUSED_AGGS) {
                                groups.emplace_back();
                                sums = 0;
                            }

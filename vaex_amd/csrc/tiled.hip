@@ -86,7 +86,48 @@ struct TileParams {
     uint32_t debug;            // experiment switches (VH_TILE_DEBUG), 0 in production
     const uint32_t *tile_of;   // [T] region id -> grid tile (XCD-resident path), nullptr = identity
     const uint32_t *abort_word;  // XCD-resident path's state word: pass B skips an aborted launch
+    // 4-byte value slots (every summed column <= 4 bytes: int8/16/32, uint8/16/32, bool,
+    // float32 -- exact): slot s is float32 bits when bit s of vfloat is set, else the low 32
+    // bits of the int64 slot, sign-extended back when bit s of vsigned is set
+    uint32_t vnarrow, vfloat, vsigned, pad2;
+    int32_t vdt[2];            // value slot -> column dtype (fast ordinal kernel)
 };
+
+// value of row h (0/1) of a loaded pair of a column of dtype dt, as the 8-byte slot pass A
+// carries (float data as double, integer / bool data as int64 / uint64 bits); `pr` holds
+// the pair's raw bits: both doubles for float64, else packed in pr.x from the low byte up
+__host__ __device__ inline int dtype_itemsize_dev(int dt) {
+    switch (dt) {
+    case VH_F64: case VH_I64: case VH_U64: return 8;
+    case VH_F32: case VH_I32: case VH_U32: return 4;
+    case VH_I16: case VH_U16: return 2;
+    default: return 1;
+    }
+}
+
+__device__ __forceinline__ double pair_slot(const double2 &pr, int dt, int h) {
+    if (dt == VH_F64 || dt == VH_I64 || dt == VH_U64) return h ? pr.y : pr.x;
+    const uint64_t raw = __builtin_bit_cast(uint64_t, pr.x);
+    switch (dt) {
+    case VH_F32: return (double)__builtin_bit_cast(float, (uint32_t)(raw >> (32 * h)));
+    case VH_I32: return __builtin_bit_cast(double, (int64_t)(int32_t)(uint32_t)(raw >> (32 * h)));
+    case VH_U32: return __builtin_bit_cast(double, (uint64_t)(uint32_t)(raw >> (32 * h)));
+    case VH_I16: return __builtin_bit_cast(double, (int64_t)(int16_t)(uint16_t)(raw >> (16 * h)));
+    case VH_U16: return __builtin_bit_cast(double, (uint64_t)(uint16_t)(raw >> (16 * h)));
+    case VH_I8: return __builtin_bit_cast(double, (int64_t)(int8_t)(uint8_t)(raw >> (8 * h)));
+    case VH_BOOL: return __builtin_bit_cast(double, (uint64_t)(((raw >> (8 * h)) & 0xff) ? 1 : 0));
+    default: return __builtin_bit_cast(double, (uint64_t)(uint8_t)(raw >> (8 * h)));  // VH_U8
+    }
+}
+
+// a carried 8-byte slot value (double, or int64 / uint64 bits) as its 4-byte form and back
+__device__ __forceinline__ uint32_t slot_narrow(double v, bool is_float) {
+    return is_float ? __builtin_bit_cast(uint32_t, (float)v) : (uint32_t)__builtin_bit_cast(uint64_t, v);
+}
+__device__ __forceinline__ double slot_wide(uint32_t u, bool is_float, bool is_signed) {
+    if (is_float) return (double)__builtin_bit_cast(float, u);
+    return __builtin_bit_cast(double, is_signed ? (uint64_t)(int64_t)(int32_t)u : (uint64_t)u);
+}
 
 struct WorkUnit {
     uint32_t tile, w_begin, w_end, pad;
@@ -324,7 +365,12 @@ __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, co
             if (tp.flags_mode) reinterpret_cast<uint32_t *>(tp.entries)[e] = e32;
             else reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)(e32 & 0xffffu);
 #pragma unroll
-            for (int s = 0; s < NV; s++) tp.values[s][e] = l.sv[s * TA_BATCH + k];
+            for (int s = 0; s < NV; s++) {
+                if (tp.vnarrow)
+                    reinterpret_cast<uint32_t *>(tp.values[s])[e] = slot_narrow(l.sv[s * TA_BATCH + k], (tp.vfloat >> s) & 1);
+                else
+                    tp.values[s][e] = l.sv[s * TA_BATCH + k];
+            }
         } else {
             // region overflow (a sampling miss): apply the staged row with global atomics
             const uint32_t t = dest & ~DEST_OVERFLOW;
@@ -417,7 +463,12 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
             const uint64_t e = region0 + dest;
             reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)kk;
 #pragma unroll
-            for (int s = 0; s < NV; s++) tp.values[s][e] = l.sv[s * CAP + k];
+            for (int s = 0; s < NV; s++) {
+                if (tp.vnarrow)
+                    reinterpret_cast<uint32_t *>(tp.values[s])[e] = slot_narrow(l.sv[s * CAP + k], (tp.vfloat >> s) & 1);
+                else
+                    tp.values[s][e] = l.sv[s * CAP + k];
+            }
         } else {
             // region overflow (a sampling miss): apply the staged row with global atomics
             const uint64_t c = ((uint64_t)t << tp.s_log2) | (kk & 0xffffu);
@@ -435,7 +486,11 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
                 if (fa.a[a].kind == VH_AGG_COUNT) {
                     atomicAdd((unsigned long long *)fa.a[a].grid + c, 1ULL);
                 } else if constexpr (NV > 0) {
-                    atomicAdd(reinterpret_cast<double *>(fa.a[a].grid) + c, l.sv[tp.val_slot[a] * CAP + k]);
+                    const double v = l.sv[tp.val_slot[a] * CAP + k];
+                    if (fa.a[a].vint)
+                        atomicAdd(reinterpret_cast<unsigned long long *>(fa.a[a].grid) + c, __builtin_bit_cast(unsigned long long, v));
+                    else
+                        atomicAdd(reinterpret_cast<double *>(fa.a[a].grid) + c, v);
                 }
             }
         }
@@ -766,7 +821,9 @@ __device__ inline uint32_t set_ord_cell(int64_t o, uint64_t count) {
 // random lookups in flight instead of walking one probe chain at a time (the per-row form
 // fetched ~114 B per row at ~2.4 TB/s of random lines: 27 ms for C3); the rare rows whose
 // first slot holds another key continue their probe sequence afterwards.
-template <int NV, int SB, bool SET = false>
+// DT0 / DT1: value slot dtypes as compile-time constants (VH_F64 = the float64 kernel), or -1:
+// any dtype through a run-time switch (slower: the branches around the prefetch loads)
+template <int NV, int SB, bool SET = false, int DT0 = VH_F64, int DT1 = VH_F64>
 __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
     constexpr int PAIRS = TA_RPT / 2;
     extern __shared__ __align__(16) unsigned char lds_raw[];
@@ -785,7 +842,8 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
     for (int k = 0; k < MAX_FUSED_AGGS; k++) {
         if (k >= fa.na) break;
         keyed_slot_of[k] = fa.a[k].kind == VH_AGG_COUNT ? (uint32_t)tp.cnt_slot[k] : (uint32_t)tp.val_slot[k];
-        if (fa.a[k].kind == VH_AGG_COUNT && tp.cnt_slot[k] == CNT_ALWAYS) count_mask |= 1u << k;
+        // count(*) and integer sums take every row (int64 bits are not NaN-tested)
+        if ((fa.a[k].kind == VH_AGG_COUNT && tp.cnt_slot[k] == CNT_ALWAYS) || fa.a[k].vint) count_mask |= 1u << k;
         else
 #pragma unroll
             for (int s = 0; s < NV; s++)
@@ -800,6 +858,14 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
         int2 k[PAIRS];
         double2 v[PAIRS][NV > 0 ? NV : 1];
     };
+    int vsz[NV > 0 ? NV : 1];
+#pragma unroll
+    for (int s = 0; s < NV; s++) {
+        const int dts = s == 0 ? DT0 : DT1;
+        vsz[s] = dts >= 0 ? dtype_itemsize_dev(dts) : dtype_itemsize_dev(tp.vdt[s]);
+    }
+    // row pairs: keys as int2, values by item size (float64 16 B; narrower types' pair bits
+    // packed into .x, decoded per row by pair_slot when used, so the prefetch stays in flight)
     auto load = [&](uint64_t b0, Regs &R) {
 #pragma unroll
         for (int q = 0; q < PAIRS; q++) {
@@ -807,7 +873,18 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
             const uint64_t is = i < n - 2 ? i : n - 2;
             R.k[q] = *reinterpret_cast<const int2 *>(keys + is);
 #pragma unroll
-            for (int s = 0; s < NV; s++) R.v[q][s] = *reinterpret_cast<const double2 *>(col[s] + is);
+            for (int s = 0; s < NV; s++) {
+                const char *cb = reinterpret_cast<const char *>(col[s]);
+                if (vsz[s] == 8) {
+                    R.v[q][s] = *reinterpret_cast<const double2 *>(cb + is * 8);
+                } else if (vsz[s] == 4) {
+                    R.v[q][s].x = __builtin_bit_cast(double, *reinterpret_cast<const uint64_t *>(cb + is * 4));
+                } else if (vsz[s] == 2) {
+                    R.v[q][s].x = __builtin_bit_cast(double, (uint64_t)*reinterpret_cast<const uint32_t *>(cb + is * 2));
+                } else {
+                    R.v[q][s].x = __builtin_bit_cast(double, (uint64_t)*reinterpret_cast<const uint16_t *>(cb + is));
+                }
+            }
         }
     };
     const SetDev sd = p.b[0].set;
@@ -852,7 +929,8 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
             uint32_t f = count_mask;
 #pragma unroll
             for (int s = 0; s < NV; s++) {
-                vals[r][s] = h ? cur.v[q][s].y : cur.v[q][s].x;
+                const int dts = s == 0 ? DT0 : DT1;
+                vals[r][s] = pair_slot(cur.v[q][s], dts >= 0 ? dts : tp.vdt[s], h);
                 f |= vals[r][s] == vals[r][s] ? nan_keyed[s] : 0u;
             }
             f = i < row_end ? f : 0u;
@@ -925,7 +1003,7 @@ template <int NV> constexpr int tb_vu() { return VH_TB_VU ? VH_TB_VU : NV == 0 ?
 // short the regions are; a lane finds the region of its chunk by a forward scan (chunk
 // indices of a lane only grow).  Entries are reduced with LDS atomics, then the tile is
 // flushed with coalesced global atomics.
-template <int NV>
+template <int NV, bool NARROW = false>
 __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TileParams tp, const WorkUnit *units) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
     __shared__ uint32_t s_fill[1024];
@@ -984,9 +1062,20 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                 rem[j] = c < C ? min(8u, s_fill[kk] - q) : 0u;
                 ev[j] = *reinterpret_cast<const uint4 *>(ent16 + e);
 #pragma unroll
-                for (int s = 0; s < NV; s++)
+                for (int s = 0; s < NV; s++) {
+                    if constexpr (NARROW) {  // 8 x 4-byte slots: two 16-byte loads, widened
+                        const bool fl = (tp.vfloat >> s) & 1, sg = (tp.vsigned >> s) & 1;
+                        const uint4 a = *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint32_t *>(tp.values[s]) + e);
+                        const uint4 b = *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint32_t *>(tp.values[s]) + e + 4);
+                        vv[j][s][0] = make_double2(slot_wide(a.x, fl, sg), slot_wide(a.y, fl, sg));
+                        vv[j][s][1] = make_double2(slot_wide(a.z, fl, sg), slot_wide(a.w, fl, sg));
+                        vv[j][s][2] = make_double2(slot_wide(b.x, fl, sg), slot_wide(b.y, fl, sg));
+                        vv[j][s][3] = make_double2(slot_wide(b.z, fl, sg), slot_wide(b.w, fl, sg));
+                    } else {
 #pragma unroll
-                    for (int h = 0; h < 4; h++) vv[j][s][h] = *reinterpret_cast<const double2 *>(tp.values[s] + e + 2 * h);
+                        for (int h = 0; h < 4; h++) vv[j][s][h] = *reinterpret_cast<const double2 *>(tp.values[s] + e + 2 * h);
+                    }
+                }
             }
 #pragma unroll
             for (int j = 0; j < VU; j++) {
@@ -1017,7 +1106,13 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                         const uint64_t e = base + q;
                         ent[j] = reinterpret_cast<const uint32_t *>(tp.entries)[e];
 #pragma unroll
-                        for (int s = 0; s < NV; s++) v[j][s] = tp.values[s][e];
+                        for (int s = 0; s < NV; s++) {
+                            if constexpr (NARROW)
+                                v[j][s] = slot_wide(reinterpret_cast<const uint32_t *>(tp.values[s])[e], (tp.vfloat >> s) & 1,
+                                                    (tp.vsigned >> s) & 1);
+                            else
+                                v[j][s] = tp.values[s][e];
+                        }
                     }
                 }
 #pragma unroll
@@ -1598,16 +1693,38 @@ template <int NV> static int scatter_blocks_per_cu_nd(int nd, int fast, size_t l
     }
 }
 
-template <bool SET> static const void *ord_kernel_t(int nv, int fast_mode) {
-    if (nv == 0) return reinterpret_cast<const void *>(k_tile_scatter_ord<0, 1, SET>);
-    if (nv == 1)
-        return fast_mode == 2 ? reinterpret_cast<const void *>(k_tile_scatter_ord<1, fast_sb(1), SET>)
-                              : reinterpret_cast<const void *>(k_tile_scatter_ord<1, 1, SET>);
-    return fast_mode == 2 ? reinterpret_cast<const void *>(k_tile_scatter_ord<2, fast_sb(2), SET>)
-                          : reinterpret_cast<const void *>(k_tile_scatter_ord<2, 1, SET>);
+// value-dtype combinations with their own ordinal kernel (0: float64; h2o's int8 / float32
+// sums; others take the run-time-switch kernel, -1)
+template <int NV, int SB, bool SET, typename F> static void ord_by_dts(int dt0, int dt1, F &&f) {
+#define VH_ORD_DT(a, b) if (dt0 == (a) && (NV < 2 || dt1 == (b))) return f(k_tile_scatter_ord<NV, SB, SET, (a), NV < 2 ? VH_F64 : (b)>);
+    VH_ORD_DT(VH_F64, VH_F64)
+    if constexpr (!SET) {
+        VH_ORD_DT(VH_I8, VH_I8)
+        VH_ORD_DT(VH_I8, VH_F32)
+        VH_ORD_DT(VH_F32, VH_I8)
+        VH_ORD_DT(VH_F32, VH_F32)
+        VH_ORD_DT(VH_I32, VH_I32)
+        VH_ORD_DT(VH_I32, VH_F64)
+        VH_ORD_DT(VH_F32, VH_F64)
+    }
+#undef VH_ORD_DT
+    f(k_tile_scatter_ord<NV, SB, SET, -1, -1>);
 }
-static const void *ord_kernel(int nv, int fast_mode, bool set) {
-    return set ? ord_kernel_t<true>(nv, fast_mode) : ord_kernel_t<false>(nv, fast_mode);
+template <bool SET> static const void *ord_kernel_t(int nv, int fast_mode, int dt0, int dt1) {
+    const void *k = nullptr;
+    auto take = [&](auto kern) { k = reinterpret_cast<const void *>(kern); };
+    if (nv == 0) ord_by_dts<0, 1, SET>(VH_F64, VH_F64, take);
+    else if (nv == 1) {
+        if (fast_mode == 2) ord_by_dts<1, fast_sb(1), SET>(dt0, dt1, take);
+        else ord_by_dts<1, 1, SET>(dt0, dt1, take);
+    } else {
+        if (fast_mode == 2) ord_by_dts<2, fast_sb(2), SET>(dt0, dt1, take);
+        else ord_by_dts<2, 1, SET>(dt0, dt1, take);
+    }
+    return k;
+}
+static const void *ord_kernel(int nv, int fast_mode, bool set, int dt0, int dt1) {
+    return set ? ord_kernel_t<true>(nv, fast_mode, dt0, dt1) : ord_kernel_t<false>(nv, fast_mode, dt0, dt1);
 }
 
 // 0 = not tiled (caller takes another path), 1 = done, 2 = the XCD-resident launch aborted
@@ -1633,7 +1750,10 @@ static bool ord_fast_ok(const BinPlan &plan, const FusedAggs &fa) {
         const FusedAgg &a = fa.a[k];
         if (a.mask) return false;
         if (a.kind != VH_AGG_COUNT) {
-            if (!a.data || a.dtype != VH_F64 || (reinterpret_cast<uintptr_t>(a.data) & 15)) return false;
+            // any native value dtype; pair loads need 2 x itemsize alignment
+            if (!a.data) return false;
+            const int isz = a.dtype == VH_F64 ? 16 : 2 * dtype_itemsize(a.dtype);
+            if (reinterpret_cast<uintptr_t>(a.data) % isz) return false;
         } else if (a.data) {
             bool keyed = false;  // count(v) of a summed column rides on that sum's value
             for (int j = 0; j < fa.na; j++)
@@ -1684,6 +1804,10 @@ static int res_mode() {
     if (g_res_off.load()) return 0;
     const char *e = getenv("VH_RESIDENT");
     return e ? atoi(e) : 0;
+}
+static bool getenv_flag_off(const char *name) {  // NAME=0 turns a default-on path off (A/B runs)
+    const char *e = getenv(name);
+    return e && atoi(e) == 0;
 }
 static uint64_t res_min_rows() {  // VH_RES_MIN_ROWS: tests run the path at small sizes
     const char *e = getenv("VH_RES_MIN_ROWS");
@@ -1776,8 +1900,12 @@ static int try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t 
         if (fa.a[k].kind == VH_AGG_COUNT && fa.a[k].data && fa.a[k].dtype != VH_F64) fast = false;
     }
     const bool ord = !fast && n % 2 == 0 && ord_fast_ok(plan, fa);
+    tp.vdt[0] = tp.vdt[1] = VH_F64;
     if (ord) for (int k = 0; k < fa.na; k++)
-        if (fa.a[k].kind != VH_AGG_COUNT) tp.vdata[tp.val_slot[k]] = fa.a[k].data;
+        if (fa.a[k].kind != VH_AGG_COUNT) {
+            tp.vdata[tp.val_slot[k]] = fa.a[k].data;
+            tp.vdt[tp.val_slot[k]] = fa.a[k].dtype;
+        }
     // fast kernel: several batches per commit when that staging fits the LDS
     const int fast_mode = !(fast || ord) ? 0 : fast_lds_bytes(nv, T, (uint32_t)(fast_sb(nv) * TA_BATCH)) <= LDS_MAX_BYTES ? 2 : 1;
     const size_t lds_a = fast_mode == 2   ? fast_lds_bytes(nv, T, (uint32_t)(fast_sb(nv) * TA_BATCH))
@@ -1789,12 +1917,12 @@ static int try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t 
         static std::mutex mu;
         static std::map<std::tuple<int, int, int, int, size_t>, int> cache;
         std::lock_guard<std::mutex> lk(mu);
-        const auto key = std::make_tuple(current_device(), ord ? (has_set ? -3 : -2) : nd_k, nv, fast_mode, lds_a);
+        const auto key = std::make_tuple(current_device(), ord ? (has_set ? -3 : -2) - 4 * (tp.vdt[0] + 32 * tp.vdt[1]) : nd_k, nv, fast_mode, lds_a);
         auto it = cache.find(key);
         if (it == cache.end()) {
             int v = 0;
             if (ord) {
-                const void *kf = ord_kernel(nv, fast_mode, has_set);
+                const void *kf = ord_kernel(nv, fast_mode, has_set, tp.vdt[0], tp.vdt[1]);
                 VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kf, TA_THREADS, lds_a));
             } else {
                 v = nv == 0 ? scatter_blocks_per_cu_nd<0>(nd_k, fast_mode, lds_a)
@@ -1915,7 +2043,20 @@ static int try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t 
     const uint64_t total = stride * W;
     const int ebytes = flags_mode ? 4 : 2;
     ws.entries.ensure(total * ebytes);
-    if (nv) ws.values.ensure(total * 8 * nv);
+    // 4-byte value slots when every summed column of a generic plan is <= 4 bytes (exact)
+    bool vnarrow = fa.generic_vals && nv > 0 && !fast && !getenv_flag_off("VH_TILE_NARROW");
+    uint32_t vfloat = 0, vsigned = 0;
+    for (int k = 0; k < fa.na && vnarrow; k++) {
+        if (fa.a[k].kind == VH_AGG_COUNT) continue;
+        const int dt = fa.a[k].dtype, s = tp.val_slot[k];
+        if (dtype_itemsize(dt) > 4) vnarrow = false;
+        if (dt == VH_F32) vfloat |= 1u << s;
+        if (dt == VH_I32 || dt == VH_I16 || dt == VH_I8) vsigned |= 1u << s;
+    }
+    if (nv) ws.values.ensure(total * (vnarrow ? 4 : 8) * nv + 64);
+    tp.vnarrow = vnarrow ? 1u : 0u;
+    tp.vfloat = vfloat;
+    tp.vsigned = vsigned;
     tp.s_log2 = s_log2;
     tp.ntiles = T;
     tp.flags_mode = flags_mode ? 1 : 0;
@@ -1928,7 +2069,9 @@ static int try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t 
     tp.toff = d_toff;
     tp.fills = d_fills;
     tp.entries = ws.entries.ptr;
-    for (int s = 0; s < nv; s++) tp.values[s] = ws.values.as<double>() + (uint64_t)s * total;
+    for (int s = 0; s < nv; s++)
+        tp.values[s] = vnarrow ? reinterpret_cast<double *>(ws.values.as<uint32_t>() + (uint64_t)s * total)
+                               : ws.values.as<double>() + (uint64_t)s * total;
     VH_HIP(hipMemcpyAsync(d_cap, cap.data(), 4 * (uint64_t)T, hipMemcpyHostToDevice, st));
     VH_HIP(hipMemcpyAsync(d_toff, toff.data(), 8 * (uint64_t)T, hipMemcpyHostToDevice, st));
 
@@ -2029,21 +2172,9 @@ static int try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t 
         TimedScope ts(fast ? "tile_scatter_f64" : ord ? (has_set ? "tile_scatter_set" : "tile_scatter_ord") : "tile_scatter");
         const size_t lds = lds_a;
         if (ord) {
-            auto launch_ord = [&](auto setc) {
-                constexpr bool SET = decltype(setc)::value;
-                switch (nv) {
-                case 0: hipLaunchKernelGGL((k_tile_scatter_ord<0, 1, SET>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n); break;
-                case 1:
-                    if (fast_mode == 2) hipLaunchKernelGGL((k_tile_scatter_ord<1, fast_sb(1), SET>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
-                    else hipLaunchKernelGGL((k_tile_scatter_ord<1, 1, SET>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
-                    break;
-                default:
-                    if (fast_mode == 2) hipLaunchKernelGGL((k_tile_scatter_ord<2, fast_sb(2), SET>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
-                    else hipLaunchKernelGGL((k_tile_scatter_ord<2, 1, SET>), dim3(W), dim3(TA_THREADS), lds, st, plan, fa, tp, n);
-                }
-            };
-            if (has_set) launch_ord(std::true_type());
-            else launch_ord(std::false_type());
+            const void *kf = ord_kernel(nv, fast_mode, has_set, tp.vdt[0], tp.vdt[1]);
+            void *args[] = {(void *)&plan, (void *)&fa, (void *)&tp, (void *)&n};
+            VH_HIP(hipLaunchKernel(kf, dim3(W), dim3(TA_THREADS), args, lds, st));
         } else {
             switch (nv) {
             case 0: launch_scatter_nd<0>(nd_k, fast_mode, W, lds, plan, fa, tp, n); break;
@@ -2059,8 +2190,13 @@ static int try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t 
         const unsigned g = (unsigned)units.size();
         switch (nv) {
         case 0: hipLaunchKernelGGL(k_tile_reduce<0>, dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units); break;
-        case 1: hipLaunchKernelGGL(k_tile_reduce<1>, dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units); break;
-        default: hipLaunchKernelGGL(k_tile_reduce<2>, dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
+        case 1:
+            if (vnarrow) hipLaunchKernelGGL((k_tile_reduce<1, true>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
+            else hipLaunchKernelGGL(k_tile_reduce<1>, dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
+            break;
+        default:
+            if (vnarrow) hipLaunchKernelGGL((k_tile_reduce<2, true>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
+            else hipLaunchKernelGGL(k_tile_reduce<2>, dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
         }
         VH_HIP(hipGetLastError());
     }
