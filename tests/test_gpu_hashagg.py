@@ -303,6 +303,48 @@ def test_dense_int32_keys_fast_ordinal_any_value_dtype(vdtypes, device):
             np.testing.assert_array_equal(g[f"s{j}"].to_numpy(), es)
 
 
+@pytest.mark.parametrize("vdtype", ["int8", "float32", "float64", "int64", "uint16", "int32"])
+@pytest.mark.parametrize("device", [False, True])
+def test_dense_keys_min_max_through_tile_path(vdtype, device):
+    """h2o q7's shape: max / min per group over a 2.5e5-group dense grid go through the
+    tile path (LDS min / max cells) instead of per-row global atomics; equal to numpy."""
+    import vaex_amd
+    from vaex_amd import _lib
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(len(vdtype))
+    n = 2_000_000
+    keys = (5 + rng.integers(0, 250_000, n)).astype(np.int32)
+    if vdtype.startswith("float"):
+        v = rng.normal(size=n).astype(vdtype)
+        v[::29] = np.nan
+    else:
+        info = np.iinfo(vdtype)
+        v = rng.integers(info.min, info.max, n, endpoint=True).astype(vdtype)
+    cols = {"key": keys, "v": v}
+    df = vaex_amd.from_arrays(**({k: DeviceArray.from_numpy(a) for k, a in cols.items()} if device else cols))
+    _lib.timing_reset()
+    _lib.timing_enable(True)
+    g = df.groupby("key", agg={"mx": vaex_amd.agg.max("v"), "mn": vaex_amd.agg.min("v"), "n": "count"})
+    _lib.synchronize()
+    _lib.timing_enable(False)
+    assert _lib.timing_read("bin_aggregate")[0] == 0, "min / max took the generic global-atomic path"
+    uk, inv = np.unique(keys, return_inverse=True)
+    np.testing.assert_array_equal(g["key"].to_numpy(), uk)
+    np.testing.assert_array_equal(g["n"].to_numpy(), np.bincount(inv))
+    order = np.argsort(inv, kind="stable")
+    starts = np.r_[0, np.cumsum(np.bincount(inv))[:-1]]
+    vs = v[order]
+    if vdtype.startswith("float"):
+        # NaN never enters (superagg.cpp AggMax/AggMin): an all-NaN group keeps the -inf / +inf fill
+        exp_mx = np.nan_to_num(np.fmax.reduceat(vs, starts), nan=-np.inf)
+        exp_mn = np.nan_to_num(np.fmin.reduceat(vs, starts), nan=np.inf)
+    else:
+        exp_mx = np.maximum.reduceat(vs, starts)
+        exp_mn = np.minimum.reduceat(vs, starts)
+    np.testing.assert_array_equal(g["mx"].to_numpy(), exp_mx)
+    np.testing.assert_array_equal(g["mn"].to_numpy(), exp_mn)
+
+
 @pytest.mark.parametrize("n,card", [(3_000_000, 1_000_000), (600_000, 3)])
 @pytest.mark.parametrize("kdtype", ["int64", "uint64"])
 def test_64bit_keys_partitioned_and_chunked(kdtype, n, card):

@@ -335,6 +335,35 @@ def test_xcd_resident_path_matches_oracle(monkeypatch, mode, with_sum):
         np.testing.assert_array_equal(np.asarray(aggs[2]), _oracle_grid([bx, by], "count", data=w))
 
 
+@pytest.mark.parametrize("dtype", ["float64", "float32", "int16"])
+def test_tile_path_min_max_large_grid(dtype):
+    """AggMin / AggMax on the C2-shape 1027^2 grid take the tile path (LDS min / max cells,
+    typed CAS flush); equal to the oracle, NaN rows skipped, untouched cells keep the fill."""
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(41)
+    n = 3_000_000
+    x, y = rng.normal(size=n), rng.normal(size=n)
+    if dtype.startswith("float"):
+        w = rng.normal(size=n).astype(dtype)
+        w[::17] = np.nan
+    else:
+        w = rng.integers(-30000, 30000, n).astype(dtype)
+    bx = oracle.Binner("scalar", x, vmin=-4, vmax=4, bins=1024)
+    by = oracle.Binner("scalar", y, vmin=-4, vmax=4, bins=1024)
+    gx, gy = sa().BinnerScalar_float64("x", -4, 4, 1024), sa().BinnerScalar_float64("y", -4, 4, 1024)
+    gx.set_data(DeviceArray.from_numpy(x))
+    gy.set_data(DeviceArray.from_numpy(y))
+    grid = sa().Grid([gx, gy])
+    dw = DeviceArray.from_numpy(w)
+    mx = getattr(sa(), "AggMax_" + dtype)(grid)
+    mn = getattr(sa(), "AggMin_" + dtype)(grid)
+    mx.set_data(dw, 0)
+    mn.set_data(dw, 0)
+    grid.bin([mx, mn])
+    np.testing.assert_array_equal(np.asarray(mx), _oracle_grid([bx, by], "max", data=w))
+    np.testing.assert_array_equal(np.asarray(mn), _oracle_grid([bx, by], "min", data=w))
+
+
 def test_host_staging_multiple_chunks():
     """Host columns longer than one staging chunk (16 Mi rows)."""
     n = (1 << 24) + 12345

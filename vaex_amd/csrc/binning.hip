@@ -65,62 +65,6 @@ template <> __device__ inline void atomic_add_grid<uint64_t>(uint64_t *a, uint64
     atomicAdd((unsigned long long *)a, (unsigned long long)v);
 }
 
-// exact std::min/std::max(value, grid) semantics (superagg.cpp:226,274) with CAS
-template <typename T> __device__ inline T minmax_apply(T g, T value, bool is_max) {
-    return is_max ? ((value < g) ? g : value) : ((g < value) ? g : value);
-}
-
-template <typename T> __device__ inline void atomic_minmax(T *addr, T value, bool is_max) {
-    if constexpr (sizeof(T) == 8 || sizeof(T) == 4) {
-        using W = typename std::conditional<sizeof(T) == 8, unsigned long long, unsigned int>::type;
-        W *a = reinterpret_cast<W *>(addr);
-        W old = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (;;) {
-            T g;
-            __builtin_memcpy(&g, &old, sizeof(T));
-            T nv = minmax_apply(g, value, is_max);
-            W nb;
-            __builtin_memcpy(&nb, &nv, sizeof(T));
-            if (nb == old) return;
-            W prev = atomicCAS(a, old, nb);
-            if (prev == old) return;
-            old = prev;
-        }
-    } else {
-        uintptr_t addr_u = reinterpret_cast<uintptr_t>(addr);
-        unsigned int *word = reinterpret_cast<unsigned int *>(addr_u & ~(uintptr_t)3);
-        const unsigned shift = (unsigned)(addr_u & 3) * 8;
-        const unsigned mask = (sizeof(T) == 2 ? 0xffffu : 0xffu) << shift;
-        unsigned int old = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (;;) {
-            unsigned cur_bits = (old & mask) >> shift;
-            T g;
-            if constexpr (sizeof(T) == 2) {
-                uint16_t cb = (uint16_t)cur_bits;
-                __builtin_memcpy(&g, &cb, 2);
-            } else {
-                uint8_t cb = (uint8_t)cur_bits;
-                __builtin_memcpy(&g, &cb, 1);
-            }
-            T nv = minmax_apply(g, value, is_max);
-            unsigned nbits;
-            if constexpr (sizeof(T) == 2) {
-                uint16_t t;
-                __builtin_memcpy(&t, &nv, 2);
-                nbits = t;
-            } else {
-                uint8_t t;
-                __builtin_memcpy(&t, &nv, 1);
-                nbits = t;
-            }
-            if (nbits == cur_bits) return;
-            unsigned int nw = (old & ~mask) | (nbits << shift);
-            unsigned int prev = atomicCAS(word, old, nw);
-            if (prev == old) return;
-            old = prev;
-        }
-    }
-}
 
 template <typename T> struct Upcast { using type = int64_t; };
 template <> struct Upcast<double> { using type = double; };
@@ -1249,10 +1193,13 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
     // (any number of them: run in groups of at most MAX_FUSED_AGGS with at most two sums, one
     // tile pass per group over the same staged chunk)
     bool tile_generic = !all_fusable && L * 8 > LDS_AGG_MAX_BYTES;
-    for (int k = 0; k < naggs && tile_generic; k++) {
-        const vh_agg *a = aggs[k];
-        tile_generic = (a->kind == VH_AGG_COUNT || (a->kind == VH_AGG_SUM && a->data.set)) && !a->mask.set && !a->flip;
-    }
+    // (min / max too: LDS min / max cells in pass B; not of bool data)
+    auto tile_kind = [](const vh_agg *a) {
+        return (a->kind == VH_AGG_COUNT || (a->kind == VH_AGG_SUM && a->data.set) ||
+                ((a->kind == VH_AGG_MIN || a->kind == VH_AGG_MAX) && a->data.set && a->dtype != VH_BOOL)) &&
+               !a->mask.set && !a->flip;
+    };
+    for (int k = 0; k < naggs && tile_generic; k++) tile_generic = tile_kind(aggs[k]);
     if (!all_fusable && !tile_generic && !any_host && naggs > 1 && L * 8 > LDS_AGG_MAX_BYTES) {
         // a mix on a large grid (e.g. groupby count(*) + min + max): the count / sum
         // aggregators take the tile path, only the rest pays the generic path's global
@@ -1260,7 +1207,7 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
         std::vector<vh_agg *> tiled, rest;
         for (int k = 0; k < naggs; k++) {
             const vh_agg *a = aggs[k];
-            const bool t = (a->kind == VH_AGG_COUNT || (a->kind == VH_AGG_SUM && a->data.set)) && !a->mask.set && !a->flip;
+            const bool t = tile_kind(a);
             (t && tiled.size() < (size_t)MAX_FUSED_AGGS ? tiled : rest).push_back(aggs[k]);
         }
         if (!tiled.empty() && !rest.empty()) {
@@ -1319,11 +1266,12 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                        std::vector<std::vector<int>> groups(1);
                        int sums = 0;
                        for (int k = 0; k < naggs; k++) {
-                           if ((aggs[k]->kind == VH_AGG_SUM && sums == 2) || groups.back().size() == (size_t)MAX_FUSED_AGGS) {
+                           const bool slot = aggs[k]->kind != VH_AGG_COUNT;  // sums, min, max carry a value
+                           if ((slot && sums == 2) || groups.back().size() == (size_t)MAX_FUSED_AGGS) {
                                groups.emplace_back();
                                sums = 0;
                            }
-                           if (aggs[k]->kind == VH_AGG_SUM) sums++;
+                           if (slot) sums++;
                            groups.back().push_back(k);
                        }
                        for (size_t gi = 0; gi < groups.size(); gi++) {

@@ -56,6 +56,63 @@ struct AggDev {
     void *s_row;
 };
 
+// exact std::min/std::max(value, grid) semantics (superagg.cpp:226,274) with CAS
+template <typename T> __device__ inline T minmax_apply(T g, T value, bool is_max) {
+    return is_max ? ((value < g) ? g : value) : ((g < value) ? g : value);
+}
+
+template <typename T> __device__ inline void atomic_minmax(T *addr, T value, bool is_max) {
+    if constexpr (sizeof(T) == 8 || sizeof(T) == 4) {
+        using W = typename std::conditional<sizeof(T) == 8, unsigned long long, unsigned int>::type;
+        W *a = reinterpret_cast<W *>(addr);
+        W old = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (;;) {
+            T g;
+            __builtin_memcpy(&g, &old, sizeof(T));
+            T nv = minmax_apply(g, value, is_max);
+            W nb;
+            __builtin_memcpy(&nb, &nv, sizeof(T));
+            if (nb == old) return;
+            W prev = atomicCAS(a, old, nb);
+            if (prev == old) return;
+            old = prev;
+        }
+    } else {
+        uintptr_t addr_u = reinterpret_cast<uintptr_t>(addr);
+        unsigned int *word = reinterpret_cast<unsigned int *>(addr_u & ~(uintptr_t)3);
+        const unsigned shift = (unsigned)(addr_u & 3) * 8;
+        const unsigned mask = (sizeof(T) == 2 ? 0xffffu : 0xffu) << shift;
+        unsigned int old = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (;;) {
+            unsigned cur_bits = (old & mask) >> shift;
+            T g;
+            if constexpr (sizeof(T) == 2) {
+                uint16_t cb = (uint16_t)cur_bits;
+                __builtin_memcpy(&g, &cb, 2);
+            } else {
+                uint8_t cb = (uint8_t)cur_bits;
+                __builtin_memcpy(&g, &cb, 1);
+            }
+            T nv = minmax_apply(g, value, is_max);
+            unsigned nbits;
+            if constexpr (sizeof(T) == 2) {
+                uint16_t t;
+                __builtin_memcpy(&t, &nv, 2);
+                nbits = t;
+            } else {
+                uint8_t t;
+                __builtin_memcpy(&t, &nv, 1);
+                nbits = t;
+            }
+            if (nbits == cur_bits) return;
+            unsigned int nw = (old & ~mask) | (nbits << shift);
+            unsigned int prev = atomicCAS(word, old, nw);
+            if (prev == old) return;
+            old = prev;
+        }
+    }
+}
+
 // count / sum(float64) aggregators of the fused path
 struct FusedAgg {
     int32_t kind;

@@ -129,6 +129,64 @@ __device__ __forceinline__ double slot_wide(uint32_t u, bool is_float, bool is_s
     return __builtin_bit_cast(double, is_signed ? (uint64_t)(int64_t)(int32_t)u : (uint64_t)u);
 }
 
+// ---- min / max in the tile path (AggMin / AggMax, superagg.cpp:195-285) ----------------
+// Pass A carries the value slot like a sum's; pass B keeps an order-preserving 64-bit form
+// per LDS cell (float: sign-flipped bits, ds_min/max_u64; signed: int64, ds_min/max_i64;
+// unsigned: uint64), cells start at the kind's identity, and touched cells are flushed into
+// the typed grid with the CAS min / max of the generic path (std::min/max semantics; NaN
+// never enters, as the reference's comparisons skip it).
+__host__ __device__ inline bool is_minmax(int kind) { return kind == VH_AGG_MIN || kind == VH_AGG_MAX; }
+__device__ inline bool dt_float(int dt) { return dt == VH_F64 || dt == VH_F32; }
+__device__ inline bool dt_signed(int dt) { return dt == VH_I64 || dt == VH_I32 || dt == VH_I16 || dt == VH_I8; }
+__device__ inline uint64_t ord_bits(double d) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, d);
+    return (u >> 63) ? ~u : (u | (1ull << 63));
+}
+__device__ inline double unord_bits(uint64_t o) {
+    return __builtin_bit_cast(double, (o >> 63) ? (o & ~(1ull << 63)) : ~o);
+}
+__device__ inline uint64_t mm_identity(int dt, bool mx) {
+    if (dt_signed(dt)) return mx ? (uint64_t)INT64_MIN : (uint64_t)INT64_MAX;
+    return mx ? 0ull : ~0ull;  // float (ordered bits) and unsigned
+}
+// one carried slot value into an LDS cell
+__device__ inline void mm_lds(uint64_t *cell, int dt, bool mx, double v) {
+    if (dt_float(dt)) {
+        if (v != v) return;
+        const uint64_t o = ord_bits(v);
+        if (mx) atomicMax((unsigned long long *)cell, (unsigned long long)o);
+        else atomicMin((unsigned long long *)cell, (unsigned long long)o);
+    } else if (dt_signed(dt)) {
+        const long long x = (long long)__builtin_bit_cast(int64_t, v);
+        if (mx) atomicMax((long long *)cell, x);
+        else atomicMin((long long *)cell, x);
+    } else {
+        const unsigned long long x = __builtin_bit_cast(unsigned long long, v);
+        if (mx) atomicMax((unsigned long long *)cell, x);
+        else atomicMin((unsigned long long *)cell, x);
+    }
+}
+// a value (LDS cell form when `cellform`, else a carried slot) into the typed grid
+__device__ inline void mm_grid(void *grid, uint64_t c, int dt, bool mx, uint64_t x, bool cellform) {
+    double d = 0.0;
+    if (dt_float(dt)) {
+        d = cellform ? unord_bits(x) : __builtin_bit_cast(double, x);
+        if (d != d) return;
+    }
+    switch (dt) {
+    case VH_F64: atomic_minmax<double>(static_cast<double *>(grid) + c, d, mx); break;
+    case VH_F32: atomic_minmax<float>(static_cast<float *>(grid) + c, (float)d, mx); break;
+    case VH_I64: atomic_minmax<int64_t>(static_cast<int64_t *>(grid) + c, (int64_t)x, mx); break;
+    case VH_I32: atomic_minmax<int32_t>(static_cast<int32_t *>(grid) + c, (int32_t)(int64_t)x, mx); break;
+    case VH_I16: atomic_minmax<int16_t>(static_cast<int16_t *>(grid) + c, (int16_t)(int64_t)x, mx); break;
+    case VH_I8: atomic_minmax<int8_t>(static_cast<int8_t *>(grid) + c, (int8_t)(int64_t)x, mx); break;
+    case VH_U64: atomic_minmax<uint64_t>(static_cast<uint64_t *>(grid) + c, x, mx); break;
+    case VH_U32: atomic_minmax<uint32_t>(static_cast<uint32_t *>(grid) + c, (uint32_t)x, mx); break;
+    case VH_U16: atomic_minmax<uint16_t>(static_cast<uint16_t *>(grid) + c, (uint16_t)x, mx); break;
+    default: atomic_minmax<uint8_t>(static_cast<uint8_t *>(grid) + c, (uint8_t)x, mx); break;  // VH_U8
+    }
+}
+
 struct WorkUnit {
     uint32_t tile, w_begin, w_end, pad;
 };
@@ -382,6 +440,10 @@ __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, co
                 if (!((f >> a) & 1)) continue;
                 if (fa.a[a].kind == VH_AGG_COUNT) {
                     atomicAdd((unsigned long long *)fa.a[a].grid + c, 1ULL);
+                } else if (is_minmax(fa.a[a].kind)) {
+                    if constexpr (NV > 0)
+                        mm_grid(fa.a[a].grid, c, fa.a[a].dtype, fa.a[a].kind == VH_AGG_MAX,
+                                __builtin_bit_cast(uint64_t, l.sv[tp.val_slot[a] * TA_BATCH + k]), false);
                 } else if constexpr (NV > 0) {
                     const double v = l.sv[tp.val_slot[a] * TA_BATCH + k];
                     if (fa.a[a].vint)
@@ -485,6 +547,10 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
                 if (!take) continue;
                 if (fa.a[a].kind == VH_AGG_COUNT) {
                     atomicAdd((unsigned long long *)fa.a[a].grid + c, 1ULL);
+                } else if (is_minmax(fa.a[a].kind)) {
+                    if constexpr (NV > 0)
+                        mm_grid(fa.a[a].grid, c, fa.a[a].dtype, fa.a[a].kind == VH_AGG_MAX,
+                                __builtin_bit_cast(uint64_t, l.sv[tp.val_slot[a] * CAP + k]), false);
                 } else if constexpr (NV > 0) {
                     const double v = l.sv[tp.val_slot[a] * CAP + k];
                     if (fa.a[a].vint)
@@ -843,7 +909,9 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
         if (k >= fa.na) break;
         keyed_slot_of[k] = fa.a[k].kind == VH_AGG_COUNT ? (uint32_t)tp.cnt_slot[k] : (uint32_t)tp.val_slot[k];
         // count(*) and integer sums take every row (int64 bits are not NaN-tested)
-        if ((fa.a[k].kind == VH_AGG_COUNT && tp.cnt_slot[k] == CNT_ALWAYS) || fa.a[k].vint) count_mask |= 1u << k;
+        if ((fa.a[k].kind == VH_AGG_COUNT && tp.cnt_slot[k] == CNT_ALWAYS) || fa.a[k].vint ||
+            (is_minmax(fa.a[k].kind) && fa.a[k].dtype != VH_F64 && fa.a[k].dtype != VH_F32))
+            count_mask |= 1u << k;
         else
 #pragma unroll
             for (int s = 0; s < NV; s++)
@@ -977,6 +1045,12 @@ __device__ inline void reduce_entry(const FusedAggs &fa, const TileParams &tp, u
                     if (s == cs) take = v[s] == v[s];
             }
             if (take) atomicAdd(reinterpret_cast<uint32_t *>(lds + fa.a[k].lds_off) + local, 1u);
+        } else if (is_minmax(fa.a[k].kind)) {
+#pragma unroll
+            for (int s = 0; s < NV; s++) {
+                if (s != tp.val_slot[k]) continue;
+                mm_lds(reinterpret_cast<uint64_t *>(lds + fa.a[k].lds_off) + local, fa.a[k].dtype, fa.a[k].kind == VH_AGG_MAX, v[s]);
+            }
         } else {
 #pragma unroll
             for (int s = 0; s < NV; s++) {
@@ -1040,6 +1114,21 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
         if (lane == 63) s_pre[nw] = inc;
     }
     __syncthreads();
+    bool any_mm = false;
+    #pragma unroll
+    for (int k = 0; k < MAX_FUSED_AGGS; k++)
+        if (k < fa.na && is_minmax(fa.a[k].kind)) any_mm = true;
+    if (any_mm) {  // min / max cells start at the kind's identity (after the zero fill)
+        const uint32_t ncells = 1u << tp.s_log2;
+        #pragma unroll
+        for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+            if (k >= fa.na || !is_minmax(fa.a[k].kind)) continue;
+            uint64_t *cells = reinterpret_cast<uint64_t *>(lds_raw + fa.a[k].lds_off);
+            const uint64_t id = mm_identity(fa.a[k].dtype, fa.a[k].kind == VH_AGG_MAX);
+            for (uint32_t i = threadIdx.x; i < ncells; i += TB_THREADS) cells[i] = id;
+        }
+        __syncthreads();
+    }
     if (!tp.flags_mode) {
         constexpr int VU = tb_vu<NV>();
         const uint32_t C = s_pre[nw];
@@ -1134,6 +1223,10 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
             if (fa.a[k].kind == VH_AGG_COUNT) {
                 const uint32_t v = reinterpret_cast<const uint32_t *>(lds_raw + fa.a[k].lds_off)[i];
                 if (v) atomicAdd((unsigned long long *)fa.a[k].grid + c0 + i, (unsigned long long)v);
+            } else if (is_minmax(fa.a[k].kind)) {
+                const bool mx = fa.a[k].kind == VH_AGG_MAX;
+                const uint64_t v = reinterpret_cast<const uint64_t *>(lds_raw + fa.a[k].lds_off)[i];
+                if (v != mm_identity(fa.a[k].dtype, mx)) mm_grid(fa.a[k].grid, c0 + i, fa.a[k].dtype, mx, v, true);
             } else if (fa.a[k].vint) {
                 const unsigned long long v = reinterpret_cast<const unsigned long long *>(lds_raw + fa.a[k].lds_off)[i];
                 if (v) atomicAdd(reinterpret_cast<unsigned long long *>(fa.a[k].grid) + c0 + i, v);
@@ -1936,7 +2029,9 @@ static int try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t 
     bpc = std::max(1, std::min(bpc, TA_WG_PER_CU));
     // XCD-resident variant: the fast f64 pass A with <= 1 value slot, one workgroup per CU,
     // P owners per XCD holding TPW tiles each in LDS (resident_lds_bytes + static arrays)
-    const int rmode = allow_res && fast && nv <= 1 && nd_f64 >= 1 && nd_f64 <= 3 && n >= res_min_rows() ? res_mode() : 0;
+    bool res_kinds = true;  // the resident launch applies counts and sums only
+    for (int k = 0; k < fa.na; k++) res_kinds = res_kinds && !is_minmax(fa.a[k].kind);
+    const int rmode = allow_res && res_kinds && fast && nv <= 1 && nd_f64 >= 1 && nd_f64 <= 3 && n >= res_min_rows() ? res_mode() : 0;
     uint32_t rP = 0, rTPW = 0;
     if (rmode && cu_count() % 8 == 0 && cu_count() / 8 <= (int)RES_HDR - 1) {
         rP = (uint32_t)cu_count() / 8;
