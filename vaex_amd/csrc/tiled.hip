@@ -48,6 +48,9 @@ constexpr int TA_THREADS = VH_TA_THREADS;
 #ifndef VH_TA_RPT
 #define VH_TA_RPT 8
 #endif
+#ifndef VH_TA_NT
+#define VH_TA_NT 0
+#endif
 #ifndef VH_TA_DRAIN
 #define VH_TA_DRAIN 1  // fast pass A: the prefetched batch lands before the commit's stores
 #endif
@@ -794,7 +797,15 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan
             const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + threadIdx.x);
             const uint64_t is = i < n - 2 ? i : n - 2;
 #pragma unroll
-            for (int c = 0; c < NC; c++) dst[q][c] = *reinterpret_cast<const double2 *>(col[c] + is);
+            for (int c = 0; c < NC; c++) {
+#if VH_TA_NT  // experiment: non-temporal loads of the once-read columns
+                typedef double v2d __attribute__((ext_vector_type(2)));
+                const v2d t = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(col[c] + is));
+                dst[q][c] = make_double2(t.x, t.y);
+#else
+                dst[q][c] = *reinterpret_cast<const double2 *>(col[c] + is);
+#endif
+            }
         }
     };
     // rank the rows of one batch: cell, take flags, (tile << 16 | cell) key, rank in tile
