@@ -200,27 +200,60 @@ __global__ __launch_bounds__(256) void k_agg_lds(BinPlan p, AggDev a, uint64_t n
 // column (cells < 2^16 by the LDS bound), and each aggregator's pass reads that column.
 constexpr int CELL_U = 4;  // rows per thread per step, loads issued together
 
+// 8 consecutive rows of a column into registers: one 8- to 64-byte load when the column is
+// 8 * sizeof(T) aligned (one byte per lane per instruction made the small-grid passes
+// instruction-bound), else per row; `cnt` < 8 rows (the tail) load per row
+constexpr int RU = 8;
+template <typename T> __device__ __forceinline__ void load_rows8(const T *p, uint64_t j, uint32_t cnt, bool al, T (&out)[RU]) {
+    if (al && cnt == RU) {
+        if constexpr (sizeof(T) == 1) {
+            const uint2 v = *reinterpret_cast<const uint2 *>(p + j);
+            __builtin_memcpy(out, &v, 8);
+        } else {
+            uint4 v[sizeof(T) / 2];
+#pragma unroll
+            for (int k = 0; k < (int)sizeof(T) / 2; k++) v[k] = reinterpret_cast<const uint4 *>(p + j)[k];
+            __builtin_memcpy(out, v, sizeof(out));
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < RU; u++) out[u] = (uint32_t)u < cnt ? p[j + u] : T{};
+    }
+}
+__device__ __forceinline__ bool aligned_rows8(const void *p, int isz) {
+    return (reinterpret_cast<uintptr_t>(p) % (uintptr_t)(8 * isz)) == 0;
+}
+
 template <int KIND_B, typename T>
 __global__ __launch_bounds__(256) void k_cells_dim(BinnerDev b, uint64_t n, uint16_t *cells, int first) {
-    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j0 < n; j0 += step * CELL_U) {
-        T raw[CELL_U];
-        bool m[CELL_U];
-        uint16_t prev[CELL_U];
+    // thread = 8 consecutive rows per step: wide loads of the key, mask and previous cells,
+    // one 16-byte store of the cells
+    const bool al = aligned_rows8(b.data, sizeof(T)) && (!b.mask || aligned_rows8(b.mask, 1)) &&
+                    aligned_rows8(cells, 2);
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x * RU;
+    for (uint64_t j = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) * RU; j < n; j += step) {
+        const uint32_t cnt = (uint32_t)min<uint64_t>(RU, n - j);
+        T raw[RU];
+        uint8_t m[RU];
+        uint16_t prev[RU];
+        load_rows8<T>(reinterpret_cast<const T *>(b.data), j, cnt, al, raw);
+        if (b.mask) load_rows8<uint8_t>(b.mask, j, cnt, al, m);
+        if (!first) load_rows8<uint16_t>(cells, j, cnt, al, prev);
+        uint16_t out[RU];
 #pragma unroll
-        for (int u = 0; u < CELL_U; u++) {
-            const uint64_t j = j0 + (uint64_t)u * step;
-            const bool in = j < n;
-            raw[u] = in ? reinterpret_cast<const T *>(b.data)[j] : T{};
-            m[u] = (in && b.mask) ? b.mask[j] == 1 : false;
-            prev[u] = (in && !first) ? cells[j] : (uint16_t)0;
+        for (int u = 0; u < RU; u++) {
+            const bool mu = b.mask ? m[u] == 1 : false;
+            const uint64_t c = KIND_B == 0 ? scalar_cell<T>(b, raw[u], mu) : ordinal_cell<T>(b, raw[u], mu);
+            out[u] = (uint16_t)((first ? 0 : prev[u]) + c * b.stride);
         }
+        if (al && cnt == RU) {
+            uint4 v;
+            __builtin_memcpy(&v, out, 16);
+            *reinterpret_cast<uint4 *>(cells + j) = v;
+        } else {
 #pragma unroll
-        for (int u = 0; u < CELL_U; u++) {
-            const uint64_t j = j0 + (uint64_t)u * step;
-            if (j >= n) continue;
-            const uint64_t c = KIND_B == 0 ? scalar_cell<T>(b, raw[u], m[u]) : ordinal_cell<T>(b, raw[u], m[u]);
-            cells[j] = (uint16_t)(prev[u] + c * b.stride);
+            for (int u = 0; u < RU; u++)
+                if ((uint32_t)u < cnt) cells[j + u] = out[u];
         }
     }
 }
@@ -241,22 +274,25 @@ __global__ __launch_bounds__(256) void k_agg_lds_c(AggDev a, const uint16_t *cel
         else g[c] = (C)0;
     }
     __syncthreads();
-    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j0 < n; j0 += step * CELL_U) {
-        uint16_t cell[CELL_U];
-        bool keep[CELL_U];
-        T v[CELL_U];
+    // a thread takes RU consecutive rows per step (wide loads; the host's narrow-cell bound is
+    // rows_per_wg(n, grid, block, RU))
+    const bool al = aligned_rows8(cells, 2) && (!a.data || aligned_rows8(a.data, sizeof(T))) &&
+                    (!a.mask || aligned_rows8(a.mask, 1));
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x * RU;
+    for (uint64_t j = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) * RU; j < n; j += step) {
+        const uint32_t cnt = (uint32_t)min<uint64_t>(RU, n - j);
+        uint16_t cell[RU];
+        uint8_t m[RU];
+        T v[RU];
+        load_rows8<uint16_t>(cells, j, cnt, al, cell);
+        if (a.mask) load_rows8<uint8_t>(a.mask, j, cnt, al, m);
+        if (a.data) load_rows8<T>(reinterpret_cast<const T *>(a.data), j, cnt, al, v);
+        else
 #pragma unroll
-        for (int u = 0; u < CELL_U; u++) {
-            const uint64_t j = j0 + (uint64_t)u * step;
-            const bool in = j < n;
-            cell[u] = in ? cells[j] : (uint16_t)0;
-            keep[u] = in && (!a.mask || a.mask[j] == 1);
-            v[u] = (in && a.data) ? reinterpret_cast<const T *>(a.data)[j] : T{};
-        }
+            for (int u = 0; u < RU; u++) v[u] = T{};
 #pragma unroll
-        for (int u = 0; u < CELL_U; u++) {
-            if (!keep[u]) continue;
+        for (int u = 0; u < RU; u++) {
+            if ((uint32_t)u >= cnt || (a.mask && m[u] != 1)) continue;
             const uint32_t c = cell[u];
             if constexpr (KIND == VH_AGG_COUNT) {
                 if (a.data && is_nan_v(a.flip ? bswap_v(v[u]) : v[u])) continue;
@@ -353,21 +389,21 @@ struct SmallAggs {
 };
 
 template <typename T>
-__device__ inline void sf_rows(const AggDev &a, unsigned char *lds, const uint16_t (&cell)[SF_U], uint64_t j0,
-                               uint64_t step, uint64_t n, bool narrow) {
+__device__ inline void sf_rows(const AggDev &a, unsigned char *lds, const uint16_t (&cell)[SF_U], uint64_t j, uint32_t cnt,
+                               bool narrow) {
     using G = typename Upcast<T>::type;
+    static_assert(SF_U == RU, "sf_rows takes one load_rows8 group");
     T v[SF_U];
-    bool keep[SF_U];
+    uint8_t m[SF_U];
+    const bool al = (!a.data || aligned_rows8(a.data, sizeof(T))) && (!a.mask || aligned_rows8(a.mask, 1));
+    if (a.data) load_rows8<T>(reinterpret_cast<const T *>(a.data), j, cnt, al, v);
+    else
+#pragma unroll
+        for (int u = 0; u < SF_U; u++) v[u] = T{};
+    if (a.mask) load_rows8<uint8_t>(a.mask, j, cnt, al, m);
 #pragma unroll
     for (int u = 0; u < SF_U; u++) {
-        const uint64_t j = j0 + (uint64_t)u * step;
-        const bool in = j < n;
-        keep[u] = in && (!a.mask || a.mask[j] == 1);
-        v[u] = (in && a.data) ? reinterpret_cast<const T *>(a.data)[j] : T{};
-    }
-#pragma unroll
-    for (int u = 0; u < SF_U; u++) {
-        if (!keep[u]) continue;
+        if ((uint32_t)u >= cnt || (a.mask && m[u] != 1)) continue;
         const T x = a.flip ? bswap_v(v[u]) : v[u];
         if (a.kind == VH_AGG_COUNT) {
             if (a.data && is_nan_v(x)) continue;
@@ -408,20 +444,20 @@ __global__ __launch_bounds__(256) void k_small_fused(SmallAggs sa, const uint16_
     uint32_t *w = reinterpret_cast<uint32_t *>(lds_raw);
     for (uint32_t i = threadIdx.x; i < lds_words; i += blockDim.x) w[i] = 0;
     __syncthreads();
-    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j0 < n; j0 += step * SF_U) {
+    // a thread takes SF_U consecutive rows per step (wide loads; rows per workgroup stay
+    // within rows_per_wg(n, grid, block, SF_U), the narrow-cell overflow bound)
+    const bool cal = aligned_rows8(cells, 2);
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x * SF_U;
+    for (uint64_t j = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) * SF_U; j < n; j += step) {
+        const uint32_t cnt = (uint32_t)min<uint64_t>(SF_U, n - j);
         uint16_t cell[SF_U];
-#pragma unroll
-        for (int u = 0; u < SF_U; u++) {
-            const uint64_t j = j0 + (uint64_t)u * step;
-            cell[u] = j < n ? cells[j] : (uint16_t)0;
-        }
+        load_rows8<uint16_t>(cells, j, cnt, cal, cell);
         for (int k = 0; k < sa.na; k++) {
             if ((sa.shared >> k) & 1) continue;
             const AggDev &a = sa.a[k];
             unsigned char *lds = lds_raw + sa.lds_off[k];
             const bool nw = (sa.narrow >> k) & 1;
-            VH_DEV_DISPATCH(a.dtype, T, sf_rows<T>(a, lds, cell, j0, step, n, nw); break)
+            VH_DEV_DISPATCH(a.dtype, T, sf_rows<T>(a, lds, cell, j, cnt, nw); break)
         }
     }
     __syncthreads();
@@ -1426,7 +1462,7 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                     const size_t shm32 = (size_t)((L * 4 + 15) & ~uint64_t(15));
                     const bool mx = ad.kind == VH_AGG_MAX;
                     // rows one workgroup adds into its sub-grid (bounds 32-bit partials)
-                    const uint64_t rows_wg = rows_per_wg(len, grd.x, blk.x, CELL_U);
+                    const uint64_t rows_wg = rows_per_wg(len, grd.x, blk.x, RU);
                     const bool narrow_sum = !ad.flip && (((ad.dtype == VH_I8 || ad.dtype == VH_U8) && rows_wg < (1ull << 23)) ||
                                                          ((ad.dtype == VH_I16 || ad.dtype == VH_U16) && rows_wg < (1ull << 15)));
                     switch (ad.kind) {
