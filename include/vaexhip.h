@@ -204,8 +204,10 @@ int vh_hashagg_destroy(vh_hashagg *h);
  * (the caller then falls back to the ordered_set path) */
 int vh_hashagg_update(vh_hashagg *h, const void *keys, const void *const *vals, uint64_t n, int loc);
 int vh_hashagg_finish(vh_hashagg *h, uint64_t *ngroups);
-/* host outputs, ngroups items each: keys as int64, count(*) int64, per value column its sum
- * (8 bytes: double for float columns, int64/uint64 for integers) and non-NaN count int64 */
+/* outputs, ngroups items each: keys as int64, count(*) int64, per value column its sum
+ * (8 bytes: double for float columns, int64/uint64 for integers) and non-NaN count int64;
+ * any output may be host or HBM memory (a caller that decodes combined multi-key keys on the
+ * device keeps them there) */
 int vh_hashagg_read(vh_hashagg *h, int64_t *keys, int64_t *counts, void *const *sums, int64_t *const *nonnull);
 /* ---- multi-GPU (comm.hip): RCCL bound by the library, one process per GPU ----------
  * The reference has no multi-process path; its ExecutorLocal reduces per-thread task
