@@ -198,14 +198,23 @@ def test_groupby_then_agg_takes_the_same_routes(monkeypatch):
 
 
 @pytest.mark.parametrize("n", [1, 2, 1000, 300_001])
-def test_dense_rank_i64(n):
+@pytest.mark.parametrize("keyset", ["signed", "nonneg_47bit", "zeros_and_ones", "nonneg_wide"])
+def test_dense_rank_i64(n, keyset):
     """vh_dense_rank_i64 == np.unique(return_inverse): ranks bit-exact, distinct keys sorted
-    (signed order across negative keys and the int64 extremes)."""
+    (signed order across negative keys and the int64 extremes; non-negative keys take the
+    unsigned sort over only the bits their maximum needs)."""
     import ctypes
     from vaex_amd import _lib
     from vaex_amd.device import DeviceArray
     rng = np.random.default_rng(n)
-    pool = np.concatenate([rng.integers(-2 ** 62, 2 ** 62, 50), [np.iinfo(np.int64).min, np.iinfo(np.int64).max, 0, -1]])
+    if keyset == "signed":
+        pool = np.concatenate([rng.integers(-2 ** 62, 2 ** 62, 50), [np.iinfo(np.int64).min, np.iinfo(np.int64).max, 0, -1]])
+    elif keyset == "nonneg_47bit":
+        pool = np.concatenate([rng.integers(0, 10 ** 14, 200), [0, 10 ** 14 - 1]])
+    elif keyset == "zeros_and_ones":
+        pool = np.array([0, 1])
+    else:
+        pool = np.concatenate([rng.integers(0, 2 ** 62, 50), [np.iinfo(np.int64).max, 0]])
     keys = pool[rng.integers(0, len(pool), n)].astype(np.int64)
     d_keys = DeviceArray.from_numpy(keys)
     rank = DeviceArray.empty(n, np.int32)
