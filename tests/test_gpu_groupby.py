@@ -186,6 +186,47 @@ def test_set_ordinal_grid_through_hash_aggregation(kdtype):
     np.testing.assert_allclose(dfg["s"].to_numpy()[order], s, rtol=1e-6, atol=1e-9)
 
 
+@pytest.mark.parametrize("vdtype", ["float64", "float32", "int32", "int64"])
+def test_set_ordinal_min_max_tile_path(vdtype):
+    """assume_sparse=True with min / max (+ count): the set-ordinal binner's fused LUT probe
+    (k_tile_scatter_ord<SET = true>) feeding the tile path's min / max slots -- exact per-key
+    extrema (NaN skipped, as AggMin/AggMax do), groups in first-appearance order."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(33)
+    n = (1 << 22) + 5
+    keys = rng.integers(-5_000, 200_000, n).astype(np.int32)
+    if vdtype.startswith("float"):
+        v = rng.normal(size=n).astype(vdtype)
+        v[rng.random(n) < 0.01] = np.nan
+    else:
+        info = np.iinfo(vdtype)
+        v = rng.integers(max(info.min, -(1 << 40)), min(info.max, 1 << 40), n).astype(vdtype)
+    df = vaex_amd.from_arrays(key=DeviceArray.from_numpy(keys), v=DeviceArray.from_numpy(v))
+    dfg = df.groupby("key", agg={"lo": vaex_amd.agg.min("v"), "hi": vaex_amd.agg.max("v"),
+                                 "n": vaex_amd.agg.count()}, assume_sparse=True)
+    gk = dfg["key"].to_numpy()
+    first = np.unique(keys, return_index=True)
+    np.testing.assert_array_equal(gk, first[0][np.argsort(first[1])])
+    uk, inv = np.unique(keys, return_inverse=True)
+    wide = v.astype(np.float64) if vdtype.startswith("float") else v.astype(np.int64)
+    if vdtype.startswith("float"):
+        lo = np.full(len(uk), np.inf)
+        hi = np.full(len(uk), -np.inf)
+        np.fmin.at(lo, inv, wide)
+        np.fmax.at(hi, inv, wide)
+    else:
+        lo = np.full(len(uk), np.iinfo(np.int64).max)
+        hi = np.full(len(uk), np.iinfo(np.int64).min)
+        np.minimum.at(lo, inv, wide)
+        np.maximum.at(hi, inv, wide)
+    order = np.argsort(gk, kind="stable")
+    np.testing.assert_array_equal(gk[order], uk)
+    np.testing.assert_array_equal(dfg["lo"].to_numpy()[order].astype(lo.dtype), lo)
+    np.testing.assert_array_equal(dfg["hi"].to_numpy()[order].astype(hi.dtype), hi)
+    np.testing.assert_array_equal(dfg["n"].to_numpy()[order], np.bincount(inv, minlength=len(uk)))
+
+
 def test_large_grid_mixed_aggregators_split_routes():
     """count(*) + sum + min + max on a grid beyond the LDS sub-grid size with > 2^20 rows:
     count / sum take the tile path, min / max the generic one (run_bin splits the mix);
