@@ -364,6 +364,47 @@ def test_tile_path_min_max_large_grid(dtype):
     np.testing.assert_array_equal(np.asarray(mn), _oracle_grid([bx, by], "min", data=w))
 
 
+@pytest.mark.parametrize("dtype", ["float64", "float32", "int32"])
+def test_tile_path_shared_value_slots(dtype):
+    """sum / min / max of one column and the sum of a second on the 1027^2 grid: one tile
+    group carrying two value slots (the three aggregators of the first column share one);
+    equal to the oracle (integer sums exact, float sums to 1e-9)."""
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(43)
+    n = 3_000_000
+    x, y = rng.normal(size=n), rng.normal(size=n)
+    if dtype.startswith("float"):
+        w = rng.normal(size=n).astype(dtype)
+        w[::19] = np.nan
+    else:
+        w = rng.integers(-30000, 30000, n).astype(dtype)
+    w2 = rng.normal(size=n)
+    bx = oracle.Binner("scalar", x, vmin=-4, vmax=4, bins=1024)
+    by = oracle.Binner("scalar", y, vmin=-4, vmax=4, bins=1024)
+    gx, gy = sa().BinnerScalar_float64("x", -4, 4, 1024), sa().BinnerScalar_float64("y", -4, 4, 1024)
+    gx.set_data(DeviceArray.from_numpy(x))
+    gy.set_data(DeviceArray.from_numpy(y))
+    grid = sa().Grid([gx, gy])
+    dw, dw2 = DeviceArray.from_numpy(w), DeviceArray.from_numpy(w2)
+    up = "float64" if dtype.startswith("float") else "int64"
+    s = getattr(sa(), "AggSum_" + dtype)(grid)
+    mn = getattr(sa(), "AggMin_" + dtype)(grid)
+    mx = getattr(sa(), "AggMax_" + dtype)(grid)
+    s2 = sa().AggSum_float64(grid)
+    for a in (s, mn, mx):
+        a.set_data(dw, 0)
+    s2.set_data(dw2, 0)
+    grid.bin([s, mn, mx, s2])
+    np.testing.assert_array_equal(np.asarray(mx), _oracle_grid([bx, by], "max", data=w))
+    np.testing.assert_array_equal(np.asarray(mn), _oracle_grid([bx, by], "min", data=w))
+    ref_s = _oracle_grid([bx, by], "sum", data=w)
+    if up == "int64":
+        np.testing.assert_array_equal(np.asarray(s), ref_s)
+    else:
+        np.testing.assert_allclose(np.asarray(s), ref_s, rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(np.asarray(s2), _oracle_grid([bx, by], "sum", data=w2), rtol=1e-9, atol=1e-9)
+
+
 def test_host_staging_multiple_chunks():
     """Host columns longer than one staging chunk (16 Mi rows)."""
     n = (1 << 24) + 12345

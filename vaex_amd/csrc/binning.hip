@@ -1299,30 +1299,38 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                        // tile-partitioned path with per-dtype loads, in groups of at most two
                        // sums (the values a pass-A row carries); all groups or none (the
                        // eligibility of the first decides, they share the plan)
-                       std::vector<std::vector<int>> groups(1);
-                       int sums = 0;
+                       std::vector<FusedAgg> all(naggs);
                        for (int k = 0; k < naggs; k++) {
-                           const bool slot = aggs[k]->kind != VH_AGG_COUNT;  // sums, min, max carry a value
-                           if ((slot && sums == 2) || groups.back().size() == (size_t)MAX_FUSED_AGGS) {
+                           AggDev ad = agg_dev(aggs[k], st);
+                           FusedAgg &f = all[k];
+                           f = FusedAgg{};
+                           f.kind = ad.kind;
+                           f.data = reinterpret_cast<const double *>(ad.data);
+                           f.mask = nullptr;
+                           f.grid = ad.grid;
+                           f.dtype = ad.dtype;
+                           f.vint = ad.kind == VH_AGG_SUM && ad.dtype != VH_F64 && ad.dtype != VH_F32;
+                       }
+                       // at most two carried value columns per group (sums, min, max of one
+                       // column share one: same_value_slot)
+                       std::vector<std::vector<int>> groups(1);
+                       std::vector<int> slots;
+                       for (int k = 0; k < naggs; k++) {
+                           bool fresh = all[k].kind != VH_AGG_COUNT;
+                           for (int j : slots) fresh = fresh && !same_value_slot(all[j], all[k]);
+                           if ((fresh && slots.size() == 2) || groups.back().size() == (size_t)MAX_FUSED_AGGS) {
                                groups.emplace_back();
-                               sums = 0;
+                               slots.clear();
+                               fresh = all[k].kind != VH_AGG_COUNT;
                            }
-                           if (slot) sums++;
+                           if (fresh) slots.push_back(k);
                            groups.back().push_back(k);
                        }
                        for (size_t gi = 0; gi < groups.size(); gi++) {
                            FusedAggs fa{};
                            fa.na = (int)groups[gi].size();
                            fa.generic_vals = 1;
-                           for (int j = 0; j < fa.na; j++) {
-                               AggDev ad = agg_dev(aggs[groups[gi][j]], st);
-                               fa.a[j].kind = ad.kind;
-                               fa.a[j].data = reinterpret_cast<const double *>(ad.data);
-                               fa.a[j].mask = nullptr;
-                               fa.a[j].grid = ad.grid;
-                               fa.a[j].dtype = ad.dtype;
-                               fa.a[j].vint = ad.kind == VH_AGG_SUM && ad.dtype != VH_F64 && ad.dtype != VH_F32;
-                           }
+                           for (int j = 0; j < fa.na; j++) fa.a[j] = all[groups[gi][j]];
                            if (!try_tiled(plan, fa, len, L, scalar_f64_dims(g), g->ws)) {
                                if (gi == 0) return false;
                                fail(VH_ERR_RUNTIME, "tiled binning: aggregator group not eligible");

@@ -124,6 +124,12 @@ struct FusedAgg {
     int32_t vint;         // the sum accumulates 64-bit integers (integer / bool data), not float64
 };
 
+// two value-carrying aggregators (sum / min / max) read the same column the same way: the tile
+// path carries that column once per row for both
+static inline bool same_value_slot(const FusedAgg &a, const FusedAgg &b) {
+    return a.data && a.data == b.data && a.mask == b.mask && a.dtype == b.dtype && a.vint == b.vint;
+}
+
 struct FusedAggs {
     int32_t na;
     uint32_t lds_words;

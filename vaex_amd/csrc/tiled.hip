@@ -1944,12 +1944,16 @@ static int try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t 
     std::lock_guard<std::mutex> ws_lock(ws.mu);
     TileParams tp{};
     if (const char *dbg = getenv("VH_TILE_DEBUG")) tp.debug = (uint32_t)atoi(dbg);
-    // carried values: one slot per sum aggregator; counts keyed on a matching sum's value
+    // carried values: one slot per distinct value column (sum / min / max of one column share
+    // it: same data, mask, dtype and integer-sum encoding); counts keyed on a matching value
     int nv = 0;
     for (int k = 0; k < fa_in.na; k++) {
         tp.val_slot[k] = -1;
         tp.cnt_slot[k] = CNT_ALWAYS;
-        if (fa_in.a[k].kind != VH_AGG_COUNT) tp.val_slot[k] = nv++;
+        if (fa_in.a[k].kind == VH_AGG_COUNT) continue;
+        for (int j = 0; j < k && tp.val_slot[k] < 0; j++)
+            if (tp.val_slot[j] >= 0 && same_value_slot(fa_in.a[j], fa_in.a[k])) tp.val_slot[k] = tp.val_slot[j];
+        if (tp.val_slot[k] < 0) tp.val_slot[k] = nv++;
     }
     if (nv > 2) return false;
     bool flags_mode = false;
