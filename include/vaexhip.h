@@ -217,7 +217,14 @@ int vh_hashagg_read(vh_hashagg *h, int64_t *keys, int64_t *counts, void *const *
  * to every rank before vh_comm_init (vaex_amd/comm.py does it over its host channel). */
 typedef struct vh_comm vh_comm;
 int vh_comm_unique_id(void *out128);
-int vh_comm_init(const void *id128, int world, int rank, vh_comm **out); /* on the current device */
+int vh_comm_init(const void *id128, int world, int rank, vh_comm **out); /* on the current device;
+  every vh_comm_* call (and vh_hashagg_exchange) runs on that device, from any thread */
+/* `world` loopback ranks in this process on the current GPU, out[0..world): one host
+ * thread per rank calls the same collectives (a rendezvous; the last thread to arrive moves
+ * every rank's bytes with device copies, all-reduce = all-gather + rank-order device fold).
+ * A test backend: the device code around the collectives runs with N ranks' data on one
+ * GPU, where RCCL refuses two ranks on one device.  Destroy each handle. */
+int vh_comm_loopback(int world, vh_comm **out);
 int vh_comm_destroy(vh_comm *comm);
 /* in-place all-reduce of `count` items of `dtype` (host or HBM buffer) with vh_op */
 int vh_comm_allreduce(vh_comm *comm, void *buf, uint64_t count, int dtype, int op, int loc);

@@ -343,3 +343,42 @@ def test_host_comm_primitives():
     np.testing.assert_array_equal(got["mn"], [0, 8])
     assert bool(got["ok"][0])
     np.testing.assert_array_equal(got["ag"], [0, 10, 20])
+
+
+def test_thread_comm_primitives_and_group_merge():
+    """ThreadComm (the object channel of a loopback group): the same primitives and results
+    as HostComm, every rank a thread; combine_groups over it equals the one-rank merge."""
+    import concurrent.futures as cf
+    import sys
+    sys.path.insert(0, ROOT)
+    from vaex_amd.comm import ThreadComm
+    from vaex_amd.distributed import combine_groups, merge_groups
+    world = 4
+    group = ThreadComm.Group(world)
+    rng = np.random.default_rng(1)
+    keys = [np.unique(rng.integers(-50, 50, 30)).astype(np.int64) for _ in range(world)]
+    locs = [(k, np.ones(len(k), np.int64), [k.astype(np.float64) * 0.5], [np.ones(len(k), np.int64)]) for k in keys]
+
+    def rank(r):
+        c = ThreadComm(r, group)
+        a = c.allreduce(np.array([r + 1.5, -r], np.float64), "sum")
+        mn = c.allreduce(np.array([r, 10 - r], np.int64), "min")
+        got = c.alltoall([(r, d) for d in range(world)])
+        ok = all(g == (s, r) for s, g in enumerate(got))
+        g0 = c.gather(r)
+        b = c.bcast("x" if r == 0 else None)
+        merged = combine_groups(locs[r], c)
+        c.barrier()
+        return a, mn, ok, g0, b, merged
+
+    with cf.ThreadPoolExecutor(world) as ex:
+        res = [f.result(timeout=60) for f in [ex.submit(rank, r) for r in range(world)]]
+    want = merge_groups(locs)
+    for r, (a, mn, ok, g0, b, merged) in enumerate(res):
+        np.testing.assert_array_equal(a, [1.5 + 2.5 + 3.5 + 4.5, -6.0])
+        np.testing.assert_array_equal(mn, [0, 7])
+        assert ok and b == "x"
+        assert g0 == (list(range(world)) if r == 0 else None)
+        np.testing.assert_array_equal(merged[0], want[0])
+        np.testing.assert_array_equal(merged[1], want[1])
+        np.testing.assert_array_equal(merged[2][0], want[2][0])

@@ -93,6 +93,7 @@ SIGNATURES = {
     "vh_decode_keys": (_i32, [_u64, _vp, _vp, _i32, _p(_i64), _p(_i64), _p(_i64), _p(_i32), _p(_vp)]),
     "vh_comm_unique_id": (_i32, [_vp]),
     "vh_comm_init": (_i32, [_vp, _i32, _i32, _p(_vp)]),
+    "vh_comm_loopback": (_i32, [_i32, _p(_vp)]),
     "vh_comm_destroy": (_i32, [_vp]),
     "vh_comm_allreduce": (_i32, [_vp, _vp, _u64, _i32, _i32, _i32]),
     "vh_comm_allgather": (_i32, [_vp, _vp, _vp, _u64, _i32]),

@@ -10,6 +10,9 @@ One process per GPU.  Two communicators with the same interface:
   unique id to the other ranks before ``vh_comm_init``, and it is the CPU fake the
   multi-process tests run the SAME exchange code on (no GPU needed); several ranks
   sharing one GPU (RCCL refuses two ranks on one device) use it too.
+* :class:`LoopbackComm` -- N virtual ranks in one process on one GPU (threads), the
+  library's loopback communicator (``vh_comm_loopback``): the device-side multi-rank code
+  of :class:`RcclComm` runs with N ranks' data where only one GPU exists (tests).
 
 Rendezvous: ``RANK`` / ``WORLD_SIZE`` / ``MASTER_ADDR`` from the environment (what
 ``torch.distributed.run`` exports); the host channel listens on ``VAEX_AMD_COMM_PORT``, or
@@ -258,27 +261,73 @@ class HostComm:
         self._peers, self._sock = {}, None
 
 
-class RcclComm:
-    """RCCL through libvaexhip (``vh_comm_*``): device collectives on the library stream.
-    Object exchange (key arrays, flags) rides the host channel used for the rendezvous."""
+class ThreadComm:
+    """Host collectives among the threads of one process (the object channel of a
+    loopback group, :func:`loopback_group`): same interface and results as
+    :class:`HostComm`, every rank a thread."""
+
+    device = False
+    backend = "threads"
+
+    class Group:
+        def __init__(self, world, timeout=120.0):
+            import threading
+            self.world = world
+            self.barrier = threading.Barrier(world, timeout=timeout)
+            self.slots = [None] * world
+
+    def __init__(self, rank, group):
+        self.rank, self.world = int(rank), group.world
+        self._g = group
+
+    def _exchange(self, obj):
+        g = self._g
+        g.slots[self.rank] = obj
+        g.barrier.wait()
+        got = list(g.slots)
+        g.barrier.wait()  # slots are reused by the next call
+        return got
+
+    def gather(self, obj):
+        got = self._exchange(obj)
+        return got if self.rank == 0 else None
+
+    def bcast(self, obj=None):
+        return self._exchange(obj if self.rank == 0 else None)[0]
+
+    def allgather(self, obj):
+        return self._exchange(obj)
+
+    def alltoall(self, objs):
+        if len(objs) != self.world:
+            raise ValueError("alltoall needs one item per rank")
+        got = self._exchange(list(objs))
+        return [got[s][self.rank] for s in range(self.world)]
+
+    def allreduce(self, arr, op="sum"):
+        return reduce_arrays(self.allgather(np.asarray(arr)), op)
+
+    def barrier(self):
+        self._exchange(None)
+
+    def close(self):
+        pass
+
+
+class DeviceComm:
+    """A libvaexhip communicator (``vh_comm_*``): device collectives on the library stream
+    -- in-place grid all-reduce, the groupby partition exchange.  Object exchange (key
+    arrays, flags) rides the host channel ``host``."""
 
     device = True
-    backend = "rccl"
+    backend = "device"
 
-    def __init__(self, host):
-        import ctypes
+    def __init__(self, host, handle):
         from . import _lib
         self._lib = _lib
         self.host = host
         self.rank, self.world = host.rank, host.world
-        uid = ctypes.create_string_buffer(128)
-        if self.rank == 0:
-            _lib.call("vh_comm_unique_id", uid)
-        raw = host.bcast(uid.raw if self.rank == 0 else None)
-        ctypes.memmove(uid, raw, 128)
-        h = ctypes.c_void_p()
-        _lib.call("vh_comm_init", uid, self.world, self.rank, ctypes.byref(h))
-        self._h = h
+        self._h = handle
 
     @property
     def handle(self):
@@ -320,6 +369,59 @@ class RcclComm:
         self.host.close()
 
 
+class RcclComm(DeviceComm):
+    """RCCL through libvaexhip: one process per GPU, rank 0's unique id sent to the other
+    ranks over the host channel, then ``vh_comm_init`` on this process's GPU."""
+
+    backend = "rccl"
+
+    def __init__(self, host):
+        import ctypes
+        from . import _lib
+        uid = ctypes.create_string_buffer(128)
+        if host.rank == 0:
+            _lib.call("vh_comm_unique_id", uid)
+        raw = host.bcast(uid.raw if host.rank == 0 else None)
+        ctypes.memmove(uid, raw, 128)
+        h = ctypes.c_void_p()
+        _lib.call("vh_comm_init", uid, host.world, host.rank, ctypes.byref(h))
+        super().__init__(host, h)
+
+
+class LoopbackComm(DeviceComm):
+    """One virtual rank of a loopback group (``vh_comm_loopback``): N ranks in one process on
+    one GPU, one thread per rank.  The collectives are device copies and rank-order device
+    folds behind the same C-ABI as RCCL's, so the multi-rank device code (grid all-reduce
+    folds, AggFirst across ranks, the groupby all-to-all and its fold) runs with N ranks'
+    data on a one-GPU box."""
+
+    backend = "loopback"
+
+
+def loopback_group(world):
+    """``world`` :class:`LoopbackComm` ranks of this process (use each from its own thread)."""
+    import ctypes
+    from . import _lib
+    hs = (ctypes.c_void_p * world)()
+    _lib.call("vh_comm_loopback", int(world), hs)
+    group = ThreadComm.Group(world)
+    return [LoopbackComm(ThreadComm(r, group), ctypes.c_void_p(hs[r])) for r in range(world)]
+
+
+def select_device(local_rank=None):
+    """Make GPU ``LOCAL_RANK`` (mod the device count) this process's device -- for every
+    thread of the process (vh_set_device): one process per GPU under torch.distributed.run.
+    Returns the device, or None without a GPU."""
+    from . import _lib
+    n = _lib.device_count()
+    if n < 1:
+        return None
+    lr = _env_int("LOCAL_RANK", 0) if local_rank is None else int(local_rank)
+    dev = lr % n
+    _lib.call("vh_set_device", dev)
+    return dev
+
+
 _default = None
 
 
@@ -337,10 +439,13 @@ def init(backend="auto", rank=None, world=None, addr=None, port=None, timeout=60
     addr = addr or os.environ.get("MASTER_ADDR", "127.0.0.1")
     if port is None:
         port = _env_int("VAEX_AMD_COMM_PORT", 0) or (_env_int("MASTER_PORT", 29510) + 1)
+    if backend in ("auto", "rccl"):
+        # the GPU is chosen before any other GPU call: every rank on device 0 would make
+        # RCCL refuse the duplicate device
+        dev = select_device()
+        if backend == "auto":
+            backend = "rccl" if dev is not None else "host"
     host = HostComm(rank, world, addr, port, timeout)
-    if backend == "auto":
-        from . import _lib
-        backend = "rccl" if _lib.device_count() > 0 else "host"
     _default = RcclComm(host) if backend == "rccl" else host
     return _default
 

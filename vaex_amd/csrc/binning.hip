@@ -1281,6 +1281,10 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
         BinPlan plan{};
         plan.nb = (int)g->binners.size();
         for (int d = 0; d < plan.nb; d++) plan.b[d] = binner_dev(g->binners[d], g->strides[d], st);
+        // aggregators a tile group already binned in this chunk (a later group the tile path
+        // refuses -- more carried values or bytes per cell than the first -- falls back to
+        // the generic path below for its own aggregators only)
+        std::vector<char> tdone(naggs, 0);
         if (all_fusable) {
             FusedAggs fa{};
             fa.na = naggs;
@@ -1295,10 +1299,10 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
             }
             launch_fused(plan, fa, len, L, scalar_f64_dims(g), g->ws);
         } else if (tile_generic && [&] {
-                       // count / sum of any native dtype over a grid too large for LDS: the
-                       // tile-partitioned path with per-dtype loads, in groups of at most two
-                       // sums (the values a pass-A row carries); all groups or none (the
-                       // eligibility of the first decides, they share the plan)
+                       // count / sum / min / max of any native dtype over a grid too large for
+                       // LDS: the tile-partitioned path with per-dtype loads, in groups of at
+                       // most two carried value columns; a group the path refuses leaves its
+                       // aggregators (and the later groups') to the generic path
                        std::vector<FusedAgg> all(naggs);
                        for (int k = 0; k < naggs; k++) {
                            AggDev ad = agg_dev(aggs[k], st);
@@ -1331,10 +1335,8 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                            fa.na = (int)groups[gi].size();
                            fa.generic_vals = 1;
                            for (int j = 0; j < fa.na; j++) fa.a[j] = all[groups[gi][j]];
-                           if (!try_tiled(plan, fa, len, L, scalar_f64_dims(g), g->ws)) {
-                               if (gi == 0) return false;
-                               fail(VH_ERR_RUNTIME, "tiled binning: aggregator group not eligible");
-                           }
+                           if (!try_tiled(plan, fa, len, L, scalar_f64_dims(g), g->ws)) return false;
+                           for (int k : groups[gi]) tdone[k] = 1;
                        }
                        return true;
                    }()) {
@@ -1352,7 +1354,7 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
             uint16_t *cells = nullptr;
             uint64_t *idx = nullptr;
             for (int k = 0; k < naggs && !idx; k++) {
-                if (lds_ok(ads[k].kind)) continue;
+                if (tdone[k] || lds_ok(ads[k].kind)) continue;
                 g->ws.idx.ensure(len * 8);
                 idx = g->ws.idx.as<uint64_t>();
                 TimedScope ts("bin_indices");
@@ -1396,11 +1398,11 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
             };
             // count / sum aggregators share one pass over the cells, as many per launch as
             // their sub-grids fit the LDS budget
-            std::vector<char> done(naggs, 0);
+            std::vector<char> done(tdone);
             if (cells_ok && len) {
                 std::vector<int> pend;
                 for (int k = 0; k < naggs; k++)
-                    if (ads[k].kind == VH_AGG_COUNT || ads[k].kind == VH_AGG_SUM) pend.push_back(k);
+                    if (!done[k] && (ads[k].kind == VH_AGG_COUNT || ads[k].kind == VH_AGG_SUM)) pend.push_back(k);
                 size_t i = 0;
                 while (i < pend.size()) {
                     SmallAggs sa{};

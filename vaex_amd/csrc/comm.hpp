@@ -11,6 +11,7 @@ struct vh_comm;
 namespace vh {
 int comm_rank(const vh_comm *c);
 int comm_world(const vh_comm *c);
+int comm_device(const vh_comm *c);  // the GPU the communicator was created on
 std::mutex &comm_mutex(vh_comm *c);
 void comm_allreduce_dev(vh_comm *c, void *buf, uint64_t count, int dtype, int op);
 void comm_allgather_dev(vh_comm *c, const void *send, void *recv, uint64_t bytes);

@@ -180,6 +180,15 @@ bool host_registered(const void *p, uint64_t bytes);  // inside a vh_host_regist
 int current_device();
 int cu_count();
 
+// `dev` is this thread's current device for the scope (restored after)
+struct DeviceScope {
+    int prev, dev;
+    explicit DeviceScope(int dev);
+    ~DeviceScope();
+    DeviceScope(const DeviceScope &) = delete;
+    DeviceScope &operator=(const DeviceScope &) = delete;
+};
+
 // grid size for a grid-stride kernel over n items
 inline unsigned blocks_for(uint64_t n, unsigned threads, unsigned per_cu = 8) {
     uint64_t b = (n + threads - 1) / threads;

@@ -2397,6 +2397,7 @@ extern "C" {
 int vh_hashagg_exchange(vh_hashagg *h, vh_comm *c, int gather) {
     VH_API_BEGIN
     if (!h->finished) fail(VH_ERR_RUNTIME, "hashagg: exchange before finish");
+    DeviceScope ds(comm_device(c));
     std::lock_guard<std::mutex> lk(comm_mutex(c));
     hipStream_t st = stream();
     const int world = comm_world(c), me = comm_rank(c);

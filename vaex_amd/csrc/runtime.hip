@@ -27,10 +27,28 @@ static std::mutex g_mu;
 static std::map<int, hipStream_t> g_streams;
 static std::map<int, int> g_cus;
 
+// The process's GPU (one process per GPU): vh_set_device records it, and every other thread
+// adopts it on its first library call -- HIP's current device is per thread, so a task run
+// from a worker thread (the executor allows that) would otherwise land on device 0.
+static int g_default_device = -1;
+static thread_local bool t_device_adopted = false;
+
 int current_device() {
+    if (!t_device_adopted) {
+        t_device_adopted = true;
+        const int want = __atomic_load_n(&g_default_device, __ATOMIC_ACQUIRE);
+        if (want >= 0) VH_HIP(hipSetDevice(want));
+    }
     int d = 0;
     VH_HIP(hipGetDevice(&d));
     return d;
+}
+
+DeviceScope::DeviceScope(int dev) : prev(current_device()), dev(dev) {
+    if (prev != dev) VH_HIP(hipSetDevice(dev));
+}
+DeviceScope::~DeviceScope() {
+    if (prev != dev) (void)hipSetDevice(prev);
 }
 
 // ---- device block cache (common.hpp) ---------------------------------------------------
@@ -406,6 +424,8 @@ int vh_device_count(int *count) {
 int vh_set_device(int device) {
     VH_API_BEGIN
     VH_HIP(hipSetDevice(device));
+    t_device_adopted = true;
+    __atomic_store_n(&g_default_device, device, __ATOMIC_RELEASE);
     VH_API_END
 }
 
@@ -423,6 +443,7 @@ int vh_synchronize(void) {
 
 int vh_malloc(void **dptr, uint64_t bytes) {
     VH_API_BEGIN
+    (void)current_device();  // this thread on the process's GPU
     hipError_t e = hipMalloc(dptr, bytes ? bytes : 1);
     if (e != hipSuccess) {
         (void)hipGetLastError();
