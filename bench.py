@@ -5,8 +5,10 @@ One step = one query pass over resident synthetic columns:
 binners (one merged pass, as ExecutorLocal merges them), 1e9 float64 rows per GPU
 (weak scaling), through the superagg surface -> libvaexhip C-ABI -> HIP kernels; with
 N > 1 GPUs the rows are sharded by rank and the dense grids are all-reduced over RCCL.
-Fresh aggregator grids are created in every step (as a query does); the grid read-back to
-the host is not in the timed region.
+Fresh aggregator grids are created in every step (as a query does), and every step reads
+both grids back to host numpy arrays (get_result, cpu.py:592-605) inside the timed region.
+The roofline's kernel durations come from HIP events in a second, instrumented run of the
+same steps (no timers inside the timed region).
 
 Prints ONE JSON line (rank 0) with the roofline of the binning pipeline (HIP events on the
 library stream) and the CPU baseline (the oracle's C restatement with the reference
@@ -40,6 +42,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
     p.add_argument("--no-groupby", action="store_true")
     p.add_argument("--no-count-only", action="store_true")
+    p.add_argument("--no-layouts", action="store_true", help="skip the sorted-layout legs")
     p.add_argument("--host-rows", type=float, default=2e8,
                    help="rows of the PCIe-inclusive measurement (host numpy columns); 0 = skip")
     p.add_argument("--groupby-rows", type=float, default=1e9)
@@ -162,6 +165,7 @@ def main():
         "traffic": None,
         "algorithmic_bytes_per_launch": algo_bytes,
         "kernel_ms": round(dom_ms, 4) if dom_ms else None,
+        "kernel_timing": "HIP events on the library stream, a second instrumented run of the same steps",
         "per_kernel_ms": {k: round(ms / c, 4) for k, (c, ms) in kernel_ms.items()},
         # whole binning pipeline (sample + pass A + pass B) against the same 24 B/row
         "pipeline_ms": round(pipeline_ms, 4),
@@ -174,8 +178,8 @@ def main():
 
     # full-size properties of the last timed step's result (every run): every row lands in
     # one cell (the synthetic columns hold no NaN, NaN rows would sit in cell 0), and the
-    # grid's sum equals an independent reduction of w (a 0-d sum: the small-grid LDS path,
-    # not the tile path) within 1e-6 relative
+    # grid's sum equals an independent reduction of w (a 0-d sum: the reduction kernel, not
+    # the tile path) within 1e-6 relative
     count, total = res
     local_w = float(vaex_amd.from_arrays(w=w).sum("w"))
     ref_sum = vdist.allreduce_scalar(local_w, "sum") if dist is not None else local_w
@@ -187,8 +191,14 @@ def main():
     check["ok"] = bool(check["count_equal"] and check["sum_rel_err"] is not None and check["sum_rel_err"] < 1e-6)
 
     extra = {}
+    if rank == 0 and world == 1:
+        extra["zero_d"] = bench_zero_d(w, n, args)
+    if rank == 0 and world == 1 and not args.no_layouts:
+        extra["c2_sorted_y"] = bench_c2_layout(x, w, n, bins, args)
     if rank == 0 and world == 1 and not args.no_groupby:
         extra["groupby"] = bench_groupby(int(args.groupby_rows), args)
+        if not args.no_layouts:
+            extra["groupby_sorted_keys"] = bench_groupby(int(args.groupby_rows), args, layout="sorted")
     if rank == 0 and world == 1 and not args.no_count_only:
         extra["count_only"] = bench_count_only(x, y, n, bins, args)
     if rank == 0 and world == 1 and args.host_rows > 0:
@@ -295,6 +305,39 @@ def bench_count_only(x, y, n, bins, args):
             "kernel_frac": round(16 * n / (per[dom] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if dom else None,
             "pipeline_GBps": round(16 * n / (pipe * 1e-3) / 1e9, 1) if pipe else None,
             "pipeline_frac": round(16 * n / (pipe * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if pipe else None}
+
+
+def bench_zero_d(w, n, args):
+    """0-d aggregations (no binby; agg.hpp:76-105 with no binners): df.sum('w'),
+    df.mean('w') (sum + non-NaN count of w in one pass) and df.count() on the resident w
+    column, end to end (median of steps), with the reduction kernel's HIP-event time against
+    8 B/row (count(*) reads nothing: the count is the row count)."""
+    import vaex_amd
+    from vaex_amd import _lib
+    df = vaex_amd.from_arrays(w=w)
+    out = {"rows": n, "algorithmic_bytes_per_row": 8}
+    for name, f in (("sum", lambda: df.sum("w")), ("mean", lambda: df.mean("w")), ("count", lambda: df.count())):
+        f()
+        _lib.synchronize()
+        ts = []
+        _lib.timing_reset()
+        _lib.timing_enable(True)
+        for _ in range(max(3, args.steps)):
+            t0 = time.perf_counter()
+            r = f()
+            ts.append(time.perf_counter() - t0)
+        _lib.synchronize()
+        _lib.timing_enable(False)
+        c, ms = _lib.timing_read("bin_reduce0")
+        k_ms = ms / c if c else None
+        t = float(np.median(ts))
+        out[name] = {"ms": round(t * 1e3, 4), "rows_per_s": n / t, "value": float(r),
+                     "kernel_ms": round(k_ms, 4) if k_ms else None}
+        if name != "count" and k_ms:
+            out[name]["kernel_GBps"] = round(8 * n / (k_ms * 1e-3) / 1e9, 1)
+            out[name]["kernel_frac"] = round(8 * n / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+    out["count_equal"] = int(out["count"]["value"]) == n
+    return out
 
 
 def bench_host_columns(x, y, w, m, bins):
@@ -445,7 +488,42 @@ def bench_c4(rows, bins, repeats=2):
     return out
 
 
-def bench_groupby(n, args):
+def bench_c2_layout(x, w, n, bins, args):
+    """Row-order robustness: the headline C2 query (count + sum(w), 1027^2 grid) with y sorted
+    (ascending normal quantiles, x random), timed like the headline step, and the tile path's
+    overflow rows (pass-A rows that missed their region; global atomics)."""
+    from vaex_amd import _lib, superagg
+    from vaex_amd.device import DeviceArray
+    ys = DeviceArray.random(n, "sorted_normal", a=0.0, b=1.0)
+
+    def step():
+        bx = superagg.BinnerScalar_float64("x", -4.0, 4.0, bins)
+        by = superagg.BinnerScalar_float64("y", -4.0, 4.0, bins)
+        bx.set_data(x)
+        by.set_data(ys)
+        grid = superagg.Grid([bx, by])
+        count = superagg.AggCount_int64(grid)
+        total = superagg.AggSum_float64(grid)
+        total.set_data(w, 0)
+        grid.bin([count, total])
+        return np.asarray(count), np.asarray(total)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    _lib.synchronize()
+    _lib.stat_read("tile_overflow_rows", reset=True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        c, _s = step()
+    _lib.synchronize()
+    t = (time.perf_counter() - t0) / args.steps
+    over = _lib.stat_read("tile_overflow_rows", reset=True) / max(1, args.steps)
+    del ys
+    return {"layout": "y sorted (ascending normal quantiles), x random", "rows": n, "ms_per_step": t * 1e3,
+            "rows_per_s": n / t, "overflow_rows_per_step": over, "count_equal": int(c.sum()) == n}
+
+
+def bench_groupby(n, args, layout="random"):
     """C3: groupby(int32 key, 1e6 distinct).agg({v: [sum, count]}) on resident columns, end to
     end (every pass, result read-back into host numpy columns), best of 3:
       auto  -- what DataFrame.groupby picks for this dense key range: one min/max pass, then
@@ -459,10 +537,13 @@ def bench_groupby(n, args):
     from vaex_amd.device import DeviceArray
     from vaex_amd.hashagg import HashAgg
     import vaex_amd
-    keys = DeviceArray.random(n, "randint", seed=5, a=5, b=5 + 1_000_000, dtype="int32")
+    if layout == "sorted":  # every key's rows consecutive, keys ascending
+        keys = DeviceArray.random(n, "sorted_int", a=5, b=5 + 1_000_000, dtype="int32")
+    else:
+        keys = DeviceArray.random(n, "randint", seed=5, a=5, b=5 + 1_000_000, dtype="int32")
     v = DeviceArray.random(n, "normal", seed=6)
     df = vaex_amd.from_arrays(key=keys, v=v)
-    out = {"rows": n, "algorithmic_bytes_per_row": 12}
+    out = {"rows": n, "algorithmic_bytes_per_row": 12, "layout": layout}
     names = ["minmax", "tile_sample", "tile_scatter", "tile_scatter_ord", "tile_scatter_set", "tile_reduce", "ha_sample",
              "ha_scatter", "ha_scatter_f64", "ha_reduce", "ha_finish", "set_sample", "set_insert", "set_reduce", "set_rank",
              "bin_fused_global"]
@@ -488,6 +569,8 @@ def bench_groupby(n, args):
         if os.environ.get("BENCH_PROFILE_GROUPBY"):
             import cProfile
             prof = cProfile.Profile()
+        for name in ("tile_overflow_rows", "hashagg_overflow_rows", "set_overflow_rows"):
+            _lib.stat_read(name, reset=True)
         for _ in range(max(1, min(3, args.steps))):
             _lib.timing_reset()
             _lib.timing_enable(True)
@@ -524,8 +607,10 @@ def bench_groupby(n, args):
                                                 and np.array_equal(gc[order], ref_groups[1]))
         check["ok"] = check["count_equal"] and check["sum_rel_err"] < 1e-6 and check.get("same_groups_as_auto", True)
         groups = len(gk)
+        over = {name: _lib.stat_read(name, reset=True) for name in ("tile_overflow_rows", "hashagg_overflow_rows",
+                                                                     "set_overflow_rows")}
         out[mode] = {"groups": groups, "check": check, "seconds": t, "rows_per_s": n / t, "algorithmic_GBps": 12 * n / t / 1e9,
-                     "kernel_ms_last": per}
+                     "kernel_ms_last": per, "overflow_rows": {k: v for k, v in over.items() if v}}
     del keys, v, df
     return out
 

@@ -89,13 +89,19 @@ int vh_memset(void *dptr, int value, uint64_t bytes);
 /* synthetic columns generated in HBM (bench/test data; counter-based
  * splitmix64, so any sub-range can be regenerated on the host):
  * dist 0 = uniform [a, b) f64, 1 = normal(mean a, sd b) f64,
- *      2 = uniform integer [a, b) stored as `dtype` (I32/I64). */
+ *      2 = uniform integer [a, b) stored as `dtype` (I32/I64),
+ *      3 = sorted: a + b * normal quantile of (i + 0.5) / n (f64, ascending),
+ *      4 = sorted integers [a, b) in equal consecutive runs (I32/I64). */
 int vh_fill_random(void *dptr, uint64_t n, int dtype, int dist, uint64_t seed, double a, double b);
 /* kernel timing with hipEvents on the library stream (bench roofline) */
 int vh_timing_enable(int on);
 int vh_timing_reset(void);
 int vh_timing_read(const char *kernel, uint64_t *launches, double *total_ms);
 int vh_stream(void **stream);
+/* engine statistics since the last reset (this device): "tile_overflow_rows" (tile path rows
+ * that missed their pass-A region and took global atomics), "hashagg_overflow_rows",
+ * "set_overflow_rows" (the groupby / ordered_set partition overflow paths) */
+int vh_stat_read(const char *name, uint64_t *value, int reset);
 
 /* ---- Binners: superagg_binners.cpp ------------------------------------- */
 /* BinnerScalar_<dtype>[_non_native](expression, vmin, vmax, bins)

@@ -1,4 +1,6 @@
 #!/bin/bash
+# the experiment switches exist only in the ablation build (make -C vaex_amd/csrc ablation)
+export VAEX_AMD_LIB="${GRAFT_REPO_ROOT:-$(pwd)}/vaex_amd/libvaexhip_ablation.so"
 # pass A of the C2 tile path with parts switched off (VH_TILE_DEBUG bits, tiled.hip):
 # 0 full; 128 no region stores; 32 no commit; 96 no commit + no ranking; 16 no pass-B flush
 cd "$GRAFT_REPO_ROOT" || exit 1

@@ -1,4 +1,6 @@
 #!/bin/bash
+# the experiment switches exist only in the ablation build (make -C vaex_amd/csrc ablation)
+export VAEX_AMD_LIB="${GRAFT_REPO_ROOT:-$(pwd)}/vaex_amd/libvaexhip_ablation.so"
 # Pass-A time breakdown: the C2 bench under VH_TILE_DEBUG switches / experiment builds
 # (results are wrong by design).  usage: RUNS="lib:dbg lib:dbg ..." scripts/exp_debug.sh
 cd "$GRAFT_REPO_ROOT" || exit 1

@@ -4,7 +4,10 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+# the switches exist only in the ablation build (make -C vaex_amd/csrc ablation)
+os.environ.setdefault("VAEX_AMD_LIB", os.path.join(ROOT, "vaex_amd", "libvaexhip_ablation.so"))
 from vaex_amd import _lib, superagg  # noqa: E402
 from vaex_amd.device import DeviceArray  # noqa: E402
 

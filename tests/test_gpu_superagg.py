@@ -300,20 +300,36 @@ def test_tiled_path_large_grid(dist, n, with_sum):
         np.testing.assert_allclose(np.asarray(aggs[1]), _oracle_grid([bx, by], "sum", data=w), rtol=1e-6, atol=1e-12)
 
 
-@pytest.mark.parametrize("mode", ["0", "1", "2"])
+def _layout(x, y, w, layout):
+    """The same rows in another order: sorted by y (the slow binby dimension), sorted by x,
+    or clustered (runs of 50 000 rows from random places)."""
+    if layout == "shuffled":
+        return x, y, w
+    if layout == "sorted_y":
+        o = np.argsort(y, kind="stable")
+    elif layout == "sorted_x":
+        o = np.argsort(x, kind="stable")
+    else:  # runs of 50 000 rows of similar y, the runs in random order
+        o = np.argsort(y, kind="stable")
+        chunks = [o[b:b + 50_000] for b in range(0, len(x), 50_000)]
+        np.random.default_rng(5).shuffle(chunks)
+        o = np.concatenate(chunks)
+    return x[o], y[o], w[o]
+
+
+@pytest.mark.parametrize("layout", ["shuffled", "sorted_y", "sorted_x", "clustered"])
 @pytest.mark.parametrize("with_sum", [False, True])
-def test_xcd_resident_path_matches_oracle(monkeypatch, mode, with_sum):
-    """The opt-in XCD-resident tile launch (VH_RESIDENT=1: L2 hand-off, 2: write-through)
-    gives the oracle's counts bit-exactly and its sums within 1e-6, NaN rows included; a
-    mean's NaN-keyed count rides on the summed value."""
+def test_tile_path_row_layouts_match_oracle(layout, with_sum):
+    """Pass-A workgroups take batches w, w + W, ... so sorted or clustered rows spread over
+    every workgroup like shuffled ones: bit-exact counts, sums within 1e-6, for every row
+    order of the C2-shape query (1027^2 grid, NaN rows included)."""
     from vaex_amd.device import DeviceArray
-    monkeypatch.setenv("VH_RESIDENT", mode)
-    monkeypatch.setenv("VH_RES_MIN_ROWS", "1048576")
-    n = 3_000_000
+    n = 6_000_000
     rng = np.random.default_rng(29)
     x, y, w = rng.normal(size=n), rng.normal(size=n), rng.random(n)
     x[::997] = np.nan
     w[::13] = np.nan
+    x, y, w = _layout(x, y, w, layout)
     bx = oracle.Binner("scalar", x, vmin=-4, vmax=4, bins=1024)
     by = oracle.Binner("scalar", y, vmin=-4, vmax=4, bins=1024)
     gx, gy = sa().BinnerScalar_float64("x", -4, 4, 1024), sa().BinnerScalar_float64("y", -4, 4, 1024)
@@ -333,6 +349,41 @@ def test_xcd_resident_path_matches_oracle(monkeypatch, mode, with_sum):
     if with_sum:
         np.testing.assert_allclose(np.asarray(aggs[1]), _oracle_grid([bx, by], "sum", data=w), rtol=1e-6, atol=1e-12)
         np.testing.assert_array_equal(np.asarray(aggs[2]), _oracle_grid([bx, by], "count", data=w))
+
+
+def test_removed_experiment_switches_change_nothing(monkeypatch):
+    """The product library reads no ablation switch: the old experiment variables (results
+    wrong by design) and the removed XCD-resident switch leave every result unchanged."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    n = 4_000_000
+    rng = np.random.default_rng(3)
+    x, y, w = rng.normal(size=n), rng.normal(size=n), rng.random(n)
+    keys = rng.integers(0, 300_000, n).astype(np.int32) * 13
+    cols = {"x": DeviceArray.from_numpy(x), "y": DeviceArray.from_numpy(y), "w": DeviceArray.from_numpy(w),
+            "k": DeviceArray.from_numpy(keys)}
+
+    def run():
+        df = vaex_amd.from_arrays(**cols)
+        c = np.asarray(df.count(binby=["x", "y"], limits=[[-4, 4], [-4, 4]], shape=1024))
+        s = np.asarray(df.sum("w", binby=["x", "y"], limits=[[-4, 4], [-4, 4]], shape=1024))
+        g = df.groupby("k", agg={"n": "count", "s": vaex_amd.agg.sum("w")}, sort=True)
+        h = df.groupby("k", agg={"n": "count"}, sort=True, assume_sparse=True)
+        return c, s, g["k"].to_numpy(), g["n"].to_numpy(), g["s"].to_numpy(), h["k"].to_numpy(), h["n"].to_numpy()
+
+    ref = run()
+    for var in ("VH_TILE_DEBUG", "VH_HA_DEBUG", "VH_SI_DEBUG"):
+        monkeypatch.setenv(var, "4095")  # every experiment bit
+        got = run()
+        monkeypatch.delenv(var)
+        for a, b in zip(got, ref):
+            if a.dtype.kind == "f":
+                np.testing.assert_allclose(a, b, rtol=1e-9, atol=1e-12, err_msg=var)
+            else:
+                np.testing.assert_array_equal(a, b, err_msg=var)
+    monkeypatch.setenv("VH_RESIDENT", "1")
+    got = run()
+    np.testing.assert_array_equal(got[0], ref[0])
 
 
 @pytest.mark.parametrize("dtype", ["float64", "float32", "int16"])

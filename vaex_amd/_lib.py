@@ -45,6 +45,7 @@ SIGNATURES = {
     "vh_timing_reset": (_i32, []),
     "vh_timing_read": (_i32, [ctypes.c_char_p, _p(_u64), _p(_dbl)]),
     "vh_stream": (_i32, [_p(_vp)]),
+    "vh_stat_read": (_i32, [ctypes.c_char_p, _p(_u64), _i32]),
     "vh_binner_scalar_create": (_i32, [ctypes.c_char_p, _i32, _i32, _dbl, _dbl, _u64, _p(_vp)]),
     "vh_binner_ordinal_create": (_i32, [ctypes.c_char_p, _i32, _i32, _u64, _u64, _p(_vp)]),
     "vh_binner_set_ordinal_create": (_i32, [ctypes.c_char_p, _vp, _u64, _p(_vp)]),
@@ -190,6 +191,13 @@ def device_count():
 
 def synchronize():
     call("vh_synchronize")
+
+
+def stat_read(name, reset=True):
+    """An engine statistic (vh_stat_read), e.g. "tile_overflow_rows"."""
+    v = ctypes.c_uint64()
+    call("vh_stat_read", name.encode(), ctypes.byref(v), int(bool(reset)))
+    return v.value
 
 
 def timing_enable(on=True):

@@ -629,6 +629,174 @@ __global__ __launch_bounds__(256) void k_fused(BinPlan p, FusedAggs fa, uint64_t
     }
 }
 
+
+// ============================================================================
+// device: 0-d aggregation -- no binners (df.count() / df.sum('w') / df.mean('w'); the
+// reference's Grid::bin with a length and no binners, agg.hpp:76-105, puts every row in
+// cell 0), so the grid is a reduction: 16-B loads of each distinct float64 column
+// (R0_U in flight per lane), per-lane accumulators, a wave reduction with cross-lane
+// shuffles, per-workgroup partials, and a one-workgroup finisher that folds the partials in
+// a fixed order (run-to-run identical sums) into the grid cell.
+// ============================================================================
+constexpr int R0_U = 4;
+struct Reduce0 {
+    int32_t na, ncol, nmask, all_rows;  // all_rows: bit k = count(*) of every row (no read)
+    const double2 *col[MAX_FUSED_AGGS];    // distinct float64 data columns (16-B aligned)
+    const uint16_t *mask[MAX_FUSED_AGGS];  // distinct aggregator masks, 1 = keep (2-B aligned)
+    int8_t acol[MAX_FUSED_AGGS], amask[MAX_FUSED_AGGS], akind[MAX_FUSED_AGGS], pad[4];
+    void *grid[MAX_FUSED_AGGS];
+};
+
+__device__ inline double wave_sum_f64(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ inline uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// rows 2v, 2v+1 of every aggregator: x = its column's pair, m = its mask's pair
+template <bool HAS_MASK>
+__device__ inline void r0_rows(const Reduce0 &r, int k, double2 x, uint16_t m, double &s, uint64_t &c) {
+    bool k0 = true, k1 = true;
+    if constexpr (HAS_MASK) {
+        k0 = (m & 0xff) == 1;
+        k1 = (m >> 8) == 1;
+    }
+    if (r.acol[k] >= 0) {
+        k0 = k0 && x.x == x.x;
+        k1 = k1 && x.y == x.y;
+    }
+    c += (uint64_t)k0 + (uint64_t)k1;
+    if (r.akind[k] == VH_AGG_SUM) s += (k0 ? x.x : 0.0) + (k1 ? x.y : 0.0);
+}
+
+template <bool HAS_MASK>
+__global__ __launch_bounds__(256) void k_reduce0(Reduce0 r, uint64_t n, double *psum, uint64_t *pcnt) {
+    double s[MAX_FUSED_AGGS];
+    uint64_t c[MAX_FUSED_AGGS];
+#pragma unroll
+    for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+        s[k] = 0.0;
+        c[k] = 0;
+    }
+    const uint64_t nvec = n / 2, stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t v = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    for (; v + (R0_U - 1) * stride < nvec; v += R0_U * stride) {
+        double2 x[MAX_FUSED_AGGS][R0_U];
+        uint16_t m[MAX_FUSED_AGGS][R0_U];
+#pragma unroll
+        for (int q = 0; q < MAX_FUSED_AGGS; q++) {
+            if (q >= r.ncol) break;
+#pragma unroll
+            for (int u = 0; u < R0_U; u++) x[q][u] = r.col[q][v + u * stride];
+        }
+        if constexpr (HAS_MASK) {
+#pragma unroll
+            for (int q = 0; q < MAX_FUSED_AGGS; q++) {
+                if (q >= r.nmask) break;
+#pragma unroll
+                for (int u = 0; u < R0_U; u++) m[q][u] = r.mask[q][v + u * stride];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+            if (k >= r.na) break;
+#pragma unroll
+            for (int u = 0; u < R0_U; u++) {
+                double2 xv = make_double2(0.0, 0.0);
+                uint16_t mv = 0x0101;
+#pragma unroll
+                for (int q = 0; q < MAX_FUSED_AGGS; q++) {
+                    if (q == r.acol[k]) xv = x[q][u];
+                    if constexpr (HAS_MASK)
+                        if (q == r.amask[k]) mv = m[q][u];
+                }
+                r0_rows<HAS_MASK>(r, k, xv, mv, s[k], c[k]);
+            }
+        }
+    }
+    for (; v < nvec; v += stride) {
+#pragma unroll
+        for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+            if (k >= r.na) break;
+            const double2 xv = r.acol[k] >= 0 ? r.col[r.acol[k]][v] : make_double2(0.0, 0.0);
+            const uint16_t mv = HAS_MASK && r.amask[k] >= 0 ? r.mask[r.amask[k]][v] : (uint16_t)0x0101;
+            r0_rows<HAS_MASK>(r, k, xv, mv, s[k], c[k]);
+        }
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {  // the odd last row
+#pragma unroll
+        for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+            if (k >= r.na) break;
+            bool keep = true;
+            double xv = 0.0;
+            if (HAS_MASK && r.amask[k] >= 0) keep = reinterpret_cast<const uint8_t *>(r.mask[r.amask[k]])[n - 1] == 1;
+            if (r.acol[k] >= 0) {
+                xv = reinterpret_cast<const double *>(r.col[r.acol[k]])[n - 1];
+                keep = keep && xv == xv;
+            }
+            c[k] += keep ? 1 : 0;
+            if (r.akind[k] == VH_AGG_SUM && keep) s[k] += xv;
+        }
+    }
+    __shared__ double ss[4][MAX_FUSED_AGGS];
+    __shared__ uint64_t sc[4][MAX_FUSED_AGGS];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+        if (k >= r.na) break;
+        const double ws = wave_sum_f64(s[k]);
+        const uint64_t wc = wave_sum_u64(c[k]);
+        if (lane == 0) {
+            ss[wave][k] = ws;
+            sc[wave][k] = wc;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)r.na) {
+        const int k = threadIdx.x;
+        psum[(uint64_t)blockIdx.x * MAX_FUSED_AGGS + k] = (ss[0][k] + ss[1][k]) + (ss[2][k] + ss[3][k]);
+        pcnt[(uint64_t)blockIdx.x * MAX_FUSED_AGGS + k] = sc[0][k] + sc[1][k] + sc[2][k] + sc[3][k];
+    }
+}
+
+// fold `nb` workgroup partials in a fixed order and add them to the grid cells
+__global__ __launch_bounds__(256) void k_reduce0_fin(Reduce0 r, const double *psum, const uint64_t *pcnt, unsigned nb,
+                                                      uint64_t n) {
+    __shared__ double ss[4][MAX_FUSED_AGGS];
+    __shared__ uint64_t sc[4][MAX_FUSED_AGGS];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+        if (k >= r.na) break;
+        double s = 0.0;
+        uint64_t c = 0;
+        for (unsigned b = threadIdx.x; b < nb; b += blockDim.x) {
+            s += psum[(uint64_t)b * MAX_FUSED_AGGS + k];
+            c += pcnt[(uint64_t)b * MAX_FUSED_AGGS + k];
+        }
+        s = wave_sum_f64(s);
+        c = wave_sum_u64(c);
+        if (lane == 0) {
+            ss[wave][k] = s;
+            sc[wave][k] = c;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)r.na) {
+        const int k = threadIdx.x;
+        if (r.akind[k] == VH_AGG_COUNT) {
+            const uint64_t c = ((r.all_rows >> k) & 1) ? n : sc[0][k] + sc[1][k] + sc[2][k] + sc[3][k];
+            reinterpret_cast<int64_t *>(r.grid[k])[0] += (int64_t)c;
+        } else {
+            reinterpret_cast<double *>(r.grid[k])[0] += (ss[0][k] + ss[1][k]) + (ss[2][k] + ss[3][k]);
+        }
+    }
+}
 }  // namespace vh
 
 // ============================================================================
@@ -1570,7 +1738,52 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
     VH_HIP(hipStreamSynchronize(stream()));
 }
 
+// 0-d grids (no binners) of count / float64-sum aggregators: a reduction (k_reduce0);
+// false when a column is not aligned for the vector loads (k_fused takes it)
+static bool launch_reduce0(const FusedAggs &fa, uint64_t n, Workspace &ws) {
+    Reduce0 r{};
+    r.na = fa.na;
+    for (int k = 0; k < fa.na; k++) {
+        const FusedAgg &a = fa.a[k];
+        r.akind[k] = (int8_t)a.kind;
+        r.grid[k] = a.grid;
+        r.acol[k] = r.amask[k] = -1;
+        if (a.data) {
+            if (reinterpret_cast<uintptr_t>(a.data) & 15) return false;
+            int q = 0;
+            while (q < r.ncol && r.col[q] != reinterpret_cast<const double2 *>(a.data)) q++;
+            if (q == r.ncol) r.col[r.ncol++] = reinterpret_cast<const double2 *>(a.data);
+            r.acol[k] = (int8_t)q;
+        }
+        if (a.mask) {
+            if (reinterpret_cast<uintptr_t>(a.mask) & 1) return false;
+            int q = 0;
+            while (q < r.nmask && r.mask[q] != reinterpret_cast<const uint16_t *>(a.mask)) q++;
+            if (q == r.nmask) r.mask[r.nmask++] = reinterpret_cast<const uint16_t *>(a.mask);
+            r.amask[k] = (int8_t)q;
+        }
+        if (a.kind == VH_AGG_COUNT && !a.data && !a.mask) r.all_rows |= 1 << k;
+    }
+    const bool reads = r.ncol > 0 || r.nmask > 0;
+    const unsigned nb = reads ? blocks_for(std::max<uint64_t>(n / 2, 1), 256, 8) : 0;
+    ws.idx.ensure(std::max<uint64_t>((uint64_t)nb * MAX_FUSED_AGGS * 16, 16));
+    double *psum = ws.idx.as<double>();
+    uint64_t *pcnt = reinterpret_cast<uint64_t *>(psum + (uint64_t)nb * MAX_FUSED_AGGS);
+    TimedScope ts("bin_reduce0");
+    if (nb) {
+        if (r.nmask)
+            hipLaunchKernelGGL(k_reduce0<true>, dim3(nb), dim3(256), 0, stream(), r, n, psum, pcnt);
+        else
+            hipLaunchKernelGGL(k_reduce0<false>, dim3(nb), dim3(256), 0, stream(), r, n, psum, pcnt);
+        VH_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_reduce0_fin, dim3(1), dim3(256), 0, stream(), r, psum, pcnt, nb, n);
+    VH_HIP(hipGetLastError());
+    return true;
+}
+
 void launch_fused(const BinPlan &plan, FusedAggs &fa, uint64_t n, uint64_t cells, int nd_f64, Workspace &ws) {
+    if (plan.nb == 0 && cells == 1 && launch_reduce0(fa, n, ws)) return;
     // LDS-privatised sub-grids when every aggregator's grid fits (u32 counts, f64 sums)
     uint64_t off = 0;
     for (int k = 0; k < fa.na; k++) {

@@ -15,6 +15,16 @@
 
 namespace vh {
 
+// Ablation switches (VH_TILE_DEBUG / VH_HA_DEBUG / VH_SI_DEBUG: timing breakdowns whose
+// results are wrong by design) exist only in the `make ablation` build
+// (libvaexhip_ablation.so, -DVH_ABLATION) that scripts/ load; in the product library DBG(x)
+// is 0, the environment is never read for them and every switch compiles away.
+#ifdef VH_ABLATION
+#define DBG(x) (x)
+#else
+#define DBG(x) 0u
+#endif
+
 // ---- errors --------------------------------------------------------------
 struct Error : std::runtime_error {
     int code;

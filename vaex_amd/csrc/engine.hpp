@@ -178,6 +178,11 @@ void launch_fused(const BinPlan &plan, FusedAggs &fa, uint64_t n, uint64_t cells
 // tile-partitioned LDS aggregation for grids too large for one workgroup's LDS
 // (tiled.hip); returns false when the plan is not eligible
 bool try_tiled(const BinPlan &plan, const FusedAggs &fa, uint64_t n, uint64_t cells, int nd_f64, Workspace &ws);
+// rows of the partitioned engines' pass A that missed their region since the last reset
+// (tiled.hip: applied with global atomics; hashagg.hip / hashset.hip: their overflow paths)
+uint64_t stat_tile_overflow(bool reset);
+uint64_t stat_hashagg_overflow(bool reset);
+uint64_t stat_set_overflow(bool reset);
 // a set-ordinal grid (one set-ordinal binner over an integer key) with count / float64 sum
 // aggregators through the fused hash aggregation (hashagg.hip); false when not eligible
 bool hashagg_bin_set_ordinal(const BinPlan &plan, const FusedAggs &fa, uint64_t n);

@@ -403,6 +403,9 @@ template <typename KB, int NV, bool N> __device__ inline void lt_merge(const Lds
     if (threadIdx.x == 0 && s_new && atomicAdd(g.used, s_new) + s_new > g.max_used) atomicOr(g.err, 1u);
 }
 
+// pass-A rows that missed their region since the last reset (vh_stat_read)
+__device__ unsigned long long d_ha_overflow_rows;
+
 // ---- partition parameters -----------------------------------------------------------------
 struct HaParams {
     const void *keys;
@@ -438,11 +441,18 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_sample(const K *keys, uint64_
     __shared__ uint32_t h[1u << HA_FINE_LOG2];
     for (uint32_t t = threadIdx.x; t < (1u << HA_FINE_LOG2); t += HA_THREADS) h[t] = 0;
     __syncthreads();
-    const uint64_t row0 = blockIdx.x * block_stride;
+    // rows at pseudo-random positions (block_stride: the block's seed): the distinct-key
+    // estimate and the bucket histogram hold for any row order (evenly spaced blocks of a
+    // sorted column saw a few keys each); each sampled row is also compared with the next
+    // row -- the fraction of equal neighbours tells clustered keys (runs) apart
+    uint32_t adj = 0;
     for (uint64_t r = threadIdx.x; r < HA_BATCH; r += HA_THREADS) {
-        const uint64_t i = row0 + r;
-        if (i >= n) break;
+        // a sample as large as the rows covers each row once (exact estimate)
+        const uint64_t lin = blockIdx.x * (uint64_t)HA_BATCH + r;
+        if ((uint64_t)gridDim.x * HA_BATCH >= n && lin >= n) break;
+        const uint64_t i = (uint64_t)gridDim.x * HA_BATCH >= n ? lin : hash64(block_stride * 0x9E3779B97F4A7C15ULL + lin) % n;
         const auto kb = ha_kb(keys[i]);
+        if (i + 1 < n && ha_kb(keys[i + 1]) == kb) adj++;
         atomicAdd(&h[ha_h(kb) >> (32 - HA_FINE_LOG2)], 1u);
         const uint64_t key = (uint64_t)kb;
         if (key == SET_EMPTY) continue;  // the estimate can miss one key
@@ -458,6 +468,8 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_sample(const K *keys, uint64_
             pos = (pos + 1) & smask;
         }
     }
+    for (int off = 32; off > 0; off >>= 1) adj += __shfl_down(adj, off, 64);
+    if ((threadIdx.x & 63) == 0 && adj) atomicAdd(&fine_hist[(1u << HA_FINE_LOG2) + 3], (unsigned long long)adj);
     __syncthreads();
     for (uint32_t t = threadIdx.x; t < (1u << HA_FINE_LOG2); t += HA_THREADS)
         if (h[t]) atomicAdd(&fine_hist[t], (unsigned long long)h[t]);
@@ -603,13 +615,16 @@ __device__ inline void ha_commit(const HaScatterLds<KB> &l, const HaParams &hp, 
         }
     }
     if (s_over) {
+        uint32_t novf = 0;
         for (uint32_t k = threadIdx.x; k < tot; k += HA_THREADS) {
             if (!(l.sd[k] & HA_DEST_OVERFLOW)) continue;
             uint64_t vv[NV > 0 ? NV : 1];
 #pragma unroll
             for (int v = 0; v < NV; v++) vv[v] = l.sv[v * (HA_BATCH + 1) + k];
             ha_global_row<NV>(g, (uint64_t)l.sk[k], vv);
+            novf++;
         }
+        if (novf) atomicAdd(&d_ha_overflow_rows, (unsigned long long)novf);
     }
     ha_lds_barrier();
     for (uint32_t t = threadIdx.x; t < P; t += HA_THREADS) {
@@ -631,12 +646,12 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter(HaParams hp, HaTable 
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const HaScatterLds<KB> l = ha_scatter_lds<KB, NV>(lds_raw, hp);
     __syncthreads();
+    // batches w, w + W, w + 2W, ...: every workgroup's rows spread over the whole range
     const uint32_t w = blockIdx.x;
-    const uint64_t row_begin = (uint64_t)w * hp.rows_per_wg;
-    const uint64_t row_end = min(hp.n, row_begin + hp.rows_per_wg);
+    const uint64_t row_end = hp.n;
     const uint64_t region0 = (uint64_t)w * hp.wg_stride;
     const K *keys = static_cast<const K *>(hp.keys);
-    for (uint64_t b0 = row_begin; b0 < row_end; b0 += HA_BATCH) {
+    for (uint64_t b0 = (uint64_t)w * HA_BATCH; b0 < row_end; b0 += (uint64_t)hp.W * HA_BATCH) {
         uint32_t bkt[HA_RPT];
         KB kb[HA_RPT];
         int32_t rank[HA_RPT];
@@ -670,8 +685,8 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter(HaParams hp, HaTable 
 // A lane owns 8 rows per batch in groups of KPL consecutive rows (one 16-byte key load
 // each: KPL = 4 for 4-byte keys, 2 for 8-byte keys) and each value column as KPL / 2
 // 16-byte loads; the next batch is prefetched into registers while this one is ranked and
-// sorted.  Workgroup ranges are multiples of HA_BATCH, so a group is wholly inside or
-// wholly past the range; past-the-end groups load a clamped in-range address and drop.
+// sorted.  Batches start at multiples of HA_BATCH, so a group is wholly inside or wholly
+// past the rows; past-the-end groups load a clamped in-range address and drop.
 template <typename K, int NV>
 __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_f64(HaParams hp, HaTable g) {
     static_assert(sizeof(K) == 4 || sizeof(K) == 8, "fast pass A takes 4- or 8-byte keys");
@@ -681,8 +696,7 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_f64(HaParams hp, HaTa
     const HaScatterLds<KB> l = ha_scatter_lds<KB, NV>(lds_raw, hp);
     __syncthreads();
     const uint32_t w = blockIdx.x;
-    const uint64_t row_begin = (uint64_t)w * hp.rows_per_wg;
-    const uint64_t row_end = min(hp.n, row_begin + hp.rows_per_wg);
+    const uint64_t row_end = hp.n, bstep = (uint64_t)hp.W * HA_BATCH;  // batches w, w + W, ...
     const uint64_t region0 = (uint64_t)w * hp.wg_stride;
     const K *keys = static_cast<const K *>(hp.keys);
     const double *vcol[NV > 0 ? NV : 1];
@@ -705,10 +719,10 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_f64(HaParams hp, HaTa
         }
     };
     Regs cur, nxt;
-    load(row_begin, cur);
+    load((uint64_t)w * HA_BATCH, cur);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): cur is not pending at the loop header
-    for (uint64_t b0 = row_begin; b0 < row_end; b0 += HA_BATCH) {
-        load(b0 + HA_BATCH, nxt);
+    for (uint64_t b0 = (uint64_t)w * HA_BATCH; b0 < row_end; b0 += bstep) {
+        load(b0 + bstep, nxt);
         uint32_t bkt[HA_RPT];
         KB kb[HA_RPT];
         int32_t rank[HA_RPT];
@@ -750,12 +764,42 @@ __host__ __device__ constexpr size_t ha_fast_lds_bytes(int nv, int sb, uint32_t 
     return (size_t)(8 * nv + 4) * sb * HA_BATCH + 20 * ((size_t)P + 1) + 64;
 }
 
-template <typename K, int NV, int SB>
+// A run of rows with one key (count(*), non-NaN values: their sum and count)
+struct HaRun {
+    uint32_t cnt, nn;
+    double sum;
+};
+__device__ inline HaRun ha_run_of(double v) { return HaRun{1u, v == v ? 1u : 0u, v == v ? v : 0.0}; }
+__device__ inline HaRun ha_run_add(HaRun a, HaRun b) { return HaRun{a.cnt + b.cnt, a.nn + b.nn, a.sum + b.sum}; }
+__device__ inline HaRun ha_run_shfl_up(HaRun a, int off) {
+    return HaRun{(uint32_t)__shfl_up((int)a.cnt, off, 64), (uint32_t)__shfl_up((int)a.nn, off, 64), __shfl_up(a.sum, off, 64)};
+}
+
+// a whole run into the HBM table (new keys counted in the workgroup's LDS counter)
+template <int NV> __device__ inline void ha_global_run(const HaTable &g, uint64_t key, const HaRun &r, uint32_t *s_new) {
+    const uint64_t s = ha_slot(g, key, s_new);
+    if (s == ~0ULL) return;
+    atomicAdd(&g.cnt[s], (unsigned long long)r.cnt);
+    if constexpr (NV > 0) {
+        if (r.nn) {
+            atomicAdd(reinterpret_cast<double *>(g.sum[0]) + s, r.sum);
+            atomicAdd(&g.nn[0][s], (unsigned long long)r.nn);
+        }
+    }
+}
+
+// RUNS (clustered keys -- the sample saw most rows equal to their neighbour, e.g. a sorted
+// key column): a wave's 128 consecutive rows of one pair group that hold at most 16 runs of
+// equal keys are folded per run (segmented scan over the lanes) and each run goes to the HBM
+// table as ONE update at its last row; those rows skip the partition.  Other groups (and
+// every group of shuffled keys, which never take this variant) are partitioned row by row.
+template <typename K, int NV, int SB, bool RUNS>
 __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTable g) {
     static_assert(sizeof(K) == 4 && NV <= 1, "4-byte keys, at most one float64 value");
     constexpr int PAIRS = HA_RPT / 2;
     constexpr uint32_t CAP = SB * HA_BATCH;
     extern __shared__ __align__(16) unsigned char lds_raw[];
+    __shared__ uint32_t s_new;
     const uint32_t P = hp.P;
     double *sv = reinterpret_cast<double *>(lds_raw);
     uint32_t *sk = reinterpret_cast<uint32_t *>(lds_raw + (size_t)8 * NV * CAP);
@@ -767,22 +811,25 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTab
         base[t] = (uint32_t)hp.toff[t];
         lim[t] = (uint32_t)hp.toff[t] + hp.cap[t];
     }
+    if (threadIdx.x == 0) s_new = 0;
     __syncthreads();
+    // batches w, w + W, w + 2W, ... of HA_BATCH rows: every workgroup's rows spread over
+    // the whole range, so its bucket distribution is the global one whatever the row order
     const uint32_t w = blockIdx.x;
-    const uint64_t n = hp.n;
-    const uint64_t row_begin = (uint64_t)w * hp.rows_per_wg;
-    const uint64_t row_end = min(n, row_begin + hp.rows_per_wg);
+    const uint64_t n = hp.n, bstep = (uint64_t)hp.W * HA_BATCH;
+    const uint64_t row_end = n;
     const uint64_t region0 = (uint64_t)w * hp.wg_stride;
     const K *keys = static_cast<const K *>(hp.keys);
     const double *vcol = static_cast<const double *>(hp.vals[0]);
     uint32_t *ekeys = static_cast<uint32_t *>(hp.ent);
     uint64_t *evals = hp.vbits[0];
+    const int lane = threadIdx.x & 63;
     struct Regs {
         uint2 k[PAIRS];
         double2 v[PAIRS][NV > 0 ? NV : 1];
     };
-    // branch-free pair loads: n is a multiple of 8 here and workgroup ranges are multiples
-    // of HA_BATCH, so a pair is wholly inside the range or past it (clamped, then dropped)
+    // branch-free pair loads: n is a multiple of 8 here and batches start at multiples of
+    // HA_BATCH, so a pair is wholly inside the rows or past them (clamped, then dropped)
     auto load = [&](uint64_t b0, Regs &R) {
 #pragma unroll
         for (int q = 0; q < PAIRS; q++) {
@@ -793,6 +840,43 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTab
         }
     };
     auto rows = [&](uint64_t b0, const Regs &cur, uint32_t *kb, int32_t *rank, double *vals) {
+        bool folded[PAIRS];
+#pragma unroll
+        for (int q = 0; q < PAIRS; q++) folded[q] = false;
+        if constexpr (RUNS) {
+#pragma unroll
+            for (int q = 0; q < PAIRS; q++) {
+                const uint64_t i0 = b0 + 2 * ((uint64_t)q * HA_THREADS + threadIdx.x);
+                const uint32_t k0 = ha_kb(__builtin_bit_cast(K, cur.k[q].x)), k1 = ha_kb(__builtin_bit_cast(K, cur.k[q].y));
+                const double v0 = NV > 0 ? cur.v[q][0].x : 0.0, v1 = NV > 0 ? cur.v[q][0].y : 0.0;
+                const uint32_t kp = (uint32_t)__shfl_up((int)k1, 1, 64);
+                const bool cin = lane > 0 && kp == k0;  // row 2l continues the previous lane's run
+                const bool same = k1 == k0;
+                const uint64_t heads = __builtin_popcountll(__ballot(!cin)) + __builtin_popcountll(__ballot(!same));
+                const bool all_in = __ballot(i0 >= row_end) == 0;
+                if (!all_in || heads > 16) continue;  // wave-uniform
+                // segmented inclusive scan of the run through row 2l+1 (flag: starts in this lane)
+                HaRun a = same ? ha_run_add(ha_run_of(v0), ha_run_of(v1)) : ha_run_of(v1);
+                bool f = !(same && cin);
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const HaRun up = ha_run_shfl_up(a, off);
+                    const bool uf = __shfl_up((int)f, off, 64) != 0;
+                    if (lane >= off && !f) {
+                        a = ha_run_add(up, a);
+                        f = uf;
+                    }
+                }
+                const HaRun prev = ha_run_shfl_up(a, 1);  // the run through row 2l-1
+                const bool cin_next = __shfl_down((int)cin, 1, 64) != 0 && lane < 63;
+                if (!same) {  // row 2l ends its run (row 2l+1 starts a new one)
+                    const HaRun r0 = cin ? ha_run_add(prev, ha_run_of(v0)) : ha_run_of(v0);
+                    ha_global_run<NV>(g, (uint64_t)k0, r0, &s_new);
+                }
+                if (!cin_next) ha_global_run<NV>(g, (uint64_t)k1, a, &s_new);
+                folded[q] = true;
+            }
+        }
 #pragma unroll
         for (int r = 0; r < HA_RPT; r++) {
             const int q = r >> 1, h = r & 1;
@@ -800,26 +884,27 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTab
             kb[r] = ha_kb(__builtin_bit_cast(K, h ? cur.k[q].y : cur.k[q].x));
             if constexpr (NV > 0) vals[r] = h ? cur.v[q][0].y : cur.v[q][0].x;
             const uint32_t t = ha_bucket(hp, kb[r]);
-            const uint32_t rk = atomicAdd(&hist[i < row_end ? t : P], 1u);
-            rank[r] = i < row_end ? (int32_t)rk : -1;
+            const bool take = i < row_end && !folded[q];
+            const uint32_t rk = atomicAdd(&hist[take ? t : P], 1u);
+            rank[r] = take ? (int32_t)rk : -1;
         }
     };
+    uint32_t novf = 0;
     Regs cur, nxt;
-    load(row_begin, cur);
-    for (uint64_t b0 = row_begin; b0 < row_end; b0 += CAP) {
+    load((uint64_t)w * HA_BATCH, cur);
+    for (uint64_t b0 = (uint64_t)w * HA_BATCH; b0 < row_end; b0 += SB * bstep) {
         uint32_t kb[SB * HA_RPT];
         int32_t rank[SB * HA_RPT];
         double vals[SB * HA_RPT];
 #pragma unroll
         for (int sb = 0; sb < SB; sb++) {
-            load(b0 + (uint64_t)(sb + 1) * HA_BATCH, nxt);
-            rows(b0 + (uint64_t)sb * HA_BATCH, cur, kb + sb * HA_RPT, rank + sb * HA_RPT, vals + sb * HA_RPT);
+            load(b0 + (uint64_t)(sb + 1) * bstep, nxt);
+            rows(b0 + (uint64_t)sb * bstep, cur, kb + sb * HA_RPT, rank + sb * HA_RPT, vals + sb * HA_RPT);
             cur = nxt;
         }
         // B1: every rank taken -> wave 0 scans the histogram
         ha_lds_barrier();
         if (threadIdx.x < 64) {
-            const uint32_t lane = threadIdx.x;
             const uint32_t per = (P + 63) / 64;
             const uint32_t t0 = lane * per;
             uint32_t s = 0;
@@ -828,7 +913,7 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTab
 #pragma unroll
             for (int off = 1; off < 64; off <<= 1) {
                 const uint32_t y = __shfl_up(inc, off, 64);
-                if ((int)lane >= off) inc += y;
+                if (lane >= off) inc += y;
             }
             uint32_t acc = inc - s;
             for (uint32_t t = t0; t < t0 + per && t < P; t++) {
@@ -867,11 +952,14 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTab
                 uint64_t vb[NV > 0 ? NV : 1];
                 if constexpr (NV > 0) vb[0] = __builtin_bit_cast(uint64_t, sv[k]);
                 ha_global_row<NV>(g, (uint64_t)key, vb);
+                novf++;
             }
         }
     }
+    if (novf) atomicAdd(&d_ha_overflow_rows, (unsigned long long)novf);
     ha_lds_barrier();
     for (uint32_t t = threadIdx.x; t < P; t += HA_THREADS) hp.fills[(uint64_t)t * hp.W + w] = base[t] - (uint32_t)hp.toff[t];
+    if (RUNS && threadIdx.x == 0 && s_new && atomicAdd(g.used, s_new) + s_new > g.max_used) atomicOr(g.err, 1u);
 }
 
 // rows [row0, n) straight into the HBM table (the < 8-row tail of the fast pass A)
@@ -955,7 +1043,7 @@ __global__ __launch_bounds__(HB_THREADS) void k_ha_reduce(HaParams hp, HaTable g
         }
     };
     auto process = [&](const Batch &B) {
-        if (hp.debug & 1) {  // experiment: entry stream only (wrong results)
+        if (DBG(hp.debug) & 1) {  // experiment: entry stream only (wrong results)
 #pragma unroll
             for (int j = 0; j < HB_M; j++) asm volatile("" ::"v"(B.kb[j]), "v"(B.vb[j][0]));
         } else {
@@ -982,7 +1070,7 @@ __global__ __launch_bounds__(HB_THREADS) void k_ha_reduce(HaParams hp, HaTable g
         }
     }
     __syncthreads();
-    if (hp.debug & 1) return;
+    if (DBG(hp.debug) & 1) return;
     lt_merge<KB, NV, N>(t, g, HB_THREADS);
 }
 
@@ -1457,12 +1545,14 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
         hipLaunchKernelGGL(k_ha_sample_stats, dim3(blocks_for(sslots, 256, 4)), dim3(256), 0, st, scnt, sslots, stats);
         VH_HIP(hipGetLastError());
     }
-    std::vector<uint64_t> fh(FINE + 3);
-    VH_HIP(hipMemcpyAsync(fh.data(), fine, 8 * (FINE + 3), hipMemcpyDeviceToHost, st));
+    std::vector<uint64_t> fh(FINE + 4);
+    VH_HIP(hipMemcpyAsync(fh.data(), fine, 8 * (FINE + 4), hipMemcpyDeviceToHost, st));
     VH_HIP(hipStreamSynchronize(st));
     uint64_t sampled = 0;
     for (uint32_t i = 0; i < FINE; i++) sampled += fh[i];
     const double ds = (double)fh[FINE], f1 = (double)fh[FINE + 1], f2 = (double)fh[FINE + 2];
+    // clustered keys: most sampled rows equal their next row (a sorted key column)
+    const bool runs = sampled > 0 && (double)fh[FINE + 3] > 0.5 * (double)sampled;
     double dest;
     if (sampled >= n) dest = ds;  // every row sampled: exact
     else dest = f2 > 0 ? ds + f1 * f1 / (2 * f2) : ds + f1 * (f1 - 1) / 2;  // Chao1
@@ -1491,7 +1581,9 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
         hp.vdtype[v] = h->vdtype[v];
     }
     hp.n = n;
+#ifdef VH_ABLATION
     if (const char *dbg = getenv("VH_HA_DEBUG")) hp.debug = (uint32_t)atoi(dbg);
+#endif
     hp.p_log2 = p_log2;
     hp.P = 1u << p_log2;
     const size_t lt_lds = lt_bytes(nv, kbs, narrow);
@@ -1548,7 +1640,8 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     auto k4_kernel = [&](auto kc, auto nvc, auto sbc) {
         using K = decltype(kc);
         constexpr int NV = decltype(nvc)::value, SB = decltype(sbc)::value;
-        return reinterpret_cast<const void *>(k_ha_scatter_k4<K, NV, SB>);
+        return runs ? reinterpret_cast<const void *>(k_ha_scatter_k4<K, NV, SB, true>)
+                    : reinterpret_cast<const void *>(k_ha_scatter_k4<K, NV, SB, false>);
     };
     auto with_k4 = [&](auto &&f) {  // f(kernel instance) for this key type / NV / SB
         auto by_sb = [&](auto kc, auto nvc) {
@@ -1573,7 +1666,8 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     }
     bpc = std::min(bpc, 4);
     const uint32_t W = std::min<uint32_t>(1024, (uint32_t)cu_count() * bpc);
-    const uint64_t rows_per_wg = ((n + W - 1) / W + HA_BATCH - 1) / HA_BATCH * HA_BATCH;
+    // pass-A workgroup w takes batches w, w + W, ...: at most ceil(batches / W) of them
+    const uint64_t rows_per_wg = (nbatch + W - 1) / W * HA_BATCH;
     std::vector<uint32_t> cap(P);
     std::vector<uint64_t> toff(P);
     uint64_t stride = 0;
@@ -1631,7 +1725,8 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
                 with_k4([&](auto kc, auto nvc, auto sbc) {
                     using K = decltype(kc);
                     constexpr int NV = decltype(nvc)::value, SB = decltype(sbc)::value;
-                    hipLaunchKernelGGL((k_ha_scatter_k4<K, NV, SB>), dim3(W), dim3(HA_THREADS), lds_a, st, hp, g);
+                    if (runs) hipLaunchKernelGGL((k_ha_scatter_k4<K, NV, SB, true>), dim3(W), dim3(HA_THREADS), lds_a, st, hp, g);
+                    else hipLaunchKernelGGL((k_ha_scatter_k4<K, NV, SB, false>), dim3(W), dim3(HA_THREADS), lds_a, st, hp, g);
                     if (n8 < n) {
                         HaParams ht = hp;
                         ht.n = n;
@@ -2555,3 +2650,16 @@ int vh_argsort(uint64_t n, const void *keys, int dtype, int64_t *order) {
 }
 
 }  // extern "C"
+
+namespace vh {
+uint64_t stat_hashagg_overflow(bool reset) {
+    unsigned long long v = 0;
+    VH_HIP(hipStreamSynchronize(stream()));
+    VH_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(d_ha_overflow_rows), sizeof(v)));
+    if (reset) {
+        const unsigned long long z = 0;
+        VH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(d_ha_overflow_rows), &z, sizeof(z)));
+    }
+    return v;
+}
+}  // namespace vh

@@ -58,6 +58,9 @@ struct vh_set {
 };
 
 namespace vh {
+// pass-A rows that missed their region since the last reset (vh_stat_read)
+__device__ unsigned long long d_si_overflow_rows;
+
 
 // ---- update: hash-partitioned insert ------------------------------------------------------
 // Per update chunk (hash_primitives.hpp:96-281 `_update` over one chunk of keys):
@@ -357,10 +360,13 @@ __global__ __launch_bounds__(SI_THREADS) void k_si_sample(SiParams sp, uint64_t 
     for (uint32_t t = threadIdx.x; t < (1u << SI_FINE_LOG2); t += SI_THREADS) h[t] = 0;
     si_special_init(&spec);
     __syncthreads();
-    const uint64_t r0 = blockIdx.x * block_stride;
+    // rows at pseudo-random positions: the distinct-key estimate holds for any row order
+    // (evenly spaced blocks of a sorted column saw a few keys each)
     for (uint64_t r = threadIdx.x; r < SI_BATCH; r += SI_THREADS) {
-        const uint64_t i = r0 + r;
-        if (i >= sp.n) break;
+        // a sample as large as the rows covers each row once (exact estimate)
+        const uint64_t lin = blockIdx.x * (uint64_t)SI_BATCH + r;
+        if ((uint64_t)gridDim.x * SI_BATCH >= sp.n && lin >= sp.n) break;
+        const uint64_t i = (uint64_t)gridDim.x * SI_BATCH >= sp.n ? lin : hash64(block_stride * 0x9E3779B97F4A7C15ULL + lin) % sp.n;
         si_kb_t<T> kb;
         if (!si_row<T>(sp, i, &spec, &kb)) continue;
         atomicAdd(&h[si_h32(kb) >> (32 - SI_FINE_LOG2)], 1u);
@@ -447,12 +453,13 @@ __global__ __launch_bounds__(SI_THREADS) void k_si_scatter(SiParams sp, SiTable 
     }
     si_special_init(&spec);
     __syncthreads();
+    // batches w, w + W, w + 2W, ...: every workgroup's rows spread over the whole range
     const uint32_t w = blockIdx.x, P = sp.P;
-    const uint64_t row_begin = (uint64_t)w * sp.rows_per_wg;
-    const uint64_t row_end = min(sp.n, row_begin + sp.rows_per_wg);
+    const uint64_t row_end = sp.n;
     const uint64_t region0 = (uint64_t)w * sp.wg_stride;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (uint64_t b0 = row_begin; b0 < row_end; b0 += SI_BATCH) {
+    uint32_t novf = 0;
+    for (uint64_t b0 = (uint64_t)w * SI_BATCH; b0 < row_end; b0 += (uint64_t)sp.W * SI_BATCH) {
         KB kb[SI_RPT];
         uint32_t bkt[SI_RPT];
         int32_t rank[SI_RPT];
@@ -462,7 +469,13 @@ __global__ __launch_bounds__(SI_THREADS) void k_si_scatter(SiParams sp, SiTable 
             rank[r] = -1;
             bkt[r] = 0;
             kb[r] = 0;
-            if (i < row_end && si_row<T>(sp, i, &spec, &kb[r])) {
+            bool ok = i < row_end && si_row<T>(sp, i, &spec, &kb[r]);
+            // a regular row whose key equals the previous row's (also regular) cannot be a
+            // first appearance: dropped (a sorted or clustered key column sends one row per run)
+            const bool pok = __shfl_up((int)ok, 1, 64) != 0;
+            const KB pk = __shfl_up(kb[r], 1, 64);
+            if (ok && pok && lane > 0 && pk == kb[r]) ok = false;
+            if (ok) {
                 bkt[r] = si_bucket((uint64_t)kb[r], sp.p_log2);
                 rank[r] = (int32_t)atomicAdd(&hist[bkt[r]], 1u);
             }
@@ -526,7 +539,10 @@ __global__ __launch_bounds__(SI_THREADS) void k_si_scatter(SiParams sp, SiTable 
         }
         if (s_over) {  // a full region (sampling miss): those rows go to the HBM table
             for (uint32_t k = threadIdx.x; k < tot; k += SI_THREADS)
-                if (sdst[k] & SI_DEST_OVER) si_global(g, skb[k], sp.row0 + srow[k]);
+                if (sdst[k] & SI_DEST_OVER) {
+                    si_global(g, skb[k], sp.row0 + srow[k]);
+                    novf++;
+                }
         }
         si_lds_barrier();
         for (uint32_t t = threadIdx.x; t < P; t += SI_THREADS) {
@@ -535,6 +551,7 @@ __global__ __launch_bounds__(SI_THREADS) void k_si_scatter(SiParams sp, SiTable 
         }
         si_lds_barrier();
     }
+    if (novf) atomicAdd(&d_si_overflow_rows, (unsigned long long)novf);
     __syncthreads();
     for (uint32_t t = threadIdx.x; t < P; t += SI_THREADS) sp.fills[(uint64_t)t * sp.W + w] = base[t] - (uint32_t)sp.toff[t];
     si_special_flush(&spec, sp.row0, g.ctr);
@@ -577,19 +594,21 @@ __global__ __launch_bounds__(SI_THREADS) void k_si_scatter4(SiParams sp, SiTable
     }
     si_special_init(&spec);
     __syncthreads();
+    // batches w, w + W, w + 2W, ...: every workgroup's rows spread over the whole range
     const uint32_t w = blockIdx.x;
-    const uint64_t row_begin = (uint64_t)w * sp.rows_per_wg;
-    const uint64_t row_end = min(sp.n, row_begin + sp.rows_per_wg);
+    const uint64_t row_end = sp.n, bstep = (uint64_t)sp.W * SI_BATCH;
     const uint64_t region0 = (uint64_t)w * sp.wg_stride;
+    const int lane = threadIdx.x & 63;
     uint64_t *ent = static_cast<uint64_t *>(sp.ent);
     constexpr int QUADS = SI_RPT / 4;
-    // row of slot r of a batch: plain -- lane-owned quads; else -- one row per lane per step
+    // row of slot r (batch r / SI_RPT of the commit starting at b0): plain -- lane-owned
+    // quads; else -- one row per lane per step
     auto row_of = [&](uint64_t b0, int r) -> uint64_t {
+        const int sb = r / SI_RPT, rr = r % SI_RPT;
         if constexpr (PLAIN) {
-            const int sb = r / SI_RPT, rr = r % SI_RPT;
-            return b0 + (uint64_t)sb * SI_BATCH + 4 * ((uint64_t)(rr >> 2) * SI_THREADS + threadIdx.x) + (rr & 3);
+            return b0 + (uint64_t)sb * bstep + 4 * ((uint64_t)(rr >> 2) * SI_THREADS + threadIdx.x) + (rr & 3);
         } else {
-            return b0 + (uint64_t)r * SI_THREADS + threadIdx.x;
+            return b0 + (uint64_t)sb * bstep + (uint64_t)rr * SI_THREADS + threadIdx.x;
         }
     };
     uint4 cur[QUADS], nxt[QUADS];
@@ -601,22 +620,30 @@ __global__ __launch_bounds__(SI_THREADS) void k_si_scatter4(SiParams sp, SiTable
             R[q] = *reinterpret_cast<const uint4 *>(static_cast<const T *>(sp.keys) + is);
         }
     };
-    if constexpr (PLAIN) load(row_begin, cur);
-    for (uint64_t b0 = row_begin; b0 < row_end; b0 += CAP) {
+    uint32_t novf = 0;
+    if constexpr (PLAIN) load((uint64_t)w * SI_BATCH, cur);
+    for (uint64_t b0 = (uint64_t)w * SI_BATCH; b0 < row_end; b0 += SB * bstep) {
         uint32_t kb[SB * SI_RPT];
         int32_t rank[SB * SI_RPT];
+        // a row whose key equals the previous row's cannot be a first appearance: dropped
+        // (a sorted or clustered key column sends one row per run)
         if constexpr (PLAIN) {
 #pragma unroll
             for (int sb = 0; sb < SB; sb++) {
-                load(b0 + (uint64_t)(sb + 1) * SI_BATCH, nxt);
+                load(b0 + (uint64_t)(sb + 1) * bstep, nxt);
 #pragma unroll
-                for (int rr = 0; rr < SI_RPT; rr++) {
-                    const int r = sb * SI_RPT + rr;
-                    const uint32_t w4[4] = {cur[rr >> 2].x, cur[rr >> 2].y, cur[rr >> 2].z, cur[rr >> 2].w};
-                    kb[r] = w4[rr & 3];
-                    const bool ok = row_of(b0, r) < row_end;
-                    const uint32_t rk = atomicAdd(&hist[ok ? si_bucket((uint64_t)kb[r], sp.p_log2) : P], 1u);
-                    rank[r] = ok ? (int32_t)rk : -1;
+                for (int q = 0; q < QUADS; q++) {
+                    const uint32_t w4[4] = {cur[q].x, cur[q].y, cur[q].z, cur[q].w};
+                    const uint32_t prev3 = (uint32_t)__shfl_up((int)cur[q].w, 1, 64);
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int rr = 4 * q + j, r = sb * SI_RPT + rr;
+                        kb[r] = w4[j];
+                        const bool dup = j > 0 ? w4[j] == w4[j - 1] : (lane > 0 && w4[0] == prev3);
+                        const bool ok = row_of(b0, r) < row_end && !dup;
+                        const uint32_t rk = atomicAdd(&hist[ok ? si_bucket((uint64_t)kb[r], sp.p_log2) : P], 1u);
+                        rank[r] = ok ? (int32_t)rk : -1;
+                    }
                 }
 #pragma unroll
                 for (int q = 0; q < QUADS; q++) cur[q] = nxt[q];
@@ -626,7 +653,10 @@ __global__ __launch_bounds__(SI_THREADS) void k_si_scatter4(SiParams sp, SiTable
             for (int r = 0; r < SB * SI_RPT; r++) {
                 const uint64_t i = row_of(b0, r);
                 kb[r] = 0;
-                const bool ok = i < row_end && si_row<T>(sp, i, &spec, &kb[r]);
+                bool ok = i < row_end && si_row<T>(sp, i, &spec, &kb[r]);
+                const bool pok = __shfl_up((int)ok, 1, 64) != 0;
+                const uint32_t pk = (uint32_t)__shfl_up((int)kb[r], 1, 64);
+                if (ok && pok && lane > 0 && pk == kb[r]) ok = false;
                 const uint32_t rk = atomicAdd(&hist[ok ? si_bucket((uint64_t)kb[r], sp.p_log2) : P], 1u);
                 rank[r] = ok ? (int32_t)rk : -1;
             }
@@ -670,10 +700,15 @@ __global__ __launch_bounds__(SI_THREADS) void k_si_scatter4(SiParams sp, SiTable
             const uint32_t key = sk[k], row = srow[k];
             const uint32_t t = si_bucket((uint64_t)key, sp.p_log2);
             const uint32_t dest = dbase[t] + k;
-            if (dest < lim[t]) ent[region0 + dest] = ((uint64_t)row << 32) | key;
-            else si_global(g, (uint64_t)key, sp.row0 + row);  // a full region (sampling miss)
+            if (dest < lim[t]) {
+                ent[region0 + dest] = ((uint64_t)row << 32) | key;
+            } else {
+                si_global(g, (uint64_t)key, sp.row0 + row);  // a full region (sampling miss)
+                novf++;
+            }
         }
     }
+    if (novf) atomicAdd(&d_si_overflow_rows, (unsigned long long)novf);
     si_lds_barrier();
     for (uint32_t t = threadIdx.x; t < P; t += SI_THREADS) sp.fills[(uint64_t)t * sp.W + w] = base[t] - (uint32_t)sp.toff[t];
     si_special_flush(&spec, sp.row0, g.ctr);
@@ -742,7 +777,7 @@ __global__ __launch_bounds__(SB_THREADS) void k_si_reduce(SiParams sp, SiTable g
                 row[j] = sp.ent_row[e];
             }
         }
-        if (sp.debug & 2) {
+        if (DBG(sp.debug) & 2) {
 #pragma unroll
             for (int j = 0; j < SB_M; j++) asm volatile("" ::"v"(kb[j]), "v"(row[j]));
         } else {
@@ -752,7 +787,7 @@ __global__ __launch_bounds__(SB_THREADS) void k_si_reduce(SiParams sp, SiTable g
         }
     }
     __syncthreads();
-    if (!(sp.debug & 1)) si_lt_merge<KB>(t, g, sp.row0, SB_THREADS);
+    if (!(DBG(sp.debug) & 1)) si_lt_merge<KB>(t, g, sp.row0, SB_THREADS);
     __syncthreads();
     si_new_flush(&s_new, g.ctr);
 }
@@ -1186,7 +1221,9 @@ static void si_chunk(vh_set *s, SiScratch &S, const void *keys, const uint8_t *m
     sp.select = select;
     sp.n = n;
     sp.row0 = row0;
+#ifdef VH_ABLATION
     if (const char *dbg = getenv("VH_SI_DEBUG")) sp.debug = (uint32_t)atoi(dbg);
+#endif
     // ---- sample: fine bucket histogram + distinct estimate, read back with the counters
     const uint64_t sslots = 1ull << 21;
     const uint64_t nbatch = (n + SI_BATCH - 1) / SI_BATCH;
@@ -1301,7 +1338,8 @@ static void si_chunk(vh_set *s, SiScratch &S, const void *keys, const uint8_t *m
                               bpc = si_blocks_per_cu(reinterpret_cast<const void *>(k_si_scatter<T>), SI_THREADS, lds_a));
         bpc = std::min(bpc, 4);
         W = std::min<uint32_t>(1024, (uint32_t)cu_count() * bpc);
-        const uint64_t rows_per_wg = ((n + W - 1) / W + SI_BATCH - 1) / SI_BATCH * SI_BATCH;
+        // pass-A workgroup w takes batches w, w + W, ...: at most ceil(batches / W) of them
+        const uint64_t rows_per_wg = (nbatch + W - 1) / W * SI_BATCH;
         cap.resize(P);
         toff.resize(P);
         uint64_t stride = 0;
@@ -1540,3 +1578,16 @@ int vh_set_map_ordinal(vh_set *s, const void *keys, uint64_t n, int loc, void *o
 }
 
 }  // extern "C"
+
+namespace vh {
+uint64_t stat_set_overflow(bool reset) {
+    unsigned long long v = 0;
+    VH_HIP(hipStreamSynchronize(stream()));
+    VH_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(d_si_overflow_rows), sizeof(v)));
+    if (reset) {
+        const unsigned long long z = 0;
+        VH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(d_si_overflow_rows), &z, sizeof(z)));
+    }
+    return v;
+}
+}  // namespace vh

@@ -8,6 +8,7 @@
 #include <cstring>
 
 #include "common.hpp"
+#include "engine.hpp"
 
 namespace vh {
 
@@ -282,6 +283,17 @@ __global__ void k_fill_random(void *dst, uint64_t n, int dtype, int dist, uint64
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         uint64_t r1 = splitmix64(s ^ (2 * i));
+        if (dist == 3) {  // sorted: a + b * the normal quantile of (i + 0.5) / n (ascending)
+            reinterpret_cast<double *>(dst)[i] = a + b * normcdfinv(((double)i + 0.5) / (double)n);
+            continue;
+        }
+        if (dist == 4) {  // sorted integers: [a, b) in equal consecutive runs
+            const uint64_t span = (uint64_t)(int64_t)(b - a);
+            const int64_t v = (int64_t)a + (int64_t)(span ? (uint64_t)(((unsigned __int128)i * span) / n) : 0);
+            if (dtype == VH_I32) reinterpret_cast<int32_t *>(dst)[i] = (int32_t)v;
+            else reinterpret_cast<int64_t *>(dst)[i] = v;
+            continue;
+        }
         if (dist == 0) {
             reinterpret_cast<double *>(dst)[i] = a + (b - a) * u01(r1);
         } else if (dist == 1) {
@@ -531,9 +543,9 @@ int vh_memset(void *dptr, int value, uint64_t bytes) {
 
 int vh_fill_random(void *dptr, uint64_t n, int dtype, int dist, uint64_t seed, double a, double b) {
     VH_API_BEGIN
-    if (dist < 0 || dist > 2) fail(VH_ERR_ARG, "unknown distribution");
-    if (dist < 2 && dtype != VH_F64) fail(VH_ERR_ARG, "uniform/normal fill needs float64");
-    if (dist == 2 && dtype != VH_I32 && dtype != VH_I64) fail(VH_ERR_ARG, "integer fill needs int32/int64");
+    if (dist < 0 || dist > 4) fail(VH_ERR_ARG, "unknown distribution");
+    if ((dist < 2 || dist == 3) && dtype != VH_F64) fail(VH_ERR_ARG, "uniform/normal fill needs float64");
+    if ((dist == 2 || dist == 4) && dtype != VH_I32 && dtype != VH_I64) fail(VH_ERR_ARG, "integer fill needs int32/int64");
     if (n) {
         hipLaunchKernelGGL(k_fill_random, dim3(blocks_for(n, 256)), dim3(256), 0, stream(), dptr, n, dtype,
                            dist, seed, a, b);
@@ -576,6 +588,16 @@ int vh_timing_read(const char *kernel, uint64_t *launches, double *total_ms) {
         *total_ms += ms;
         *launches += 1;
     }
+    VH_API_END
+}
+
+int vh_stat_read(const char *name, uint64_t *value, int reset) {
+    VH_API_BEGIN
+    const std::string n = name ? name : "";
+    if (n == "tile_overflow_rows") *value = stat_tile_overflow(reset != 0);
+    else if (n == "hashagg_overflow_rows") *value = stat_hashagg_overflow(reset != 0);
+    else if (n == "set_overflow_rows") *value = stat_set_overflow(reset != 0);
+    else fail(VH_ERR_ARG, "vh_stat_read: unknown statistic '" + n + "'");
     VH_API_END
 }
 

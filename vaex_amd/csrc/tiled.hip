@@ -76,19 +76,24 @@ struct TileParams {
     uint64_t cells;
     uint32_t W;                // pass-A workgroups
     uint32_t pad;
-    uint64_t rows_per_wg;
+    uint64_t rows_per_wg;      // upper bound (region sizing): batches of a workgroup x TA_BATCH
     uint64_t wg_stride;        // entries of one workgroup's regions
     const uint32_t *cap;       // [T]
     const uint64_t *toff;      // [T] region offset inside a workgroup's block
     uint32_t *fills;           // [T][W] entries produced (may exceed cap)
+    // spill areas: rows past their (workgroup, tile) region go to their tile's spill area
+    // (one atomic reservation per tile and commit), read by pass B like one more region;
+    // past the spill area too (should not happen): global atomics
+    uint32_t *spill_fill;         // [T] entries reserved (may exceed spill_cap)
+    const uint32_t *spill_cap;    // [T]
+    const uint64_t *spill_start;  // [T] entry index of the area, relative to spill_base
+    uint64_t spill_base;          // first entry of the spill areas (after the W regions)
     void *entries;             // u16 / u32, W * wg_stride
     double *values[2];         // per value slot, W * wg_stride
     int32_t val_slot[MAX_FUSED_AGGS];  // sum agg k -> value slot
     int32_t cnt_slot[MAX_FUSED_AGGS];  // count agg k -> CNT_ALWAYS / CNT_FLAG / value slot
     const double *vdata[2];    // value slot -> source column (fast kernel)
-    uint32_t debug;            // experiment switches (VH_TILE_DEBUG), 0 in production
-    const uint32_t *tile_of;   // [T] region id -> grid tile (XCD-resident path), nullptr = identity
-    const uint32_t *abort_word;  // XCD-resident path's state word: pass B skips an aborted launch
+    uint32_t debug;            // experiment switches (VH_TILE_DEBUG), ablation build only (DBG)
     // 4-byte value slots (every summed column <= 4 bytes: int8/16/32, uint8/16/32, bool,
     // float32 -- exact): slot s is float32 bits when bit s of vfloat is set, else the low 32
     // bits of the int64 slot, sign-extended back when bit s of vsigned is set
@@ -261,9 +266,13 @@ __device__ inline uint32_t row_contrib(const FusedAggs &fa, const TileParams &tp
 }
 
 // ---- sample: per-tile histogram of SAMPLE_BLOCKS evenly spaced row blocks ----
+// rows of the whole launch that missed their pass-A region (applied with global atomics);
+// read and reset by vh_stat_read("tile_overflow_rows")
+__device__ unsigned long long d_tile_overflow_rows;
+
 template <int ND>
 __global__ __launch_bounds__(TA_THREADS) void k_tile_sample(BinPlan p, uint64_t n, uint32_t s_log2, uint32_t ntiles,
-                                                            uint64_t block_stride, uint64_t *hist) {
+                                                            uint64_t block_stride, uint64_t *hist, uint64_t *hist2) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
     uint32_t *h = reinterpret_cast<uint32_t *>(lds_raw);
     for (uint32_t t = threadIdx.x; t < ntiles; t += TA_THREADS) h[t] = 0;
@@ -276,7 +285,10 @@ __global__ __launch_bounds__(TA_THREADS) void k_tile_sample(BinPlan p, uint64_t 
     }
     __syncthreads();
     for (uint32_t t = threadIdx.x; t < ntiles; t += TA_THREADS)
-        if (h[t]) atomicAdd((unsigned long long *)&hist[t], (unsigned long long)h[t]);
+        if (h[t]) {  // per-tile count and its square: the block-to-block spread (clustering)
+            atomicAdd((unsigned long long *)&hist[t], (unsigned long long)h[t]);
+            atomicAdd((unsigned long long *)&hist2[t], (unsigned long long)h[t] * h[t]);
+        }
 }
 
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup fence +
@@ -293,6 +305,24 @@ __device__ inline void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+}
+
+// rank of a row in its tile's LDS histogram.  Every lane of the wave calls it (no exec
+// divergence).  When all taking lanes share one tile (sorted or clustered rows) one atomic
+// reserves the wave's ranks and each lane takes its position among them -- 64 same-address
+// LDS atomics would serialise; otherwise one atomic per lane.
+__device__ __forceinline__ int32_t tile_rank(uint32_t *hist, uint32_t t, bool take) {
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+    const uint64_t act = __ballot(take);
+    if (__ballot(take && t != t0) == 0) {
+        if (!act) return -1;
+        const int lane = threadIdx.x & 63, lead = __builtin_ctzll(act);
+        uint32_t base = 0;
+        if (lane == lead) base = atomicAdd(&hist[t0], (uint32_t)__builtin_popcountll(act));
+        base = (uint32_t)__shfl((int)base, lead, 64);
+        return take ? (int32_t)(base + (uint32_t)__builtin_popcountll(act & ((1ull << lane) - 1))) : -1;
+    }
+    return take ? (int32_t)atomicAdd(&hist[t], 1u) : -1;
 }
 
 // exclusive scan of in[0..T) into out[0..T), returns the total (all threads)
@@ -328,12 +358,12 @@ __device__ inline uint32_t block_exclusive_scan(const uint32_t *in, uint32_t *ou
 struct ScatterLds {
     double *sv;
     uint64_t *sp;
-    uint32_t *hist, *boff, *base, *lim, *dbase, *wave_sums;
+    uint32_t *hist, *boff, *base, *lim, *dbase, *soff, *wave_sums;
 };
 
 // LDS bytes of pass A (must match scatter_lds)
 __host__ __device__ inline size_t scatter_lds_bytes(int nv, uint32_t T) {
-    return (size_t)8 * nv * TA_BATCH + (size_t)8 * TA_BATCH + 20 * (size_t)T + 64;
+    return (size_t)8 * nv * TA_BATCH + (size_t)8 * TA_BATCH + 24 * (size_t)T + 64;
 }
 
 template <int NV> __device__ inline ScatterLds scatter_lds(unsigned char *raw, uint32_t T) {
@@ -345,7 +375,8 @@ template <int NV> __device__ inline ScatterLds scatter_lds(unsigned char *raw, u
     l.base = l.boff + T;
     l.lim = l.base + T;
     l.dbase = l.lim + T;
-    l.wave_sums = l.dbase + T;
+    l.soff = l.dbase + T;
+    l.wave_sums = l.soff + T;
     return l;
 }
 
@@ -362,7 +393,7 @@ __host__ __device__ constexpr int fast_sb(int nv) { return nv == 0 ? VH_TA_SB0 :
 
 // LDS of the fast kernels: staged values | staged 4-byte keys | tile arrays
 __host__ __device__ inline size_t fast_lds_bytes(int nv, uint32_t T, uint32_t cap) {
-    return (size_t)8 * nv * cap + (size_t)4 * cap + 20 * (size_t)T + 64;
+    return (size_t)8 * nv * cap + (size_t)4 * cap + 24 * (size_t)T + 64;
 }
 
 template <int NV> __device__ inline ScatterLds fast_lds(unsigned char *raw, uint32_t T, uint32_t cap) {
@@ -374,7 +405,8 @@ template <int NV> __device__ inline ScatterLds fast_lds(unsigned char *raw, uint
     l.base = l.boff + T;
     l.lim = l.base + T;
     l.dbase = l.lim + T;
-    l.wave_sums = l.dbase + T;
+    l.soff = l.dbase + T;
+    l.wave_sums = l.soff + T;
     return l;
 }
 
@@ -388,7 +420,8 @@ __device__ inline void scatter_lds_init(const ScatterLds &l, const TileParams &t
     }
 }
 
-constexpr uint32_t DEST_OVERFLOW = 0x80000000u;  // | tile: region full, global atomics
+constexpr uint32_t DEST_OVERFLOW = 0x80000000u;  // | tile: region and spill full, global atomics
+constexpr uint32_t DEST_SPILL = 0x40000000u;     // | entry of the spill areas
 
 // phases 2-5 of a batch, after every row has its tile, entry, rank (-1 = drop) and
 // carried values: exclusive scan of the tile histogram; every row computes its final
@@ -402,6 +435,14 @@ __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, co
     lds_barrier();
     const uint32_t total = block_exclusive_scan(l.hist, l.boff, T, l.wave_sums);
     if (threadIdx.x == 0) *s_total = total;
+    // a tile whose rows run past its region reserves the excess in its spill area
+    for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) {
+        const uint32_t b = l.base[t], h = l.hist[t], lim = l.lim[t];
+        if (b + h > lim) {
+            const uint32_t first = max(b, lim);
+            l.soff[t] = atomicAdd(&tp.spill_fill[t], b + h - first) - first;
+        }
+    }
     lds_barrier();
 #pragma unroll
     for (int r = 0; r < TA_RPT; r++) {
@@ -409,7 +450,13 @@ __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, co
         const uint32_t t = tile[r];
         const uint32_t pos = l.boff[t] + (uint32_t)rank[r];
         const uint32_t d = l.base[t] + (uint32_t)rank[r];
-        const uint32_t dest = d < l.lim[t] ? d : (DEST_OVERFLOW | t);
+        // past the region: the tile's spill area (DEST_SPILL | entry relative to
+        // spill_base), past that too: global atomics (DEST_OVERFLOW | tile)
+        uint32_t dest = d;
+        if (d >= l.lim[t]) {
+            const uint32_t si = d + l.soff[t];
+            dest = si < tp.spill_cap[t] ? (DEST_SPILL | (uint32_t)(tp.spill_start[t] + si)) : (DEST_OVERFLOW | t);
+        }
         l.sp[pos] = ((uint64_t)dest << 32) | ent[r];
 #pragma unroll
         for (int s = 0; s < NV; s++) l.sv[s * TA_BATCH + pos] = vals[r][s];
@@ -419,10 +466,10 @@ __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, co
     for (uint32_t k = threadIdx.x; k < tot; k += TA_THREADS) {
         const uint64_t pk = l.sp[k];
         const uint32_t dest = (uint32_t)(pk >> 32), e32 = (uint32_t)pk;
-        if (tp.debug & 1) {
+        if (DBG(tp.debug) & 1) {
             asm volatile("" :: "v"(e32), "v"(dest));
         } else if (!(dest & DEST_OVERFLOW)) {
-            const uint64_t e = region0 + dest;
+            const uint64_t e = (dest & DEST_SPILL) ? tp.spill_base + (dest & ~DEST_SPILL) : region0 + dest;
             if (tp.flags_mode) reinterpret_cast<uint32_t *>(tp.entries)[e] = e32;
             else reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)(e32 & 0xffffu);
 #pragma unroll
@@ -433,9 +480,10 @@ __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, co
                     tp.values[s][e] = l.sv[s * TA_BATCH + k];
             }
         } else {
-            // region overflow (a sampling miss): apply the staged row with global atomics
+            // past the region and the spill area: apply the staged row with global atomics
             const uint32_t t = dest & ~DEST_OVERFLOW;
             const uint64_t c = ((uint64_t)t << tp.s_log2) | (e32 & 0xffffu);
+            atomicAdd(&d_tile_overflow_rows, 1ull);
             const uint32_t f = e32 >> 16;
             #pragma unroll
             for (int a = 0; a < MAX_FUSED_AGGS; a++) {
@@ -473,7 +521,7 @@ __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, co
 // The next batch's ranking may start while slower waves still stream: it only touches
 // hist, which the scan already cleared; boff/dbase/sp/sv are rewritten only after the next
 // B1, which every wave reaches after its stream-out.
-__device__ inline void fast_scan(const ScatterLds &l, uint32_t T) {
+__device__ inline void fast_scan(const ScatterLds &l, const TileParams &tp, uint32_t T) {
     if (threadIdx.x >= 64) return;
     const uint32_t lane = threadIdx.x;
     const uint32_t per = (T + 63) / 64;
@@ -488,12 +536,16 @@ __device__ inline void fast_scan(const ScatterLds &l, uint32_t T) {
     }
     uint32_t acc = inc - s;
     for (uint32_t t = t0; t < t0 + per && t < T; t++) {
-        const uint32_t h = l.hist[t], b = l.base[t];
+        const uint32_t h = l.hist[t], b = l.base[t], lim = l.lim[t];
         l.boff[t] = acc;
         l.dbase[t] = b - acc;
         l.base[t] = b + h;
         l.hist[t] = 0;
         acc += h;
+        if (b + h > lim) {  // rows past the region: reserve them in the tile's spill area
+            const uint32_t first = max(b, lim);
+            l.soff[t] = atomicAdd(&tp.spill_fill[t], b + h - first) - first;
+        }
     }
     if (lane == 63) l.wave_sums[0] = inc;
 }
@@ -506,7 +558,7 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
     constexpr uint32_t CAP = R * TA_THREADS;
     uint32_t *sk = reinterpret_cast<uint32_t *>(l.sp);
     lds_barrier();
-    fast_scan(l, T);
+    fast_scan(l, tp, T);
     lds_barrier();
     const uint32_t tot = l.wave_sums[0];
 #pragma unroll
@@ -522,10 +574,11 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
         const uint32_t kk = sk[k];
         const uint32_t t = kk >> 16;
         const uint32_t dest = l.dbase[t] + k;
-        if (tp.debug & 128) {  // experiment: no region stores
+        if (DBG(tp.debug) & 128) {  // experiment: no region stores
             asm volatile("" ::"v"(kk), "v"(dest));
-        } else if (dest < l.lim[t]) {
-            const uint64_t e = region0 + dest;
+        } else if (dest < l.lim[t] || dest + l.soff[t] < tp.spill_cap[t]) {
+            // the region, or past it the tile's spill area
+            const uint64_t e = dest < l.lim[t] ? region0 + dest : tp.spill_base + tp.spill_start[t] + (dest + l.soff[t]);
             reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)kk;
 #pragma unroll
             for (int s = 0; s < NV; s++) {
@@ -535,8 +588,9 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
                     tp.values[s][e] = l.sv[s * CAP + k];
             }
         } else {
-            // region overflow (a sampling miss): apply the staged row with global atomics
+            // past the region and the spill area: apply the staged row with global atomics
             const uint64_t c = ((uint64_t)t << tp.s_log2) | (kk & 0xffffu);
+            atomicAdd(&d_tile_overflow_rows, 1ull);
             #pragma unroll
             for (int a = 0; a < MAX_FUSED_AGGS; a++) {
                 if (a >= fa.na) break;
@@ -646,12 +700,12 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter(BinPlan p, 
     __shared__ uint32_t s_total;
     scatter_lds_init(l, tp, T);
     __syncthreads();
+    // batches w, w + W, w + 2W, ... (tile distribution of every workgroup = the global one)
     const uint32_t w = blockIdx.x;
-    const uint64_t row_begin = (uint64_t)w * tp.rows_per_wg;
-    const uint64_t row_end = min(n, row_begin + tp.rows_per_wg);
+    const uint64_t row_end = n;
     const uint32_t smask = (1u << tp.s_log2) - 1;
     const uint64_t region0 = (uint64_t)w * tp.wg_stride;
-    for (uint64_t b0 = row_begin; b0 < row_end; b0 += TA_BATCH) {
+    for (uint64_t b0 = (uint64_t)w * TA_BATCH; b0 < n; b0 += (uint64_t)tp.W * TA_BATCH) {
         uint32_t tile[TA_RPT], ent[TA_RPT];
         int32_t rank[TA_RPT];
         double vals[TA_RPT][NV > 0 ? NV : 1];
@@ -712,14 +766,11 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter(BinPlan p, 
     #pragma unroll
             for (int r = 0; r < TA_RPT; r++) {
                 const uint64_t i = b0 + (uint64_t)r * TA_THREADS + threadIdx.x;
-                rank[r] = -1;
-                if (i < row_end) {
-                    const uint64_t c = cell[r];
-                    const uint32_t f = fl[r];
-                    tile[r] = (uint32_t)(c >> tp.s_log2);
-                    ent[r] = ((uint32_t)c & smask) | (f << 16);
-                    if (f) rank[r] = (int32_t)atomicAdd(&l.hist[tile[r]], 1u);
-                }
+                const uint64_t c = cell[r];
+                const uint32_t f = i < row_end ? fl[r] : 0u;
+                tile[r] = (uint32_t)(c >> tp.s_log2);
+                ent[r] = ((uint32_t)c & smask) | (f << 16);
+                rank[r] = tile_rank(l.hist, tile[r], f != 0);
             }
         }
         batch_commit<NV>(l, fa, tp, T, region0, tile, ent, rank, vals, &s_total);
@@ -780,17 +831,17 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan
             for (int s = 0; s < NV; s++)
                 if ((uint32_t)s == keyed_slot_of[k]) nan_keyed[s] |= 1u << k;
     }
+    // batches w, w + W, w + 2W, ... of TA_BATCH rows (tile distribution of every workgroup
+    // = the global one, whatever the row order)
     const uint32_t w = blockIdx.x;
-    const uint64_t row_begin = (uint64_t)w * tp.rows_per_wg;
-    const uint64_t row_end = min(n, row_begin + tp.rows_per_wg);
+    const uint64_t row_end = n, bstep = (uint64_t)tp.W * TA_BATCH;
     const uint32_t smask = (1u << tp.s_log2) - 1, s_log2 = tp.s_log2;
     const uint64_t region0 = (uint64_t)w * tp.wg_stride;
     // Branch-free 16-byte loads: n is even on this path (the host bins an odd last row
-    // separately) and workgroup ranges are multiples of TA_BATCH, so a pair is either
-    // wholly inside [row_begin, row_end) or wholly past it; past-the-end pairs load the
-    // clamped last pair and are dropped by the i < row_end test.  With no load behind an
-    // exec branch the compiler counts vmcnt instead of draining to 0, so the prefetched
-    // batch stays in flight.
+    // separately) and batches start at multiples of TA_BATCH, so a pair is either wholly
+    // inside [0, n) or wholly past it; past-the-end pairs load the clamped last pair and
+    // are dropped by the i < n test.  With no load behind an exec branch the compiler
+    // counts vmcnt instead of draining to 0, so the prefetched batch stays in flight.
     auto load = [&](uint64_t b0, double2 (&dst)[PAIRS][NC]) {
 #pragma unroll
         for (int q = 0; q < PAIRS; q++) {
@@ -831,16 +882,16 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan
             const uint32_t t = c >> s_log2;
             key[r] = (t << 16) | (c & smask);
             rank[r] = -1;
-            if (tp.debug & 64) {  // experiment: no ranking
+            if (DBG(tp.debug) & 64) {  // experiment: no ranking
                 asm volatile("" ::"v"(key[r]), "v"(f));
-            } else if (f) {
-                rank[r] = (int32_t)atomicAdd(&l.hist[t], 1u);
+            } else {
+                rank[r] = tile_rank(l.hist, t, f != 0);
             }
         }
     };
     double2 cur[PAIRS][NC], nxt[PAIRS][NC];
-    load(row_begin, cur);
-    for (uint64_t b0 = row_begin; b0 < row_end; b0 += SB * TA_BATCH) {
+    load((uint64_t)w * TA_BATCH, cur);
+    for (uint64_t b0 = (uint64_t)w * TA_BATCH; b0 < n; b0 += SB * bstep) {
         uint32_t key[SB * TA_RPT];
         int32_t rank[SB * TA_RPT];
         double vals[SB * TA_RPT][NV > 0 ? NV : 1];
@@ -848,15 +899,15 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan
         // after the commit (a copy before it would wait for those loads)
 #pragma unroll
         for (int sb = 0; sb < SB; sb++) {
-            load(b0 + (sb + 1) * TA_BATCH, nxt);
-            rows(b0 + sb * TA_BATCH, cur, key + sb * TA_RPT, rank + sb * TA_RPT, vals + sb * TA_RPT);
+            load(b0 + (sb + 1) * bstep, nxt);
+            rows(b0 + sb * bstep, cur, key + sb * TA_RPT, rank + sb * TA_RPT, vals + sb * TA_RPT);
             if (sb + 1 < SB || VH_TA_DRAIN)
 #pragma unroll
                 for (int q = 0; q < PAIRS; q++)
 #pragma unroll
                     for (int c = 0; c < NC; c++) cur[q][c] = nxt[q][c];
         }
-        if (tp.debug & 32) {  // experiment: no commit (loads, cell math, ranking only)
+        if (DBG(tp.debug) & 32) {  // experiment: no commit (loads, cell math, ranking only)
 #pragma unroll
             for (int r = 0; r < SB * TA_RPT; r++) asm volatile("" ::"v"(key[r]), "v"(rank[r]));
         } else {
@@ -928,9 +979,9 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
             for (int s = 0; s < NV; s++)
                 if ((uint32_t)s == keyed_slot_of[k]) nan_keyed[s] |= 1u << k;
     }
+    // batches w, w + W, w + 2W, ... (as k_tile_scatter_f64)
     const uint32_t w = blockIdx.x;
-    const uint64_t row_begin = (uint64_t)w * tp.rows_per_wg;
-    const uint64_t row_end = min(n, row_begin + tp.rows_per_wg);
+    const uint64_t row_end = n, bstep = (uint64_t)tp.W * TA_BATCH;
     const uint32_t smask = (1u << tp.s_log2) - 1, s_log2 = tp.s_log2;
     const uint64_t region0 = (uint64_t)w * tp.wg_stride;
     struct Regs {
@@ -1015,20 +1066,19 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
             f = i < row_end ? f : 0u;
             const uint32_t t = c >> s_log2;
             key[r] = (t << 16) | (c & smask);
-            rank[r] = -1;
-            if (f) rank[r] = (int32_t)atomicAdd(&l.hist[t], 1u);
+            rank[r] = tile_rank(l.hist, t, f != 0);
         }
     };
     Regs cur, nxt;
-    load(row_begin, cur);
-    for (uint64_t b0 = row_begin; b0 < row_end; b0 += SB * TA_BATCH) {
+    load((uint64_t)w * TA_BATCH, cur);
+    for (uint64_t b0 = (uint64_t)w * TA_BATCH; b0 < n; b0 += SB * bstep) {
         uint32_t key[SB * TA_RPT];
         int32_t rank[SB * TA_RPT];
         double vals[SB * TA_RPT][NV > 0 ? NV : 1];
 #pragma unroll
         for (int sb = 0; sb < SB; sb++) {
-            load(b0 + (sb + 1) * TA_BATCH, nxt);
-            rows(b0 + sb * TA_BATCH, cur, key + sb * TA_RPT, rank + sb * TA_RPT, vals + sb * TA_RPT);
+            load(b0 + (sb + 1) * bstep, nxt);
+            rows(b0 + sb * bstep, cur, key + sb * TA_RPT, rank + sb * TA_RPT, vals + sb * TA_RPT);
             if (sb + 1 < SB || VH_TA_DRAIN) cur = nxt;
         }
         batch_commit_fast<NV, SB * TA_RPT>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
@@ -1076,6 +1126,58 @@ __device__ inline void reduce_entry(const FusedAggs &fa, const TileParams &tp, u
     }
 }
 
+// a run of entries of one LDS cell (count / sum aggregators): entries, and per value slot
+// the non-NaN count, the float sum of non-NaN values and the 64-bit integer sum
+template <int NV> struct TileRun {
+    uint32_t cnt, nn[NV > 0 ? NV : 1];
+    double sum[NV > 0 ? NV : 1];
+    unsigned long long isum[NV > 0 ? NV : 1];
+    __device__ void clear() {
+        cnt = 0;
+#pragma unroll
+        for (int s = 0; s < NV; s++) {
+            nn[s] = 0;
+            sum[s] = 0.0;
+            isum[s] = 0;
+        }
+    }
+    __device__ void add(const TileParams &, const double *v) {
+        cnt++;
+#pragma unroll
+        for (int s = 0; s < NV; s++) {
+            isum[s] += __builtin_bit_cast(unsigned long long, v[s]);
+            if (v[s] == v[s]) {
+                nn[s]++;
+                sum[s] += v[s];
+            }
+        }
+    }
+    // the run into the LDS tile, as reduce_entry would add its entries one by one
+    __device__ void flush(const FusedAggs &fa, const TileParams &tp, unsigned char *lds, uint32_t local) const {
+#pragma unroll
+        for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+            if (k >= fa.na) break;
+            if (fa.a[k].kind == VH_AGG_COUNT) {
+                const int cs = tp.cnt_slot[k];
+                uint32_t c = cs == CNT_ALWAYS || cs == CNT_FLAG ? cnt : 0u;
+#pragma unroll
+                for (int s = 0; s < NV; s++)
+                    if (s == cs) c = nn[s];
+                if (c) atomicAdd(reinterpret_cast<uint32_t *>(lds + fa.a[k].lds_off) + local, c);
+            } else {
+#pragma unroll
+                for (int s = 0; s < NV; s++) {
+                    if (s != tp.val_slot[k]) continue;
+                    if (fa.a[k].vint)
+                        atomicAdd(reinterpret_cast<unsigned long long *>(lds + fa.a[k].lds_off) + local, isum[s]);
+                    else if (nn[s])
+                        atomicAdd(reinterpret_cast<double *>(lds + fa.a[k].lds_off) + local, sum[s]);
+                }
+            }
+        }
+    }
+};
+
 constexpr int TB_UNROLL = 8;
 #ifndef VH_TB_VU
 #define VH_TB_VU 0  // 8-entry chunks per lane per step (0 = by NV)
@@ -1091,16 +1193,22 @@ template <int NV> constexpr int tb_vu() { return VH_TB_VU ? VH_TB_VU : NV == 0 ?
 template <int NV, bool NARROW = false>
 __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TileParams tp, const WorkUnit *units) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
-    __shared__ uint32_t s_fill[1024];
-    __shared__ uint32_t s_pre[1025];
-    if (tp.abort_word && *tp.abort_word != 1u) return;  // resident launch not committed: rerun by the host
+    __shared__ uint32_t s_fill[1024 + 1];
+    __shared__ uint32_t s_pre[1024 + 2];
     const WorkUnit u = units[blockIdx.x];
     const uint32_t t = u.tile;
     const uint32_t cap = tp.cap[t];
-    const uint32_t nw = u.w_end - u.w_begin;  // <= W <= 1024 (host checks)
+    // regions of pass-A workgroups w_begin .. w_end - 1 (<= W <= 1024, host checks), then
+    // region nwr: this unit's slice `part` of `parts` of the tile's spill area (8-aligned)
+    const uint32_t nwr = u.w_end - u.w_begin, nw = nwr + 1;
+    const uint32_t part = u.pad & 0xffffu, parts = u.pad >> 16;
+    const uint32_t F = min(tp.spill_fill[t], tp.spill_cap[t]);
+    const uint32_t s0 = part == 0 ? 0u : min(F, (uint32_t)((uint64_t)F * part / parts) & ~7u);
+    const uint32_t s1 = part + 1 >= parts ? F : min(F, (uint32_t)((uint64_t)F * (part + 1) / parts) & ~7u);
+    const uint64_t spill0 = tp.spill_base + tp.spill_start[t] + s0;  // first entry of the slice
     bool any = false;
     for (uint32_t k = threadIdx.x; k < nw; k += TB_THREADS) {
-        const uint32_t f = min(tp.fills[(uint64_t)t * tp.W + u.w_begin + k], cap);
+        const uint32_t f = k < nwr ? min(tp.fills[(uint64_t)t * tp.W + u.w_begin + k], cap) : (s1 > s0 ? s1 - s0 : 0u);
         s_fill[k] = f;
         any |= f != 0;
     }
@@ -1108,17 +1216,17 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
     uint32_t *lw = reinterpret_cast<uint32_t *>(lds_raw);
     for (uint32_t i = threadIdx.x; i < fa.lds_words; i += TB_THREADS) lw[i] = 0;
     if (!tp.flags_mode && threadIdx.x < 64) {
-        // exclusive scan of the chunk counts by the first wave (16 regions per lane)
-        const uint32_t lane = threadIdx.x, k0 = lane * 16;
+        // exclusive scan of the chunk counts by the first wave (per regions per lane)
+        const uint32_t lane = threadIdx.x, per = (nw + 63) / 64, k0 = lane * per;
         uint32_t sum = 0;
-        for (uint32_t k = k0; k < k0 + 16 && k < nw; k++) sum += (s_fill[k] + 7) >> 3;
+        for (uint32_t k = k0; k < k0 + per && k < nw; k++) sum += (s_fill[k] + 7) >> 3;
         uint32_t inc = sum;
         for (int off = 1; off < 64; off <<= 1) {
             const uint32_t y = __shfl_up(inc, off, 64);
             if ((int)lane >= off) inc += y;
         }
         uint32_t acc = inc - sum;
-        for (uint32_t k = k0; k < k0 + 16 && k < nw; k++) {
+        for (uint32_t k = k0; k < k0 + per && k < nw; k++) {
             s_pre[k] = acc;
             acc += (s_fill[k] + 7) >> 3;
         }
@@ -1158,7 +1266,7 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                 const uint32_t q = (cc - s_pre[kk]) * 8;
                 // regions start at multiples of 8 entries and hold a multiple of 8, so the
                 // chunk never leaves its region (entries past the fill are ignored)
-                const uint64_t e = (uint64_t)(u.w_begin + kk) * tp.wg_stride + toff_t + q;
+                const uint64_t e = kk < nwr ? (uint64_t)(u.w_begin + kk) * tp.wg_stride + toff_t + q : spill0 + q;
                 rem[j] = c < C ? min(8u, s_fill[kk] - q) : 0u;
                 ev[j] = *reinterpret_cast<const uint4 *>(ent16 + e);
 #pragma unroll
@@ -1177,25 +1285,52 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                     }
                 }
             }
+            if (!any_mm) {
+                // consecutive entries of one cell (sorted / clustered rows) are added up in
+                // registers first: one LDS atomic per run of a chunk, not per entry
 #pragma unroll
-            for (int j = 0; j < VU; j++) {
-                const uint32_t words[4] = {ev[j].x, ev[j].y, ev[j].z, ev[j].w};
+                for (int j = 0; j < VU; j++) {
+                    const uint32_t words[4] = {ev[j].x, ev[j].y, ev[j].z, ev[j].w};
+                    TileRun<NV> run;
+                    uint32_t cur = ~0u;
 #pragma unroll
-                for (int x = 0; x < 8; x++) {
-                    if ((uint32_t)x >= rem[j]) break;
-                    double v[NV > 0 ? NV : 1];
+                    for (int x = 0; x < 8; x++) {
+                        const uint32_t local = (words[x >> 1] >> (16 * (x & 1))) & 0xffffu;
+                        if ((uint32_t)x < rem[j]) {
+                            if (local != cur) {
+                                if (cur != ~0u) run.flush(fa, tp, lds_raw, cur);
+                                cur = local;
+                                run.clear();
+                            }
+                            double v[NV > 0 ? NV : 1];
 #pragma unroll
-                    for (int s = 0; s < NV; s++) v[s] = (x & 1) ? vv[j][s][x >> 1].y : vv[j][s][x >> 1].x;
-                    const uint32_t local = (words[x >> 1] >> (16 * (x & 1))) & 0xffffu;
-                    if (tp.debug & 8) asm volatile("" :: "v"(local));
-                    else reduce_entry<NV>(fa, tp, lds_raw, local, 0xfu, v);
+                            for (int s = 0; s < NV; s++) v[s] = (x & 1) ? vv[j][s][x >> 1].y : vv[j][s][x >> 1].x;
+                            run.add(tp, v);
+                        }
+                    }
+                    if (cur != ~0u) run.flush(fa, tp, lds_raw, cur);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < VU; j++) {
+                    const uint32_t words[4] = {ev[j].x, ev[j].y, ev[j].z, ev[j].w};
+#pragma unroll
+                    for (int x = 0; x < 8; x++) {
+                        if ((uint32_t)x >= rem[j]) break;
+                        double v[NV > 0 ? NV : 1];
+#pragma unroll
+                        for (int s = 0; s < NV; s++) v[s] = (x & 1) ? vv[j][s][x >> 1].y : vv[j][s][x >> 1].x;
+                        const uint32_t local = (words[x >> 1] >> (16 * (x & 1))) & 0xffffu;
+                        if (DBG(tp.debug) & 8) asm volatile("" :: "v"(local));
+                        else reduce_entry<NV>(fa, tp, lds_raw, local, 0xfu, v);
+                    }
                 }
             }
         }
     } else {
         for (uint32_t k = 0; k < nw; k++) {
             const uint32_t cnt = s_fill[k];
-            const uint64_t base = (uint64_t)(u.w_begin + k) * tp.wg_stride + tp.toff[t];
+            const uint64_t base = k < nwr ? (uint64_t)(u.w_begin + k) * tp.wg_stride + tp.toff[t] : spill0;
             for (uint32_t q0 = 0; q0 < cnt; q0 += TB_THREADS * TB_UNROLL) {
                 uint32_t ent[TB_UNROLL];
                 double v[TB_UNROLL][NV > 0 ? NV : 1];
@@ -1224,8 +1359,8 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
         }
     }
     __syncthreads();
-    if (tp.debug & 16) return;
-    const uint64_t c0 = (uint64_t)(tp.tile_of ? tp.tile_of[t] : t) << tp.s_log2;
+    if (DBG(tp.debug) & 16) return;
+    const uint64_t c0 = (uint64_t)t << tp.s_log2;
     const uint32_t ncell = (uint32_t)min((uint64_t)1 << tp.s_log2, tp.cells - c0);
     #pragma unroll
     for (int k = 0; k < MAX_FUSED_AGGS; k++) {
@@ -1246,496 +1381,6 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                 if (v != 0.0) atomicAdd(reinterpret_cast<double *>(fa.a[k].grid) + c0 + i, v);
             }
         }
-    }
-}
-
-// ---- XCD-resident hot tiles: one persistent launch replaces pass A + most of pass B ----
-//
-// The two-pass path moves every row through HBM twice more (pass A writes a 10-B entry,
-// pass B reads it back): 44 B of traffic per 24-B count+sum row, and HBM read/write
-// turnaround caps such a mix at ~3.6 TB/s of reads.  Here one workgroup
-// per CU (8 XCDs x P) runs the whole query.  Each XCD keeps its own replica of the H
-// densest tiles (sample histogram), spread over the LDS of its P workgroups (TPW tiles
-// each).  A workgroup reads its row range like pass A, counting-sorts each batch by
-// region id (hot tiles first, in owner order) and
-//   * hands the hot prefix to the owners on its own XCD through a batch slot (K slots per
-//     producer, plain stores that stay in the XCD's L2, read back with L1-bypassing `sc1`
-//     loads by workgroups whose HW_REG_XCC_ID is the same), and
-//   * streams the cold suffix to per-(workgroup, tile) regions for pass B, as pass A does.
-// Between batches it consumes what the producers of its XCD published for its tiles (LDS
-// atomics).  Flags: `sc1` stores / loads (ready[x][p] = batches published by p;
-// cons[x][p][c] = batches of p consumed by c; a producer reuses slot b % K once every
-// consumer acknowledged batch b - K).  No wait is unbounded: a workgroup that sees no
-// progress for `timeout` ticks (or finds more workgroups on its XCD than slots) sets the
-// state word to ABORT; the launch then writes nothing to the grids, pass B skips, and the
-// host reruns the query on the two-pass path.  Otherwise the last workgroup to finish
-// commits, every owner flushes its LDS tiles with coalesced global atomics and applies its
-// few cold-region overflows.  Results are the same sums of the same rows (counts exact,
-// float sums within 1e-6 relative).
-#ifndef VH_RES_K
-#define VH_RES_K 4
-#endif
-constexpr uint32_t RES_HDR = 64;   // run offsets per batch-slot header (P + 1 <= 64)
-constexpr uint32_t RES_OVF = 2048; // cold-region overflow entries kept per workgroup
-enum : uint32_t { RES_RUNNING = 0, RES_COMMIT = 1, RES_ABORT = 2 };
-
-struct ResidentParams {
-    uint32_t P, K, H, TPW, nb, G, wt, pad;
-    uint64_t timeout;          // wall-clock ticks without progress before ABORT
-    uint32_t *ctl;             // [0] state, [1] finished workgroups, [2 + x] slots taken on XCD x
-    uint32_t *ready;           // [8][P]
-    uint32_t *cons;            // [8][P producer][P consumer]
-    uint32_t *hdr;             // [8][P][K][RES_HDR]
-    uint32_t *skeys;           // [8][P][K][TA_BATCH] owner-local cell
-    double *svals;             // [8][P][K][TA_BATCH]
-    const uint32_t *tmap;      // [T] grid tile -> region id (hot ids 0..H-1)
-    const uint32_t *tile_of;   // [T] region id -> grid tile
-    uint32_t *ovf_key;         // [G][RES_OVF] id << 16 | cell in tile
-    double *ovf_val;           // [G][RES_OVF]
-};
-
-__device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p) {
-    return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_sc1(const double *p) {
-    return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<uint64_t *>(const_cast<double *>(p)),
-                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(double *p, double v) {
-    __hip_atomic_store(reinterpret_cast<uint64_t *>(p), __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// LDS of the resident kernel: owner tiles (fr.lds_words words) | pass-A staging | tmap[T]
-__host__ __device__ inline size_t resident_lds_bytes(uint32_t tile_words, int nv, uint32_t T) {
-    return (size_t)4 * tile_words + fast_lds_bytes(nv, T, TA_BATCH) + (size_t)4 * T;
-}
-
-// apply one staged row to the grids with global atomics (region overflow)
-template <int NV>
-__device__ inline void apply_row_global(const FusedAggs &fa, const TileParams &tp, uint64_t c, uint32_t count_mask,
-                                        const uint32_t *keyed_slot_of, const double *v) {
-    #pragma unroll
-    for (int a = 0; a < MAX_FUSED_AGGS; a++) {
-        if (a >= fa.na) break;
-        bool take = (count_mask >> a) & 1;
-        if constexpr (NV > 0) {
-            if (!take) take = v[keyed_slot_of[a]] == v[keyed_slot_of[a]];
-        }
-        if (!take) continue;
-        if (fa.a[a].kind == VH_AGG_COUNT) {
-            atomicAdd((unsigned long long *)fa.a[a].grid + c, 1ULL);
-        } else if constexpr (NV > 0) {
-            atomicAdd(reinterpret_cast<double *>(fa.a[a].grid) + c, v[tp.val_slot[a]]);
-        }
-    }
-}
-
-// Roles inside the workgroup: waves 0..RES_PW-1 produce (pass-A pipeline, synchronised by
-// an LDS counter barrier among themselves), RES_CW consumer waves poll the producers of
-// their XCD independently (no workgroup barrier), so neither side waits on the other's
-// memory latency.
-constexpr int RES_PW = TA_THREADS / 64;
-#ifndef VH_RES_CW
-#define VH_RES_CW 4
-#endif
-constexpr int RES_CW = VH_RES_CW;
-constexpr int RES_THREADS = TA_THREADS + 64 * RES_CW;
-constexpr int RES_CU = 4;  // slot entries per consumer lane in flight
-
-// barrier of the producer waves only: one lane per wave adds, then spins on the LDS counter
-__device__ __forceinline__ void prod_barrier(uint32_t *ctr, uint32_t &target) {
-    target += RES_PW;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if ((threadIdx.x & 63) == 0) {
-        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-            __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-}
-
-template <int ND, int NV>
-__global__ __launch_bounds__(RES_THREADS) void k_tile_resident(BinPlan p, FusedAggs fa, FusedAggs fr, TileParams tp,
-                                                               ResidentParams rp, uint64_t n) {
-    constexpr int NC = ND + NV;
-    constexpr int PAIRS = TA_RPT / 2;
-    constexpr uint32_t CAP = TA_BATCH;
-    extern __shared__ __align__(16) unsigned char lds_raw[];
-    __shared__ uint32_t s_ctl[8], s_bar;
-    __shared__ uint32_t s_wpre[RES_CW][65], s_wbeg[RES_CW][64], s_wsb[RES_CW][64];
-    const uint32_t T = tp.ntiles;
-    unsigned char *tl = lds_raw;
-    const ScatterLds l = fast_lds<NV>(lds_raw + (size_t)4 * fr.lds_words, T, CAP);
-    uint32_t *s_tmap = reinterpret_cast<uint32_t *>(lds_raw + (size_t)4 * fr.lds_words + fast_lds_bytes(NV, T, CAP));
-    uint32_t *sk = reinterpret_cast<uint32_t *>(l.sp);
-    const uint32_t tid = threadIdx.x;
-    {
-        uint32_t *lw = reinterpret_cast<uint32_t *>(tl);
-        for (uint32_t i = tid; i < fr.lds_words; i += RES_THREADS) lw[i] = 0;
-    }
-    for (uint32_t t = tid; t < T; t += RES_THREADS) s_tmap[t] = rp.tmap[t];
-    for (uint32_t t = tid; t < T; t += RES_THREADS) {
-        l.hist[t] = 0;
-        l.base[t] = (uint32_t)tp.toff[t];
-        l.lim[t] = (uint32_t)tp.toff[t] + tp.cap[t];
-    }
-    if (tid == 0) {
-        uint32_t xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        xcc &= 0xfu;
-        const uint32_t slot = xcc < 8 ? atomicAdd(&rp.ctl[2 + xcc], 1u) : 0xffffffffu;
-        bool ab = ld_sc1(&rp.ctl[0]) == RES_ABORT;
-        if (slot >= rp.P) {  // placement the slots do not cover: the two-pass path reruns the query
-            atomicCAS(&rp.ctl[0], RES_RUNNING, RES_ABORT);
-            ab = true;
-        }
-        s_ctl[0] = xcc;
-        s_ctl[1] = slot;
-        s_ctl[3] = ab ? 1u : 0u;  // abort seen
-        s_ctl[6] = 0;             // overflow entries
-        s_ctl[7] = 0;             // overflow list full
-        s_bar = 0;
-    }
-    __syncthreads();
-    if (s_ctl[3]) return;
-    const uint32_t xcc = s_ctl[0], me = s_ctl[1];
-    const uint32_t P = rp.P, K = rp.K, H = rp.H, TPW = rp.TPW, nb = rp.nb;
-    const uint32_t smask = (1u << tp.s_log2) - 1, s_log2 = tp.s_log2;
-    const uint64_t xp0 = (uint64_t)xcc * P;
-    const uint32_t w = blockIdx.x;
-    uint32_t count_mask = 0, keyed_slot_of[MAX_FUSED_AGGS], nan_keyed[NV > 0 ? NV : 1] = {};
-    #pragma unroll
-    for (int k = 0; k < MAX_FUSED_AGGS; k++) {
-        keyed_slot_of[k] = 0;
-        if (k >= fa.na) break;
-        keyed_slot_of[k] = fa.a[k].kind == VH_AGG_COUNT ? (uint32_t)tp.cnt_slot[k] : (uint32_t)tp.val_slot[k];
-        if (fa.a[k].kind == VH_AGG_COUNT && tp.cnt_slot[k] == CNT_ALWAYS) count_mask |= 1u << k;
-        else
-#pragma unroll
-            for (int s = 0; s < NV; s++)
-                if ((uint32_t)s == keyed_slot_of[k]) nan_keyed[s] |= 1u << k;
-    }
-    uint32_t *ovf_key = rp.ovf_key + (uint64_t)w * RES_OVF;
-    double *ovf_val = rp.ovf_val + (uint64_t)w * RES_OVF;
-
-    if (tid < TA_THREADS) {
-        // ================= producer waves =================
-        const double *col[NC];
-        double vmin[ND], scale[ND], bins_d[ND];
-        uint32_t bins2[ND], stride[ND];
-#pragma unroll
-        for (int d = 0; d < ND; d++) {
-            col[d] = reinterpret_cast<const double *>(p.b[d].data);
-            vmin[d] = p.b[d].vmin;
-            scale[d] = p.b[d].scale;
-            bins_d[d] = (double)p.b[d].bins;
-            bins2[d] = (uint32_t)p.b[d].bins + 2;
-            stride[d] = (uint32_t)p.b[d].stride;
-        }
-#pragma unroll
-        for (int s = 0; s < NV; s++) col[ND + s] = tp.vdata[s];
-        const uint64_t row_begin = (uint64_t)w * tp.rows_per_wg;
-        const uint64_t row_end = min(n, row_begin + tp.rows_per_wg);
-        const uint64_t region0 = (uint64_t)w * tp.wg_stride;
-        uint32_t bar = 0;
-        uint32_t cmin = 0;  // wave 0: least batch count every consumer acknowledged (cached)
-        uint64_t last = wall_clock64();
-        auto load = [&](uint64_t b0, double2 (&dst)[PAIRS][NC]) {
-#pragma unroll
-            for (int q = 0; q < PAIRS; q++) {
-                const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + tid);
-                const uint64_t is = i < n - 2 ? i : n - 2;
-#pragma unroll
-                for (int c = 0; c < NC; c++) dst[q][c] = *reinterpret_cast<const double2 *>(col[c] + is);
-            }
-        };
-        // one batch: `cur` holds its rows (loaded one step earlier), `nxt` receives the next
-        auto step = [&](uint32_t b, double2 (&cur)[PAIRS][NC], double2 (&nxt)[PAIRS][NC]) -> bool {
-            const uint64_t b0 = row_begin + (uint64_t)b * CAP;
-            // this batch's loads and the previous batch's stores complete; then the previous
-            // batch is published (every producer wave's stores have reached L2)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            prod_barrier(&s_bar, bar);
-            if (tid == 0 && b > 0) {
-                if (rp.wt) st_sc1(&rp.ready[xp0 + me], b);
-                else rp.ready[xp0 + me] = b;  // same XCD: the flag stays in the L2 the pollers read
-            }
-            if (b + 1 < nb) load(b0 + CAP, nxt);
-            uint32_t key[TA_RPT];
-            int32_t rank[TA_RPT];
-            double vals[TA_RPT][NV > 0 ? NV : 1];
-            if (tp.debug & 2048) {  // experiment: loads + cell math only, nothing published
-                uint32_t acc = 0;
-#pragma unroll
-                for (int r = 0; r < TA_RPT; r++) {
-                    const int q = r >> 1, h = r & 1;
-                    uint32_t c = 0;
-#pragma unroll
-                    for (int d = 0; d < ND; d++)
-                        c += scalar_f64_index32(h ? cur[q][d].y : cur[q][d].x, vmin[d], scale[d], bins_d[d], bins2[d]) * stride[d];
-                    acc += c;
-                }
-                asm volatile("" ::"v"(acc));
-                return true;
-            }
-#pragma unroll
-            for (int r = 0; r < TA_RPT; r++) {
-                const int q = r >> 1, h = r & 1;
-                const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + tid) + h;
-                uint32_t c = 0;
-#pragma unroll
-                for (int d = 0; d < ND; d++) {
-                    const double v = h ? cur[q][d].y : cur[q][d].x;
-                    c += scalar_f64_index32(v, vmin[d], scale[d], bins_d[d], bins2[d]) * stride[d];
-                }
-                uint32_t f = count_mask;
-#pragma unroll
-                for (int s = 0; s < NV; s++) {
-                    vals[r][s] = h ? cur[q][ND + s].y : cur[q][ND + s].x;
-                    f |= vals[r][s] == vals[r][s] ? nan_keyed[s] : 0u;
-                }
-                f = i < row_end ? f : 0u;
-                const uint32_t id = s_tmap[c >> s_log2];
-                key[r] = (id << 16) | (c & smask);
-                rank[r] = f ? (int32_t)atomicAdd(&l.hist[id], 1u) : -1;
-            }
-            prod_barrier(&s_bar, bar);
-            fast_scan(l, T);
-            prod_barrier(&s_bar, bar);
-            const uint32_t tot = l.wave_sums[0];
-            const uint32_t hot_n = H < T ? l.boff[H] : tot;
-#pragma unroll
-            for (int r = 0; r < TA_RPT; r++) {
-                if (rank[r] < 0) continue;
-                const uint32_t pos = l.boff[key[r] >> 16] + (uint32_t)rank[r];
-                sk[pos] = key[r];
-#pragma unroll
-                for (int s = 0; s < NV; s++) l.sv[s * CAP + pos] = vals[r][s];
-            }
-            // wave 0: slot b % K is free once every owner acknowledged batch b - K
-            if (tid < 64 && b >= K && cmin < b - K + 1) {
-                const uint32_t target = b - K + 1;
-                for (;;) {
-                    const uint32_t v = tid < P ? ld_sc1(&rp.cons[(xp0 + me) * P + tid]) : 0xffffffffu;
-                    uint32_t m = v;
-#pragma unroll
-                    for (int off = 32; off; off >>= 1) m = min(m, (uint32_t)__shfl_xor(m, off, 64));
-                    if (m >= target) {
-                        cmin = m;
-                        last = wall_clock64();
-                        break;
-                    }
-                    if (tid == 0) {
-                        const uint64_t now = wall_clock64();
-                        if (ld_sc1(&rp.ctl[0]) == RES_ABORT) s_ctl[3] = 1;
-                        else if (now - last > rp.timeout) {
-                            atomicCAS(&rp.ctl[0], RES_RUNNING, RES_ABORT);
-                            s_ctl[3] = 1;
-                        }
-                    }
-                    if (__shfl(s_ctl[3], 0, 64)) break;
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            // the stop decision every producer wave reads: written by lane 0 before the barrier
-            // (s_ctl[3] may change under the consumer waves at any time)
-            if (tid == 0) s_ctl[5] = s_ctl[3];
-            prod_barrier(&s_bar, bar);
-            if (s_ctl[5]) return false;
-            const uint64_t sb = (xp0 + me) * K + b % K;
-            uint32_t *dk = rp.skeys + sb * CAP;
-            double *dv = rp.svals + sb * CAP;
-            for (uint32_t k = tid; k < hot_n && !(tp.debug & 512); k += TA_THREADS) {  // 512: no slot stores
-                const uint32_t kk = sk[k];
-                const uint32_t loc = (((kk >> 16) % TPW) << s_log2) | (kk & smask);
-                if (rp.wt) st_sc1(dk + k, loc);
-                else dk[k] = loc;
-#pragma unroll
-                for (int s = 0; s < NV; s++) {
-                    if (rp.wt) st_sc1(dv + k, l.sv[s * CAP + k]);
-                    else dv[k] = l.sv[s * CAP + k];
-                }
-            }
-            for (uint32_t o = tid; o <= P; o += TA_THREADS) {
-                const uint32_t id = o * TPW;
-                const uint32_t v = id < H ? l.boff[id] : hot_n;
-                if (rp.wt) st_sc1(&rp.hdr[sb * RES_HDR + o], v);
-                else rp.hdr[sb * RES_HDR + o] = v;
-            }
-            for (uint32_t k = hot_n + tid; k < tot && !(tp.debug & 1024); k += TA_THREADS) {  // 1024: no cold stores
-                const uint32_t kk = sk[k];
-                const uint32_t t = kk >> 16;
-                const uint32_t dest = l.dbase[t] + k;
-                if (dest < l.lim[t]) {
-                    const uint64_t e = region0 + dest;
-                    reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)kk;
-#pragma unroll
-                    for (int s = 0; s < NV; s++) tp.values[s][e] = l.sv[s * CAP + k];
-                } else {  // region overflow (a sampling miss): kept until the launch commits
-                    const uint32_t pos = atomicAdd(&s_ctl[6], 1u);
-                    if (pos < RES_OVF) {
-                        ovf_key[pos] = kk;
-                        if constexpr (NV > 0) ovf_val[pos] = l.sv[k];
-                    } else {
-                        s_ctl[7] = 1;
-                    }
-                }
-            }
-            return true;
-        };
-        double2 A[PAIRS][NC], B[PAIRS][NC];
-        load(row_begin, A);
-        bool ok = true;
-        for (uint32_t b = 0; b < nb && ok; b += 2) {
-            ok = step(b, A, B);
-            if (ok && b + 1 < nb) ok = step(b + 1, B, A);
-        }
-        if (ok) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            prod_barrier(&s_bar, bar);
-            if (tid == 0) {
-                if (rp.wt) st_sc1(&rp.ready[xp0 + me], nb);
-                else rp.ready[xp0 + me] = nb;
-            }
-        }
-        for (uint32_t t = tid; t < T; t += TA_THREADS)
-            tp.fills[(uint64_t)t * tp.W + w] = t < H ? 0u : l.base[t] - (uint32_t)tp.toff[t];
-    } else {
-        // ================= consumer waves =================
-        const uint32_t cw = (tid - TA_THREADS) >> 6, lane = tid & 63;
-        const uint32_t nq = P > cw ? (P - cw + RES_CW - 1) / RES_CW : 0;  // producers of this wave
-        const uint32_t q = cw + lane * RES_CW;                             // this lane's producer
-        uint32_t *wpre = s_wpre[cw], *wbeg = s_wbeg[cw], *wsb = s_wsb[cw];
-        uint32_t nx = 0, idle = 0;
-        uint64_t last = wall_clock64();
-        for (;;) {
-            const bool mine = lane < nq && nx < nb && !(tp.debug & 4096);  // 4096: experiment, no consumers
-            if (!__any(mine)) break;
-            bool av = false;
-            uint32_t beg = 0, cnt = 0, sbq = 0;
-            if (mine && ld_sc1(&rp.ready[xp0 + q]) > nx) {
-                sbq = (uint32_t)((xp0 + q) * K + nx % K);
-                beg = ld_sc1(&rp.hdr[(uint64_t)sbq * RES_HDR + me]);
-                cnt = ld_sc1(&rp.hdr[(uint64_t)sbq * RES_HDR + me + 1]) - beg;
-                av = true;
-            }
-            uint32_t inc = cnt;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t y = __shfl_up(inc, off, 64);
-                if ((int)lane >= off) inc += y;
-            }
-            const uint32_t total = __shfl(inc, 63, 64);
-            if (total) {
-                wpre[lane] = inc - cnt;
-                wbeg[lane] = beg;
-                wsb[lane] = sbq;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_wave_barrier();
-                for (uint32_t i0 = 0; i0 < total; i0 += 64 * RES_CU) {
-                    uint32_t loc[RES_CU];
-                    double v[RES_CU][NV > 0 ? NV : 1];
-#pragma unroll
-                    for (int u = 0; u < RES_CU; u++) {
-                        const uint32_t i = i0 + u * 64 + lane;
-                        loc[u] = 0xffffffffu;
-                        if (i < total && !(tp.debug & 256)) {  // 256: experiment, consumers only acknowledge
-                            uint32_t k = 0;
-#pragma unroll
-                            for (uint32_t stp = 8; stp; stp >>= 1)
-                                if (k + stp < nq && wpre[k + stp] <= i) k += stp;
-                            const uint64_t e = (uint64_t)wsb[k] * CAP + wbeg[k] + (i - wpre[k]);
-                            loc[u] = ld_sc1(rp.skeys + e);
-#pragma unroll
-                            for (int s = 0; s < NV; s++) v[u][s] = ld_sc1(rp.svals + e);
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < RES_CU; u++)
-                        if (loc[u] != 0xffffffffu) reduce_entry<NV>(fr, tp, tl, loc[u], 0xfu, v[u]);
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-            if (av) {
-                nx++;
-                if (rp.wt) st_sc1(&rp.cons[(xp0 + q) * P + me], nx);
-                else rp.cons[(xp0 + q) * P + me] = nx;
-            }
-            if (__any(av)) {
-                idle = 0;
-                if (lane == 0) last = wall_clock64();
-            } else {
-                __builtin_amdgcn_s_sleep(4);
-                if ((++idle & 15) == 0) {
-                    uint32_t stop = 0;
-                    if (lane == 0) {
-                        if (s_ctl[3] || ld_sc1(&rp.ctl[0]) == RES_ABORT) stop = 1;
-                        else if (wall_clock64() - last > rp.timeout) {
-                            atomicCAS(&rp.ctl[0], RES_RUNNING, RES_ABORT);
-                            stop = 1;
-                        }
-                        if (stop) s_ctl[3] = 1;
-                    }
-                    if (__shfl(stop, 0, 64)) break;
-                }
-            }
-        }
-    }
-    // commit when every workgroup finished; abort otherwise
-    __syncthreads();
-    if (tid == 0) {
-        if (!s_ctl[3]) {
-            if (s_ctl[7]) atomicCAS(&rp.ctl[0], RES_RUNNING, RES_ABORT);
-            atomicAdd(&rp.ctl[1], 1u);
-            const uint64_t t0 = wall_clock64();
-            for (;;) {
-                if (ld_sc1(&rp.ctl[1]) >= rp.G) {
-                    atomicCAS(&rp.ctl[0], RES_RUNNING, RES_COMMIT);
-                    break;
-                }
-                if (ld_sc1(&rp.ctl[0]) != RES_RUNNING) break;
-                if (wall_clock64() - t0 > rp.timeout) {
-                    atomicCAS(&rp.ctl[0], RES_RUNNING, RES_ABORT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(8);
-            }
-        }
-        s_ctl[2] = ld_sc1(&rp.ctl[0]) == RES_COMMIT ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!s_ctl[2]) return;
-    // flush the owner tiles
-    const uint32_t Sp = TPW << s_log2;
-    #pragma unroll
-    for (int k = 0; k < MAX_FUSED_AGGS; k++) {
-        if (k >= fr.na) break;
-        for (uint32_t i = tid; i < Sp; i += RES_THREADS) {
-            const uint32_t id = me * TPW + (i >> s_log2);
-            if (id >= H) continue;
-            const uint64_t c = ((uint64_t)rp.tile_of[id] << s_log2) | (i & smask);
-            if (c >= tp.cells) continue;
-            if (fr.a[k].kind == VH_AGG_COUNT) {
-                const uint32_t v = reinterpret_cast<const uint32_t *>(tl + fr.a[k].lds_off)[i];
-                if (v) atomicAdd((unsigned long long *)fr.a[k].grid + c, (unsigned long long)v);
-            } else {
-                const double v = reinterpret_cast<const double *>(tl + fr.a[k].lds_off)[i];
-                if (v != 0.0) atomicAdd(reinterpret_cast<double *>(fr.a[k].grid) + c, v);
-            }
-        }
-    }
-    const uint32_t novf = min(s_ctl[6], RES_OVF);
-    for (uint32_t i = tid; i < novf; i += RES_THREADS) {
-        const uint32_t kk = ovf_key[i];
-        const uint64_t c = ((uint64_t)rp.tile_of[kk >> 16] << s_log2) | (kk & smask);
-        double v[NV > 0 ? NV : 1];
-        if constexpr (NV > 0) v[0] = ovf_val[i];
-        apply_row_global<NV>(fa, tp, c, count_mask, keyed_slot_of, v);
     }
 }
 
@@ -1831,16 +1476,7 @@ static const void *ord_kernel(int nv, int fast_mode, bool set, int dt0, int dt1)
     return set ? ord_kernel_t<true>(nv, fast_mode, dt0, dt1) : ord_kernel_t<false>(nv, fast_mode, dt0, dt1);
 }
 
-// 0 = not tiled (caller takes another path), 1 = done, 2 = the XCD-resident launch aborted
-// (nothing written to the grids): run again on the two-pass path
-static int try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64,
-                          Workspace &ws, bool allow_res);
-static bool try_tiled_once(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64,
-                           Workspace &ws) {
-    const int r = try_tiled_impl(plan, fa_in, n, cells, nd_f64, ws, true);
-    if (r == 2) return try_tiled_impl(plan, fa_in, n, cells, nd_f64, ws, false) == 1;
-    return r == 1;
-}
+static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64);
 
 // the fast ordinal pass A applies: one native int32 BinnerOrdinal without mask, every
 // sum a 16-byte aligned float64 column, no aggregator masks, no counts of other columns
@@ -1873,7 +1509,7 @@ bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t
     if ((n & 1) && !fa_in.generic_vals && (nd_f64 > 0 || ord_fast_ok(plan, fa_in))) {
         // the fast pass A reads row pairs: tile all rows but the last, which takes the
         // global-atomic path
-        if (!try_tiled_once(plan, fa_in, n - 1, cells, nd_f64, ws)) return false;
+        if (!try_tiled_impl(plan, fa_in, n - 1, cells, nd_f64)) return false;
         BinPlan p1 = plan;
         FusedAggs f1 = fa_in;
         for (int d = 0; d < p1.nb; d++) {
@@ -1887,7 +1523,7 @@ bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t
         launch_fused(p1, f1, 1, cells, nd_f64, ws);
         return true;
     }
-    return try_tiled_once(plan, fa_in, n, cells, nd_f64, ws);
+    return try_tiled_impl(plan, fa_in, n, cells, nd_f64);
 }
 
 // Partition scratch shared by every grid of a device: a 1e9-row count+sum needs ~10 GB of
@@ -1896,38 +1532,12 @@ bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t
 // by the library stream.
 struct TileScratch {
     std::mutex mu;
-    DevBuf entries, values, meta, res;
+    DevBuf entries, values, meta;
 };
 
-// XCD-resident path switch (opt-in; measured slower than the two-pass path, DESIGN.md
-// §5.1): VH_RESIDENT=0 off (default), 1 on (slot data and flags by plain stores kept in the
-// XCD's L2), 2 on with write-through (`sc1`) stores; an aborted launch turns it off for the
-// process
-static std::atomic<bool> g_res_off{false};
-static int res_mode() {
-    if (g_res_off.load()) return 0;
-    const char *e = getenv("VH_RESIDENT");
-    return e ? atoi(e) : 0;
-}
 static bool getenv_flag_off(const char *name) {  // NAME=0 turns a default-on path off (A/B runs)
     const char *e = getenv(name);
     return e && atoi(e) == 0;
-}
-static uint64_t res_min_rows() {  // VH_RES_MIN_ROWS: tests run the path at small sizes
-    const char *e = getenv("VH_RES_MIN_ROWS");
-    return e ? strtoull(e, nullptr, 10) : (1ull << 24);
-}
-static uint64_t wall_clock_khz() {
-    static std::mutex mu;
-    static std::map<int, uint64_t> m;
-    std::lock_guard<std::mutex> lk(mu);
-    const int dev = current_device();
-    auto it = m.find(dev);
-    if (it != m.end()) return it->second;
-    int khz = 0;
-    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
-    m[dev] = (uint64_t)khz;
-    return (uint64_t)khz;
 }
 static TileScratch &tile_scratch() {
     static std::mutex g;
@@ -1938,12 +1548,13 @@ static TileScratch &tile_scratch() {
     return *p;
 }
 
-static int try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64,
-                          Workspace &, bool allow_res) {
+static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64) {
     TileScratch &ws = tile_scratch();
     std::lock_guard<std::mutex> ws_lock(ws.mu);
     TileParams tp{};
+#ifdef VH_ABLATION
     if (const char *dbg = getenv("VH_TILE_DEBUG")) tp.debug = (uint32_t)atoi(dbg);
+#endif
     // carried values: one slot per distinct value column (sum / min / max of one column share
     // it: same data, mask, dtype and integer-sum encoding); counts keyed on a matching value
     int nv = 0;
@@ -2042,115 +1653,100 @@ static int try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t 
         bpc = it->second;
     }
     bpc = std::max(1, std::min(bpc, TA_WG_PER_CU));
-    // XCD-resident variant: the fast f64 pass A with <= 1 value slot, one workgroup per CU,
-    // P owners per XCD holding TPW tiles each in LDS (resident_lds_bytes + static arrays)
-    bool res_kinds = true;  // the resident launch applies counts and sums only
-    for (int k = 0; k < fa.na; k++) res_kinds = res_kinds && !is_minmax(fa.a[k].kind);
-    const int rmode = allow_res && res_kinds && fast && nv <= 1 && nd_f64 >= 1 && nd_f64 <= 3 && n >= res_min_rows() ? res_mode() : 0;
-    uint32_t rP = 0, rTPW = 0;
-    if (rmode && cu_count() % 8 == 0 && cu_count() / 8 <= (int)RES_HDR - 1) {
-        rP = (uint32_t)cu_count() / 8;
-        for (uint32_t k = 1; (S * k) <= 65536; k++) {
-            const uint64_t words = ((S * k * per_cell + 15) & ~uint64_t(15)) / 4;
-            if (resident_lds_bytes((uint32_t)words, nv, T) + 4096 > LDS_MAX_BYTES) break;
-            rTPW = k;
-        }
-    }
-    bool res = rTPW > 0;
-    const uint32_t W = res ? 8 * rP : std::min<uint32_t>(1024, (uint32_t)cu_count() * bpc);
+    const uint32_t W = std::min<uint32_t>(1024, (uint32_t)cu_count() * bpc);
     // pass-B work units: sum over tiles of ceil(e_t / target) <= T + 4 cu (target = n / 4 cu)
     const uint64_t max_units = (uint64_t)T + 4 * (uint64_t)cu_count() + 16;
     DevBuf &meta = ws.meta;
-    const uint64_t meta_bytes = 8 * (uint64_t)T /*hist*/ + 4 * (uint64_t)T /*cap*/ + 8 * (uint64_t)T /*toff*/ +
-                                4 * (uint64_t)T * W /*fills*/ + 16 * max_units /*units*/ + 8 * (uint64_t)T /*tmap, tile_of*/ + 256;
+    const uint64_t meta_bytes = 8 * (uint64_t)T /*hist*/ + 8 * (uint64_t)T /*hist2*/ + 8 * (uint64_t)T /*toff*/ +
+                                8 * (uint64_t)T /*spill_start*/ + 4 * (uint64_t)T /*spill_cap*/ + 4 * (uint64_t)T /*spill_fill*/ +
+                                4 * (uint64_t)T /*cap*/ + 4 * (uint64_t)T * W /*fills*/ + 16 * max_units /*units*/ + 256;
     meta.ensure(meta_bytes);
     unsigned char *mb = meta.as<unsigned char>();
     uint64_t *d_hist = reinterpret_cast<uint64_t *>(mb);
-    uint64_t *d_toff = d_hist + T;
-    uint32_t *d_cap = reinterpret_cast<uint32_t *>(d_toff + T);
+    uint64_t *d_hist2 = d_hist + T;
+    uint64_t *d_toff = d_hist2 + T;
+    uint64_t *d_sstart = d_toff + T;
+    uint32_t *d_scap = reinterpret_cast<uint32_t *>(d_sstart + T);
+    uint32_t *d_sfill = d_scap + T;
+    uint32_t *d_cap = d_sfill + T;
     uint32_t *d_fills = d_cap + ((T + 3) & ~3u);
     WorkUnit *d_units = reinterpret_cast<WorkUnit *>(d_fills + (uint64_t)T * W + 4 - ((uint64_t)T * W) % 4);
-    uint32_t *d_tmap = reinterpret_cast<uint32_t *>(d_units + max_units);
-    uint32_t *d_tile_of = d_tmap + T;
     const uint64_t nb = (n + TA_BATCH - 1) / TA_BATCH;
     const uint64_t sblocks = std::min<uint64_t>(nb, SAMPLE_BLOCKS);
     const uint64_t bstride = std::max<uint64_t>(TA_BATCH, (n / sblocks));
-    VH_HIP(hipMemsetAsync(d_hist, 0, 8 * (uint64_t)T, st));
+    VH_HIP(hipMemsetAsync(d_hist, 0, 16 * (uint64_t)T, st));
     {
         TimedScope ts("tile_sample");
         const size_t lds = 4 * (size_t)T;
         switch (nd_f64) {
-        case 1: hipLaunchKernelGGL(k_tile_sample<1>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist); break;
-        case 2: hipLaunchKernelGGL(k_tile_sample<2>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist); break;
-        case 3: hipLaunchKernelGGL(k_tile_sample<3>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist); break;
-        default: hipLaunchKernelGGL(k_tile_sample<0>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist);
+        case 1: hipLaunchKernelGGL(k_tile_sample<1>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist, d_hist2); break;
+        case 2: hipLaunchKernelGGL(k_tile_sample<2>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist, d_hist2); break;
+        case 3: hipLaunchKernelGGL(k_tile_sample<3>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist, d_hist2); break;
+        default: hipLaunchKernelGGL(k_tile_sample<0>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist, d_hist2);
         }
         VH_HIP(hipGetLastError());
     }
-    std::vector<uint64_t> hist(T);
-    VH_HIP(hipMemcpyAsync(hist.data(), d_hist, 8 * (uint64_t)T, hipMemcpyDeviceToHost, st));
+    std::vector<uint64_t> hist(2 * (uint64_t)T);
+    VH_HIP(hipMemcpyAsync(hist.data(), d_hist, 16 * (uint64_t)T, hipMemcpyDeviceToHost, st));
     VH_HIP(hipStreamSynchronize(st));
     uint64_t sampled = 0;
-    for (auto h : hist) sampled += h;
+    for (uint32_t t = 0; t < T; t++) sampled += hist[t];
     if (!sampled) return false;
 
-    // ---- resident plan: the H densest tiles get region ids 0..H-1 (owner o holds ids
-    // o*TPW .. o*TPW+TPW-1, dense and sparse ranks interleaved), cold tiles H..T-1
-    std::vector<uint32_t> tile_of(T), tmap(T);
-    for (uint32_t t = 0; t < T; t++) tile_of[t] = t;
-    uint32_t H = 0;
-    if (res) {
-        std::vector<uint32_t> order(T);
-        for (uint32_t t = 0; t < T; t++) order[t] = t;
-        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hist[a] > hist[b]; });
-        H = std::min<uint32_t>(T, rP * rTPW);
-        uint64_t hot_mass = 0;
-        for (uint32_t r = 0; r < H; r++) hot_mass += hist[order[r]];
-        if (hot_mass * 4 < sampled) res = false;  // < 25 % of the rows would stay on chip
-    }
-    if (res) {
-        std::vector<uint32_t> hot_ids(H);
-        for (uint32_t r = 0; r < H; r++) {
-            uint32_t id = r;
-            if (H == rP * rTPW) {  // every owner full: balance dense and sparse tiles
-                const uint32_t j = r / rP, q = r % rP;
-                const uint32_t o = (j & 1) ? rP - 1 - q : q;
-                id = o * rTPW + j;
-            }
-            hot_ids[r] = id;
-        }
-        std::vector<uint32_t> order(T);
-        for (uint32_t t = 0; t < T; t++) order[t] = t;
-        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hist[a] > hist[b]; });
-        std::vector<char> hot(T, 0);
-        for (uint32_t r = 0; r < H; r++) {
-            tile_of[hot_ids[r]] = order[r];
-            hot[order[r]] = 1;
-        }
-        uint32_t nid = H;
-        for (uint32_t t = 0; t < T; t++)
-            if (!hot[t]) tile_of[nid++] = t;
-        for (uint32_t id = 0; id < T; id++) tmap[tile_of[id]] = id;
-    }
-
-    // ---- region capacities per workgroup (by region id; hot ids have none)
-    const uint64_t rows_per_wg = ((n + W - 1) / W + TA_BATCH - 1) / TA_BATCH * TA_BATCH;
-    std::vector<uint32_t> cap(T);
-    std::vector<uint64_t> toff(T);
-    uint64_t stride = 0;
-    for (uint32_t id = 0; id < T; id++) {
-        const uint32_t t = tile_of[id];
-        const double e = (double)rows_per_wg * (double)hist[t] / (double)sampled;
+    // ---- region capacities per workgroup.  Pass-A workgroup w takes batches w, w + W,
+    // w + 2W, ... (TA_BATCH rows each), so every workgroup's rows are spread over the whole
+    // row range and its tile distribution is the global one whatever the row order (a sorted
+    // or clustered column would otherwise send a contiguous range's rows to a few tiles and
+    // overflow their regions).  Regions are sized for shuffled rows (Poisson spread); a
+    // workgroup's rows past its region go to the tile's spill area, sized from the spread the
+    // sample measures per batch-sized block (clustered rows: each block all in or all out of
+    // a tile) -- half the tile's expected rows when the rows are clustered.
+    const uint64_t kbat = (nb + W - 1) / W;  // batches per workgroup (at most)
+    const uint64_t rows_per_wg = kbat * TA_BATCH;
+    std::vector<uint32_t> cap(T), scap(T);
+    std::vector<uint64_t> toff(T), sstart(T);
+    uint64_t stride = 0, stotal = 0;
+    const double blocks = (double)sblocks;  // every sample block is TA_BATCH rows, like a batch
+    for (uint32_t t = 0; t < T; t++) {
+        const double p = (double)hist[t] / (double)sampled, e = (double)rows_per_wg * p;
         uint64_t c = (uint64_t)(e * 1.04 + 6.0 * std::sqrt(e + 1.0)) + 32;
         c = std::min<uint64_t>((c + 7) & ~uint64_t(7), rows_per_wg + 8);
-        if (res && id < H) c = 0;
-        cap[id] = (uint32_t)c;
-        toff[id] = stride;
+        cap[t] = (uint32_t)c;
+        toff[t] = stride;
         stride += c;
+        const double m = (double)hist[t] / blocks, var_b = std::max(0.0, (double)hist[T + t] / blocks - m * m);
+        const bool clustered = var_b > 4.0 * m + 1.0;
+        uint64_t sc = (uint64_t)(0.02 * (double)n * p) + TA_BATCH;
+        if (clustered) {
+            // whole batches land in a tile: a workgroup's batches in tile t ~ Poisson(K p_hi)
+            // (p_hi: p plus two standard errors of a block sample); spill = the expected
+            // excess over the region, x 2, for all workgroups (<= 1.25 n p_hi)
+            const double p_hi = std::min(1.0, p + 2.0 * std::sqrt(p * (1.0 - p) / blocks));
+            const double lam = (double)kbat * p_hi;
+            double excess = 0.0, pk = std::exp(-lam);
+            for (uint64_t x = 0; x <= kbat && (double)x <= lam + 12.0 * std::sqrt(lam) + 12.0; x++) {
+                if (x) pk *= lam / (double)x;
+                excess += pk * std::max(0.0, (double)x * TA_BATCH - (double)c);
+            }
+            sc = (uint64_t)std::min(1.25 * (double)n * p_hi, 2.0 * (double)W * excess) + 4 * TA_BATCH;
+        }
+        scap[t] = (uint32_t)std::min<uint64_t>((sc + 7) & ~uint64_t(7), (uint64_t)n + 8);
+        sstart[t] = stotal;
+        stotal += scap[t];
     }
-    // pass A keeps region positions in u32 (destination | overflow bit)
-    if (stride + rows_per_wg >= (uint64_t)DEST_OVERFLOW) return false;
-    const uint64_t total = stride * W;
+    // pass A keeps region positions in u32 (destination | overflow bit), spill entries below
+    // DEST_SPILL
+    if (stride + rows_per_wg >= (uint64_t)DEST_SPILL) return false;
+    if (stotal >= (uint64_t)DEST_SPILL) {  // very large launches: shrink the spill areas
+        const double f = (double)(DEST_SPILL - 8 * (uint64_t)T) / (double)stotal;
+        stotal = 0;
+        for (uint32_t t = 0; t < T; t++) {
+            scap[t] = (uint32_t)(((uint64_t)(scap[t] * f)) & ~uint64_t(7));
+            sstart[t] = stotal;
+            stotal += scap[t];
+        }
+    }
+    const uint64_t total = stride * W + stotal + 16;  // regions | spill areas | padding
     const int ebytes = flags_mode ? 4 : 2;
     ws.entries.ensure(total * ebytes);
     // 4-byte value slots when every summed column of a generic plan is <= 4 bytes (exact)
@@ -2178,104 +1774,33 @@ static int try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t 
     tp.cap = d_cap;
     tp.toff = d_toff;
     tp.fills = d_fills;
+    tp.spill_fill = d_sfill;
+    tp.spill_cap = d_scap;
+    tp.spill_start = d_sstart;
+    tp.spill_base = stride * W;
     tp.entries = ws.entries.ptr;
     for (int s = 0; s < nv; s++)
         tp.values[s] = vnarrow ? reinterpret_cast<double *>(ws.values.as<uint32_t>() + (uint64_t)s * total)
                                : ws.values.as<double>() + (uint64_t)s * total;
     VH_HIP(hipMemcpyAsync(d_cap, cap.data(), 4 * (uint64_t)T, hipMemcpyHostToDevice, st));
     VH_HIP(hipMemcpyAsync(d_toff, toff.data(), 8 * (uint64_t)T, hipMemcpyHostToDevice, st));
+    VH_HIP(hipMemcpyAsync(d_sstart, sstart.data(), 8 * (uint64_t)T, hipMemcpyHostToDevice, st));
+    VH_HIP(hipMemcpyAsync(d_scap, scap.data(), 4 * (uint64_t)T, hipMemcpyHostToDevice, st));
+    VH_HIP(hipMemsetAsync(d_sfill, 0, 4 * (uint64_t)T, st));
 
-    // ---- pass B work units: tiles split over ranges of pass-A workgroups by expected size
+    // ---- pass B work units: tiles split over ranges of pass-A workgroups by expected size;
+    // unit k of g of a tile also reads slice k of g of the tile's spill area
     std::vector<WorkUnit> units;
     const double target = std::max(1.0, (double)n / ((double)cu_count() * 4));
-    for (uint32_t id = res ? H : 0; id < T; id++) {
-        const double e = (double)n * (double)hist[tile_of[id]] / (double)sampled;
+    for (uint32_t t = 0; t < T; t++) {
+        const double e = (double)n * (double)hist[t] / (double)sampled;
         uint32_t g = (uint32_t)std::min<double>(W, std::max(1.0, std::ceil(e / target)));
-        for (uint32_t k = 0; k < g; k++) units.push_back({id, (uint32_t)((uint64_t)W * k / g), (uint32_t)((uint64_t)W * (k + 1) / g), 0});
+        for (uint32_t k = 0; k < g; k++)
+            units.push_back({t, (uint32_t)((uint64_t)W * k / g), (uint32_t)((uint64_t)W * (k + 1) / g), k | (g << 16)});
     }
     if (units.size() > max_units) fail(VH_ERR_RUNTIME, "tiled binning: work-unit table overflow");
     if (!units.empty())
         VH_HIP(hipMemcpyAsync(d_units, units.data(), sizeof(WorkUnit) * units.size(), hipMemcpyHostToDevice, st));
-
-    if (res) {
-        // ---- XCD-resident launch (replaces pass A; pass B only for the cold tiles)
-        const uint32_t P = rP, K = VH_RES_K, G = 8 * rP;
-        FusedAggs fr = fa;  // owner tiles: TPW * S cells per aggregator
-        uint64_t roff = 0;
-        for (int k = 0; k < fr.na; k++) {
-            roff = (roff + 7) & ~uint64_t(7);
-            fr.a[k].lds_off = (uint32_t)roff;
-            roff += S * rTPW * (fr.a[k].kind == VH_AGG_COUNT ? 4 : 8);
-        }
-        fr.lds_words = (uint32_t)(((roff + 15) & ~uint64_t(15)) / 4);
-        const uint64_t ctl_b = 256, ready_b = 4ull * 8 * P, cons_b = 4ull * 8 * P * P;
-        const uint64_t hdr_b = 4ull * 8 * P * K * RES_HDR, keys_b = 4ull * 8 * P * K * TA_BATCH;
-        const uint64_t vals_b = 8ull * 8 * P * K * TA_BATCH * (nv ? 1 : 0);
-        const uint64_t okey_b = 4ull * G * RES_OVF, oval_b = 8ull * G * RES_OVF;
-        auto al = [](uint64_t b) { return (b + 255) & ~uint64_t(255); };
-        const uint64_t flags_b = al(ctl_b) + al(ready_b) + al(cons_b);
-        ws.res.ensure(flags_b + al(hdr_b) + al(keys_b) + al(vals_b) + al(okey_b) + al(oval_b));
-        unsigned char *rb = ws.res.as<unsigned char>();
-        ResidentParams rp{};
-        rp.P = P;
-        rp.K = K;
-        rp.H = H;
-        rp.TPW = rTPW;
-        rp.nb = (uint32_t)(rows_per_wg / TA_BATCH);
-        rp.G = G;
-        rp.wt = rmode == 2 ? 1u : 0u;
-        rp.timeout = 200 * wall_clock_khz();  // 200 ms without progress
-        rp.ctl = reinterpret_cast<uint32_t *>(rb);
-        rp.ready = reinterpret_cast<uint32_t *>(rb + al(ctl_b));
-        rp.cons = reinterpret_cast<uint32_t *>(rb + al(ctl_b) + al(ready_b));
-        unsigned char *q = rb + flags_b;
-        rp.hdr = reinterpret_cast<uint32_t *>(q);
-        q += al(hdr_b);
-        rp.skeys = reinterpret_cast<uint32_t *>(q);
-        q += al(keys_b);
-        rp.svals = reinterpret_cast<double *>(q);
-        q += al(vals_b);
-        rp.ovf_key = reinterpret_cast<uint32_t *>(q);
-        q += al(okey_b);
-        rp.ovf_val = reinterpret_cast<double *>(q);
-        rp.tmap = d_tmap;
-        rp.tile_of = d_tile_of;
-        tp.tile_of = d_tile_of;
-        tp.abort_word = rp.ctl;
-        VH_HIP(hipMemcpyAsync(d_tmap, tmap.data(), 4 * (uint64_t)T, hipMemcpyHostToDevice, st));
-        VH_HIP(hipMemcpyAsync(d_tile_of, tile_of.data(), 4 * (uint64_t)T, hipMemcpyHostToDevice, st));
-        VH_HIP(hipMemsetAsync(rb, 0, flags_b, st));
-        const size_t lds = resident_lds_bytes(fr.lds_words, nv, T);
-        {
-            TimedScope ts("tile_resident");
-            switch (nd_f64 * 2 + nv) {
-            case 2: hipLaunchKernelGGL((k_tile_resident<1, 0>), dim3(G), dim3(RES_THREADS), lds, st, plan, fa, fr, tp, rp, n); break;
-            case 3: hipLaunchKernelGGL((k_tile_resident<1, 1>), dim3(G), dim3(RES_THREADS), lds, st, plan, fa, fr, tp, rp, n); break;
-            case 4: hipLaunchKernelGGL((k_tile_resident<2, 0>), dim3(G), dim3(RES_THREADS), lds, st, plan, fa, fr, tp, rp, n); break;
-            case 5: hipLaunchKernelGGL((k_tile_resident<2, 1>), dim3(G), dim3(RES_THREADS), lds, st, plan, fa, fr, tp, rp, n); break;
-            case 6: hipLaunchKernelGGL((k_tile_resident<3, 0>), dim3(G), dim3(RES_THREADS), lds, st, plan, fa, fr, tp, rp, n); break;
-            default: hipLaunchKernelGGL((k_tile_resident<3, 1>), dim3(G), dim3(RES_THREADS), lds, st, plan, fa, fr, tp, rp, n);
-            }
-            VH_HIP(hipGetLastError());
-        }
-        if (!units.empty()) {
-            TimedScope ts("tile_reduce");
-            const unsigned g = (unsigned)units.size();
-            if (nv == 0) hipLaunchKernelGGL(k_tile_reduce<0>, dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
-            else hipLaunchKernelGGL(k_tile_reduce<1>, dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
-            VH_HIP(hipGetLastError());
-        }
-        uint32_t state = 0;
-        VH_HIP(hipMemcpyAsync(&state, rp.ctl, 4, hipMemcpyDeviceToHost, st));
-        VH_HIP(hipStreamSynchronize(st));
-        if (state != RES_COMMIT) {
-            g_res_off.store(true);
-            fprintf(stderr, "vaexhip: XCD-resident tile launch not committed (state %u); two-pass tile path from now on\n",
-                    state);
-            return 2;
-        }
-        return 1;
-    }
 
     // ---- pass A
     {
@@ -2311,6 +1836,17 @@ static int try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t 
         VH_HIP(hipGetLastError());
     }
     return true;
+}
+
+uint64_t stat_tile_overflow(bool reset) {
+    unsigned long long v = 0;
+    VH_HIP(hipStreamSynchronize(stream()));
+    VH_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(d_tile_overflow_rows), sizeof(v)));
+    if (reset) {
+        const unsigned long long z = 0;
+        VH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(d_tile_overflow_rows), &z, sizeof(z)));
+    }
+    return v;
 }
 
 }  // namespace vh

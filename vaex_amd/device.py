@@ -43,10 +43,11 @@ class DeviceArray:
 
     @classmethod
     def random(cls, length, dist="normal", seed=0, a=0.0, b=1.0, dtype="float64"):
-        """Synthetic column generated in HBM: dist 'uniform' [a, b), 'normal' (mean a, sd b)
-        or 'randint' [a, b) (int32/int64)."""
+        """Synthetic column generated in HBM: dist 'uniform' [a, b), 'normal' (mean a, sd b),
+        'randint' [a, b) (int32/int64), or the sorted layouts 'sorted_normal' (ascending normal
+        quantiles, mean a, sd b) and 'sorted_int' ([a, b) in equal consecutive runs)."""
         d = cls(length, dtype)
-        code = {"uniform": 0, "normal": 1, "randint": 2}[dist]
+        code = {"uniform": 0, "normal": 1, "randint": 2, "sorted_normal": 3, "sorted_int": 4}[dist]
         dcode, _ = _lib.dtype_code(d.dtype)
         _lib.call("vh_fill_random", d.ptr, d.length, dcode, code, seed, float(a), float(b))
         return d
