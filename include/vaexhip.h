@@ -80,6 +80,9 @@ int vh_host_free(void *ptr, uint64_t bytes);
 /* Register a page-aligned host range (typically a column memory-mapped from a file) for
  * direct DMA: host columns whose chunks lie inside it stream to HBM with no bounce copy.
  * The range must stay mapped until vh_host_unregister(ptr) (which drains the device). */
+/* free the page-locked blocks the library caches for read-backs and pipeline buffers
+ * (capped per process: VAEX_AMD_PINNED_CACHE_MB, else 8 GiB / LOCAL_WORLD_SIZE) */
+int vh_host_cache_trim(void);
 int vh_host_register(void *ptr, uint64_t bytes);
 int vh_host_unregister(void *ptr);
 int vh_memcpy_htod(void *dst, const void *src, uint64_t bytes);

@@ -457,3 +457,109 @@ def minmax_f64(x):
     x = np.ascontiguousarray(x, dtype=np.float64)
     lib().or_minmax_f64(_ptr(x), len(x), ctypes.addressof(lo), ctypes.addressof(hi))
     return lo.value, hi.value
+
+
+# ---- multi-key / multi-aggregate groupby (groupby.py) -------------------------------------
+def _grouper(values, sort=True):
+    """Grouper of one key column with sort=True (groupby.py:97-168): the set's keys sorted
+    (NaN after the numbers, groupby.py:137-156), each row's ordinal into them.  Returns
+    (labels, ordinal per row)."""
+    values = np.asarray(values)
+    if values.dtype.kind == "f":
+        nan = np.isnan(values)
+        labels = np.unique(values[~nan])
+        ordinal = np.searchsorted(labels, values).astype(np.int64)
+        if nan.any():
+            ordinal[nan] = len(labels)
+            labels = np.append(labels, np.nan)
+        return labels, ordinal
+    labels, ordinal = np.unique(values, return_inverse=True)
+    return labels, ordinal.astype(np.int64)
+
+
+def _combine(ordinals, counts):
+    """_combine (groupby.py:248-288): the cartesian ordinal of as many leading groupers as
+    fit below 2**63 (first grouper most significant, cumulative_counts multipliers), made
+    into one GrouperCombined whose bins are the combined values that occur (a set, sorted);
+    the remaining groupers are combined with it recursively.  Returns (ordinal per row,
+    [per grouper: its ordinal of each combined group])."""
+    ords, ns = list(ordinals), list(counts)
+    take, prod = 1, ns[0]
+    while take < len(ns) and prod * ns[take] < 2 ** 63 - 1:
+        prod *= ns[take]
+        take += 1
+    cum = [1]
+    for nk in reversed(ns[1:take]):
+        cum.insert(0, cum[0] * nk)
+    combined = np.zeros(len(ords[0]), np.int64)
+    for o, m in zip(ords[:take], cum):
+        combined += o * np.int64(m)
+    bins, ordinal = np.unique(combined, return_inverse=True)
+    parts = [(bins // np.int64(m)) % np.int64(nk) for nk, m in zip(ns[:take], cum)]
+    if take == len(ns):
+        return ordinal.astype(np.int64), parts
+    inner, inner_parts = _combine([ordinal.astype(np.int64)] + ords[take:], [len(bins)] + ns[take:])
+    first = inner_parts[0]
+    return inner, [p[first] for p in parts] + inner_parts[1:]
+
+
+def groupby_agg(columns, by, aggs, combine="auto"):
+    """``df.groupby(by, sort=True, combine=combine).agg(...)`` restated on numpy
+    (groupby.py:97-168 Grouper, :248-288 _combine, :313-333 combine='auto', :484-533 agg):
+    groups in the lexicographic order of the sorted key labels, only the key combinations
+    that occur; aggregates per group as the superagg grids compute them in row order --
+    count(*) of every row, count(v) of the non-NaN rows, sum(v) upcast (float64 / int64 /
+    uint64, NaN skipped), mean = sum / count(v), min / max ignoring NaN (an all-NaN group
+    keeps the AggMin/AggMax fill, superagg.cpp:199-204,246-251).
+
+    columns: {name: numpy array}; by: key names; aggs: [(out_name, op, column or None)] with
+    op in count / sum / mean / min / max.  Returns {name: numpy array} with the key labels
+    first."""
+    by = [by] if isinstance(by, str) else list(by)
+    n = len(columns[by[0]])
+    groupers = [_grouper(columns[b]) for b in by]
+    counts = [len(g[0]) for g in groupers]
+    cells = int(np.prod([float(c) for c in counts]))
+    if len(by) >= 2 and (combine is True or (combine == "auto" and n / max(cells, 1) < 10)):
+        ordinal, parts = _combine([g[1] for g in groupers], counts)
+        ngroups = len(parts[0])
+        labels = [g[0][p] for g, p in zip(groupers, parts)]
+        keep = None
+    else:
+        # cartesian grid (C order of the ordinals = meshgrid 'ij'), empty cells dropped
+        ordinal = np.zeros(n, np.int64)
+        for g, c in zip(groupers, counts):
+            ordinal = ordinal * c + g[1]
+        ngroups = int(np.prod(counts))
+        present = np.bincount(ordinal, minlength=ngroups) > 0 if len(by) > 1 else np.ones(ngroups, bool)
+        keep = np.flatnonzero(present)
+        idx = np.unravel_index(keep, counts)
+        labels = [g[0][i] for g, i in zip(groupers, idx)]
+    out = {b: lab for b, lab in zip(by, labels)}
+    cnt_all = np.bincount(ordinal, minlength=ngroups)
+    for name, op, col in aggs:
+        if op == "count" and col is None:
+            r = cnt_all
+        else:
+            v = np.asarray(columns[col])
+            ok = ~np.isnan(v) if v.dtype.kind == "f" else np.ones(n, bool)
+            cnt = np.bincount(ordinal[ok], minlength=ngroups).astype(np.int64)
+            if op == "count":
+                r = cnt
+            elif op in ("sum", "mean"):
+                up = np.float64 if v.dtype.kind == "f" else (np.uint64 if v.dtype.kind in "ub" else np.int64)
+                s = np.zeros(ngroups, up)
+                np.add.at(s, ordinal[ok], v[ok].astype(up))
+                if op == "sum":
+                    r = s
+                else:
+                    with np.errstate(divide="ignore", invalid="ignore"):
+                        r = s.astype(np.float64) / cnt
+            elif op in ("min", "max"):
+                g, _ = new_grid(op, v.dtype.name, (ngroups,))
+                (np.minimum if op == "min" else np.maximum).at(g, ordinal[ok], v[ok])
+                r = g
+            else:
+                raise ValueError(op)
+        out[name] = r if keep is None else r[keep]
+    return out

@@ -3,23 +3,29 @@ combined on the GPU into one int64 cartesian ordinal (``vh_combine_keys``) and t
 single-key routes (dense grid, fused hash pass, set grouper for other aggregators), or,
 with >= 10 rows per cell, the cartesian grid of dense groupers.
 
-The checker is numpy: ``np.unique`` over the row tuples gives the groups in lexicographic
-order (the reference's ``sort=True`` order), ``np.bincount`` the counts and sums.  Counts,
-labels and integer sums are bit-exact; float sums within 1e-6 relative (north_star)."""
+The checker is the oracle's groupby restatement (oracle.groupby_agg: Grouper sort=True,
+_combine, GroupBy.agg; pinned by the reference's groupby KATs in test_oracle_kats.py): the
+groups in lexicographic order of the sorted labels (the reference's ``sort=True`` order),
+counts, sums, min / max per group.  Counts, labels, integer sums and min / max are
+bit-exact; float sums within 1e-6 relative (north_star)."""
 import numpy as np
 import pytest
+
+from oracle import oracle
 
 pytestmark = pytest.mark.gpu
 
 
-def _expected(keys, v):
-    tup = np.stack([k.astype(np.int64) for k in keys], axis=1)
-    uniq, inv = np.unique(tup, axis=0, return_inverse=True)
-    inv = inv.ravel()
-    ok = ~np.isnan(v)
-    return (uniq, np.bincount(inv, minlength=len(uniq)),
-            np.bincount(inv[ok], weights=v[ok], minlength=len(uniq)),
-            np.bincount(inv[ok], minlength=len(uniq)), inv)
+def _expected(keys, v, extra=()):
+    """(labels as an (n_groups, n_keys) int64 array, count(*), sum(v), count(v), *extra) from
+    the oracle; extra: more (name, op) aggregates of v."""
+    cols = {f"k{i}": k for i, k in enumerate(keys)}
+    cols["v"] = v
+    names = [f"k{i}" for i in range(len(keys))]
+    r = oracle.groupby_agg(cols, names, [("n", "count", None), ("s", "sum", "v"), ("c", "count", "v")] +
+                           [(name, op, "v") for name, op in extra])
+    uniq = np.stack([r[nm].astype(np.int64) for nm in names], axis=1)
+    return (uniq, r["n"], r["s"], r["c"]) + tuple(r[name] for name, _ in extra)
 
 
 def _frame(keys, v, device):
@@ -33,7 +39,7 @@ def _frame(keys, v, device):
 
 
 def _check(keys, v, res, sort_result=False):
-    uniq, cnt, s, nn, _ = _expected(keys, v)
+    uniq, cnt, s, nn = _expected(keys, v)
     names = [f"k{i}" for i in range(len(keys))]
     got = [res[n].to_numpy() for n in names]
     order = np.lexsort(got[::-1]) if sort_result else np.arange(len(got[0]))
@@ -121,16 +127,12 @@ def test_three_keys_mixed_dtypes_other_aggregators():
     df = _frame([k0, k1, k2], v, True)
     res = df.groupby(["k0", "k1", "k2"], agg={"lo": vaex_amd.agg.min("v"), "hi": vaex_amd.agg.max("v"),
                                               "n": "count"})
-    uniq, cnt, _, _, inv = _expected([k0, k1, k2], v)
+    uniq, cnt, _, _, lo, hi = _expected([k0, k1, k2], v, extra=(("lo", "min"), ("hi", "max")))
     got = [res[c].to_numpy() for c in ("k0", "k1", "k2")]
     order = np.lexsort(got[::-1])
     for j, g in enumerate(got):
         np.testing.assert_array_equal(g[order].astype(np.int64), uniq[:, j])
     np.testing.assert_array_equal(res["n"].to_numpy()[order], cnt)
-    lo = np.full(len(uniq), np.inf)
-    hi = np.full(len(uniq), -np.inf)
-    np.minimum.at(lo, inv, v)
-    np.maximum.at(hi, inv, v)
     np.testing.assert_array_equal(res["lo"].to_numpy()[order], lo)
     np.testing.assert_array_equal(res["hi"].to_numpy()[order], hi)
 

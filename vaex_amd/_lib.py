@@ -34,6 +34,7 @@ SIGNATURES = {
     "vh_free": (_i32, [_vp]),
     "vh_host_alloc": (_i32, [_p(_vp), _u64]),
     "vh_host_free": (_i32, [_vp, _u64]),
+    "vh_host_cache_trim": (_i32, []),
     "vh_host_register": (_i32, [_vp, _u64]),
     "vh_host_unregister": (_i32, [_vp]),
     "vh_memcpy_htod": (_i32, [_vp, _vp, _u64]),
@@ -254,7 +255,10 @@ def host_register(a):
     """Register the file mapping under a host column (vaex_amd.open maps HDF5 columns
     with mmap) once, so the binning pipeline DMAs its chunks in place instead of copying
     them into pinned bounce buffers.  The registration lives while any column array over
-    the mapping does (finalizers run before the arrays release the mapping).
+    the mapping does (finalizers run before the arrays release the mapping).  A bin() call
+    cannot race the unregistration: the binners / aggregators it reads hold their column
+    arrays (and so the root array) until they are destroyed, and vh_host_unregister drains
+    the device before it unpins.
     VH_HOST_REGISTER=0 turns this off.  Returns True when `a` lies in a registered mapping."""
     if os.environ.get("VH_HOST_REGISTER", "1") == "0" or not isinstance(a, np.ndarray) or a.nbytes < (64 << 20):
         return False

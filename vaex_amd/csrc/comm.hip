@@ -321,6 +321,7 @@ int vh_comm_destroy(vh_comm *c) {
         (void)hipStreamSynchronize(stream());
         if (c->comm) (void)ncclCommDestroy(c->comm);
         delete c;
+        host_cache_trim();  // the end of a distributed run: release the locked host memory
     }
     VH_API_END
 }

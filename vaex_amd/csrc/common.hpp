@@ -256,6 +256,7 @@ struct DevBuf {
 
 void *host_block_alloc(uint64_t bytes);  // page-locked, from the library's block cache
 void host_block_free(void *ptr, uint64_t bytes);
+void host_cache_trim();  // free every cached page-locked block
 
 // page-locked host buffer (DMA source of the H2D staging pipeline)
 struct PinnedBuf {

@@ -118,12 +118,30 @@ void dev_free(void *ptr, uint64_t bytes) {
 // pageable D2H runs at ~5-10 GB/s, page-locked at PCIe/xGMI rate, and hipHostMalloc itself
 // (and hipHostFree) are slow, so freed blocks are kept (sizes rounded to 64 KiB, <= 8 GiB
 // cached: a 1e8-group result is three 800 MB columns); the host pipeline's bounce buffers come from the same cache.
+// The cap is per process: VAEX_AMD_PINNED_CACHE_MB, else 8 GiB divided by the processes of
+// this node (LOCAL_WORLD_SIZE, one per GPU), so eight ranks keep at most 8 GiB locked in all.
 namespace {
-constexpr uint64_t HCACHE_MAX_BYTES = 8ull << 30;
 std::mutex g_hcache_mu;
 std::multimap<uint64_t, void *> g_hcache;
 uint64_t g_hcached = 0;
+uint64_t hcache_max_bytes() {
+    static const uint64_t cap = []() -> uint64_t {
+        if (const char *e = getenv("VAEX_AMD_PINNED_CACHE_MB")) return (uint64_t)strtoull(e, nullptr, 10) << 20;
+        uint64_t ranks = 1;
+        if (const char *e = getenv("LOCAL_WORLD_SIZE")) ranks = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+        return (8ull << 30) / ranks;
+    }();
+    return cap;
+}
 }  // namespace
+
+// return every cached page-locked block to the system (vh_host_cache_trim; vh_comm_destroy)
+void host_cache_trim() {
+    std::lock_guard<std::mutex> lk(g_hcache_mu);
+    for (auto &kv : g_hcache) (void)hipHostFree(kv.second);
+    g_hcache.clear();
+    g_hcached = 0;
+}
 
 static uint64_t host_round(uint64_t bytes) { return (std::max<uint64_t>(bytes, 1) + 65535) & ~uint64_t(65535); }
 
@@ -153,7 +171,7 @@ void host_block_free(void *ptr, uint64_t bytes) {
     const uint64_t b = host_round(bytes);
     {
         std::lock_guard<std::mutex> lk(g_hcache_mu);
-        if (g_hcached + b <= HCACHE_MAX_BYTES) {
+        if (g_hcached + b <= hcache_max_bytes()) {
             g_hcache.emplace(b, ptr);
             g_hcached += b;
             return;
@@ -480,6 +498,12 @@ int vh_host_alloc(void **ptr, uint64_t bytes) {
 int vh_host_free(void *ptr, uint64_t bytes) {
     VH_API_BEGIN
     host_block_free(ptr, bytes);
+    VH_API_END
+}
+
+int vh_host_cache_trim(void) {
+    VH_API_BEGIN
+    host_cache_trim();
     VH_API_END
 }
 

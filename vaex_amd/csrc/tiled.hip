@@ -272,18 +272,34 @@ __device__ unsigned long long d_tile_overflow_rows;
 
 template <int ND>
 __global__ __launch_bounds__(TA_THREADS) void k_tile_sample(BinPlan p, uint64_t n, uint32_t s_log2, uint32_t ntiles,
-                                                            uint64_t block_stride, uint64_t *hist, uint64_t *hist2) {
+                                                            uint64_t block_stride, uint64_t *hist, uint64_t *hist2,
+                                                            uint32_t *brange) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
     uint32_t *h = reinterpret_cast<uint32_t *>(lds_raw);
+    __shared__ uint32_t s_lo, s_hi;
     for (uint32_t t = threadIdx.x; t < ntiles; t += TA_THREADS) h[t] = 0;
+    if (threadIdx.x == 0) {
+        s_lo = ~0u;
+        s_hi = 0;
+    }
     __syncthreads();
     const uint64_t row0 = blockIdx.x * block_stride;
+    uint32_t lo = ~0u, hi = 0;
     for (uint64_t r = threadIdx.x; r < TA_BATCH; r += TA_THREADS) {
         const uint64_t i = row0 + r;
         if (i >= n) break;
-        atomicAdd(&h[cell_of<ND>(p, i) >> s_log2], 1u);
+        const uint32_t t = (uint32_t)(cell_of<ND>(p, i) >> s_log2);
+        atomicAdd(&h[t], 1u);
+        lo = min(lo, t);
+        hi = max(hi, t);
     }
+    atomicMin(&s_lo, lo);  // the block's tile range: sorted rows give ranges in order
+    atomicMax(&s_hi, hi);
     __syncthreads();
+    if (threadIdx.x == 0) {
+        brange[2 * blockIdx.x] = s_lo;
+        brange[2 * blockIdx.x + 1] = s_hi;
+    }
     for (uint32_t t = threadIdx.x; t < ntiles; t += TA_THREADS)
         if (h[t]) {  // per-tile count and its square: the block-to-block spread (clustering)
             atomicAdd((unsigned long long *)&hist[t], (unsigned long long)h[t]);
@@ -1659,7 +1675,8 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     DevBuf &meta = ws.meta;
     const uint64_t meta_bytes = 8 * (uint64_t)T /*hist*/ + 8 * (uint64_t)T /*hist2*/ + 8 * (uint64_t)T /*toff*/ +
                                 8 * (uint64_t)T /*spill_start*/ + 4 * (uint64_t)T /*spill_cap*/ + 4 * (uint64_t)T /*spill_fill*/ +
-                                4 * (uint64_t)T /*cap*/ + 4 * (uint64_t)T * W /*fills*/ + 16 * max_units /*units*/ + 256;
+                                4 * (uint64_t)T /*cap*/ + 4 * (uint64_t)T * W /*fills*/ + 16 * max_units /*units*/ +
+                                8 * (uint64_t)SAMPLE_BLOCKS /*brange*/ + 256;
     meta.ensure(meta_bytes);
     unsigned char *mb = meta.as<unsigned char>();
     uint64_t *d_hist = reinterpret_cast<uint64_t *>(mb);
@@ -1671,6 +1688,7 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     uint32_t *d_cap = d_sfill + T;
     uint32_t *d_fills = d_cap + ((T + 3) & ~3u);
     WorkUnit *d_units = reinterpret_cast<WorkUnit *>(d_fills + (uint64_t)T * W + 4 - ((uint64_t)T * W) % 4);
+    uint32_t *d_brange = reinterpret_cast<uint32_t *>(d_units + max_units);
     const uint64_t nb = (n + TA_BATCH - 1) / TA_BATCH;
     const uint64_t sblocks = std::min<uint64_t>(nb, SAMPLE_BLOCKS);
     const uint64_t bstride = std::max<uint64_t>(TA_BATCH, (n / sblocks));
@@ -1679,16 +1697,27 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         TimedScope ts("tile_sample");
         const size_t lds = 4 * (size_t)T;
         switch (nd_f64) {
-        case 1: hipLaunchKernelGGL(k_tile_sample<1>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist, d_hist2); break;
-        case 2: hipLaunchKernelGGL(k_tile_sample<2>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist, d_hist2); break;
-        case 3: hipLaunchKernelGGL(k_tile_sample<3>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist, d_hist2); break;
-        default: hipLaunchKernelGGL(k_tile_sample<0>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist, d_hist2);
+        case 1: hipLaunchKernelGGL(k_tile_sample<1>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist, d_hist2, d_brange); break;
+        case 2: hipLaunchKernelGGL(k_tile_sample<2>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist, d_hist2, d_brange); break;
+        case 3: hipLaunchKernelGGL(k_tile_sample<3>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist, d_hist2, d_brange); break;
+        default: hipLaunchKernelGGL(k_tile_sample<0>, dim3(sblocks), dim3(TA_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist, d_hist2, d_brange);
         }
         VH_HIP(hipGetLastError());
     }
     std::vector<uint64_t> hist(2 * (uint64_t)T);
+    std::vector<uint32_t> brange(2 * sblocks);
     VH_HIP(hipMemcpyAsync(hist.data(), d_hist, 16 * (uint64_t)T, hipMemcpyDeviceToHost, st));
+    VH_HIP(hipMemcpyAsync(brange.data(), d_brange, 8 * sblocks, hipMemcpyDeviceToHost, st));
     VH_HIP(hipStreamSynchronize(st));
+    // sample blocks whose tile ranges follow each other (a column sorted, up or down, along
+    // the grid index): each workgroup's evenly spaced batches then meet a tile floor or ceil
+    // of K p_t times, and p_t is exact to a block
+    uint64_t up = 0, down = 0;
+    for (uint64_t b = 0; b + 1 < sblocks; b++) {
+        up += brange[2 * b + 1] > brange[2 * b + 2];    // block b ends past block b + 1's start
+        down += brange[2 * b] < brange[2 * b + 3];
+    }
+    const bool monotone = sblocks > 8 && std::min(up, down) * 100 <= sblocks;
     uint64_t sampled = 0;
     for (uint32_t t = 0; t < T; t++) sampled += hist[t];
     if (!sampled) return false;
@@ -1707,17 +1736,29 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     std::vector<uint64_t> toff(T), sstart(T);
     uint64_t stride = 0, stotal = 0;
     const double blocks = (double)sblocks;  // every sample block is TA_BATCH rows, like a batch
+    // clustered rows (block variance well above the Poisson value: each sample block all in
+    // or all out of a tile) anywhere in the sample
+    bool any_clustered = false;
+    for (uint32_t t = 0; t < T; t++) {
+        const double m = (double)hist[t] / blocks, var_b = std::max(0.0, (double)hist[T + t] / blocks - m * m);
+        any_clustered = any_clustered || var_b > 4.0 * m + 1.0;
+    }
     for (uint32_t t = 0; t < T; t++) {
         const double p = (double)hist[t] / (double)sampled, e = (double)rows_per_wg * p;
-        uint64_t c = (uint64_t)(e * 1.04 + 6.0 * std::sqrt(e + 1.0)) + 32;
+        const double m = (double)hist[t] / blocks, var_b = std::max(0.0, (double)hist[T + t] / blocks - m * m);
+        const bool clustered = var_b > 4.0 * m + 1.0;
+        // a clustered tile gets one batch of slack: a workgroup's evenly spaced batches meet a
+        // sorted column's tile floor or ceil of K p_t times
+        uint64_t c = (uint64_t)(e * 1.04 + 6.0 * std::sqrt(e + 1.0)) + 32 + (clustered ? TA_BATCH : 0);
         c = std::min<uint64_t>((c + 7) & ~uint64_t(7), rows_per_wg + 8);
         cap[t] = (uint32_t)c;
         toff[t] = stride;
         stride += c;
-        const double m = (double)hist[t] / blocks, var_b = std::max(0.0, (double)hist[T + t] / blocks - m * m);
-        const bool clustered = var_b > 4.0 * m + 1.0;
         uint64_t sc = (uint64_t)(0.02 * (double)n * p) + TA_BATCH;
-        if (clustered) {
+        // a tile the sample missed between two clustered sample blocks holds at most the rows
+        // between them
+        if (any_clustered && hist[t] == 0) sc = std::min<uint64_t>(n, bstride) + TA_BATCH;
+        if (clustered && !monotone) {
             // whole batches land in a tile: a workgroup's batches in tile t ~ Poisson(K p_hi)
             // (p_hi: p plus two standard errors of a block sample); spill = the expected
             // excess over the region, x 2, for all workgroups (<= 1.25 n p_hi)
