@@ -545,7 +545,7 @@ def bench_groupby(n, args, layout="random"):
     df = vaex_amd.from_arrays(key=keys, v=v)
     out = {"rows": n, "algorithmic_bytes_per_row": 12, "layout": layout}
     names = ["minmax", "tile_sample", "tile_scatter", "tile_scatter_ord", "tile_scatter_set", "tile_reduce", "ha_sample",
-             "ha_scatter", "ha_scatter_f64", "ha_reduce", "ha_finish", "set_sample", "set_insert", "set_reduce", "set_rank",
+             "ha_scatter", "ha_scatter_f64", "ha_reduce", "ha_finish", "ha_first", "set_sample", "set_insert", "set_reduce", "set_rank",
              "bin_fused_global"]
 
     def run(mode):

@@ -218,6 +218,13 @@ int vh_hashagg_finish(vh_hashagg *h, uint64_t *ngroups);
  * any output may be host or HBM memory (a caller that decodes combined multi-key keys on the
  * device keeps them there) */
 int vh_hashagg_read(vh_hashagg *h, int64_t *keys, int64_t *counts, void *const *sums, int64_t *const *nonnull);
+/* after vh_hashagg_finish: reorder the groups by the row each key first appears at -- the
+ * ordinal order of an ordered_set built over the same keys (hash_primitives.hpp:96-281,289-312;
+ * groupby(key, assume_sparse=True, sort=False), groupby.py:97-168) -- so vh_hashagg_read
+ * returns them in that order.  `keys` is the whole key column the updates saw, in order (n =
+ * their total rows).  A prefix of the rows is scanned until every group has its first row
+ * (run heads only); keys that first appear late fall back to an ordered_set over all rows. */
+int vh_hashagg_order_first(vh_hashagg *h, const void *keys, uint64_t n, int loc);
 /* ---- multi-GPU (comm.hip): RCCL bound by the library, one process per GPU ----------
  * The reference has no multi-process path; its ExecutorLocal reduces per-thread task
  * parts serially (execution.py:285, Aggregator::reduce superagg.cpp:160-167,205-212,

@@ -38,7 +38,7 @@ for name, lim in (("bin", [-5.0, 5.0]), ("minmax+bin", None)):
         df.count(binby="x", shape=256, limits=lim)
     _lib.synchronize()
     _lib.timing_enable(False)
-    for k in ("minmax", "bin_cells", "bin_aggregate_lds", "bin_fused_lds", "bin_fused_global", "bin_reduce0"):
+    for k in ("minmax", "bin_cells", "bin_aggregate_lds", "bin_fused_lds", "bin_fused_global", "bin_reduce0", "bin_small_f64"):
         c, ms = _lib.timing_read(k)
         if c:
             print(f"   kernel {k:20s} {c / 50:4.1f}/query {ms / c * 1e3:8.2f} us")

@@ -631,6 +631,131 @@ __global__ __launch_bounds__(256) void k_fused(BinPlan p, FusedAggs fa, uint64_t
 
 
 // ============================================================================
+// device: small grids of float64 scalar binners with count / float64-sum aggregators
+// (C1: df.count(binby='x', shape=256), agg.hpp:106-136 over a grid that fits LDS).  Each
+// lane takes two rows per 16-B load of every column (SG_U loads in flight), bins them with
+// the reference's scalar math, adds into the workgroup's LDS sub-grids, and the workgroup
+// writes its sub-grids out as partials (plain stores): with a few hundred cells every
+// workgroup touches every hot cell, and one global atomic per (workgroup, cell) serialised
+// on those cells cost more than the scan.  k_small_f64_fin folds the partials, CHUNK
+// workgroups per lane, with one atomic per (chunk, cell).
+// ============================================================================
+constexpr int SG_U = 4;
+constexpr unsigned SG_FIN_CHUNK = 64;
+struct SmallF64 {
+    int32_t na, ncol;
+    uint32_t lds_words, pad;
+    const double2 *col[MAX_FUSED_AGGS];  // distinct aggregator data columns (16-B aligned)
+    int8_t acol[MAX_FUSED_AGGS], akind[MAX_FUSED_AGGS];
+    uint32_t lds_off[MAX_FUSED_AGGS];    // byte offset of each aggregator's sub-grid
+    void *grid[MAX_FUSED_AGGS];
+};
+
+template <int ND, int NC>
+__device__ inline void sg_row(const BinPlan &p, const SmallF64 &s, unsigned char *lds, const double *bx,
+                              const double *ax) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int d = 0; d < ND; d++) c += (uint32_t)scalar_cell<double>(p.b[d], bx[d], false) * (uint32_t)p.b[d].stride;
+#pragma unroll
+    for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+        if (k >= s.na) break;
+        double v = 0.0;  // count(*) reads nothing (selected by compare: no indexed registers)
+#pragma unroll
+        for (int q = 0; q < NC; q++)
+            if (q == s.acol[k]) v = ax[q];
+        if (v != v) continue;  // count(expr) skips NaN, sum skips NaN
+        if (s.akind[k] == VH_AGG_COUNT)
+            atomicAdd(reinterpret_cast<uint32_t *>(lds + s.lds_off[k]) + c, 1u);
+        else
+            atomicAdd(reinterpret_cast<double *>(lds + s.lds_off[k]) + c, v);
+    }
+}
+
+template <int ND, int NC>
+__global__ __launch_bounds__(256) void k_small_f64(BinPlan p, SmallF64 s, uint64_t n, uint32_t *part) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    uint32_t *w = reinterpret_cast<uint32_t *>(lds_raw);
+    for (uint32_t i = threadIdx.x; i < s.lds_words; i += blockDim.x) w[i] = 0;
+    __syncthreads();
+    const uint64_t nvec = n / 2, stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t v = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    for (; v + (SG_U - 1) * stride < nvec; v += SG_U * stride) {
+        double2 b[ND][SG_U], a[NC > 0 ? NC : 1][SG_U];
+#pragma unroll
+        for (int d = 0; d < ND; d++)
+#pragma unroll
+            for (int u = 0; u < SG_U; u++) b[d][u] = reinterpret_cast<const double2 *>(p.b[d].data)[v + u * stride];
+#pragma unroll
+        for (int q = 0; q < NC; q++)
+#pragma unroll
+            for (int u = 0; u < SG_U; u++) a[q][u] = s.col[q][v + u * stride];
+#pragma unroll
+        for (int u = 0; u < SG_U; u++) {
+            double bx[ND], ax[NC > 0 ? NC : 1];
+#pragma unroll
+            for (int d = 0; d < ND; d++) bx[d] = b[d][u].x;
+#pragma unroll
+            for (int q = 0; q < NC; q++) ax[q] = a[q][u].x;
+            sg_row<ND, NC>(p, s, lds_raw, bx, ax);
+#pragma unroll
+            for (int d = 0; d < ND; d++) bx[d] = b[d][u].y;
+#pragma unroll
+            for (int q = 0; q < NC; q++) ax[q] = a[q][u].y;
+            sg_row<ND, NC>(p, s, lds_raw, bx, ax);
+        }
+    }
+    // the rest of the pairs one at a time, then the odd last row (block 0, lane 0)
+    for (; v < nvec; v += stride) {
+        double2 b2[ND], a2[NC > 0 ? NC : 1];
+        double bx[ND], ax[NC > 0 ? NC : 1];
+#pragma unroll
+        for (int d = 0; d < ND; d++) b2[d] = reinterpret_cast<const double2 *>(p.b[d].data)[v];
+#pragma unroll
+        for (int q = 0; q < NC; q++) a2[q] = s.col[q][v];
+#pragma unroll
+        for (int d = 0; d < ND; d++) bx[d] = b2[d].x;
+#pragma unroll
+        for (int q = 0; q < NC; q++) ax[q] = a2[q].x;
+        sg_row<ND, NC>(p, s, lds_raw, bx, ax);
+#pragma unroll
+        for (int d = 0; d < ND; d++) bx[d] = b2[d].y;
+#pragma unroll
+        for (int q = 0; q < NC; q++) ax[q] = a2[q].y;
+        sg_row<ND, NC>(p, s, lds_raw, bx, ax);
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+        double bx[ND], ax[NC > 0 ? NC : 1];
+#pragma unroll
+        for (int d = 0; d < ND; d++) bx[d] = reinterpret_cast<const double *>(p.b[d].data)[n - 1];
+#pragma unroll
+        for (int q = 0; q < NC; q++) ax[q] = reinterpret_cast<const double *>(s.col[q])[n - 1];
+        sg_row<ND, NC>(p, s, lds_raw, bx, ax);
+    }
+    __syncthreads();
+    uint32_t *dst = part + (uint64_t)blockIdx.x * s.lds_words;
+    for (uint32_t i = threadIdx.x; i < s.lds_words; i += blockDim.x) dst[i] = w[i];
+}
+
+// grid (cells / 256, chunks of SG_FIN_CHUNK workgroups, aggregators): fold partials in order
+__global__ __launch_bounds__(256) void k_small_f64_fin(SmallF64 s, const uint32_t *part, unsigned nb, uint64_t L) {
+    const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const int k = blockIdx.z;
+    if (c >= L) return;
+    const unsigned b0 = blockIdx.y * SG_FIN_CHUNK, b1 = min(nb, b0 + SG_FIN_CHUNK);
+    if (s.akind[k] == VH_AGG_COUNT) {
+        uint64_t t = 0;
+        for (unsigned b = b0; b < b1; b++) t += part[(uint64_t)b * s.lds_words + s.lds_off[k] / 4 + c];
+        if (t) atomicAdd(reinterpret_cast<unsigned long long *>(s.grid[k]) + c, (unsigned long long)t);
+    } else {
+        double t = 0.0;
+        for (unsigned b = b0; b < b1; b++)
+            t += reinterpret_cast<const double *>(part + (uint64_t)b * s.lds_words + s.lds_off[k] / 4)[c];
+        if (t != 0.0) atomicAdd(reinterpret_cast<double *>(s.grid[k]) + c, t);
+    }
+}
+
+// ============================================================================
 // device: 0-d aggregation -- no binners (df.count() / df.sum('w') / df.mean('w'); the
 // reference's Grid::bin with a length and no binners, agg.hpp:76-105, puts every row in
 // cell 0), so the grid is a reduction: 16-B loads of each distinct float64 column
@@ -862,7 +987,8 @@ void init_agg_grid(vh_agg *a) {
         VH_HIP(hipMemsetAsync(a->s_key.ptr, 0xff, L * 8, stream()));
         VH_HIP(hipMemsetAsync(a->s_row.ptr, 0xff, L * 8, stream()));
     }
-    VH_HIP(hipStreamSynchronize(stream()));
+    // no host wait: every later use of the grid is ordered after the fills on the library
+    // stream, and every host read (download, device_ptr users) synchronises the stream
 }
 
 // chunk-relative device pointer of a column: HBM columns in place, host columns from the
@@ -1211,8 +1337,17 @@ int vh_agg_download(vh_agg *a, void *host, uint64_t bytes) {
     std::lock_guard<std::mutex> lk(a->grid->mu);
     if (bytes != a->grid->length1d * a->grid_isz) fail(VH_ERR_ARG, "download size mismatch");
     nunique_finalize(a);
-    VH_HIP(hipMemcpyAsync(host, a->g.ptr, bytes, hipMemcpyDeviceToHost, stream()));
-    VH_HIP(hipStreamSynchronize(stream()));
+    if (bytes <= (1u << 20)) {
+        // small grids through a page-locked block: a pageable read-back is a staged copy
+        thread_local PinnedBuf small;
+        small.ensure(1u << 20);
+        VH_HIP(hipMemcpyAsync(small.ptr, a->g.ptr, bytes, hipMemcpyDeviceToHost, stream()));
+        VH_HIP(hipStreamSynchronize(stream()));
+        memcpy(host, small.ptr, bytes);
+    } else {
+        VH_HIP(hipMemcpyAsync(host, a->g.ptr, bytes, hipMemcpyDeviceToHost, stream()));
+        VH_HIP(hipStreamSynchronize(stream()));
+    }
     VH_API_END
 }
 
@@ -1250,6 +1385,7 @@ int vh_agg_device_ptr(vh_agg *a, void **grid_dptr, void **grid2_dptr) {
     VH_API_BEGIN
     std::lock_guard<std::mutex> lk(a->grid->mu);
     nunique_finalize(a);
+    VH_HIP(hipStreamSynchronize(stream()));  // the grid's fills and bins are done for any stream
     if (grid_dptr) *grid_dptr = a->g.ptr;
     if (grid2_dptr) *grid2_dptr = a->g2.ptr;
     VH_API_END
@@ -1782,6 +1918,61 @@ static bool launch_reduce0(const FusedAggs &fa, uint64_t n, Workspace &ws) {
     return true;
 }
 
+// small grids over float64 scalar binners (k_small_f64): false when a column is masked or
+// not 16-B aligned (k_fused takes it)
+static bool launch_small_f64(const BinPlan &plan, const FusedAggs &fa, uint64_t n, uint64_t cells, int nd_f64,
+                             Workspace &ws) {
+    if (nd_f64 < 1 || nd_f64 > 3 || n < 2) return false;
+    for (int d = 0; d < plan.nb; d++)
+        if (plan.b[d].mask || (reinterpret_cast<uintptr_t>(plan.b[d].data) & 15)) return false;
+    SmallF64 s{};
+    s.na = fa.na;
+    s.lds_words = fa.lds_words;
+    for (int k = 0; k < fa.na; k++) {
+        const FusedAgg &a = fa.a[k];
+        if (a.mask) return false;
+        s.akind[k] = (int8_t)a.kind;
+        s.lds_off[k] = a.lds_off;
+        s.grid[k] = a.grid;
+        s.acol[k] = -1;
+        if (a.data) {
+            if (reinterpret_cast<uintptr_t>(a.data) & 15) return false;
+            int q = 0;
+            while (q < s.ncol && s.col[q] != reinterpret_cast<const double2 *>(a.data)) q++;
+            if (q == s.ncol) s.col[s.ncol++] = reinterpret_cast<const double2 *>(a.data);
+            s.acol[k] = (int8_t)q;
+        }
+    }
+    if (s.ncol > 2) return false;
+    const uint64_t lds_bytes = 4ull * fa.lds_words;
+    const unsigned per_cu = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8, (64 * 1024) / std::max<uint64_t>(lds_bytes, 1)));
+    // at least two unrolled steps per lane before a workgroup pays its sub-grid flush
+    const unsigned nb = blocks_for((n / 2 + 2 * SG_U - 1) / (2 * SG_U), 256, per_cu);
+    ws.idx.ensure((uint64_t)nb * lds_bytes);
+    uint32_t *part = ws.idx.as<uint32_t>();
+    TimedScope ts("bin_small_f64");
+    const dim3 grd(nb), blk(256);
+#define VH_SG(ND, NC) hipLaunchKernelGGL((k_small_f64<ND, NC>), grd, blk, lds_bytes, stream(), plan, s, n, part)
+#define VH_SG_NC(ND) \
+    switch (s.ncol) { \
+    case 0: VH_SG(ND, 0); break; \
+    case 1: VH_SG(ND, 1); break; \
+    default: VH_SG(ND, 2); \
+    }
+    switch (nd_f64) {
+    case 1: VH_SG_NC(1); break;
+    case 2: VH_SG_NC(2); break;
+    default: VH_SG_NC(3);
+    }
+#undef VH_SG_NC
+#undef VH_SG
+    VH_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_small_f64_fin, dim3((unsigned)((cells + 255) / 256), (nb + SG_FIN_CHUNK - 1) / SG_FIN_CHUNK, fa.na),
+                       blk, 0, stream(), s, part, nb, cells);
+    VH_HIP(hipGetLastError());
+    return true;
+}
+
 void launch_fused(const BinPlan &plan, FusedAggs &fa, uint64_t n, uint64_t cells, int nd_f64, Workspace &ws) {
     if (plan.nb == 0 && cells == 1 && launch_reduce0(fa, n, ws)) return;
     // LDS-privatised sub-grids when every aggregator's grid fits (u32 counts, f64 sums)
@@ -1796,6 +1987,7 @@ void launch_fused(const BinPlan &plan, FusedAggs &fa, uint64_t n, uint64_t cells
     fa.lds_words = (uint32_t)(lds_bytes / 4);
     if (!use_lds && hashagg_bin_set_ordinal(plan, fa, n)) return;
     if (!use_lds && try_tiled(plan, fa, n, cells, nd_f64, ws)) return;
+    if (use_lds && launch_small_f64(plan, fa, n, cells, nd_f64, ws)) return;
     const int per_cu = use_lds ? (int)std::max<uint64_t>(1, std::min<uint64_t>(8, (64 * 1024) / std::max<uint64_t>(lds_bytes, 1))) : 8;
     dim3 grd(blocks_for(n, 256, per_cu)), blk(256);
     const size_t shm = use_lds ? lds_bytes : 0;

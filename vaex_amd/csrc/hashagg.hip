@@ -1335,6 +1335,124 @@ __global__ __launch_bounds__(256) void k_ha_gather(HaTable g, const KB *skey, co
     }
 }
 
+// ---- first-appearance order of the groups (groupby(key, assume_sparse=True) with sort=False:
+// the ordered_set's ordinal order, hash_primitives.hpp:96-281, without building the set) ----
+// gidx[slot] = the group's index in the key-sorted result
+__global__ __launch_bounds__(256) void k_ha_gidx(const uint32_t *sslot, uint64_t m, uint32_t *gidx) {
+    for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) gidx[sslot[j]] = (uint32_t)j;
+}
+
+// Rows [r0, r1): a row whose key differs from the row before it (a run head; every other row
+// cannot be its key's first) probes the HBM table read-only and lowers its group's first row.
+// stats[0] += groups seen for the first time, stats[1] += run heads, stats[2] |= 1 if a key is
+// missing from the table (the caller passed another column).
+// one row of the scan: a run head probes the table read-only and lowers its group's first row
+template <typename K>
+__device__ inline void ha_first_row(K k, uint64_t row, const HaTable &g, const uint32_t *gidx,
+                                    unsigned long long *first, uint32_t &newly, uint32_t &lost) {
+    const uint64_t kb = (uint64_t)ha_kb<K>(k);
+    uint64_t s = g.mask + 1;
+    if (kb != SET_EMPTY) {
+        s = hash64(kb) & g.mask;
+        int p = 0;
+        for (; p < HA_MAX_PROBE; p++) {
+            const uint64_t cur = g.keys[s];
+            if (cur == kb) break;
+            if (cur == SET_EMPTY) {
+                p = HA_MAX_PROBE;
+                break;
+            }
+            s = (s + 1) & g.mask;
+        }
+        if (p == HA_MAX_PROBE) {
+            lost = 1;
+            return;
+        }
+    }
+    unsigned long long *f = first + gidx[s];
+    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= row) return;
+    newly += atomicMin(f, (unsigned long long)row) == ~0ull;
+}
+
+// Rows [0, nrow) of a chunk starting at global row `base` (keys 16-B aligned; keys[-1] is
+// readable when base > 0): a lane takes 16 B of consecutive keys per step, two steps in
+// flight; a row whose key differs from the row before it (a run head -- every other row
+// cannot be its key's first) probes the HBM table.  stats[0] += groups seen for the first
+// time, stats[1] += run heads, stats[2] |= 1 if a key is missing from the table (the caller
+// passed another column).
+template <typename K>
+__global__ __launch_bounds__(256) void k_ha_first(const K *keys, uint64_t nrow, uint64_t base, HaTable g,
+                                                  const uint32_t *gidx, unsigned long long *first,
+                                                  unsigned long long *stats) {
+    constexpr int V = 16 / sizeof(K);
+    struct alignas(16) Vec { K k[V]; };
+    const Vec *src = reinterpret_cast<const Vec *>(keys);
+    uint32_t newly = 0, heads = 0, lost = 0;
+    const uint64_t nvec = nrow / V, stride = (uint64_t)gridDim.x * 256;
+    auto vec = [&](uint64_t v, const Vec &x) {
+        K prev = x.k[0];
+        bool has_prev = base + v * V > 0;
+        if (has_prev) prev = keys[v * V - 1];
+#pragma unroll
+        for (int j = 0; j < V; j++) {
+            const bool head = j ? x.k[j] != x.k[j - 1] : (!has_prev || x.k[0] != prev);
+            if (head) {
+                heads++;
+                ha_first_row<K>(x.k[j], base + v * V + j, g, gidx, first, newly, lost);
+            }
+        }
+    };
+    uint64_t v = blockIdx.x * 256ull + threadIdx.x;
+    for (; v + stride < nvec; v += 2 * stride) {
+        const Vec a = src[v], b = src[v + stride];
+        vec(v, a);
+        vec(v + stride, b);
+    }
+    for (; v < nvec; v += stride) vec(v, src[v]);
+    // the last nrow % V rows
+    for (uint64_t i = nvec * V + blockIdx.x * 256ull + threadIdx.x; i < nrow; i += stride) {
+        const K k = keys[i];
+        if (base + i > 0 && keys[i - 1] == k) continue;
+        heads++;
+        ha_first_row<K>(k, base + i, g, gidx, first, newly, lost);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        newly += __shfl_xor(newly, off, 64);
+        heads += __shfl_xor(heads, off, 64);
+        lost |= __shfl_xor(lost, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (newly) atomicAdd(&stats[0], (unsigned long long)newly);
+        if (heads) atomicAdd(&stats[1], (unsigned long long)heads);
+        if (lost) atomicOr(&stats[2], 1ull);
+    }
+}
+
+// fallback ranks: the ordinal of each group's key in an ordered_set built over all rows
+__global__ __launch_bounds__(256) void k_ha_set_rank(const int64_t *okey, uint64_t m, int kisz, SetDev set,
+                                                     unsigned long long *rank) {
+    for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) {
+        uint64_t kb = (uint64_t)okey[j];
+        if (kisz < 8) kb &= (1ull << (8 * kisz)) - 1;  // the set holds the native bits zero-extended
+        const int64_t o = set_lookup_bits(set, kb);
+        rank[j] = o < 0 ? ~0ull : (unsigned long long)o;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_ha_iota(uint32_t *idx, uint64_t m) {
+    for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) idx[j] = (uint32_t)j;
+}
+
+// result columns (key | count | sum[nv] | nonnull[nv], m each) permuted by order
+__global__ __launch_bounds__(256) void k_ha_permute(const int64_t *src, int64_t *dst, uint64_t m, int ncols,
+                                                    const uint32_t *order) {
+    for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) {
+        const uint64_t o = order[j];
+        for (int c = 0; c < ncols; c++) dst[(uint64_t)c * m + j] = src[(uint64_t)c * m + o];
+    }
+}
+
 // combined key of a multi-key groupby: sum_j (key_j - min_j) * mult_j as int64
 // (groupby.py:248-288 _combine: the cartesian ordinal, first key most significant)
 constexpr int HC_MAX_KEYS = 8;
@@ -2152,6 +2270,117 @@ int vh_hashagg_read(vh_hashagg *h, int64_t *keys, int64_t *counts, void *const *
         if (nonnull && nonnull[v]) VH_HIP(hipMemcpyAsync(nonnull[v], onn + (uint64_t)v * m, 8 * m, hipMemcpyDefault, st));
     }
     VH_HIP(hipStreamSynchronize(st));
+    VH_API_END
+}
+
+/* groups in first-appearance order (vh_hashagg_order_first; see vaexhip.h) */
+int vh_hashagg_order_first(vh_hashagg *h, const void *keys, uint64_t n, int loc) {
+    VH_API_BEGIN
+    if (!h->finished) fail(VH_ERR_RUNTIME, "hashagg: order_first before finish");
+    if (n != h->rows) fail(VH_ERR_ARG, "hashagg: order_first needs the key column of every update");
+    const uint64_t m = h->ngroups;
+    if (m < 2) return VH_OK;
+    loc = resolve_loc(keys, loc);
+    hipStream_t st = stream();
+    const int kisz = dtype_itemsize(h->key_dtype);
+    const int kbs = key_bits_size(h->key_dtype);
+    const uint64_t ak = (kbs * m + 255) & ~255ull, as = (4 * m + 255) & ~255ull;
+    const uint32_t *sslot2 = reinterpret_cast<const uint32_t *>(h->out.as<char>() + 2 * ak + as);
+    const int ncols = 2 + 2 * h->nv;
+    // scratch: first/rank u64 [m] | rank2 u64 [m] | idx u32 [m] | idx2 u32 [m] | gidx u32 [slots + 2] | stats | sort tmp
+    size_t tmp_bytes = 0;
+    VH_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
+                                     (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)m, 0, 64, st));
+    const uint64_t a8 = (8 * m + 255) & ~255ull, a4 = (4 * m + 255) & ~255ull, ag = (4 * (h->slots + 2) + 255) & ~255ull;
+    DevBuf work;
+    work.ensure(2 * a8 + 2 * a4 + ag + 256 + tmp_bytes + 256);
+    char *wb = work.as<char>();
+    auto *first = reinterpret_cast<unsigned long long *>(wb);
+    auto *rank2 = reinterpret_cast<unsigned long long *>(wb + a8);
+    auto *idx = reinterpret_cast<uint32_t *>(wb + 2 * a8);
+    auto *idx2 = reinterpret_cast<uint32_t *>(wb + 2 * a8 + a4);
+    auto *gidx = reinterpret_cast<uint32_t *>(wb + 2 * a8 + 2 * a4);
+    auto *stats = reinterpret_cast<unsigned long long *>(wb + 2 * a8 + 2 * a4 + ag);
+    void *tmp = wb + 2 * a8 + 2 * a4 + ag + 256;
+    thread_local PinnedBuf res_buf;
+    res_buf.ensure(64);
+    auto *hstats = res_buf.as<unsigned long long>();
+    const int64_t *okey = reinterpret_cast<const int64_t *>(h->res);
+    bool complete = false;
+    {
+        TimedScope ts("ha_first");
+        VH_HIP(hipMemsetAsync(first, 0xff, 8 * m, st));
+        VH_HIP(hipMemsetAsync(stats, 0, 24, st));
+        hipLaunchKernelGGL(k_ha_gidx, dim3(blocks_for(m, 256, 8)), dim3(256), 0, st, sslot2, m, gidx);
+        VH_HIP(hipGetLastError());
+        const HaTable g = table_view(h->tab.ptr, h->slots, h->nv, h->vfloat, h->nnmask);
+        // the prefix scan: chunks from 4 rows per group, growing by half each step, until every
+        // group has its first row; input with long key runs (sorted / clustered) probes only
+        // its run heads and scans to the end, otherwise past n / 8 rows the set build below
+        // takes over (its cost does not depend on where keys first appear)
+        HaScratch &S = scratch();
+        std::lock_guard<std::mutex> lk(S.mu);
+        uint64_t r0 = 0, chunk = std::max<uint64_t>(1u << 20, 4 * m);
+        uint64_t heads = 0;
+        const bool aligned = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
+        while (r0 < n) {
+            const uint64_t r1 = std::min(n, r0 + (chunk & ~uint64_t(1023)));
+            const void *kp = static_cast<const char *>(keys) + r0 * kisz;
+            if (loc == VH_LOC_HOST || !aligned) {
+                // staged 16-B aligned, with the rows before the chunk in the 16 bytes ahead of
+                // it (the run-head test reads row r0 - 1)
+                const uint64_t lead = std::min<uint64_t>(r0, 16 / kisz);
+                S.stage.ensure((r1 - r0) * kisz + 64);
+                char *d = S.stage.as<char>() + 16;
+                VH_HIP(hipMemcpyAsync(d - lead * kisz, static_cast<const char *>(keys) + (r0 - lead) * kisz,
+                                      (r1 - r0 + lead) * kisz, hipMemcpyDefault, st));
+                kp = d;
+            }
+            VH_DISPATCH_DTYPE(h->key_dtype, K, {
+                if constexpr (std::is_integral_v<K>) {
+                    if constexpr (sizeof(K) >= 1) {
+                        hipLaunchKernelGGL(k_ha_first<K>, dim3(blocks_for((r1 - r0) / (16 / sizeof(K)) + 1, 256, 8)), dim3(256),
+                                           0, st, static_cast<const K *>(kp), r1 - r0, r0, g, gidx, first, stats);
+                    }
+                }
+            });
+            VH_HIP(hipGetLastError());
+            VH_HIP(hipMemcpyAsync(hstats, stats, 24, hipMemcpyDeviceToHost, st));
+            VH_HIP(hipStreamSynchronize(st));
+            if (hstats[2]) fail(VH_ERR_ARG, "hashagg: order_first got a key the aggregation never saw");
+            heads = hstats[1];
+            r0 = r1;
+            if (hstats[0] >= m) {
+                complete = true;
+                break;
+            }
+            if (r0 >= n / 8 && heads * 16 > r0) break;  // no long runs: the set build is cheaper
+            chunk += chunk / 2;
+        }
+    }
+    if (!complete) {
+        // ordinals of an ordered_set over every row (the reference's structure; first rows of
+        // keys that appear late cost a probe per row in the scan above)
+        vh_set *set = nullptr;
+        if (vh_set_create(h->key_dtype, &set) != VH_OK) fail(VH_ERR_RUNTIME, vh_last_error());
+        std::unique_ptr<vh_set, int (*)(vh_set *)> guard(set, vh_set_destroy);
+        if (vh_set_update(set, keys, nullptr, n, loc) != VH_OK) fail(VH_ERR_RUNTIME, vh_last_error());
+        const SetDev sd = set_device_view(set);
+        hipLaunchKernelGGL(k_ha_set_rank, dim3(blocks_for(m, 256, 8)), dim3(256), 0, st, okey, m, kisz, sd, first);
+        VH_HIP(hipGetLastError());
+    }
+    // order the groups by first row (or ordinal), then permute every result column
+    hipLaunchKernelGGL(k_ha_iota, dim3(blocks_for(m, 256, 8)), dim3(256), 0, st, idx, m);
+    VH_HIP(hipGetLastError());
+    size_t tb = tmp_bytes;
+    VH_HIP(rocprim::radix_sort_pairs(tmp, tb, first, rank2, idx, idx2, (size_t)m, 0, 64, st));
+    h->xres.ensure(8 * m * (uint64_t)ncols);
+    int64_t *dst = h->xres.as<int64_t>();
+    if (reinterpret_cast<const char *>(dst) == h->res) fail(VH_ERR_RUNTIME, "hashagg: result buffer aliasing");
+    hipLaunchKernelGGL(k_ha_permute, dim3(blocks_for(m, 256, 8)), dim3(256), 0, st, okey, dst, m, ncols, idx2);
+    VH_HIP(hipGetLastError());
+    VH_HIP(hipStreamSynchronize(st));
+    h->res = reinterpret_cast<const char *>(dst);
     VH_API_END
 }
 

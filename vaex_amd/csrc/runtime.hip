@@ -344,9 +344,34 @@ __host__ inline double f64_from_key(uint64_t k) {
     return d;
 }
 
+// (min key, max key) of a 256-lane workgroup -> out[0..1] (written by lane 0; no atomics:
+// a few thousand same-address atomics at the end of a short launch cost more than the scan)
+__device__ inline void block_minmax_keys(uint64_t lo, uint64_t hi, uint64_t *out) {
+    __shared__ uint64_t s_lo[4], s_hi[4];
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t l2 = __shfl_down(lo, off, 64);
+        const uint64_t h2 = __shfl_down(hi, off, 64);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_lo[threadIdx.x >> 6] = lo;
+        s_hi[threadIdx.x >> 6] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); w++) {
+            lo = min(lo, s_lo[w]);
+            hi = max(hi, s_hi[w]);
+        }
+        out[2 * blockIdx.x] = lo;
+        out[2 * blockIdx.x + 1] = hi;
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_minmax(const void *data, uint64_t n, int flip,
-                                                const uint8_t *mask, uint64_t *keys) {
+                                                const uint8_t *mask, uint64_t *part) {
     uint64_t lo = ~0ULL, hi = 0ULL;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
@@ -358,17 +383,7 @@ __global__ __launch_bounds__(256) void k_minmax(const void *data, uint64_t n, in
         lo = k < lo ? k : lo;
         hi = k > hi ? k : hi;
     }
-    // wave64 reduction, then one atomic per wave
-    for (int off = 32; off > 0; off >>= 1) {
-        uint64_t l2 = __shfl_down(lo, off, 64);
-        uint64_t h2 = __shfl_down(hi, off, 64);
-        lo = l2 < lo ? l2 : lo;
-        hi = h2 > hi ? h2 : hi;
-    }
-    if ((threadIdx.x & 63) == 0) {
-        if (lo != ~0ULL) atomicMin((unsigned long long *)&keys[0], (unsigned long long)lo);
-        if (hi != 0ULL) atomicMax((unsigned long long *)&keys[1], (unsigned long long)hi);
-    }
+    block_minmax_keys(lo, hi, part);
 }
 
 // Streaming form for native, unmasked, 16-B aligned columns of a numeric T: every lane
@@ -377,7 +392,7 @@ __global__ __launch_bounds__(256) void k_minmax(const void *data, uint64_t n, in
 // NaN fails both compares and is skipped (nanmin/nanmax, tasks.py:173-185).
 constexpr int MM_UNROLL = 4;
 template <typename T>
-__global__ __launch_bounds__(256) void k_minmax_vec(const T *data, uint64_t nvec, uint64_t *keys) {
+__global__ __launch_bounds__(256) void k_minmax_vec(const T *data, uint64_t nvec, uint64_t *part) {
     constexpr int V = 16 / sizeof(T);
     struct alignas(16) Vec { T v[V]; };
     const Vec *src = reinterpret_cast<const Vec *>(data);
@@ -418,16 +433,17 @@ __global__ __launch_bounds__(256) void k_minmax_vec(const T *data, uint64_t nvec
         klo = f64_key((double)lo);
         khi = f64_key((double)hi);
     }
-    for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t l2 = __shfl_down(klo, off, 64);
-        const uint64_t h2 = __shfl_down(khi, off, 64);
-        klo = l2 < klo ? l2 : klo;
-        khi = h2 > khi ? h2 : khi;
+    block_minmax_keys(klo, khi, part);
+}
+
+// fold the `nb` workgroup partials into keys[0] (min) / keys[1] (max)
+__global__ __launch_bounds__(256) void k_minmax_fin(const uint64_t *part, unsigned nb, uint64_t *keys) {
+    uint64_t lo = ~0ULL, hi = 0ULL;
+    for (unsigned b = threadIdx.x; b < nb; b += blockDim.x) {
+        lo = min(lo, part[2 * b]);
+        hi = max(hi, part[2 * b + 1]);
     }
-    if ((threadIdx.x & 63) == 0) {
-        if (klo != ~0ULL) atomicMin((unsigned long long *)&keys[0], (unsigned long long)klo);
-        if (khi != 0ULL) atomicMax((unsigned long long *)&keys[1], (unsigned long long)khi);
-    }
+    block_minmax_keys(lo, hi, keys);
 }
 
 }  // namespace vh
@@ -649,32 +665,37 @@ int vh_minmax(const void *data, uint64_t n, int dtype, int flip, const uint8_t *
             m = mstage.as<uint8_t>();
         }
     }
-    keys.ensure(16);
-    uint64_t init[2] = {~0ULL, 0ULL};
-    VH_HIP(hipMemcpyAsync(keys.ptr, init, 16, hipMemcpyHostToDevice, stream()));
-    if (n) {
+    // per-workgroup partials, folded by one workgroup (k_minmax_fin) into keys
+    const bool vec_ok = !flip && !m && dtype != VH_BOOL && (reinterpret_cast<uintptr_t>(d) & 15) == 0;
+    const uint64_t nvec = vec_ok && n * isz >= 16 ? n * isz / 16 : 0;
+    const uint64_t done = nvec * (16 / isz);
+    const unsigned nb1 = nvec ? blocks_for(nvec, 256, 8) : 0;
+    const unsigned nb2 = done < n ? blocks_for(n - done, 256, 4) : 0;
+    keys.ensure(16 * ((uint64_t)nb1 + nb2 + 1));
+    uint64_t *part = keys.as<uint64_t>() + 2;
+    {
         TimedScope ts("minmax");
-        uint64_t done = 0;
-        const bool vec_ok = !flip && !m && dtype != VH_BOOL && (reinterpret_cast<uintptr_t>(d) & 15) == 0;
-        if (vec_ok && n * isz >= 16) {
-            const uint64_t nvec = n * isz / 16;
-            done = nvec * (16 / isz);
+        if (nb1) {
             VH_DISPATCH_DTYPE(dtype, T,
                               if constexpr (!std::is_same_v<T, vbool>)
-                                  hipLaunchKernelGGL(k_minmax_vec<T>, dim3(blocks_for(nvec, 256, 8)), dim3(256), 0,
-                                                     stream(), static_cast<const T *>(d), nvec, keys.as<uint64_t>()));
+                                  hipLaunchKernelGGL(k_minmax_vec<T>, dim3(nb1), dim3(256), 0,
+                                                     stream(), static_cast<const T *>(d), nvec, part));
             VH_HIP(hipGetLastError());
         }
-        if (done < n) {
+        if (nb2) {
             const void *rest = static_cast<const char *>(d) + done * isz;
             VH_DISPATCH_DTYPE(dtype, T,
-                              hipLaunchKernelGGL(k_minmax<T>, dim3(blocks_for(n - done, 256, 4)), dim3(256), 0,
-                                                 stream(), rest, n - done, flip, m ? m + done : m,
-                                                 keys.as<uint64_t>()));
+                              hipLaunchKernelGGL(k_minmax<T>, dim3(nb2), dim3(256), 0,
+                                                 stream(), rest, n - done, flip, m ? m + done : m, part + 2 * (uint64_t)nb1));
             VH_HIP(hipGetLastError());
         }
+        hipLaunchKernelGGL(k_minmax_fin, dim3(1), dim3(256), 0, stream(), part, nb1 + nb2, keys.as<uint64_t>());
+        VH_HIP(hipGetLastError());
     }
-    uint64_t res[2];
+    // the 16-B result through a page-locked block (a pageable read-back costs more than the scan)
+    thread_local PinnedBuf res_buf;
+    res_buf.ensure(16);
+    uint64_t *res = res_buf.as<uint64_t>();
     VH_HIP(hipMemcpyAsync(res, keys.ptr, 16, hipMemcpyDeviceToHost, stream()));
     VH_HIP(hipStreamSynchronize(stream()));
     if (res[0] == ~0ULL) {  // no non-NaN value (nanmin of all-NaN -> nan)

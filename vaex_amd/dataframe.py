@@ -615,6 +615,15 @@ class DataFrame:
                                       row_limit=row_limit)
                     if res is not None:
                         return res
+        if agg is not None and assume_sparse == True:  # noqa: E712
+            # the ordered_set grouper's result (groups in first-appearance order, or sorted)
+            # for count / sum / mean of an integer key: one hash-partitioned pass, then the
+            # groups ordered by the row their key first appears at (hashagg.order_first)
+            from .hashagg import try_groupby
+            res = try_groupby(self, by, agg, lambda a, g: parse_actions(self, a, g), sort=sort, row_limit=row_limit,
+                              first_order=not sort)
+            if res is not None:
+                return res
         groupby = GroupBy(self, by=by, sort=sort, row_limit=row_limit, dense=assume_sparse != True,  # noqa: E712
                           dense_ranges=dense_ranges)
         return groupby.agg(agg)

@@ -74,13 +74,25 @@ class HashAgg:
                 raise HashAggOverflow(msg)
             _lib.check(rc)
 
-    def finish(self, comm=None, gather=True, device_keys=False):
+    def order_first(self, keys):
+        """After finish(): put the groups in the order their keys first appear in ``keys`` (the
+        whole key column the updates saw) -- an ordered_set's ordinal order
+        (hash_primitives.hpp:96-281), what ``groupby(key, assume_sparse=True)`` returns."""
+        loc = _lib.LOC_DEVICE if isinstance(keys, DeviceArray) else _lib.LOC_HOST
+        if loc == _lib.LOC_HOST:
+            keys = np.ascontiguousarray(keys)
+        ptr = keys.ptr if loc == _lib.LOC_DEVICE else keys.ctypes.data
+        _lib.call("vh_hashagg_order_first", self._h, ptr, len(keys), loc)
+
+    def finish(self, comm=None, gather=True, device_keys=False, first_order_keys=None):
         """The groups, key-sorted: (keys, counts, sums, nonnull).  With an RCCL communicator
         (``comm.device``) the ranks' groups are first exchanged by hash partition on the
         device (vh_hashagg_exchange): each rank keeps the groups it owns, or with ``gather``
         the whole result."""
         m = ctypes.c_uint64()
         _lib.call("vh_hashagg_finish", self._h, ctypes.byref(m))
+        if first_order_keys is not None:
+            self.order_first(first_order_keys)
         if comm is not None and comm.world > 1:
             if not comm.device:
                 raise ValueError("the device exchange needs an RCCL communicator")
@@ -164,14 +176,19 @@ def _plan(df, by, actions, parse):
     return by, ops, value_names
 
 
-def try_groupby(df, by, actions, parse, sort=False, row_limit=None):
-    """The fused path of ``DataFrame.groupby(by, agg=actions)``; ``None`` = not taken."""
+def try_groupby(df, by, actions, parse, sort=False, row_limit=None, first_order=False):
+    """The fused path of ``DataFrame.groupby(by, agg=actions)``; ``None`` = not taken.  Groups
+    come out sorted by key, or with ``first_order`` in the order their keys first appear (the
+    ordered_set order of ``assume_sparse=True``; single process only)."""
     from .dataframe import DataFrame, RowLimitException
     plan = _plan(df, by, actions, parse)
     if plan is None:
         return None
     by, ops, value_names = plan
     key = df.columns[by]
+    distributed = getattr(df.executor, "world", 1) > 1
+    if first_order and distributed:
+        return None  # first appearance across row shards: the ordered_set route
     values = [df.columns[v] for v in value_names]
     nonnull = [any(op in ("nonnull", "mean") and vi == i for _, op, vi in ops) for i in range(len(values))]
     ha = HashAgg(key.dtype, [v.dtype for v in values], nonnull)
@@ -186,7 +203,6 @@ def try_groupby(df, by, actions, parse, sort=False, row_limit=None):
             ha.update(key[i1:i2], [v[i1:i2] for v in values])
     except HashAggOverflow:
         ok = False
-    distributed = getattr(executor, "world", 1) > 1
     if distributed:  # every rank takes the same route, or the collectives below would hang
         from .distributed import all_ranks_true
         ok = all_ranks_true(ok, executor.comm)
@@ -198,7 +214,8 @@ def try_groupby(df, by, actions, parse, sort=False, row_limit=None):
     if distributed and executor.comm.device:  # RCCL: hash-partition exchange on the device
         keys, counts, sums, nonnull = ha.finish(executor.comm, gather=True)
     else:
-        keys, counts, sums, nonnull = ha.finish(device_keys=device_keys)
+        keys, counts, sums, nonnull = ha.finish(device_keys=device_keys,
+                                                first_order_keys=key[start:end] if first_order else None)
         if distributed:  # CPU exchange: the same partition, merged on the host
             from .distributed import combine_groups
             keys, counts, sums, nonnull = combine_groups((keys, counts, sums, nonnull), executor.comm)
@@ -210,8 +227,9 @@ def try_groupby(df, by, actions, parse, sort=False, row_limit=None):
         labels = keys
     else:
         labels = keys.astype(kdt, copy=False)
-        if len(labels):  # groupby.py:131-133 (keys are sorted)
-            labels = labels.astype(label_dtype(kdt, labels[0], labels[-1]), copy=False)
+        if len(labels):  # groupby.py:131-133
+            lo, hi = (labels.min(), labels.max()) if first_order else (labels[0], labels[-1])
+            labels = labels.astype(label_dtype(kdt, lo, hi), copy=False)
     columns = {by: labels}
     for name, op, vi in ops:
         if op == "count":
