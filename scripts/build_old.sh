@@ -10,5 +10,5 @@ git show $REV:vaex_amd/csrc/$SRC.hip > build/var_$NAME/$SRC.hip
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -munsafe-fp-atomics -I."
 /opt/rocm/bin/hipcc $F -c build/var_$NAME/$SRC.hip -o build/var_$NAME/$SRC.o
 others=""
-for o in runtime binning tiled hashset hashagg expr nunique; do [ "$o" = "$SRC" ] || others="$others build/$o.o"; done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../libvaexhip_$NAME.so $others build/var_$NAME/$SRC.o
+for o in runtime binning tiled hashset hashagg expr nunique comm; do [ "$o" = "$SRC" ] || others="$others build/$o.o"; done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../libvaexhip_$NAME.so $others build/var_$NAME/$SRC.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib

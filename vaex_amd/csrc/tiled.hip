@@ -99,6 +99,11 @@ struct TileParams {
     // bits of the int64 slot, sign-extended back when bit s of vsigned is set
     uint32_t vnarrow, vfloat, vsigned, pad2;
     int32_t vdt[2];            // value slot -> column dtype (fast ordinal kernel)
+    // min / max aggregator k: pass B flushes its LDS cells with native global atomics into
+    // mmtmp[k] (cells x 4 or 8 bytes of the LDS cell form, identity-filled), merged into the
+    // typed grid afterwards by k_mm_merge (a CAS per cell on 1- and 2-byte grids serialised
+    // on the shared words)
+    void *mmtmp[MAX_FUSED_AGGS];
 };
 
 // value of row h (0/1) of a loaded pair of a column of dtype dt, as the 8-byte slot pass A
@@ -127,6 +132,22 @@ __device__ __forceinline__ double pair_slot(const double2 &pr, int dt, int h) {
     default: return __builtin_bit_cast(double, (uint64_t)(uint8_t)(raw >> (8 * h)));  // VH_U8
     }
 }
+
+// row h of a loaded pair as its 4-byte slot directly (narrow kernels; dt <= 4 bytes): the
+// same bits slot_narrow(pair_slot(...)) gives -- float32 bits, or the low word of the int64 /
+// uint64 upcast
+__device__ __forceinline__ uint32_t pair_slot32(const double2 &pr, int dt, int h) {
+    const uint64_t raw = __builtin_bit_cast(uint64_t, pr.x);
+    switch (dt) {
+    case VH_F32: case VH_I32: case VH_U32: return (uint32_t)(raw >> (32 * h));
+    case VH_I16: return (uint32_t)(int32_t)(int16_t)(uint16_t)(raw >> (16 * h));
+    case VH_U16: return (uint32_t)(uint16_t)(raw >> (16 * h));
+    case VH_I8: return (uint32_t)(int32_t)(int8_t)(uint8_t)(raw >> (8 * h));
+    case VH_BOOL: return ((raw >> (8 * h)) & 0xff) ? 1u : 0u;
+    default: return (uint32_t)(uint8_t)(raw >> (8 * h));  // VH_U8
+    }
+}
+__device__ __forceinline__ bool slot32_is_nan(uint32_t u, bool is_float) { return is_float && (u & 0x7fffffffu) > 0x7f800000u; }
 
 // a carried 8-byte slot value (double, or int64 / uint64 bits) as its 4-byte form and back
 __device__ __forceinline__ uint32_t slot_narrow(double v, bool is_float) {
@@ -174,6 +195,52 @@ __device__ inline void mm_lds(uint64_t *cell, int dt, bool mx, double v) {
         else atomicMin((unsigned long long *)cell, x);
     }
 }
+// 4-byte LDS cells for min / max of <= 4-byte columns (ds_min/max_i32 / _u32: half the LDS
+// of the 64-bit form, and 32-bit LDS atomics): signed as int32, unsigned as uint32, float32
+// as order-preserving bits
+__host__ __device__ inline bool mm_cell32(int dt) {
+    return dt == VH_F32 || dt == VH_I32 || dt == VH_U32 || dt == VH_I16 || dt == VH_U16 || dt == VH_I8 || dt == VH_U8;
+}
+__device__ inline uint32_t mm_identity32(int dt, bool mx) {
+    if (dt_signed(dt)) return mx ? (uint32_t)INT32_MIN : (uint32_t)INT32_MAX;
+    return mx ? 0u : ~0u;
+}
+__device__ inline uint32_t ord_bits32(float f) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, f);
+    return (u >> 31) ? ~u : (u | 0x80000000u);
+}
+__device__ inline float unord_bits32(uint32_t o) {
+    return __builtin_bit_cast(float, (o >> 31) ? (o & 0x7fffffffu) : ~o);
+}
+// one carried slot value (double: float data as a double, integers as int64 / uint64 bits)
+__device__ inline void mm_lds32(uint32_t *cell, int dt, bool mx, double v) {
+    if (dt_float(dt)) {
+        if (v != v) return;
+        const uint32_t o = ord_bits32((float)v);
+        if (mx) atomicMax(cell, o);
+        else atomicMin(cell, o);
+    } else if (dt_signed(dt)) {
+        const int x = (int)(int32_t)__builtin_bit_cast(int64_t, v);
+        if (mx) atomicMax(reinterpret_cast<int *>(cell), x);
+        else atomicMin(reinterpret_cast<int *>(cell), x);
+    } else {
+        const uint32_t x = (uint32_t)__builtin_bit_cast(uint64_t, v);
+        if (mx) atomicMax(cell, x);
+        else atomicMin(cell, x);
+    }
+}
+// a 4-byte cell as the carried-slot bits mm_grid takes
+__device__ inline uint64_t mm_cell32_slot(int dt, uint32_t x) {
+    if (dt_float(dt)) return __builtin_bit_cast(uint64_t, (double)unord_bits32(x));
+    if (dt_signed(dt)) return (uint64_t)(int64_t)(int32_t)x;
+    return (uint64_t)x;
+}
+
+// min / max scratch of the tile path (TileParams::mmtmp): identity fill, and the merge of the
+// flushed cell forms into the typed grid (std::min / std::max, superagg.cpp:226,274)
+__global__ __launch_bounds__(256) void k_mm_fill(void *tmp, uint64_t cells, int dt, int mx);
+__global__ __launch_bounds__(256) void k_mm_merge(void *grid, const void *tmp, uint64_t cells, int dt, int mx);
+
 // a value (LDS cell form when `cellform`, else a carried slot) into the typed grid
 __device__ inline void mm_grid(void *grid, uint64_t c, int dt, bool mx, uint64_t x, bool cellform) {
     double d = 0.0;
@@ -192,6 +259,43 @@ __device__ inline void mm_grid(void *grid, uint64_t c, int dt, bool mx, uint64_t
     case VH_U32: atomic_minmax<uint32_t>(static_cast<uint32_t *>(grid) + c, (uint32_t)x, mx); break;
     case VH_U16: atomic_minmax<uint16_t>(static_cast<uint16_t *>(grid) + c, (uint16_t)x, mx); break;
     default: atomic_minmax<uint8_t>(static_cast<uint8_t *>(grid) + c, (uint8_t)x, mx); break;  // VH_U8
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mm_fill(void *tmp, uint64_t cells, int dt, int mx) {
+    for (uint64_t c = blockIdx.x * 256ull + threadIdx.x; c < cells; c += (uint64_t)gridDim.x * 256) {
+        if (mm_cell32(dt)) static_cast<uint32_t *>(tmp)[c] = mm_identity32(dt, mx);
+        else static_cast<uint64_t *>(tmp)[c] = mm_identity(dt, mx);
+    }
+}
+
+template <typename T> __device__ inline void mm_merge_cell(T *g, T v, bool mx) { *g = minmax_apply(*g, v, mx); }
+
+__global__ __launch_bounds__(256) void k_mm_merge(void *grid, const void *tmp, uint64_t cells, int dt, int mx) {
+    for (uint64_t c = blockIdx.x * 256ull + threadIdx.x; c < cells; c += (uint64_t)gridDim.x * 256) {
+        uint64_t x;
+        if (mm_cell32(dt)) {
+            const uint32_t v = static_cast<const uint32_t *>(tmp)[c];
+            if (v == mm_identity32(dt, mx)) continue;
+            x = mm_cell32_slot(dt, v);
+        } else {
+            x = static_cast<const uint64_t *>(tmp)[c];
+            if (x == mm_identity(dt, mx)) continue;
+            if (dt_float(dt)) x = __builtin_bit_cast(uint64_t, unord_bits(x));
+        }
+        const double d = __builtin_bit_cast(double, x);
+        switch (dt) {
+        case VH_F64: mm_merge_cell<double>(static_cast<double *>(grid) + c, d, mx); break;
+        case VH_F32: mm_merge_cell<float>(static_cast<float *>(grid) + c, (float)d, mx); break;
+        case VH_I64: mm_merge_cell<int64_t>(static_cast<int64_t *>(grid) + c, (int64_t)x, mx); break;
+        case VH_I32: mm_merge_cell<int32_t>(static_cast<int32_t *>(grid) + c, (int32_t)(int64_t)x, mx); break;
+        case VH_I16: mm_merge_cell<int16_t>(static_cast<int16_t *>(grid) + c, (int16_t)(int64_t)x, mx); break;
+        case VH_I8: mm_merge_cell<int8_t>(static_cast<int8_t *>(grid) + c, (int8_t)(int64_t)x, mx); break;
+        case VH_U64: mm_merge_cell<uint64_t>(static_cast<uint64_t *>(grid) + c, x, mx); break;
+        case VH_U32: mm_merge_cell<uint32_t>(static_cast<uint32_t *>(grid) + c, (uint32_t)x, mx); break;
+        case VH_U16: mm_merge_cell<uint16_t>(static_cast<uint16_t *>(grid) + c, (uint16_t)x, mx); break;
+        default: mm_merge_cell<uint8_t>(static_cast<uint8_t *>(grid) + c, (uint8_t)x, mx); break;
+        }
     }
 }
 
@@ -406,17 +510,20 @@ template <int NV> __device__ inline ScatterLds scatter_lds(unsigned char *raw, u
 #define VH_TA_SB0 2  // count-only commits (same-process A/B: 1 -> 2 is 3.99 -> 3.87 ms, 3 is 4.08)
 #endif
 __host__ __device__ constexpr int fast_sb(int nv) { return nv == 0 ? VH_TA_SB0 : nv == 1 ? VH_TA_SB : (VH_TA_SB < 2 ? VH_TA_SB : 2); }
+// narrow (4-byte) value slots staged as 4 bytes: two carried columns still fit three batches
+__host__ __device__ constexpr int fast_sb_narrow(int nv) { return nv == 0 ? VH_TA_SB0 : VH_TA_SB; }
 
-// LDS of the fast kernels: staged values | staged 4-byte keys | tile arrays
-__host__ __device__ inline size_t fast_lds_bytes(int nv, uint32_t T, uint32_t cap) {
-    return (size_t)8 * nv * cap + (size_t)4 * cap + 24 * (size_t)T + 64;
+// LDS of the fast kernels: staged values (vbytes each: 8, or 4 for narrow slots) | staged
+// 4-byte keys | tile arrays
+__host__ __device__ inline size_t fast_lds_bytes(int nv, uint32_t T, uint32_t cap, int vbytes = 8) {
+    return (size_t)vbytes * nv * cap + (size_t)4 * cap + 24 * (size_t)T + 64;
 }
 
-template <int NV> __device__ inline ScatterLds fast_lds(unsigned char *raw, uint32_t T, uint32_t cap) {
+template <int NV> __device__ inline ScatterLds fast_lds(unsigned char *raw, uint32_t T, uint32_t cap, int vbytes = 8) {
     ScatterLds l;
     l.sv = reinterpret_cast<double *>(raw);
-    l.sp = reinterpret_cast<uint64_t *>(raw + (size_t)8 * NV * cap);
-    l.hist = reinterpret_cast<uint32_t *>(raw + (size_t)8 * NV * cap + (size_t)4 * cap);
+    l.sp = reinterpret_cast<uint64_t *>(raw + (size_t)vbytes * NV * cap);
+    l.hist = reinterpret_cast<uint32_t *>(raw + (size_t)vbytes * NV * cap + (size_t)4 * cap);
     l.boff = l.hist + T;
     l.base = l.boff + T;
     l.lim = l.base + T;
@@ -566,13 +673,22 @@ __device__ inline void fast_scan(const ScatterLds &l, const TileParams &tp, uint
     if (lane == 63) l.wave_sums[0] = inc;
 }
 
-template <int NV, int R>
+// VT: the carried value type -- double (8-byte slots, or narrowed at the store when
+// tp.vnarrow), or uint32_t (narrow slots computed from the raw column: staged and stored as
+// 4 bytes; widened only for the rare overflow row)
+template <typename VT> __device__ __forceinline__ double vt_wide(VT v, const TileParams &tp, int s) {
+    if constexpr (sizeof(VT) == 8) return v;
+    else return slot_wide(v, (tp.vfloat >> s) & 1, (tp.vsigned >> s) & 1);
+}
+
+template <int NV, int R, typename VT = double>
 __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &fa, const TileParams &tp, uint32_t T,
                                          uint64_t region0, const uint32_t *key, const int32_t *rank,
-                                         const double (*vals)[NV > 0 ? NV : 1], uint32_t count_mask,
+                                         const VT (*vals)[NV > 0 ? NV : 1], uint32_t count_mask,
                                          const uint32_t *keyed_slot_of) {
     constexpr uint32_t CAP = R * TA_THREADS;
     uint32_t *sk = reinterpret_cast<uint32_t *>(l.sp);
+    VT *sv = reinterpret_cast<VT *>(l.sv);
     lds_barrier();
     fast_scan(l, tp, T);
     lds_barrier();
@@ -583,7 +699,7 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
         const uint32_t pos = l.boff[key[r] >> 16] + (uint32_t)rank[r];
         sk[pos] = key[r];
 #pragma unroll
-        for (int s = 0; s < NV; s++) l.sv[s * CAP + pos] = vals[r][s];
+        for (int s = 0; s < NV; s++) sv[s * CAP + pos] = vals[r][s];
     }
     lds_barrier();
     for (uint32_t k = threadIdx.x; k < tot; k += TA_THREADS) {
@@ -598,10 +714,12 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
             reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)kk;
 #pragma unroll
             for (int s = 0; s < NV; s++) {
-                if (tp.vnarrow)
-                    reinterpret_cast<uint32_t *>(tp.values[s])[e] = slot_narrow(l.sv[s * CAP + k], (tp.vfloat >> s) & 1);
+                if constexpr (sizeof(VT) == 4)
+                    reinterpret_cast<uint32_t *>(tp.values[s])[e] = sv[s * CAP + k];
+                else if (tp.vnarrow)
+                    reinterpret_cast<uint32_t *>(tp.values[s])[e] = slot_narrow(sv[s * CAP + k], (tp.vfloat >> s) & 1);
                 else
-                    tp.values[s][e] = l.sv[s * CAP + k];
+                    tp.values[s][e] = sv[s * CAP + k];
             }
         } else {
             // past the region and the spill area: apply the staged row with global atomics
@@ -613,7 +731,7 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
                 bool take = (count_mask >> a) & 1;
                 if constexpr (NV > 0) {
                     if (!take) {
-                        const double v = l.sv[keyed_slot_of[a] * CAP + k];
+                        const double v = vt_wide<VT>(sv[keyed_slot_of[a] * CAP + k], tp, keyed_slot_of[a]);
                         take = v == v;
                     }
                 }
@@ -623,9 +741,9 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
                 } else if (is_minmax(fa.a[a].kind)) {
                     if constexpr (NV > 0)
                         mm_grid(fa.a[a].grid, c, fa.a[a].dtype, fa.a[a].kind == VH_AGG_MAX,
-                                __builtin_bit_cast(uint64_t, l.sv[tp.val_slot[a] * CAP + k]), false);
+                                __builtin_bit_cast(uint64_t, vt_wide<VT>(sv[tp.val_slot[a] * CAP + k], tp, tp.val_slot[a])), false);
                 } else if constexpr (NV > 0) {
-                    const double v = l.sv[tp.val_slot[a] * CAP + k];
+                    const double v = vt_wide<VT>(sv[tp.val_slot[a] * CAP + k], tp, tp.val_slot[a]);
                     if (fa.a[a].vint)
                         atomicAdd(reinterpret_cast<unsigned long long *>(fa.a[a].grid) + c, __builtin_bit_cast(unsigned long long, v));
                     else
@@ -967,12 +1085,16 @@ __device__ inline uint32_t set_ord_cell(int64_t o, uint64_t count) {
 // first slot holds another key continue their probe sequence afterwards.
 // DT0 / DT1: value slot dtypes as compile-time constants (VH_F64 = the float64 kernel), or -1:
 // any dtype through a run-time switch (slower: the branches around the prefetch loads)
-template <int NV, int SB, bool SET = false, int DT0 = VH_F64, int DT1 = VH_F64>
+// VN: every carried column is <= 4 bytes (narrow slots): values are carried, staged and
+// stored as their 4-byte slot bits (half the LDS staging: two columns still commit three
+// batches at once)
+template <int NV, int SB, bool SET = false, int DT0 = VH_F64, int DT1 = VH_F64, bool VN = false>
 __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
     constexpr int PAIRS = TA_RPT / 2;
+    using VT = std::conditional_t<VN, uint32_t, double>;
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const uint32_t T = tp.ntiles;
-    const ScatterLds l = fast_lds<NV>(lds_raw, T, SB * TA_BATCH);
+    const ScatterLds l = fast_lds<NV>(lds_raw, T, SB * TA_BATCH, VN ? 4 : 8);
     scatter_lds_init(l, tp, T);
     __syncthreads();
     const int32_t *keys = reinterpret_cast<const int32_t *>(p.b[0].data);
@@ -1034,7 +1156,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
         }
     };
     const SetDev sd = p.b[0].set;
-    auto rows = [&](uint64_t b0, const Regs &cur, uint32_t *key, int32_t *rank, double (*vals)[NV > 0 ? NV : 1]) {
+    auto rows = [&](uint64_t b0, const Regs &cur, uint32_t *key, int32_t *rank, VT (*vals)[NV > 0 ? NV : 1]) {
         uint32_t scell[SET ? TA_RPT : 1];
         if constexpr (SET) {
             uint64_t e[TA_RPT], pos[TA_RPT];
@@ -1076,8 +1198,13 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
 #pragma unroll
             for (int s = 0; s < NV; s++) {
                 const int dts = s == 0 ? DT0 : DT1;
-                vals[r][s] = pair_slot(cur.v[q][s], dts >= 0 ? dts : tp.vdt[s], h);
-                f |= vals[r][s] == vals[r][s] ? nan_keyed[s] : 0u;
+                if constexpr (VN) {
+                    vals[r][s] = pair_slot32(cur.v[q][s], dts >= 0 ? dts : tp.vdt[s], h);
+                    f |= slot32_is_nan(vals[r][s], (tp.vfloat >> s) & 1) ? 0u : nan_keyed[s];
+                } else {
+                    vals[r][s] = pair_slot(cur.v[q][s], dts >= 0 ? dts : tp.vdt[s], h);
+                    f |= vals[r][s] == vals[r][s] ? nan_keyed[s] : 0u;
+                }
             }
             f = i < row_end ? f : 0u;
             const uint32_t t = c >> s_log2;
@@ -1090,21 +1217,21 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
     for (uint64_t b0 = (uint64_t)w * TA_BATCH; b0 < n; b0 += SB * bstep) {
         uint32_t key[SB * TA_RPT];
         int32_t rank[SB * TA_RPT];
-        double vals[SB * TA_RPT][NV > 0 ? NV : 1];
+        VT vals[SB * TA_RPT][NV > 0 ? NV : 1];
 #pragma unroll
         for (int sb = 0; sb < SB; sb++) {
             load(b0 + (sb + 1) * bstep, nxt);
             rows(b0 + sb * bstep, cur, key + sb * TA_RPT, rank + sb * TA_RPT, vals + sb * TA_RPT);
             if (sb + 1 < SB || VH_TA_DRAIN) cur = nxt;
         }
-        batch_commit_fast<NV, SB * TA_RPT>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
+        batch_commit_fast<NV, SB * TA_RPT, VT>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
         if (!VH_TA_DRAIN) cur = nxt;
     }
     lds_barrier();
     for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.base[t] - (uint32_t)tp.toff[t];
 }
 
-template <int NV>
+template <int NV, bool MM>
 __device__ inline void reduce_entry(const FusedAggs &fa, const TileParams &tp, unsigned char *lds, uint32_t local,
                                     uint32_t fl, const double *v) {
     #pragma unroll
@@ -1123,10 +1250,14 @@ __device__ inline void reduce_entry(const FusedAggs &fa, const TileParams &tp, u
             }
             if (take) atomicAdd(reinterpret_cast<uint32_t *>(lds + fa.a[k].lds_off) + local, 1u);
         } else if (is_minmax(fa.a[k].kind)) {
+            if constexpr (!MM) continue;
 #pragma unroll
             for (int s = 0; s < NV; s++) {
                 if (s != tp.val_slot[k]) continue;
-                mm_lds(reinterpret_cast<uint64_t *>(lds + fa.a[k].lds_off) + local, fa.a[k].dtype, fa.a[k].kind == VH_AGG_MAX, v[s]);
+                if (mm_cell32(fa.a[k].dtype))
+                    mm_lds32(reinterpret_cast<uint32_t *>(lds + fa.a[k].lds_off) + local, fa.a[k].dtype, fa.a[k].kind == VH_AGG_MAX, v[s]);
+                else
+                    mm_lds(reinterpret_cast<uint64_t *>(lds + fa.a[k].lds_off) + local, fa.a[k].dtype, fa.a[k].kind == VH_AGG_MAX, v[s]);
             }
         } else {
 #pragma unroll
@@ -1206,7 +1337,7 @@ template <int NV> constexpr int tb_vu() { return VH_TB_VU ? VH_TB_VU : NV == 0 ?
 // short the regions are; a lane finds the region of its chunk by a forward scan (chunk
 // indices of a lane only grow).  Entries are reduced with LDS atomics, then the tile is
 // flushed with coalesced global atomics.
-template <int NV, bool NARROW = false>
+template <int NV, bool NARROW = false, bool MM = false>
 __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TileParams tp, const WorkUnit *units) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
     __shared__ uint32_t s_fill[1024 + 1];
@@ -1249,15 +1380,20 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
         if (lane == 63) s_pre[nw] = inc;
     }
     __syncthreads();
-    bool any_mm = false;
-    #pragma unroll
-    for (int k = 0; k < MAX_FUSED_AGGS; k++)
-        if (k < fa.na && is_minmax(fa.a[k].kind)) any_mm = true;
-    if (any_mm) {  // min / max cells start at the kind's identity (after the zero fill)
+    // MM: the plan has min / max aggregators (a separate instantiation: their code would
+    // raise the count / sum kernel's registers past the 1024-thread budget)
+    constexpr bool any_mm = MM;
+    if constexpr (MM) {  // min / max cells start at the kind's identity (after the zero fill)
         const uint32_t ncells = 1u << tp.s_log2;
         #pragma unroll
         for (int k = 0; k < MAX_FUSED_AGGS; k++) {
             if (k >= fa.na || !is_minmax(fa.a[k].kind)) continue;
+            if (mm_cell32(fa.a[k].dtype)) {
+                uint32_t *cells = reinterpret_cast<uint32_t *>(lds_raw + fa.a[k].lds_off);
+                const uint32_t id = mm_identity32(fa.a[k].dtype, fa.a[k].kind == VH_AGG_MAX);
+                for (uint32_t i = threadIdx.x; i < ncells; i += TB_THREADS) cells[i] = id;
+                continue;
+            }
             uint64_t *cells = reinterpret_cast<uint64_t *>(lds_raw + fa.a[k].lds_off);
             const uint64_t id = mm_identity(fa.a[k].dtype, fa.a[k].kind == VH_AGG_MAX);
             for (uint32_t i = threadIdx.x; i < ncells; i += TB_THREADS) cells[i] = id;
@@ -1327,20 +1463,33 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                     if (cur != ~0u) run.flush(fa, tp, lds_raw, cur);
                 }
             } else {
-#pragma unroll
-                for (int j = 0; j < VU; j++) {
+                // chunk j as a compile-time index (the unroller gave up on this body, and a
+                // run-time j indexed vv through scratch memory)
+                auto chunk = [&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
                     const uint32_t words[4] = {ev[j].x, ev[j].y, ev[j].z, ev[j].w};
 #pragma unroll
                     for (int x = 0; x < 8; x++) {
-                        if ((uint32_t)x >= rem[j]) break;
-                        double v[NV > 0 ? NV : 1];
+                        // a guard, not a break: the loop stays unrolled and vv in registers
+                        if ((uint32_t)x < rem[j]) {
+                            double v[NV > 0 ? NV : 1];
 #pragma unroll
-                        for (int s = 0; s < NV; s++) v[s] = (x & 1) ? vv[j][s][x >> 1].y : vv[j][s][x >> 1].x;
-                        const uint32_t local = (words[x >> 1] >> (16 * (x & 1))) & 0xffffu;
-                        if (DBG(tp.debug) & 8) asm volatile("" :: "v"(local));
-                        else reduce_entry<NV>(fa, tp, lds_raw, local, 0xfu, v);
+                            for (int s = 0; s < NV; s++) v[s] = (x & 1) ? vv[j][s][x >> 1].y : vv[j][s][x >> 1].x;
+                            const uint32_t local = (words[x >> 1] >> (16 * (x & 1))) & 0xffffu;
+                            if (DBG(tp.debug) & 8) asm volatile("" :: "v"(local));
+                            else reduce_entry<NV, MM>(fa, tp, lds_raw, local, 0xfu, v);
+                        }
                     }
-                }
+                };
+                static_assert(VU <= 8, "chunks per step");
+                chunk(std::integral_constant<int, 0>{});
+                if constexpr (VU > 1) chunk(std::integral_constant<int, 1>{});
+                if constexpr (VU > 2) chunk(std::integral_constant<int, 2>{});
+                if constexpr (VU > 3) chunk(std::integral_constant<int, 3>{});
+                if constexpr (VU > 4) chunk(std::integral_constant<int, 4>{});
+                if constexpr (VU > 5) chunk(std::integral_constant<int, 5>{});
+                if constexpr (VU > 6) chunk(std::integral_constant<int, 6>{});
+                if constexpr (VU > 7) chunk(std::integral_constant<int, 7>{});
             }
         }
     } else {
@@ -1369,7 +1518,7 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
 #pragma unroll
                 for (int j = 0; j < TB_UNROLL; j++) {
                     const uint32_t q = q0 + j * TB_THREADS + threadIdx.x;
-                    if (q < cnt) reduce_entry<NV>(fa, tp, lds_raw, ent[j] & 0xffffu, ent[j] >> 16, v[j]);
+                    if (q < cnt) reduce_entry<NV, MM>(fa, tp, lds_raw, ent[j] & 0xffffu, ent[j] >> 16, v[j]);
                 }
             }
         }
@@ -1386,9 +1535,27 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                 const uint32_t v = reinterpret_cast<const uint32_t *>(lds_raw + fa.a[k].lds_off)[i];
                 if (v) atomicAdd((unsigned long long *)fa.a[k].grid + c0 + i, (unsigned long long)v);
             } else if (is_minmax(fa.a[k].kind)) {
-                const bool mx = fa.a[k].kind == VH_AGG_MAX;
-                const uint64_t v = reinterpret_cast<const uint64_t *>(lds_raw + fa.a[k].lds_off)[i];
-                if (v != mm_identity(fa.a[k].dtype, mx)) mm_grid(fa.a[k].grid, c0 + i, fa.a[k].dtype, mx, v, true);
+                if constexpr (MM) {
+                    const bool mx = fa.a[k].kind == VH_AGG_MAX;
+                    const int dt = fa.a[k].dtype;
+                    void *tmp = tp.mmtmp[k];
+                    if (mm_cell32(dt)) {
+                        const uint32_t v = reinterpret_cast<const uint32_t *>(lds_raw + fa.a[k].lds_off)[i];
+                        if (v == mm_identity32(dt, mx)) continue;
+                        if (!tmp) mm_grid(fa.a[k].grid, c0 + i, dt, mx, mm_cell32_slot(dt, v), false);
+                        else if (dt_signed(dt)) mx ? atomicMax(static_cast<int *>(tmp) + c0 + i, (int)v) : atomicMin(static_cast<int *>(tmp) + c0 + i, (int)v);
+                        else mx ? atomicMax(static_cast<unsigned *>(tmp) + c0 + i, v) : atomicMin(static_cast<unsigned *>(tmp) + c0 + i, v);
+                        continue;
+                    }
+                    const uint64_t v = reinterpret_cast<const uint64_t *>(lds_raw + fa.a[k].lds_off)[i];
+                    if (v == mm_identity(dt, mx)) continue;
+                    if (!tmp) mm_grid(fa.a[k].grid, c0 + i, dt, mx, v, true);
+                    else if (dt_signed(dt))
+                        mx ? atomicMax(static_cast<long long *>(tmp) + c0 + i, (long long)v) : atomicMin(static_cast<long long *>(tmp) + c0 + i, (long long)v);
+                    else
+                        mx ? atomicMax(static_cast<unsigned long long *>(tmp) + c0 + i, (unsigned long long)v)
+                           : atomicMin(static_cast<unsigned long long *>(tmp) + c0 + i, (unsigned long long)v);
+                }
             } else if (fa.a[k].vint) {
                 const unsigned long long v = reinterpret_cast<const unsigned long long *>(lds_raw + fa.a[k].lds_off)[i];
                 if (v) atomicAdd(reinterpret_cast<unsigned long long *>(fa.a[k].grid) + c0 + i, v);
@@ -1460,6 +1627,17 @@ template <int NV> static int scatter_blocks_per_cu_nd(int nd, int fast, size_t l
 
 // value-dtype combinations with their own ordinal kernel (0: float64; h2o's int8 / float32
 // sums; others take the run-time-switch kernel, -1)
+// narrow (VN) kernels: h2o's int8 / float32 combinations and the run-time switch
+template <int NV, int SB, typename F> static void ord_by_dts_narrow(int dt0, int dt1, F &&f) {
+#define VH_ORD_DT(a, b) if (dt0 == (a) && (NV < 2 || dt1 == (b))) return f(k_tile_scatter_ord<NV, SB, false, (a), NV < 2 ? VH_F64 : (b), true>);
+    VH_ORD_DT(VH_I8, VH_I8)
+    VH_ORD_DT(VH_I8, VH_F32)
+    VH_ORD_DT(VH_F32, VH_I8)
+    VH_ORD_DT(VH_F32, VH_F32)
+    VH_ORD_DT(VH_I32, VH_I32)
+#undef VH_ORD_DT
+    f(k_tile_scatter_ord<NV, SB, false, -1, -1, true>);
+}
 template <int NV, int SB, bool SET, typename F> static void ord_by_dts(int dt0, int dt1, F &&f) {
 #define VH_ORD_DT(a, b) if (dt0 == (a) && (NV < 2 || dt1 == (b))) return f(k_tile_scatter_ord<NV, SB, SET, (a), NV < 2 ? VH_F64 : (b)>);
     VH_ORD_DT(VH_F64, VH_F64)
@@ -1478,6 +1656,13 @@ template <int NV, int SB, bool SET, typename F> static void ord_by_dts(int dt0, 
 template <bool SET> static const void *ord_kernel_t(int nv, int fast_mode, int dt0, int dt1) {
     const void *k = nullptr;
     auto take = [&](auto kern) { k = reinterpret_cast<const void *>(kern); };
+    if constexpr (!SET) {
+        if (fast_mode == 3) {  // narrow slots, fast_sb_narrow(nv) batches per commit
+            if (nv == 1) ord_by_dts_narrow<1, fast_sb_narrow(1)>(dt0, dt1, take);
+            else ord_by_dts_narrow<2, fast_sb_narrow(2)>(dt0, dt1, take);
+            return k;
+        }
+    }
     if (nv == 0) ord_by_dts<0, 1, SET>(VH_F64, VH_F64, take);
     else if (nv == 1) {
         if (fast_mode == 2) ord_by_dts<1, fast_sb(1), SET>(dt0, dt1, take);
@@ -1548,7 +1733,7 @@ bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t
 // by the library stream.
 struct TileScratch {
     std::mutex mu;
-    DevBuf entries, values, meta;
+    DevBuf entries, values, meta, mmtmp;
 };
 
 static bool getenv_flag_off(const char *name) {  // NAME=0 turns a default-on path off (A/B runs)
@@ -1598,8 +1783,12 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     if (flags_mode)
         for (int k = 0; k < fa_in.na; k++)
             if (fa_in.a[k].kind == VH_AGG_COUNT) tp.cnt_slot[k] = CNT_FLAG;
+    // LDS bytes per cell of pass B: u32 counts, 8-byte sums, min / max 4 or 8 (mm_cell32)
+    auto cell_bytes = [](const FusedAgg &a) -> uint64_t {
+        return a.kind == VH_AGG_COUNT || (is_minmax(a.kind) && mm_cell32(a.dtype)) ? 4 : 8;
+    };
     uint64_t per_cell = 0;
-    for (int k = 0; k < fa_in.na; k++) per_cell += fa_in.a[k].kind == VH_AGG_COUNT ? 4 : 8;
+    for (int k = 0; k < fa_in.na; k++) per_cell += cell_bytes(fa_in.a[k]);
     uint32_t s_log2 = 0;
     while (s_log2 < 16 && ((uint64_t)2 << s_log2) * per_cell <= TILE_LDS_BUDGET) s_log2++;
     const uint64_t S = 1ull << s_log2;
@@ -1612,7 +1801,7 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     for (int k = 0; k < fa.na; k++) {
         off = (off + 7) & ~uint64_t(7);
         fa.a[k].lds_off = (uint32_t)off;
-        off += S * (fa.a[k].kind == VH_AGG_COUNT ? 4 : 8);
+        off += S * cell_bytes(fa.a[k]);
     }
     const uint64_t lds_b = (off + 15) & ~uint64_t(15);
     fa.lds_words = (uint32_t)(lds_b / 4);
@@ -1641,9 +1830,25 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
             tp.vdata[tp.val_slot[k]] = fa.a[k].data;
             tp.vdt[tp.val_slot[k]] = fa.a[k].dtype;
         }
-    // fast kernel: several batches per commit when that staging fits the LDS
-    const int fast_mode = !(fast || ord) ? 0 : fast_lds_bytes(nv, T, (uint32_t)(fast_sb(nv) * TA_BATCH)) <= LDS_MAX_BYTES ? 2 : 1;
-    const size_t lds_a = fast_mode == 2   ? fast_lds_bytes(nv, T, (uint32_t)(fast_sb(nv) * TA_BATCH))
+    // 4-byte value slots when every summed column of a generic plan is <= 4 bytes (exact)
+    bool vnarrow = fa.generic_vals && nv > 0 && !fast && !getenv_flag_off("VH_TILE_NARROW");
+    uint32_t vfloat = 0, vsigned = 0;
+    for (int k = 0; k < fa.na && vnarrow; k++) {
+        if (fa.a[k].kind == VH_AGG_COUNT) continue;
+        const int dt = fa.a[k].dtype, s = tp.val_slot[k];
+        if (dtype_itemsize(dt) > 4) vnarrow = false;
+        if (dt == VH_F32) vfloat |= 1u << s;
+        if (dt == VH_I32 || dt == VH_I16 || dt == VH_I8) vsigned |= 1u << s;
+    }
+    // fast kernel: several batches per commit when that staging fits the LDS; the ordinal
+    // kernel with narrow slots stages 4-byte values (mode 3)
+    const bool narrow_ord = ord && vnarrow &&
+                            fast_lds_bytes(nv, T, (uint32_t)(fast_sb_narrow(nv) * TA_BATCH), 4) <= LDS_MAX_BYTES;
+    const int fast_mode = !(fast || ord) ? 0
+                          : narrow_ord  ? 3
+                          : fast_lds_bytes(nv, T, (uint32_t)(fast_sb(nv) * TA_BATCH)) <= LDS_MAX_BYTES ? 2 : 1;
+    const size_t lds_a = fast_mode == 3   ? fast_lds_bytes(nv, T, (uint32_t)(fast_sb_narrow(nv) * TA_BATCH), 4)
+                         : fast_mode == 2 ? fast_lds_bytes(nv, T, (uint32_t)(fast_sb(nv) * TA_BATCH))
                          : fast_mode == 1 ? fast_lds_bytes(nv, T, (uint32_t)TA_BATCH)
                                           : scatter_lds_bytes(nv, T);
     if (lds_a > LDS_MAX_BYTES) return false;  // very many tiles: the global-atomic path
@@ -1790,16 +1995,6 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     const uint64_t total = stride * W + stotal + 16;  // regions | spill areas | padding
     const int ebytes = flags_mode ? 4 : 2;
     ws.entries.ensure(total * ebytes);
-    // 4-byte value slots when every summed column of a generic plan is <= 4 bytes (exact)
-    bool vnarrow = fa.generic_vals && nv > 0 && !fast && !getenv_flag_off("VH_TILE_NARROW");
-    uint32_t vfloat = 0, vsigned = 0;
-    for (int k = 0; k < fa.na && vnarrow; k++) {
-        if (fa.a[k].kind == VH_AGG_COUNT) continue;
-        const int dt = fa.a[k].dtype, s = tp.val_slot[k];
-        if (dtype_itemsize(dt) > 4) vnarrow = false;
-        if (dt == VH_F32) vfloat |= 1u << s;
-        if (dt == VH_I32 || dt == VH_I16 || dt == VH_I8) vsigned |= 1u << s;
-    }
     if (nv) ws.values.ensure(total * (vnarrow ? 4 : 8) * nv + 64);
     tp.vnarrow = vnarrow ? 1u : 0u;
     tp.vfloat = vfloat;
@@ -1863,18 +2058,50 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     // ---- pass B
     {
         TimedScope ts("tile_reduce");
+        bool mm = false;
+        for (int k = 0; k < fa.na; k++) mm = mm || is_minmax(fa.a[k].kind);
+        uint64_t mm_bytes = 0;
+        for (int k = 0; k < fa.na; k++)
+            if (is_minmax(fa.a[k].kind)) mm_bytes += ((cells * (mm_cell32(fa.a[k].dtype) ? 4 : 8)) + 255) & ~uint64_t(255);
+        if (mm && mm_bytes <= (1ull << 30)) {
+            // min / max: native-atomic scratch in the LDS cell form, merged after pass B (past
+            // 1 GiB of scratch the flush takes the typed CAS into the grid instead)
+            uint64_t off = 0;
+            ws.mmtmp.ensure(mm_bytes + 256);
+            off = 0;
+            for (int k = 0; k < fa.na; k++) {
+                if (!is_minmax(fa.a[k].kind)) continue;
+                tp.mmtmp[k] = ws.mmtmp.as<char>() + off;
+                off += ((cells * (mm_cell32(fa.a[k].dtype) ? 4 : 8)) + 255) & ~uint64_t(255);
+                hipLaunchKernelGGL(k_mm_fill, dim3(blocks_for(cells, 256, 8)), dim3(256), 0, st, tp.mmtmp[k], cells,
+                                   fa.a[k].dtype, (int)(fa.a[k].kind == VH_AGG_MAX));
+                VH_HIP(hipGetLastError());
+            }
+        }
         const unsigned g = (unsigned)units.size();
+#define VH_TB(NV_, NAR_)                                                                                      \
+    do {                                                                                                      \
+        if (mm) hipLaunchKernelGGL((k_tile_reduce<NV_, NAR_, true>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units); \
+        else hipLaunchKernelGGL((k_tile_reduce<NV_, NAR_, false>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units); \
+    } while (0)
         switch (nv) {
-        case 0: hipLaunchKernelGGL(k_tile_reduce<0>, dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units); break;
+        case 0: hipLaunchKernelGGL((k_tile_reduce<0, false, false>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units); break;
         case 1:
-            if (vnarrow) hipLaunchKernelGGL((k_tile_reduce<1, true>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
-            else hipLaunchKernelGGL(k_tile_reduce<1>, dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
+            if (vnarrow) VH_TB(1, true);
+            else VH_TB(1, false);
             break;
         default:
-            if (vnarrow) hipLaunchKernelGGL((k_tile_reduce<2, true>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
-            else hipLaunchKernelGGL(k_tile_reduce<2>, dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
+            if (vnarrow) VH_TB(2, true);
+            else VH_TB(2, false);
         }
+#undef VH_TB
         VH_HIP(hipGetLastError());
+        for (int k = 0; k < fa.na; k++) {
+            if (!tp.mmtmp[k]) continue;
+            hipLaunchKernelGGL(k_mm_merge, dim3(blocks_for(cells, 256, 8)), dim3(256), 0, st, fa.a[k].grid, tp.mmtmp[k], cells,
+                               fa.a[k].dtype, (int)(fa.a[k].kind == VH_AGG_MAX));
+            VH_HIP(hipGetLastError());
+        }
     }
     return true;
 }
