@@ -40,3 +40,15 @@ for q in which:
         _lib.synchronize()
         t = time.perf_counter() - t0
     print(f"{q}: {t * 1e3:.2f} ms  {n / t / 1e9:.2f} G rows/s  groups {len(r)}", flush=True)
+if os.environ.get("H2O_PROFILE"):  # host-side breakdown of the last query: Python frames + C-ABI calls
+    import cProfile
+    import pstats
+    os.environ["VAEX_AMD_TRACE_CALLS"] = "1"
+    for q in which:
+        pr = cProfile.Profile()
+        pr.enable()
+        Q[q]()
+        _lib.synchronize()
+        pr.disable()
+        print("== profile", q)
+        pstats.Stats(pr).sort_stats("tottime").print_stats(18)

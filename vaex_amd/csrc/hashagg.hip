@@ -1389,10 +1389,12 @@ __global__ __launch_bounds__(256) void k_ha_first(const K *keys, uint64_t nrow, 
     const Vec *src = reinterpret_cast<const Vec *>(keys);
     uint32_t newly = 0, heads = 0, lost = 0;
     const uint64_t nvec = nrow / V, stride = (uint64_t)gridDim.x * 256;
+    const int lane = threadIdx.x & 63;
     auto vec = [&](uint64_t v, const Vec &x) {
-        K prev = x.k[0];
-        bool has_prev = base + v * V > 0;
-        if (has_prev) prev = keys[v * V - 1];
+        // the row before this lane's first is the previous lane's last (lane 0: a load)
+        K prev = __shfl_up(x.k[V - 1], 1, 64);
+        const bool has_prev = base + v * V > 0;
+        if (lane == 0 && has_prev) prev = keys[v * V - 1];
 #pragma unroll
         for (int j = 0; j < V; j++) {
             const bool head = j ? x.k[j] != x.k[j - 1] : (!has_prev || x.k[0] != prev);
@@ -2355,7 +2357,7 @@ int vh_hashagg_order_first(vh_hashagg *h, const void *keys, uint64_t n, int loc)
                 break;
             }
             if (r0 >= n / 8 && heads * 16 > r0) break;  // no long runs: the set build is cheaper
-            chunk += chunk / 2;
+            chunk = heads * 16 > r0 ? chunk + chunk / 2 : chunk * 4;  // runs: a full scan, few syncs
         }
     }
     if (!complete) {
