@@ -1345,7 +1345,7 @@ int vh_agg_download(vh_agg *a, void *host, uint64_t bytes) {
         VH_HIP(hipStreamSynchronize(stream()));
         memcpy(host, small.ptr, bytes);
     } else {
-        VH_HIP(hipMemcpyAsync(host, a->g.ptr, bytes, hipMemcpyDeviceToHost, stream()));
+        copy_to_host(host, a->g.ptr, bytes, stream());
         VH_HIP(hipStreamSynchronize(stream()));
     }
     VH_API_END
@@ -1356,7 +1356,7 @@ int vh_agg_download_order(vh_agg *a, void *host, uint64_t bytes) {
     std::lock_guard<std::mutex> lk(a->grid->mu);
     if (a->kind != VH_AGG_FIRST) fail(VH_ERR_ARG, "not an AggFirst");
     if (bytes != a->grid->length1d * a->grid_isz) fail(VH_ERR_ARG, "download size mismatch");
-    VH_HIP(hipMemcpyAsync(host, a->g2.ptr, bytes, hipMemcpyDeviceToHost, stream()));
+    copy_to_host(host, a->g2.ptr, bytes, stream());
     VH_HIP(hipStreamSynchronize(stream()));
     VH_API_END
 }

@@ -2265,11 +2265,15 @@ int vh_hashagg_read(vh_hashagg *h, int64_t *keys, int64_t *counts, void *const *
     hipStream_t st = stream();
     // destinations may be host or HBM (hipMemcpyDefault: unified addressing), so a caller
     // that decodes the keys on the device keeps them there
-    if (keys) VH_HIP(hipMemcpyAsync(keys, okey, 8 * m, hipMemcpyDefault, st));
-    if (counts) VH_HIP(hipMemcpyAsync(counts, ocnt, 8 * m, hipMemcpyDefault, st));
+    auto out = [&](void *dst, const void *src) {
+        if (resolve_loc(dst, VH_LOC_AUTO) == VH_LOC_DEVICE) VH_HIP(hipMemcpyAsync(dst, src, 8 * m, hipMemcpyDeviceToDevice, st));
+        else copy_to_host(dst, src, 8 * m, st);
+    };
+    if (keys) out(keys, okey);
+    if (counts) out(counts, ocnt);
     for (int v = 0; v < h->nv; v++) {
-        if (sums && sums[v]) VH_HIP(hipMemcpyAsync(sums[v], osum + (uint64_t)v * m, 8 * m, hipMemcpyDefault, st));
-        if (nonnull && nonnull[v]) VH_HIP(hipMemcpyAsync(nonnull[v], onn + (uint64_t)v * m, 8 * m, hipMemcpyDefault, st));
+        if (sums && sums[v]) out(sums[v], osum + (uint64_t)v * m);
+        if (nonnull && nonnull[v]) out(nonnull[v], onn + (uint64_t)v * m);
     }
     VH_HIP(hipStreamSynchronize(st));
     VH_API_END

@@ -135,6 +135,38 @@ uint64_t hcache_max_bytes() {
 }
 }  // namespace
 
+// device -> mapped page-locked host memory, 16 bytes per lane per step (the tail, < 16 B,
+// by lane 0 of workgroup 0)
+__global__ __launch_bounds__(256) void k_copy_to_host(const uint4 *src, uint4 *dst, uint64_t nvec, const uint8_t *tsrc,
+                                                      uint8_t *tdst, uint32_t tail) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nvec; i += (uint64_t)gridDim.x * 256) dst[i] = src[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (uint32_t k = 0; k < tail; k++) tdst[k] = tsrc[k];
+}
+
+void copy_to_host(void *dst, const void *src, uint64_t bytes, hipStream_t st) {
+    if (!bytes) return;
+    void *mapped = nullptr;
+    if (bytes >= (256u << 10) && ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0) {
+        hipPointerAttribute_t at{};
+        if (hipPointerGetAttributes(&at, dst) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer)
+            mapped = at.devicePointer;
+        else
+            (void)hipGetLastError();  // pageable memory: not an error
+    }
+    if (!mapped) {
+        VH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+        return;
+    }
+    const uint64_t nvec = bytes / 16;
+    const uint32_t tail = (uint32_t)(bytes - nvec * 16);
+    const unsigned grid = (unsigned)std::min<uint64_t>((nvec + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_copy_to_host, dim3(grid), dim3(256), 0, st, static_cast<const uint4 *>(src),
+                       static_cast<uint4 *>(mapped), nvec, static_cast<const uint8_t *>(src) + nvec * 16,
+                       static_cast<uint8_t *>(mapped) + nvec * 16, tail);
+    VH_HIP(hipGetLastError());
+}
+
 // return every cached page-locked block to the system (vh_host_cache_trim; vh_comm_destroy)
 void host_cache_trim() {
     std::lock_guard<std::mutex> lk(g_hcache_mu);
@@ -562,7 +594,7 @@ int vh_memcpy_htod(void *dst, const void *src, uint64_t bytes) {
 
 int vh_memcpy_dtoh(void *dst, const void *src, uint64_t bytes) {
     VH_API_BEGIN
-    VH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream()));
+    copy_to_host(dst, src, bytes, stream());
     VH_HIP(hipStreamSynchronize(stream()));
     VH_API_END
 }
