@@ -1,4 +1,6 @@
 cd $GRAFT_REPO_ROOT
-LOG=gpurun_out/pytest_combo.log TMO=600 bash scripts/gpu_tests.sh tests/test_gpu_hashagg_order.py tests/test_gpu_hashagg.py tests/test_gpu_groupby.py tests/test_gpu_h2o.py tests/test_gpu_superagg.py > /dev/null; tail -2 gpurun_out/pytest_combo.log
-bash scripts/prof_h2o_ab.sh vaex_amd/libvaexhip_pair.so 1e9 q3 q5 q7
-H2O_PROFILE=1 timeout -k 10 300 python scripts/exp_h2o.py 1e9 q3 > gpurun_out/h2o_prof.log 2>&1; grep -A28 "== profile q3" gpurun_out/h2o_prof.log
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 200 python scripts/prof_c3.py 1e9 > gpurun_out/prof_c3.log 2>&1; head -45 gpurun_out/prof_c3.log
+mkdir -p gpurun_out/pq10
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/pq10/trace -o run -- python3 scripts/exp_h2o.py 1e9 q10 > gpurun_out/pq10/log.txt 2>&1; grep -E "^q" gpurun_out/pq10/log.txt
+python3 scripts/prof_summary.py gpurun_out/pq10 > gpurun_out/q10_summary.txt; head -25 gpurun_out/q10_summary.txt; rm -rf gpurun_out/pq10

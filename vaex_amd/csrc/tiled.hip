@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstring>
 #include <cmath>
 #include <map>
 #include <memory>
@@ -1909,11 +1910,17 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         }
         VH_HIP(hipGetLastError());
     }
-    std::vector<uint64_t> hist(2 * (uint64_t)T);
-    std::vector<uint32_t> brange(2 * sblocks);
-    VH_HIP(hipMemcpyAsync(hist.data(), d_hist, 16 * (uint64_t)T, hipMemcpyDeviceToHost, st));
-    VH_HIP(hipMemcpyAsync(brange.data(), d_brange, 8 * sblocks, hipMemcpyDeviceToHost, st));
+    // the sample comes back and the plan goes out through a page-locked block (pageable
+    // copies are staged by the runtime, each one a host wait): [download | upload]; reuse is
+    // safe because every call waits on the stream for its download before writing the block
+    thread_local PinnedBuf tstage;
+    const uint64_t dl_bytes = (16 * (uint64_t)T + 8 * sblocks + 255) & ~uint64_t(255);
+    tstage.ensure(dl_bytes + 24 * (uint64_t)T + sizeof(WorkUnit) * max_units + 1024);
+    VH_HIP(hipMemcpyAsync(tstage.ptr, d_hist, 16 * (uint64_t)T, hipMemcpyDeviceToHost, st));
+    VH_HIP(hipMemcpyAsync(tstage.as<char>() + 16 * (uint64_t)T, d_brange, 8 * sblocks, hipMemcpyDeviceToHost, st));
     VH_HIP(hipStreamSynchronize(st));
+    const uint64_t *hist = tstage.as<uint64_t>();
+    const uint32_t *brange = reinterpret_cast<const uint32_t *>(tstage.as<char>() + 16 * (uint64_t)T);
     // sample blocks whose tile ranges follow each other (a column sorted, up or down, along
     // the grid index): each workgroup's evenly spaced batches then meet a tile floor or ceil
     // of K p_t times, and p_t is exact to a block
@@ -2018,10 +2025,16 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     for (int s = 0; s < nv; s++)
         tp.values[s] = vnarrow ? reinterpret_cast<double *>(ws.values.as<uint32_t>() + (uint64_t)s * total)
                                : ws.values.as<double>() + (uint64_t)s * total;
-    VH_HIP(hipMemcpyAsync(d_cap, cap.data(), 4 * (uint64_t)T, hipMemcpyHostToDevice, st));
-    VH_HIP(hipMemcpyAsync(d_toff, toff.data(), 8 * (uint64_t)T, hipMemcpyHostToDevice, st));
-    VH_HIP(hipMemcpyAsync(d_sstart, sstart.data(), 8 * (uint64_t)T, hipMemcpyHostToDevice, st));
-    VH_HIP(hipMemcpyAsync(d_scap, scap.data(), 4 * (uint64_t)T, hipMemcpyHostToDevice, st));
+    char *upl = tstage.as<char>() + dl_bytes;  // upload region: cap | toff | sstart | scap | units
+    auto upload = [&](void *dst, const void *src, uint64_t bytes) {
+        memcpy(upl, src, bytes);
+        VH_HIP(hipMemcpyAsync(dst, upl, bytes, hipMemcpyHostToDevice, st));
+        upl += (bytes + 15) & ~uint64_t(15);
+    };
+    upload(d_cap, cap.data(), 4 * (uint64_t)T);
+    upload(d_toff, toff.data(), 8 * (uint64_t)T);
+    upload(d_sstart, sstart.data(), 8 * (uint64_t)T);
+    upload(d_scap, scap.data(), 4 * (uint64_t)T);
     VH_HIP(hipMemsetAsync(d_sfill, 0, 4 * (uint64_t)T, st));
 
     // ---- pass B work units: tiles split over ranges of pass-A workgroups by expected size;
@@ -2035,8 +2048,7 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
             units.push_back({t, (uint32_t)((uint64_t)W * k / g), (uint32_t)((uint64_t)W * (k + 1) / g), k | (g << 16)});
     }
     if (units.size() > max_units) fail(VH_ERR_RUNTIME, "tiled binning: work-unit table overflow");
-    if (!units.empty())
-        VH_HIP(hipMemcpyAsync(d_units, units.data(), sizeof(WorkUnit) * units.size(), hipMemcpyHostToDevice, st));
+    if (!units.empty()) upload(d_units, units.data(), sizeof(WorkUnit) * units.size());
 
     // ---- pass A
     {
