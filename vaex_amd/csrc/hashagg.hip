@@ -1624,7 +1624,9 @@ static void ensure_table(vh_hashagg *h, uint64_t need) {
 // used slots (not counting the side slot) and the error word
 static uint32_t read_used(vh_hashagg *h, uint32_t *err) {
     const HaTable g = table_view(h->tab.ptr, h->slots, h->nv, h->vfloat);
-    uint32_t ue[2];
+    thread_local PinnedBuf pb;  // a page-locked target: no staged pageable copy
+    pb.ensure(64);
+    uint32_t *ue = pb.as<uint32_t>();
     VH_HIP(hipMemcpyAsync(ue, g.used, 8, hipMemcpyDeviceToHost, stream()));
     VH_HIP(hipStreamSynchronize(stream()));
     if (err) *err = ue[1];
@@ -1665,8 +1667,10 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
         hipLaunchKernelGGL(k_ha_sample_stats, dim3(blocks_for(sslots, 256, 4)), dim3(256), 0, st, scnt, sslots, stats);
         VH_HIP(hipGetLastError());
     }
-    std::vector<uint64_t> fh(FINE + 4);
-    VH_HIP(hipMemcpyAsync(fh.data(), fine, 8 * (FINE + 4), hipMemcpyDeviceToHost, st));
+    thread_local PinnedBuf fb;  // page-locked sample read-back
+    fb.ensure(8 * (FINE + 4));
+    const uint64_t *fh = fb.as<uint64_t>();
+    VH_HIP(hipMemcpyAsync(fb.ptr, fine, 8 * (FINE + 4), hipMemcpyDeviceToHost, st));
     VH_HIP(hipStreamSynchronize(st));
     uint64_t sampled = 0;
     for (uint32_t i = 0; i < FINE; i++) sampled += fh[i];
