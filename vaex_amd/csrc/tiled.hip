@@ -98,7 +98,10 @@ struct TileParams {
     // 4-byte value slots (every summed column <= 4 bytes: int8/16/32, uint8/16/32, bool,
     // float32 -- exact): slot s is float32 bits when bit s of vfloat is set, else the low 32
     // bits of the int64 slot, sign-extended back when bit s of vsigned is set
-    uint32_t vnarrow, vfloat, vsigned, pad2;
+    uint32_t vnarrow, vfloat, vsigned;
+    // two narrow slots packed per entry: values[0] holds {slot 0, slot 1} as one 8-byte pair
+    // (the narrow ordinal pass A with two carried columns: one value stream, not two)
+    uint32_t vpacked;
     int32_t vdt[2];            // value slot -> column dtype (fast ordinal kernel)
     // min / max aggregator k: pass B flushes its LDS cells with native global atomics into
     // mmtmp[k] (cells x 4 or 8 bytes of the LDS cell form, identity-filled), merged into the
@@ -713,6 +716,12 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
             // the region, or past it the tile's spill area
             const uint64_t e = dest < l.lim[t] ? region0 + dest : tp.spill_base + tp.spill_start[t] + (dest + l.soff[t]);
             reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)kk;
+            if constexpr (sizeof(VT) == 4 && NV == 2) {
+                if (tp.vpacked) {
+                    reinterpret_cast<uint2 *>(tp.values[0])[e] = make_uint2(sv[k], sv[CAP + k]);
+                    continue;
+                }
+            }
 #pragma unroll
             for (int s = 0; s < NV; s++) {
                 if constexpr (sizeof(VT) == 4)
@@ -1424,6 +1433,21 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                 ev[j] = *reinterpret_cast<const uint4 *>(ent16 + e);
 #pragma unroll
                 for (int s = 0; s < NV; s++) {
+                    if constexpr (NARROW && NV == 2) {
+                        if (tp.vpacked) {  // 8 x {slot 0, slot 1} pairs: four 16-byte loads, both slots at s == 0
+                            if (s == 0) {
+                                const uint4 *pp = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint2 *>(tp.values[0]) + e);
+                                const bool f0 = tp.vfloat & 1, g0 = tp.vsigned & 1, f1 = (tp.vfloat >> 1) & 1, g1 = (tp.vsigned >> 1) & 1;
+#pragma unroll
+                                for (int h = 0; h < 4; h++) {
+                                    const uint4 w = pp[h];
+                                    vv[j][0][h] = make_double2(slot_wide(w.x, f0, g0), slot_wide(w.z, f0, g0));
+                                    vv[j][1][h] = make_double2(slot_wide(w.y, f1, g1), slot_wide(w.w, f1, g1));
+                                }
+                            }
+                            continue;
+                        }
+                    }
                     if constexpr (NARROW) {  // 8 x 4-byte slots: two 16-byte loads, widened
                         const bool fl = (tp.vfloat >> s) & 1, sg = (tp.vsigned >> s) & 1;
                         const uint4 a = *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint32_t *>(tp.values[s]) + e);
@@ -2004,6 +2028,9 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     ws.entries.ensure(total * ebytes);
     if (nv) ws.values.ensure(total * (vnarrow ? 4 : 8) * nv + 64);
     tp.vnarrow = vnarrow ? 1u : 0u;
+    // the narrow ordinal pass A with two carried columns stores them as one 8-byte pair per
+    // entry (values[0] spans both slot arrays; values[1] is unused)
+    tp.vpacked = (fast_mode == 3 && nv == 2 && !flags_mode && !getenv_flag_off("VH_TILE_PACK")) ? 1u : 0u;
     tp.vfloat = vfloat;
     tp.vsigned = vsigned;
     tp.s_log2 = s_log2;
