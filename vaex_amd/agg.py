@@ -164,7 +164,7 @@ class AggregatorDescriptorMean(AggregatorDescriptorMulti):
 
         @delayed
         def finish(sum, count):
-            sum = np.array(sum)
+            sum = np.asarray(sum)  # a view of the grid's host image: the division makes the result
             dtype = sum.dtype
             sum_kind = sum.dtype.kind
             if sum_kind == "M":

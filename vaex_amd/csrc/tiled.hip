@@ -1347,8 +1347,9 @@ template <int NV> constexpr int tb_vu() { return VH_TB_VU ? VH_TB_VU : NV == 0 ?
 // short the regions are; a lane finds the region of its chunk by a forward scan (chunk
 // indices of a lane only grow).  Entries are reduced with LDS atomics, then the tile is
 // flushed with coalesced global atomics.
-template <int NV, bool NARROW = false, bool MM = false>
+template <int NV, bool NARROW = false, bool MM = false, bool PK = false>
 __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TileParams tp, const WorkUnit *units) {
+    static_assert(!PK || (NV == 2 && NARROW), "packed pairs of narrow slots");
     extern __shared__ __align__(16) unsigned char lds_raw[];
     __shared__ uint32_t s_fill[1024 + 1];
     __shared__ uint32_t s_pre[1024 + 2];
@@ -1433,8 +1434,8 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                 ev[j] = *reinterpret_cast<const uint4 *>(ent16 + e);
 #pragma unroll
                 for (int s = 0; s < NV; s++) {
-                    if constexpr (NARROW && NV == 2) {
-                        if (tp.vpacked) {  // 8 x {slot 0, slot 1} pairs: four 16-byte loads, both slots at s == 0
+                    if constexpr (PK) {
+                        {  // 8 x {slot 0, slot 1} pairs (tp.vpacked): four 16-byte loads, both slots at s == 0
                             if (s == 0) {
                                 const uint4 *pp = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint2 *>(tp.values[0]) + e);
                                 const bool f0 = tp.vfloat & 1, g0 = tp.vsigned & 1, f1 = (tp.vfloat >> 1) & 1, g1 = (tp.vsigned >> 1) & 1;
@@ -2130,8 +2131,14 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
             else VH_TB(1, false);
             break;
         default:
-            if (vnarrow) VH_TB(2, true);
-            else VH_TB(2, false);
+            if (tp.vpacked) {
+                if (mm) hipLaunchKernelGGL((k_tile_reduce<2, true, true, true>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
+                else hipLaunchKernelGGL((k_tile_reduce<2, true, false, true>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
+            } else if (vnarrow) {
+                VH_TB(2, true);
+            } else {
+                VH_TB(2, false);
+            }
         }
 #undef VH_TB
         VH_HIP(hipGetLastError());

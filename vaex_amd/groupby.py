@@ -109,17 +109,26 @@ class GrouperDense(BinnerBase):
     def bin_values(self):
         """min_value .. max (built on demand: a single-key groupby only needs the occupied ones)."""
         if self._bin_values is None:
-            self._bin_values = np.arange(self.min_value, self.min_value + self.N, dtype=np.int64).astype(self.value_dtype)
+            self._bin_values = _label_range(self.min_value, self.N, self.value_dtype)
         return self._bin_values
 
     def occupied_values(self, mask, all_set=False):
         """Labels of the cells where mask is set (mask over the N central cells)."""
         if all_set:
-            return np.arange(self.min_value, self.min_value + self.N, dtype=np.int64).astype(self.value_dtype)
+            return _label_range(self.min_value, self.N, self.value_dtype)
         return (np.flatnonzero(mask) + self.min_value).astype(self.value_dtype)
 
     def labels(self):
         return self.bin_values.tolist()
+
+
+def _label_range(vmin, n, dtype):
+    """min .. min + n - 1 as `dtype` (label_dtype chose it to hold them), built in that dtype
+    directly (no int64 array and cast for a 1e6-group result)."""
+    dtype = np.dtype(dtype)
+    if dtype.kind in "iu":
+        return np.arange(vmin, vmin + n, dtype=dtype)
+    return np.arange(vmin, vmin + n, dtype=np.int64).astype(dtype)
 
 
 def _dense_range(df, expression):
