@@ -99,8 +99,9 @@ struct TileParams {
     // float32 -- exact): slot s is float32 bits when bit s of vfloat is set, else the low 32
     // bits of the int64 slot, sign-extended back when bit s of vsigned is set
     uint32_t vnarrow, vfloat, vsigned;
-    // two narrow slots packed per entry: values[0] holds {slot 0, slot 1} as one 8-byte pair
-    // (the narrow ordinal pass A with two carried columns: one value stream, not two)
+    // two narrow slots in one array: values[0] holds, per 8 entries, their 8 slot-0 values then
+    // their 8 slot-1 values (the narrow ordinal pass A with two carried columns: one write
+    // stream, not two; pass B still reads each slot as 32 contiguous bytes)
     uint32_t vpacked;
     int32_t vdt[2];            // value slot -> column dtype (fast ordinal kernel)
     // min / max aggregator k: pass B flushes its LDS cells with native global atomics into
@@ -717,8 +718,10 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
             const uint64_t e = dest < l.lim[t] ? region0 + dest : tp.spill_base + tp.spill_start[t] + (dest + l.soff[t]);
             reinterpret_cast<uint16_t *>(tp.entries)[e] = (uint16_t)kk;
             if constexpr (sizeof(VT) == 4 && NV == 2) {
-                if (tp.vpacked) {
-                    reinterpret_cast<uint2 *>(tp.values[0])[e] = make_uint2(sv[k], sv[CAP + k]);
+                if (tp.vpacked) {  // blocked by 8 entries: [8 x slot 0 | 8 x slot 1] per 64 bytes
+                    uint32_t *vb = reinterpret_cast<uint32_t *>(tp.values[0]) + (e & ~uint64_t(7)) * 2 + (e & 7);
+                    vb[0] = sv[k];
+                    vb[8] = sv[CAP + k];
                     continue;
                 }
             }
@@ -1435,17 +1438,14 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
 #pragma unroll
                 for (int s = 0; s < NV; s++) {
                     if constexpr (PK) {
-                        {  // 8 x {slot 0, slot 1} pairs (tp.vpacked): four 16-byte loads, both slots at s == 0
-                            if (s == 0) {
-                                const uint4 *pp = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint2 *>(tp.values[0]) + e);
-                                const bool f0 = tp.vfloat & 1, g0 = tp.vsigned & 1, f1 = (tp.vfloat >> 1) & 1, g1 = (tp.vsigned >> 1) & 1;
-#pragma unroll
-                                for (int h = 0; h < 4; h++) {
-                                    const uint4 w = pp[h];
-                                    vv[j][0][h] = make_double2(slot_wide(w.x, f0, g0), slot_wide(w.z, f0, g0));
-                                    vv[j][1][h] = make_double2(slot_wide(w.y, f1, g1), slot_wide(w.w, f1, g1));
-                                }
-                            }
+                        {  // tp.vpacked: the chunk's 8 x slot s at 64 * (e / 8) + 32 * s bytes
+                            const bool fl = (tp.vfloat >> s) & 1, sg = (tp.vsigned >> s) & 1;
+                            const uint4 *pp = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint32_t *>(tp.values[0]) + e * 2 + 8 * s);
+                            const uint4 a = pp[0], b = pp[1];
+                            vv[j][s][0] = make_double2(slot_wide(a.x, fl, sg), slot_wide(a.y, fl, sg));
+                            vv[j][s][1] = make_double2(slot_wide(a.z, fl, sg), slot_wide(a.w, fl, sg));
+                            vv[j][s][2] = make_double2(slot_wide(b.x, fl, sg), slot_wide(b.y, fl, sg));
+                            vv[j][s][3] = make_double2(slot_wide(b.z, fl, sg), slot_wide(b.w, fl, sg));
                             continue;
                         }
                     }
@@ -2029,8 +2029,8 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     ws.entries.ensure(total * ebytes);
     if (nv) ws.values.ensure(total * (vnarrow ? 4 : 8) * nv + 64);
     tp.vnarrow = vnarrow ? 1u : 0u;
-    // the narrow ordinal pass A with two carried columns stores them as one 8-byte pair per
-    // entry (values[0] spans both slot arrays; values[1] is unused)
+    // the narrow ordinal pass A with two carried columns stores both in values[0], blocked by 8
+    // entries (values[0] spans both slot arrays; values[1] is unused)
     tp.vpacked = (fast_mode == 3 && nv == 2 && !flags_mode && !getenv_flag_off("VH_TILE_PACK")) ? 1u : 0u;
     tp.vfloat = vfloat;
     tp.vsigned = vsigned;
