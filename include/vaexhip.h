@@ -196,6 +196,13 @@ int vh_set_map_ordinal(vh_set *set, const void *keys, uint64_t n, int loc, void 
 /* ---- limits pre-pass: vaexfast.cpp:1043-1055 (op_min_max) --------------- */
 int vh_minmax(const void *data, uint64_t n, int dtype, int flip_endian, const uint8_t *mask, int loc,
               double *out_min, double *out_max);
+/* min / max (as double, NaN ignored) of `nsample` evenly spaced rows (row j * n / nsample) of
+ * a native, unmasked HBM column: the speculative key range of a dense single-key groupby
+ * (vaex_amd/groupby.py _dense_range).  No reference counterpart: the reference's Grouper
+ * builds an ordered_set instead (groupby.py:97-168); the caller verifies the guess with the
+ * grid's under/overflow cells (superagg_binners.cpp:104-142 bins out-of-range keys there)
+ * and redoes the query with the exact vh_minmax range when they are not empty. */
+int vh_minmax_sample(const void *data, uint64_t n, int dtype, uint64_t nsample, double *out_min, double *out_max);
 
 /* ---- fused hash groupby (hashagg.hip) ------------------------------------
  * groupby(key).agg({count(*), count(v), sum(v), mean(v)}) for one integer key column

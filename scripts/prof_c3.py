@@ -26,3 +26,13 @@ pr.disable()
 s = io.StringIO()
 pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
 print(s.getvalue()[:7000])
+if _lib._TRACE is not None:
+    _lib.trace_report()
+    import time
+    t0 = time.perf_counter()
+    q()
+    _lib.synchronize()
+    t1 = time.perf_counter()
+    print(f"query {1e3 * (t1 - t0):.3f} ms; C-ABI calls (calls, ms):")
+    for k, (c, s) in sorted(_lib.trace_report().items(), key=lambda kv: -kv[1][1]):
+        print(f"  {k:32s} {c:4d} {1e3 * s:8.3f}")

@@ -85,6 +85,7 @@ SIGNATURES = {
     "vh_set_key_array": (_i32, [_vp, _vp]),
     "vh_set_map_ordinal": (_i32, [_vp, _vp, _u64, _i32, _vp, _i32, _i32]),
     "vh_minmax": (_i32, [_vp, _u64, _i32, _i32, _vp, _i32, _p(_dbl), _p(_dbl)]),
+    "vh_minmax_sample": (_i32, [_vp, _u64, _i32, _u64, _p(_dbl), _p(_dbl)]),
     "vh_hashagg_create": (_i32, [_i32, _i32, _p(_i32), ctypes.c_uint32, _p(_vp)]),
     "vh_hashagg_destroy": (_i32, [_vp]),
     "vh_hashagg_update": (_i32, [_vp, _vp, _p(_vp), _u64, _i32]),

@@ -468,6 +468,21 @@ __global__ __launch_bounds__(256) void k_minmax_vec(const T *data, uint64_t nvec
     block_minmax_keys(klo, khi, part);
 }
 
+// min / max of `ns` evenly spaced rows (row floor(j * n / ns)) of a native, unmasked column:
+// the speculative key range of a dense groupby (vh_minmax_sample)
+template <typename T>
+__global__ __launch_bounds__(256) void k_minmax_sample(const T *data, uint64_t n, uint64_t ns, uint64_t *part) {
+    uint64_t lo = ~0ULL, hi = 0ULL;
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < ns; j += (uint64_t)gridDim.x * blockDim.x) {
+        const double d = to_double(data[(uint64_t)(((unsigned __int128)j * n) / ns)]);
+        if (d != d) continue;
+        const uint64_t k = f64_key(d);
+        lo = k < lo ? k : lo;
+        hi = k > hi ? k : hi;
+    }
+    block_minmax_keys(lo, hi, part);
+}
+
 // fold the `nb` workgroup partials into keys[0] (min) / keys[1] (max)
 __global__ __launch_bounds__(256) void k_minmax_fin(const uint64_t *part, unsigned nb, uint64_t *keys) {
     uint64_t lo = ~0ULL, hi = 0ULL;
@@ -679,6 +694,45 @@ int vh_stream(void **s) {
     VH_API_END
 }
 
+// the 16-B (min key, max key) result through a page-locked block (a pageable read-back
+// costs more than the scan)
+static void minmax_result(const DevBuf &keys, double *out_min, double *out_max) {
+    thread_local PinnedBuf res_buf;
+    res_buf.ensure(16);
+    uint64_t *res = res_buf.as<uint64_t>();
+    VH_HIP(hipMemcpyAsync(res, keys.ptr, 16, hipMemcpyDeviceToHost, stream()));
+    VH_HIP(hipStreamSynchronize(stream()));
+    if (res[0] == ~0ULL) {  // no non-NaN value (nanmin of all-NaN -> nan)
+        *out_min = __builtin_nan("");
+        *out_max = __builtin_nan("");
+    } else {
+        *out_min = f64_from_key(res[0]);
+        *out_max = f64_from_key(res[1]);
+    }
+}
+
+int vh_minmax_sample(const void *data, uint64_t n, int dtype, uint64_t nsample, double *out_min, double *out_max) {
+    VH_API_BEGIN
+    if (resolve_loc(data, VH_LOC_AUTO) != VH_LOC_DEVICE) throw std::runtime_error("vh_minmax_sample: column not in device memory");
+    if (dtype == VH_BOOL) throw std::runtime_error("vh_minmax_sample: bool column");
+    const uint64_t ns = std::min(n, nsample);
+    DevBuf keys;
+    const unsigned nb = ns ? (unsigned)std::min<uint64_t>((ns + 255) / 256, 256) : 0;
+    keys.ensure(16 * ((uint64_t)nb + 1));
+    uint64_t *part = keys.as<uint64_t>() + 2;
+    if (nb) {
+        VH_DISPATCH_DTYPE(dtype, T,
+                          if constexpr (!std::is_same_v<T, vbool>)
+                              hipLaunchKernelGGL(k_minmax_sample<T>, dim3(nb), dim3(256), 0, stream(),
+                                                 static_cast<const T *>(data), n, ns, part));
+        VH_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_minmax_fin, dim3(1), dim3(256), 0, stream(), part, nb, keys.as<uint64_t>());
+    VH_HIP(hipGetLastError());
+    minmax_result(keys, out_min, out_max);
+    VH_API_END
+}
+
 int vh_minmax(const void *data, uint64_t n, int dtype, int flip, const uint8_t *mask, int loc,
               double *out_min, double *out_max) {
     VH_API_BEGIN
@@ -724,19 +778,7 @@ int vh_minmax(const void *data, uint64_t n, int dtype, int flip, const uint8_t *
         hipLaunchKernelGGL(k_minmax_fin, dim3(1), dim3(256), 0, stream(), part, nb1 + nb2, keys.as<uint64_t>());
         VH_HIP(hipGetLastError());
     }
-    // the 16-B result through a page-locked block (a pageable read-back costs more than the scan)
-    thread_local PinnedBuf res_buf;
-    res_buf.ensure(16);
-    uint64_t *res = res_buf.as<uint64_t>();
-    VH_HIP(hipMemcpyAsync(res, keys.ptr, 16, hipMemcpyDeviceToHost, stream()));
-    VH_HIP(hipStreamSynchronize(stream()));
-    if (res[0] == ~0ULL) {  // no non-NaN value (nanmin of all-NaN -> nan)
-        *out_min = __builtin_nan("");
-        *out_max = __builtin_nan("");
-    } else {
-        *out_min = f64_from_key(res[0]);
-        *out_max = f64_from_key(res[1]);
-    }
+    minmax_result(keys, out_min, out_max);
     VH_API_END
 }
 

@@ -590,9 +590,9 @@ class DataFrame:
 
     # ---- groupby -----------------------------------------------------------------
     def groupby(self, by=None, agg=None, sort=False, assume_sparse="auto", row_limit=None, copy=True,
-                progress=None, delay=False):
+                progress=None, delay=False, _speculate=True):
         """dataframe.py:6622-6683."""
-        from .groupby import GroupBy, GroupByDeferred, _dense_range, groupby_multikey, parse_actions
+        from .groupby import DenseRangeMiss, GroupBy, GroupByDeferred, _dense_range, groupby_multikey, parse_actions
         if agg is None:  # df.groupby(by).agg(...): the same routes as groupby(by, agg=...)
             return GroupByDeferred(self, by, sort=sort, assume_sparse=assume_sparse, row_limit=row_limit)
         dense_ranges = {}
@@ -607,7 +607,7 @@ class DataFrame:
             from .hashagg import eligible_key, try_groupby
             key = eligible_key(self, by)
             if key is not None:
-                rng = _dense_range(self, key)
+                rng = _dense_range(self, key, speculative=_speculate)
                 if rng is not None:
                     dense_ranges[key] = rng
                 else:
@@ -626,7 +626,13 @@ class DataFrame:
                 return res
         groupby = GroupBy(self, by=by, sort=sort, row_limit=row_limit, dense=assume_sparse != True,  # noqa: E712
                           dense_ranges=dense_ranges)
-        return groupby.agg(agg)
+        try:
+            return groupby.agg(agg)
+        except DenseRangeMiss:
+            # the sampled key range missed rows: the exact min / max pass decides the route
+            dense_ranges.clear()
+            return self.groupby(by, agg=agg, sort=sort, assume_sparse=assume_sparse, row_limit=row_limit,
+                                _speculate=False)
 
     def export_hdf5(self, path, **kwargs):
         """dataframe.py export_hdf5: numeric columns (host or HBM) as vaex's HDF5 layout

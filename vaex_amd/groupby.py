@@ -92,12 +92,13 @@ class GrouperDense(BinnerBase):
 
     dense = True
 
-    def __init__(self, expression, vmin, vmax, df=None, row_limit=None):
+    def __init__(self, expression, vmin, vmax, df=None, row_limit=None, speculative=False):
         self.df = df if df is not None else expression.df
         self.expression = str(expression)
         self.label = self.expression
         self.min_value = int(vmin)
         self.N = int(vmax) - int(vmin) + 1
+        self.speculative = speculative  # [vmin, vmax] guessed from a sample (_dense_range)
         dtype = self.df.data_type(self.expression)
         self.value_dtype = label_dtype(dtype, vmin, vmax)
         self._bin_values = None
@@ -112,11 +113,23 @@ class GrouperDense(BinnerBase):
             self._bin_values = _label_range(self.min_value, self.N, self.value_dtype)
         return self._bin_values
 
-    def occupied_values(self, mask, all_set=False):
-        """Labels of the cells where mask is set (mask over the N central cells)."""
+    def occupied_values(self, mask, all_set=False, first=0):
+        """Labels of the cells where mask is set (mask over the central cells from `first` on)."""
+        vmin = self.min_value + first
         if all_set:
-            return _label_range(self.min_value, self.N, self.value_dtype)
-        return (np.flatnonzero(mask) + self.min_value).astype(self.value_dtype)
+            return _label_range(vmin, len(mask), self.value_dtype)
+        return (np.flatnonzero(mask) + vmin).astype(self.value_dtype)
+
+    def trim(self, counts_edges, mask):
+        """A speculative range: raise DenseRangeMiss when keys fell outside it (under/overflow
+        cells 1 and N + 2 of the count(*) grid), else the (first, last) occupied central cells,
+        with the label dtype taken from the keys that occur (what the exact range gives)."""
+        if counts_edges[1] or counts_edges[-1] or not mask.any():
+            raise DenseRangeMiss(self.expression)
+        first = int(np.argmax(mask))
+        last = len(mask) - 1 - int(np.argmax(mask[::-1]))
+        self.value_dtype = label_dtype(self.key_dtype, self.min_value + first, self.min_value + last)
+        return first, last
 
     def labels(self):
         return self.bin_values.tolist()
@@ -131,8 +144,43 @@ def _label_range(vmin, n, dtype):
     return np.arange(vmin, vmin + n, dtype=np.int64).astype(dtype)
 
 
-def _dense_range(df, expression):
-    """(min, max) when an integer, unmasked key spans <= DENSE_KEY_MAX values, else None."""
+# a dense key range is guessed from this many evenly spaced rows (vh_minmax_sample) when the
+# column has at least SPECULATE_MIN_ROWS rows in HBM; the guess is widened by 1/32 of its span
+# (uniform keys: the sample's extremes lie ~span / 65536 inside the true ones)
+SPECULATE_MIN_ROWS = 1 << 22
+SPECULATE_SAMPLE = 1 << 16
+
+
+class DenseRangeMiss(Exception):
+    """A speculative dense range missed keys (the grid's under/overflow cells are not empty)."""
+
+
+def _sampled_range(col, n, dtype):
+    """(lo, hi) widened from the min / max of SPECULATE_SAMPLE evenly spaced rows, or None."""
+    import ctypes
+
+    from . import _lib
+    from .device import DeviceArray
+    if not isinstance(col, DeviceArray) or n < SPECULATE_MIN_ROWS or not dtype.isnative:
+        return None
+    lo, hi = ctypes.c_double(), ctypes.c_double()
+    code, _ = _lib.dtype_code(dtype)
+    _lib.call("vh_minmax_sample", col.ptr, n, code, SPECULATE_SAMPLE, ctypes.byref(lo), ctypes.byref(hi))
+    if not (np.isfinite(lo.value) and np.isfinite(hi.value)):
+        return None
+    lo, hi = int(lo.value), int(hi.value)
+    info = np.iinfo(dtype)
+    room = int(info.max) - (hi - lo + 1)  # the binner's ordinal_count is a T: it must hold the span
+    if room < 0:
+        return None
+    margin = min(max(64, (hi - lo) // 32), room // 2)
+    return max(lo - margin, int(info.min)), min(hi + margin, int(info.max))
+
+
+def _dense_range(df, expression, speculative=False):
+    """(min, max) when an integer, unmasked key spans <= DENSE_KEY_MAX values, else None.
+    speculative: a range guessed from a row sample (no full min/max pass), as a third item
+    True; GroupBy.agg raises DenseRangeMiss when rows fall outside it."""
     expression = str(expression)
     col = df.columns.get(expression)
     if col is None or np.ma.isMaskedArray(col):
@@ -143,11 +191,17 @@ def _dense_range(df, expression):
     n = df.length_unfiltered()
     if n == 0:
         return None
+    if speculative and (rng := _sampled_range(col, n, dtype)) is not None:
+        span = rng[1] - rng[0] + 1
+        if span <= DENSE_KEY_MAX and span <= 4 * n + 1024 and abs(rng[0]) < 2 ** 53 and abs(rng[1]) < 2 ** 53:
+            return rng[0], rng[1], True
     vmin, vmax = df.minmax(expression)
     if not (abs(int(vmin)) < 2 ** 53 and abs(int(vmax)) < 2 ** 53):
         return None
     span = int(vmax) - int(vmin) + 1
-    if span > DENSE_KEY_MAX or span > 4 * n + 1024:
+    # BinnerOrdinal_<T> takes ordinal_count as a T (superagg_binners.cpp:99): e.g. int8 keys
+    # spanning more than 127 values take the hash route
+    if span > DENSE_KEY_MAX or span > 4 * n + 1024 or span > int(np.iinfo(dtype).max):
         return None
     return int(vmin), int(vmax)
 
@@ -371,7 +425,8 @@ class GroupByBase:
             elif df.is_category(by_value):
                 self.by.append(GrouperCategory(df[str(by_value)], df=df, sort=sort, row_limit=row_limit))
             elif dense and (rng := (dense_ranges or {}).get(str(by_value)) or _dense_range(df, by_value)) is not None:
-                self.by.append(GrouperDense(df[str(by_value)], rng[0], rng[1], df=df, row_limit=row_limit))
+                self.by.append(GrouperDense(df[str(by_value)], rng[0], rng[1], df=df, row_limit=row_limit,
+                                            speculative=len(rng) > 2 and rng[2]))
             else:
                 self.by.append(Grouper(df[str(by_value)], df=df, sort=sort, row_limit=row_limit,
                                        df_original=df_original))
@@ -448,8 +503,15 @@ class GroupBy(GroupByBase):
         arrays = {k: extract_central_part(np.asarray(v.get())) for k, v in arrays.items()}
         columns = {}
         if has_non_existing_pairs:
-            counts = extract_central_part(np.asarray(counts.get()))
+            counts_edges = np.asarray(counts.get())
+            counts = extract_central_part(counts_edges)
             mask = counts > 0
+            if len(self.by) == 1 and getattr(self.by[0], "speculative", False):
+                first, last = self.by[0].trim(counts_edges, mask)
+                mask = mask[first:last + 1]
+                arrays = {k: v[first:last + 1] for k, v in arrays.items()}
+            else:
+                first = 0
             if self.row_limit is not None and any(getattr(b, "dense", False) for b in self.by):
                 groups = int(np.count_nonzero(mask))
                 if groups > self.row_limit:  # what the set build of Grouper raises (groupby.py:125)
@@ -457,7 +519,7 @@ class GroupBy(GroupByBase):
                                             f"larger than the allowed row limit of {self.row_limit:,}")
             every = bool(mask.all())  # every cell occupied (e.g. a dense key range): no compaction
             if len(self.by) == 1 and isinstance(self.by[0], GrouperDense):
-                coords = [self.by[0].occupied_values(mask, all_set=every)]
+                coords = [self.by[0].occupied_values(mask, all_set=every, first=first)]
             else:
                 coords = [c[mask] for c in np.meshgrid(*[np.asarray(b.bin_values) for b in self.by], indexing="ij")]
             for b, coord in zip(self.by, coords):
