@@ -115,3 +115,23 @@ def test_host_expression_evaluation():
     df2 = df.filter("x > 4")
     assert df2.evaluate("x").tolist() == x[x > 4].tolist()
     assert df.data_type("x") == np.float64
+
+
+def test_hostops_match_numpy():
+    """Threaded host finishing (mean division, label ranges) equals the single numpy call."""
+    from vaex_amd import hostops
+    rng = np.random.default_rng(4)
+    n = 3 * hostops.MIN_SPLIT + 17
+    for a in [rng.normal(size=n), rng.integers(-10 ** 12, 10 ** 12, n), rng.integers(0, 2 ** 63, n).astype(np.uint64)]:
+        b = rng.integers(0, 4, n)  # zeros: x / 0 -> inf, 0 / 0 -> nan
+        a[::7] = 0
+        with np.errstate(divide="ignore", invalid="ignore"):
+            exp = a / b
+        got = hostops.true_divide(a, b)
+        assert got.dtype == exp.dtype
+        np.testing.assert_array_equal(got, exp)
+    for dtype, vmin in [("int32", 5), ("int64", -(2 ** 40)), ("uint16", 3), ("int8", -100)]:
+        m = min(n, np.iinfo(dtype).max - vmin)
+        got = hostops.arange(vmin, m, dtype)
+        np.testing.assert_array_equal(got, np.arange(vmin, vmin + m, dtype=dtype))
+        assert got.dtype == np.dtype(dtype)

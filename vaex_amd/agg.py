@@ -154,6 +154,7 @@ class AggregatorDescriptorMean(AggregatorDescriptorMulti):
         super().__init__(name, expression, short_name, selection=selection, edges=edges)
 
     def add_tasks(self, df, binners):
+        from . import hostops
         from .promise import delayed
         sum_agg = sum(self.expression, selection=self.selection, edges=self.edges)
         count_agg = count(self.expression, selection=self.selection, edges=self.edges)
@@ -170,8 +171,7 @@ class AggregatorDescriptorMean(AggregatorDescriptorMulti):
             if sum_kind == "M":
                 sum = sum.view("uint64")
                 count = count.view("uint64")
-            with np.errstate(divide="ignore", invalid="ignore"):
-                mean = sum / count
+            mean = hostops.true_divide(sum, count)  # sum / count, divide / invalid ignored
             if dtype.kind != mean.dtype.kind and sum_kind == "M":
                 mean = mean.astype(dtype)
             return mean

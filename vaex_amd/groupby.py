@@ -12,6 +12,7 @@ cartesian grid is filtered by count > 0.
 import numpy as np
 
 from . import agg as vagg
+from . import hostops
 from .dataframe import DataFrame, Expression, RowLimitException
 from .utils import extract_central_part, label_dtype
 
@@ -140,7 +141,7 @@ def _label_range(vmin, n, dtype):
     directly (no int64 array and cast for a 1e6-group result)."""
     dtype = np.dtype(dtype)
     if dtype.kind in "iu":
-        return np.arange(vmin, vmin + n, dtype=dtype)
+        return hostops.arange(vmin, n, dtype)
     return np.arange(vmin, vmin + n, dtype=np.int64).astype(dtype)
 
 
