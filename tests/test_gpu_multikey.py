@@ -227,3 +227,33 @@ def test_dense_rank_i64(n, keyset):
     assert m.value == len(uniq)
     np.testing.assert_array_equal(rank.to_numpy(), inv.ravel())
     np.testing.assert_array_equal(distinct[:m.value].to_numpy(), uniq)
+
+
+@pytest.mark.parametrize("n", [300_000, 3_000_000])
+def test_aliased_key_columns_share_one_minmax(n, monkeypatch):
+    """Keys that alias one column (groupbyh2o.py: id1 / id2 / id4 / id5 = df['i1_100']) get one
+    min / max pass per distinct column; the result equals the oracle's on the same values
+    (cartesian grid at n = 3e6: 1e4 cells, combined hash key at 3e5 rows)."""
+    import vaex_amd
+    from vaex_amd.dataframe import DataFrame
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(11)
+    a = rng.integers(5, 105, n).astype(np.int8)
+    b = rng.integers(5, 1005, n).astype(np.int32)
+    v = rng.normal(size=n)
+    df = vaex_amd.from_arrays(a=DeviceArray.from_numpy(a), b=DeviceArray.from_numpy(b), v=DeviceArray.from_numpy(v))
+    df.columns["id1"] = df.columns["a"]
+    df.columns["id2"] = df.columns["a"]
+    df.columns["id3"] = df.columns["b"]
+    calls = []
+    real = DataFrame.minmax
+    monkeypatch.setattr(DataFrame, "minmax", lambda self, expr, *x, **kw: calls.append(str(expr)) or real(self, expr, *x, **kw))
+    by = ["id1", "id2"] if n > 1_000_000 else ["id1", "id2", "id3"]
+    got = df.groupby(by, agg={"n": "count", "s": vaex_amd.agg.sum("v"), "c": vaex_amd.agg.count("v")}, sort=True)
+    assert sorted(c for c in calls if c in by) == sorted({"id1", "id3"} & set(by))
+    keys = [a, a] if n > 1_000_000 else [a, a, b]
+    uniq, cnt, s, c = _expected(keys, v)
+    np.testing.assert_array_equal(np.stack([got[k].to_numpy().astype(np.int64) for k in by], axis=1), uniq)
+    np.testing.assert_array_equal(got["n"].to_numpy(), cnt)
+    np.testing.assert_array_equal(got["c"].to_numpy(), c)
+    np.testing.assert_allclose(got["s"].to_numpy(), s, rtol=1e-6, atol=1e-9)
