@@ -33,18 +33,31 @@ Q = {
     "q10": lambda: df.groupby(["id1", "id2", "id3", "id4", "id5", "id6"]).agg({"v3": "sum", "v1": "count"}),
 }
 for q in which:
-    for it in range(3):
+    for it in range(int(os.environ.get("H2O_REPS", "3"))):
         _lib.synchronize()
+        if os.environ.get("H2O_CPROF_EACH"):
+            import cProfile
+            import pstats
+            pr = cProfile.Profile()
+            pr.enable()
         t0 = time.perf_counter()
         r = Q[q]()
         _lib.synchronize()
         t = time.perf_counter() - t0
+        if os.environ.get("H2O_CPROF_EACH"):
+            pr.disable()
+            if t > 1.0:
+                pstats.Stats(pr).sort_stats("tottime").print_stats(12)
+        if os.environ.get("H2O_EACH"):
+            top = sorted(_lib.trace_report().items(), key=lambda kv: -kv[1][1])[:4]
+            print(f"  {q} run {it}: {t * 1e3:.2f} ms", "  ".join(f"{k} {1e3 * v[1]:.1f}" for k, v in top), flush=True)
     print(f"{q}: {t * 1e3:.2f} ms  {n / t / 1e9:.2f} G rows/s  groups {len(r)}", flush=True)
 if os.environ.get("H2O_PROFILE"):  # host-side breakdown of the last query: Python frames + C-ABI calls
     import cProfile
     import pstats
     os.environ["VAEX_AMD_TRACE_CALLS"] = "1"
     for q in which:
+        _lib.trace_report()
         pr = cProfile.Profile()
         pr.enable()
         Q[q]()
@@ -52,3 +65,5 @@ if os.environ.get("H2O_PROFILE"):  # host-side breakdown of the last query: Pyth
         pr.disable()
         print("== profile", q)
         pstats.Stats(pr).sort_stats("tottime").print_stats(18)
+        for k, (c, sec) in sorted(_lib.trace_report().items(), key=lambda kv: -kv[1][1])[:15]:
+            print(f"  {k:32s} {c:5d} {1e3 * sec:10.3f} ms")

@@ -225,7 +225,7 @@ class _PinnedBlock:
         dtype = np.dtype(dtype)
         self.nbytes = max(1, n * dtype.itemsize)
         p = ctypes.c_void_p()
-        check(lib().vh_host_alloc(ctypes.byref(p), self.nbytes))
+        call("vh_host_alloc", ctypes.byref(p), self.nbytes)
         self.ptr = p.value
         self.__array_interface__ = {"shape": (n,), "typestr": dtype.str, "data": (self.ptr, False), "version": 3}
 

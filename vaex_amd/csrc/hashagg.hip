@@ -2519,6 +2519,21 @@ __global__ __launch_bounds__(256) void k_dr_keymax(const int64_t *keys, uint64_t
     }
 }
 
+namespace {
+struct DrScratch {
+    std::mutex mu;
+    DevBuf sk, idx, sidx, flag, scan, tmp;
+};
+DrScratch &dr_scratch() {
+    static std::mutex g;
+    static std::map<int, std::unique_ptr<DrScratch>> m;
+    std::lock_guard<std::mutex> lk(g);
+    auto &p = m[current_device()];
+    if (!p) p = std::make_unique<DrScratch>();
+    return *p;
+}
+}  // namespace
+
 extern "C" {
 
 int vh_dense_rank_i64(uint64_t n, const int64_t *keys, int32_t *rank, int64_t *distinct, uint64_t *m) {
@@ -2531,7 +2546,12 @@ int vh_dense_rank_i64(uint64_t n, const int64_t *keys, int32_t *rank, int64_t *d
         if (resolve_loc(p, VH_LOC_AUTO) != VH_LOC_DEVICE) fail(VH_ERR_ARG, "dense_rank: device buffers only");
     TimedScope ts("dense_rank");
     hipStream_t st = stream();
-    DevBuf sk, idx, sidx, flag, scan, tmp;
+    // the sort's ~36 B per row of scratch (36 GB at 1e9 rows) is kept per device between
+    // calls: allocating and freeing it per call ran into multi-second hipMalloc / hipFree
+    // stalls every few h2o q10 queries (6.1 s instead of 0.31 s)
+    DrScratch &S = dr_scratch();
+    std::lock_guard<std::mutex> lk(S.mu);
+    DevBuf &sk = S.sk, &idx = S.idx, &sidx = S.sidx, &flag = S.flag, &scan = S.scan, &tmp = S.tmp;
     sk.ensure(n * 8);
     idx.ensure(n * 4);
     sidx.ensure(n * 4);

@@ -54,12 +54,26 @@ DeviceScope::~DeviceScope() {
 
 // ---- device block cache (common.hpp) ---------------------------------------------------
 namespace {
-constexpr uint64_t CACHE_MAX_BLOCK = 1ull << 30;
-constexpr uint64_t CACHE_MAX_BYTES = 4ull << 30;
+// Freed device blocks are kept for reuse (exact sizes, 1 MiB granularity): at most 1/8 of
+// the device's memory, blocks of up to 1/16 of it.  Large blocks matter: a 1e9-row query
+// allocates multi-GB temporaries (h2o q10's 8 GB combined key column), and a fresh hipMalloc
+// of 8 GB stalled for 5.7 s every few queries on a device holding ~60 GB.  A failed
+// allocation drops the cache and retries.
 struct BlockCache {
     std::multimap<uint64_t, void *> free;
     uint64_t cached = 0;
+    uint64_t max_bytes = 0, max_block = 0;
 };
+void cache_limits(BlockCache &c) {
+    if (c.max_bytes) return;
+    size_t fr = 0, total = 0;
+    if (hipMemGetInfo(&fr, &total) != hipSuccess || total == 0) {
+        (void)hipGetLastError();
+        total = 32ull << 30;
+    }
+    c.max_bytes = total / 8;
+    c.max_block = total / 16;
+}
 std::mutex g_cache_mu;
 std::map<int, BlockCache> g_cache;
 }  // namespace
@@ -68,7 +82,7 @@ void *dev_alloc(uint64_t &bytes) {
     const uint64_t gran = bytes >= (1ull << 20) ? (1ull << 20) : 4096;
     bytes = (bytes + gran - 1) / gran * gran;
     const int d = current_device();
-    if (bytes <= CACHE_MAX_BLOCK) {
+    {
         std::lock_guard<std::mutex> lk(g_cache_mu);
         BlockCache &c = g_cache[d];
         auto it = c.free.find(bytes);
@@ -101,10 +115,11 @@ void *dev_alloc(uint64_t &bytes) {
 
 void dev_free(void *ptr, uint64_t bytes) {
     if (!ptr) return;
-    if (bytes <= CACHE_MAX_BLOCK) {
+    {
         std::lock_guard<std::mutex> lk(g_cache_mu);
         BlockCache &c = g_cache[current_device()];
-        if (c.cached + bytes <= CACHE_MAX_BYTES) {
+        cache_limits(c);
+        if (bytes <= c.max_block && c.cached + bytes <= c.max_bytes) {
             c.free.emplace(bytes, ptr);
             c.cached += bytes;
             return;
@@ -534,21 +549,45 @@ int vh_synchronize(void) {
     VH_API_END
 }
 
+// user buffers (DeviceArray) come from the device block cache too; their rounded sizes are
+// remembered for vh_free
+namespace {
+std::mutex g_user_mu;
+std::map<void *, std::pair<uint64_t, int>> g_user_blocks;  // ptr -> (bytes, device)
+}  // namespace
+
 int vh_malloc(void **dptr, uint64_t bytes) {
     VH_API_BEGIN
-    (void)current_device();  // this thread on the process's GPU
-    hipError_t e = hipMalloc(dptr, bytes ? bytes : 1);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        fail(VH_ERR_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
+    const int d = current_device();  // this thread on the process's GPU
+    uint64_t b = bytes ? bytes : 1;
+    void *p = dev_alloc(b);
+    {
+        std::lock_guard<std::mutex> lk(g_user_mu);
+        g_user_blocks[p] = {b, d};
     }
+    *dptr = p;
     VH_API_END
 }
 
 int vh_free(void *dptr) {
     VH_API_BEGIN
+    if (!dptr) return VH_OK;
     VH_HIP(hipStreamSynchronize(stream()));
-    VH_HIP(hipFree(dptr));
+    std::pair<uint64_t, int> blk{0, -1};
+    {
+        std::lock_guard<std::mutex> lk(g_user_mu);
+        auto it = g_user_blocks.find(dptr);
+        if (it != g_user_blocks.end()) {
+            blk = it->second;
+            g_user_blocks.erase(it);
+        }
+    }
+    if (blk.second < 0) {
+        VH_HIP(hipFree(dptr));
+    } else {
+        DeviceScope ds(blk.second);
+        dev_free(dptr, blk.first);
+    }
     VH_API_END
 }
 

@@ -82,8 +82,14 @@ class DeviceArray:
         return DeviceArray(stop - start, self.dtype, _ptr=self.ptr + start * self.itemsize,
                            _owner=self if self._owner is None else self._owner)
 
-    def to_numpy(self):
-        out = np.empty(self.length, self.dtype)
+    def to_numpy(self, pinned=False):
+        """A host copy; pinned: into page-locked memory from the library's block cache (read
+        back by the copy kernel at the link rate; a pageable copy runs at ~17 GB/s)."""
+        if pinned:
+            from .hostops import _empty
+            out = _empty(self.length, self.dtype)
+        else:
+            out = np.empty(self.length, self.dtype)
         if self.nbytes:
             _lib.call("vh_memcpy_dtoh", out.ctypes.data, self.ptr, self.nbytes)
         return out

@@ -342,7 +342,7 @@ def _decode_labels(df, ck, table, ranges, mults):
                   (ctypes.c_int * k)(*[dt.itemsize for dt in dtypes]), (ctypes.c_void_p * k)(*[o.ptr for o in outs]))
     # labels of the library's internal recombined keys stay in HBM: the next _decode_labels
     # (_groupby_recombine) reads them there
-    return {name: (o if name.startswith("__vaex_amd_") else o.to_numpy()) if n else np.empty(0, dt)
+    return {name: (o if name.startswith("__vaex_amd_") else o.to_numpy(pinned=True)) if n else np.empty(0, dt)
             for (name, _, _), o, dt in zip(ranges, outs, dtypes)}
 
 
