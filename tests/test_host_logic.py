@@ -135,3 +135,15 @@ def test_hostops_match_numpy():
         got = hostops.arange(vmin, m, dtype)
         np.testing.assert_array_equal(got, np.arange(vmin, vmin + m, dtype=dtype))
         assert got.dtype == np.dtype(dtype)
+
+
+def test_hostops_astype_minmax():
+    from vaex_amd import hostops
+    rng = np.random.default_rng(5)
+    n = 2 * hostops.MIN_SPLIT + 3
+    a = rng.integers(-(2 ** 40), 2 ** 40, n)
+    assert hostops.minmax(a) == (a.min(), a.max())
+    for dt in ["int32", "int16", "uint64", "int64"]:
+        got = hostops.astype(a, dt)
+        assert got.dtype == np.dtype(dt)
+        np.testing.assert_array_equal(got, a.astype(dt))

@@ -13,7 +13,7 @@ import ctypes
 
 import numpy as np
 
-from . import _lib
+from . import _lib, hostops
 from .device import DeviceArray
 from .utils import label_dtype
 
@@ -226,10 +226,10 @@ def try_groupby(df, by, actions, parse, sort=False, row_limit=None, first_order=
     if device_keys:
         labels = keys
     else:
-        labels = keys.astype(kdt, copy=False)
+        labels = hostops.astype(keys, kdt)
         if len(labels):  # groupby.py:131-133
-            lo, hi = (labels.min(), labels.max()) if first_order else (labels[0], labels[-1])
-            labels = labels.astype(label_dtype(kdt, lo, hi), copy=False)
+            lo, hi = hostops.minmax(labels) if first_order else (labels[0], labels[-1])
+            labels = hostops.astype(labels, label_dtype(kdt, lo, hi))
     columns = {by: labels}
     for name, op, vi in ops:
         if op == "count":
@@ -239,6 +239,5 @@ def try_groupby(df, by, actions, parse, sort=False, row_limit=None, first_order=
         elif op == "sum":
             columns[name] = sums[vi]
         else:
-            with np.errstate(divide="ignore", invalid="ignore"):
-                columns[name] = sums[vi] / nonnull[vi]
+            columns[name] = hostops.true_divide(sums[vi], nonnull[vi])
     return DataFrame(columns)

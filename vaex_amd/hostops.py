@@ -76,3 +76,31 @@ def arange(vmin, n, dtype):
 
     _run(part, n)
     return out
+
+
+def astype(a, dtype):
+    """a.astype(dtype, copy=False) for a 1-d array (a C cast, element-wise)."""
+    a, dtype = np.asarray(a), np.dtype(dtype)
+    if a.dtype == dtype or a.ndim != 1 or len(a) < MIN_SPLIT:
+        return a.astype(dtype, copy=False)
+    out = _empty(len(a), dtype)
+
+    def part(i0, i1):
+        out[i0:i1] = a[i0:i1]
+
+    _run(part, len(a))
+    return out
+
+
+def minmax(a):
+    """(a.min(), a.max()) of a non-empty 1-d integer array."""
+    a = np.asarray(a)
+    if a.ndim != 1 or len(a) < MIN_SPLIT:
+        return a.min(), a.max()
+    res = {}
+
+    def part(i0, i1):
+        res[i0] = (a[i0:i1].min(), a[i0:i1].max())
+
+    _run(part, len(a))
+    return min(v[0] for v in res.values()), max(v[1] for v in res.values())
