@@ -83,6 +83,10 @@ int vh_host_free(void *ptr, uint64_t bytes);
 /* free the page-locked blocks the library caches for read-backs and pipeline buffers
  * (capped per process: VAEX_AMD_PINNED_CACHE_MB, else 8 GiB / LOCAL_WORLD_SIZE) */
 int vh_host_cache_trim(void);
+/* free the device blocks the library keeps for reuse on the calling thread's device
+ * (freed scratch and DeviceArray buffers, at most 1/8 of the device's memory; the dense
+ * rank's sort scratch); the next query allocates afresh */
+int vh_device_cache_trim(void);
 int vh_host_register(void *ptr, uint64_t bytes);
 int vh_host_unregister(void *ptr);
 int vh_memcpy_htod(void *dst, const void *src, uint64_t bytes);

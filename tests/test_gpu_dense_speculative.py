@@ -101,3 +101,21 @@ def test_sampled_range_host_columns_use_exact_pass():
     df = vaex_amd.from_arrays(key=keys, v=np.ones(N))
     got = df.groupby("key", agg={"n": "count"})
     np.testing.assert_array_equal(got["n"].to_numpy(), np.bincount(keys)[np.unique(keys)])
+
+
+def test_cached_device_blocks_are_reused_and_trimmed():
+    """vh_malloc / vh_free go through the device block cache (multi-GB query temporaries
+    are reused instead of re-allocated); trim_caches hands everything back and later
+    allocations still work."""
+    from vaex_amd import _lib
+    from vaex_amd.device import DeviceArray
+    a = DeviceArray.from_numpy(np.arange(1 << 20, dtype=np.int64))
+    p = a.ptr
+    del a
+    b = DeviceArray.empty(1 << 20, np.int64)
+    assert b.ptr == p  # the freed block came back
+    del b
+    _lib.trim_caches()
+    c = DeviceArray.from_numpy(np.arange(1000, dtype=np.int32))
+    np.testing.assert_array_equal(c.to_numpy(), np.arange(1000, dtype=np.int32))
+    np.testing.assert_array_equal(c.to_numpy(pinned=True), np.arange(1000, dtype=np.int32))

@@ -35,6 +35,7 @@ SIGNATURES = {
     "vh_host_alloc": (_i32, [_p(_vp), _u64]),
     "vh_host_free": (_i32, [_vp, _u64]),
     "vh_host_cache_trim": (_i32, []),
+    "vh_device_cache_trim": (_i32, []),
     "vh_host_register": (_i32, [_vp, _u64]),
     "vh_host_unregister": (_i32, [_vp]),
     "vh_memcpy_htod": (_i32, [_vp, _vp, _u64]),
@@ -294,3 +295,10 @@ def host_register(a):
 def pinned_empty(n, dtype):
     """1-d numpy array of n items in page-locked memory (fast D2H read-back target)."""
     return np.asarray(_PinnedBlock(int(n), dtype))
+
+
+def trim_caches():
+    """Return the library's cached blocks to the system: page-locked host blocks
+    (vh_host_cache_trim) and the calling thread's device blocks (vh_device_cache_trim)."""
+    call("vh_host_cache_trim")
+    call("vh_device_cache_trim")

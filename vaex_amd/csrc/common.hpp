@@ -257,6 +257,7 @@ struct DevBuf {
 void *host_block_alloc(uint64_t bytes);  // page-locked, from the library's block cache
 void host_block_free(void *ptr, uint64_t bytes);
 void host_cache_trim();  // free every cached page-locked block
+void dense_rank_scratch_release();  // hashagg.hip: the dense rank's per-device sort scratch
 // device -> host copy on `st` (asynchronous): a page-locked destination of >= 256 KiB is
 // written by a copy kernel through its mapped address (the GPU's PCIe writes run at the
 // link rate on every box; the copy engine measured 21-54 GB/s for the same 8.4 MB grid

@@ -2534,6 +2534,14 @@ DrScratch &dr_scratch() {
 }
 }  // namespace
 
+namespace vh {
+void dense_rank_scratch_release() {
+    DrScratch &S = dr_scratch();
+    std::lock_guard<std::mutex> lk(S.mu);
+    for (DevBuf *b : {&S.sk, &S.idx, &S.sidx, &S.flag, &S.scan, &S.tmp}) b->release();
+}
+}  // namespace vh
+
 extern "C" {
 
 int vh_dense_rank_i64(uint64_t n, const int64_t *keys, int32_t *rank, int64_t *distinct, uint64_t *m) {

@@ -609,6 +609,18 @@ int vh_host_cache_trim(void) {
     VH_API_END
 }
 
+int vh_device_cache_trim(void) {
+    VH_API_BEGIN
+    VH_HIP(hipStreamSynchronize(stream()));
+    dense_rank_scratch_release();
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    BlockCache &c = g_cache[current_device()];
+    for (auto &kv : c.free) (void)hipFree(kv.second);
+    c.free.clear();
+    c.cached = 0;
+    VH_API_END
+}
+
 int vh_host_register(void *ptr, uint64_t bytes) {
     VH_API_BEGIN
     if (!ptr || !bytes) fail(VH_ERR_ARG, "vh_host_register: empty range");
