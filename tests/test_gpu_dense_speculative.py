@@ -109,6 +109,7 @@ def test_cached_device_blocks_are_reused_and_trimmed():
     allocations still work."""
     from vaex_amd import _lib
     from vaex_amd.device import DeviceArray
+    _lib.trim_caches()  # no other cached block of this size from earlier tests
     a = DeviceArray.from_numpy(np.arange(1 << 20, dtype=np.int64))
     p = a.ptr
     del a
