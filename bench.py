@@ -530,8 +530,9 @@ def bench_groupby(n, args, layout="random"):
                the BinnerOrdinal grid through the tile path (fast ordinal pass A);
       fused -- the one-pass hash-partitioned aggregation (hashagg.hip) the frame takes for
                sparse int keys, run on the same columns through its API;
-      hash  -- assume_sparse=True: the reference's structure, GPU ordered_set build pass +
-               fused map_ordinal/BinnerOrdinal pass.
+      hash  -- assume_sparse=True: the ordered_set grouper's result (groups in the order their
+               keys first appear): the fused hash aggregation + vh_hashagg_order_first (a
+               run-head prefix scan for each group's first row, a radix sort of the groups).
     Per-kernel milliseconds from HIP events on the library stream."""
     from vaex_amd import _lib
     from vaex_amd.device import DeviceArray

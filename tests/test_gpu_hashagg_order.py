@@ -115,3 +115,39 @@ def test_order_first_tiny_inputs():
         got = df.groupby("key", agg={"n": vaex_amd.agg.count()}, assume_sparse=True)
         np.testing.assert_array_equal(got["key"].to_numpy(), _first_order(k))
         np.testing.assert_array_equal(got["n"].to_numpy(), [int((k == x).sum()) for x in _first_order(k)])
+
+
+def test_order_first_wave_straddling_the_grid_stride():
+    """The first-row scan (k_ha_first) takes each row's predecessor from the neighbour lane.
+    A chunk whose vector count is not a multiple of the grid stride leaves one wave with
+    lanes in the two-vector loop and lanes in the one-vector remainder; the scan must still
+    compare each row with its true predecessor.  Layout (for the MI355X grid of 2048 x 256
+    lanes, 4 int32 keys per lane step): run-structured keys so the second scan chunk spans
+    [2^20, n) rows, a key K that first appears at the first row of the remainder wave's
+    first remainder lane, K again in the rows the neighbour lane held last, and a key M
+    first appearing right after K's first run: K must come before M."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(123)
+    S = 2048 * 256  # grid stride in 16-B vectors (blocks_for cap: 256 CUs x 8)
+    R = 3_000_148  # rows of the second chunk: 750037 vectors, boundary 225749 (lane 21 of its wave)
+    c0 = 1 << 20
+    n = c0 + R
+    keys = np.repeat(rng.integers(0, 1000, n // 64 + 1), 64)[:n].astype(np.int32)
+    K, M = 5000, 5001
+    b = R // 4 - S
+    row = lambda v: c0 + 4 * v  # noqa: E731
+    keys[row(b) - 1] = 7  # the true predecessor differs from K
+    keys[row(b):row(b) + 8] = K
+    keys[row(b) + 8:row(b) + 12] = M
+    keys[row(b) + 12:row(b) + 16] = K
+    keys[row(b - 1 + S):row(b + S)] = K  # what the neighbour lane loaded last
+    keys[row(b - 1 + S) + 4:row(b - 1 + S) + 8] = M
+    df = vaex_amd.from_arrays(key=DeviceArray.from_numpy(keys), v=DeviceArray.from_numpy(np.ones(n)))
+    got = df.groupby("key", agg={"n": vaex_amd.agg.count()}, assume_sparse=True)
+    exp = _first_order(keys)
+    np.testing.assert_array_equal(got["key"].to_numpy(), exp)
+    gk = list(got["key"].to_numpy())
+    assert gk.index(K) < gk.index(M)
+    u, cnt = np.unique(keys, return_counts=True)
+    np.testing.assert_array_equal(got["n"].to_numpy(), cnt[np.searchsorted(u, exp)])

@@ -137,27 +137,119 @@ def test_three_keys_mixed_dtypes_other_aggregators():
     np.testing.assert_array_equal(res["hi"].to_numpy()[order], hi)
 
 
-def test_same_frame_as_uncombined_path():
-    """Same groups, values and label dtypes as assume_sparse=True (per-key set groupers +
-    cartesian grid, filtered by count > 0)."""
-    rng = np.random.default_rng(5)
-    n = 200_000
-    k0 = rng.integers(0, 700, n).astype(np.int32)
-    k1 = rng.integers(-3000, 3000, n).astype(np.int32)
+def _first_appearance_order(keys):
+    """Row index of each key combination's first appearance, in appearance order (the
+    ordered_set order of GrouperCombined with one thread, groupby.py:248-288)."""
+    combined = np.zeros(len(keys[0]), np.int64)
+    for k in keys:  # NaN keys are one group (the oracle's Grouper)
+        labels, ordinal = oracle._grouper(k)
+        _, combined = np.unique(combined * len(labels) + ordinal, return_inverse=True)
+        combined = combined.astype(np.int64).ravel()
+    _, first = np.unique(combined, return_index=True)
+    return np.sort(first)
+
+
+def _check_combined(keys, v, res, names, sort):
+    """res (groupby(..., assume_sparse=True)) against oracle.groupby_agg(combine=True):
+    the same groups and aggregates; without sort the groups in first-appearance order, with
+    sort lexicographic."""
+    cols = {nm: k for nm, k in zip(names, keys)}
+    cols["v"] = v
+    exp = oracle.groupby_agg(cols, names, [("n", "count", None), ("v_sum", "sum", "v"), ("v_count", "count", "v"),
+                                           ("v_mean", "mean", "v")], combine=True)
+    got = [res[nm].to_numpy() for nm in names]
+    order = np.lexsort(got[::-1])
+    for nm, g in zip(names, got):
+        np.testing.assert_array_equal(g[order], exp[nm])
+    np.testing.assert_array_equal(res["n"].to_numpy()[order], exp["n"])
+    np.testing.assert_array_equal(res["v_count"].to_numpy()[order], exp["v_count"])
+    np.testing.assert_allclose(res["v_sum"].to_numpy()[order], exp["v_sum"], rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(res["v_mean"].to_numpy()[order], exp["v_mean"], rtol=1e-6, atol=1e-9)
+    if sort:
+        np.testing.assert_array_equal(order, np.arange(len(order)))
+    else:
+        first = _first_appearance_order(keys)
+        for nm, k in zip(names, keys):
+            np.testing.assert_array_equal(res[nm].to_numpy(), k[first])
+
+
+@pytest.mark.parametrize("nkeys", [2, 3, 6])
+@pytest.mark.parametrize("sort", [False, True])
+def test_assume_sparse_combines_like_reference(monkeypatch, nkeys, sort):
+    """assume_sparse=True is the reference's combine=True (dataframe.py:6679,
+    groupby.py:313-315): the keys are always combined into one grouper, even when the
+    cartesian grid would be small (2 and 3 keys below have >= 10 rows per cell, where
+    'auto' bins the cartesian grid).  Six keys: the h2o q10 key set (id1 / id2 / id4 / id5
+    one int8 column in [5, 105), id3 / id6 one int32 column in [5, 1e6 + 5), 1e20 cells:
+    the 64-bit recursion).  Checked against oracle.groupby_agg(combine=True)."""
+    rng = np.random.default_rng(70 + nkeys)
+    n = 600_000 if nkeys == 6 else 200_000
+    if nkeys == 6:
+        a = rng.integers(5, 105, n).astype(np.int8)
+        b = rng.integers(5, 1_000_005, n).astype(np.int32)
+        keys = [a, a, b, a, a, b]
+    elif nkeys == 3:
+        keys = [rng.integers(0, 4, n).astype(np.int16), rng.integers(-3, 3, n).astype(np.int64),
+                rng.integers(10, 20, n).astype(np.uint8)]
+    else:
+        keys = [rng.integers(0, 30, n).astype(np.int32), rng.integers(-50, 50, n).astype(np.int32)]
     v = rng.normal(size=n)
-    df = _frame([k0, k1], v, True)
-    a = df.groupby(["k0", "k1"], agg=_agg())
-    b = df.groupby(["k0", "k1"], agg=_agg(), assume_sparse=True)
-    assert a.get_column_names() == b.get_column_names()
-    oa = np.lexsort([a["k1"].to_numpy(), a["k0"].to_numpy()])
-    ob = np.lexsort([b["k1"].to_numpy(), b["k0"].to_numpy()])
-    for c in a.get_column_names():
-        x, y = a[c].to_numpy()[oa], b[c].to_numpy()[ob]
-        assert x.dtype == y.dtype, c
-        if x.dtype.kind == "f":
-            np.testing.assert_allclose(x, y, rtol=1e-6, atol=1e-9)
-        else:
-            np.testing.assert_array_equal(x, y)
+    v[::17] = np.nan
+    names = [f"k{i}" for i in range(nkeys)]
+    df = _frame(keys, v, True)
+    calls = _spy(monkeypatch)
+    res = df.groupby(names, agg=_agg(), sort=sort, assume_sparse=True)
+    assert "vh_combine_keys" in calls
+    _check_combined(keys, v, res, names, sort)
+
+
+def test_assume_sparse_false_bins_the_cartesian_grid(monkeypatch):
+    """assume_sparse=False = combine=False: never combined, the cartesian grid filtered by
+    count > 0 (groupby.py:334-335, :484-533)."""
+    rng = np.random.default_rng(77)
+    n = 50_000
+    keys = [rng.integers(0, 300, n).astype(np.int32), rng.integers(0, 200, n).astype(np.int32)]
+    v = rng.normal(size=n)
+    df = _frame(keys, v, True)
+    calls = _spy(monkeypatch)
+    res = df.groupby(["k0", "k1"], agg=_agg(), assume_sparse=False, sort=True)
+    assert "vh_combine_keys" not in calls
+    _check(keys, v, res)
+
+
+@pytest.mark.parametrize("assume_sparse", [True, "auto"])
+@pytest.mark.parametrize("device", [False, True])
+def test_float_keys_combine_through_set_ordinals(monkeypatch, assume_sparse, device):
+    """Keys that are not plain integer columns (float64 with NaN, float32): per-key GPU
+    ordered_sets, every row's set ordinal (map_ordinal), the ordinals combined -- the
+    reference's _combine over Groupers (groupby.py:248-288).  'auto' combines here too
+    (2000 x 1500 cells over 1e5 rows: occupancy < 10, groupby.py:318-333)."""
+    rng = np.random.default_rng(78)
+    n = 100_000
+    k0 = rng.integers(0, 2000, n).astype(np.float64) / 8
+    k0[::97] = np.nan
+    k1 = (rng.integers(0, 1500, n) - 700).astype(np.float32)
+    keys = [k0, k1]
+    v = rng.normal(size=n)
+    df = _frame(keys, v, device)
+    calls = _spy(monkeypatch)
+    res = df.groupby(["k0", "k1"], agg=_agg(), assume_sparse=assume_sparse)
+    assert "vh_combine_keys" in calls and "vh_set_map_ordinal" in calls
+    _check_combined(keys, v, res, ["k0", "k1"], sort=False)
+    assert res["k1"].to_numpy().dtype == np.float32
+
+
+def test_float_keys_high_occupancy_auto_keeps_cartesian(monkeypatch):
+    """'auto' with >= 10 rows per cell of the sets' sizes: the cartesian grid (no combine)."""
+    rng = np.random.default_rng(79)
+    n = 100_000
+    keys = [rng.integers(0, 20, n).astype(np.float64), rng.integers(0, 30, n).astype(np.float64)]
+    v = rng.normal(size=n)
+    df = _frame(keys, v, False)
+    calls = _spy(monkeypatch)
+    res = df.groupby(["k0", "k1"], agg=_agg(), sort=True)
+    assert "vh_combine_keys" not in calls
+    _check_combined(keys, v, res, ["k0", "k1"], sort=True)
 
 
 @pytest.mark.parametrize("device", [False, True])

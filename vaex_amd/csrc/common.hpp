@@ -105,6 +105,25 @@ inline int upcast_dtype(int dtype) {
     }
 
 // ---- device-side helpers ---------------------------------------------------
+// rank of a row in an LDS histogram (partition / tile / bucket counts).  Every lane of the
+// wave calls it (no exec divergence).  When all taking lanes share one bin (sorted or
+// clustered rows) one atomic reserves the wave's ranks and each lane takes its position among
+// them -- 64 same-address LDS atomics would serialise; otherwise one atomic per taking lane,
+// and rows that do not take (past the range, folded) touch nothing.
+__device__ __forceinline__ int32_t wave_rank(uint32_t *hist, uint32_t t, bool take) {
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+    const uint64_t act = __ballot(take);
+    if (__ballot(take && t != t0) == 0) {
+        if (!act) return -1;
+        const int lane = threadIdx.x & 63, lead = __builtin_ctzll(act);
+        uint32_t base = 0;
+        if (lane == lead) base = atomicAdd(&hist[t0], (uint32_t)__builtin_popcountll(act));
+        base = (uint32_t)__shfl((int)base, lead, 64);
+        return take ? (int32_t)(base + (uint32_t)__builtin_popcountll(act & ((1ull << lane) - 1))) : -1;
+    }
+    return take ? (int32_t)atomicAdd(&hist[t], 1u) : -1;
+}
+
 // Block-level slot reservation for compaction: every thread emits `my` items; one atomic on
 // the output counter per workgroup and call (a counter bumped by every wave is one
 // same-address atomic per 64 items: ~9 ms per 1e8).  Returns this thread's first slot.

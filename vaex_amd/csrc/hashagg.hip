@@ -885,8 +885,14 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTab
             if constexpr (NV > 0) vals[r] = h ? cur.v[q][0].y : cur.v[q][0].x;
             const uint32_t t = ha_bucket(hp, kb[r]);
             const bool take = i < row_end && !folded[q];
-            const uint32_t rk = atomicAdd(&hist[take ? t : P], 1u);
-            rank[r] = take ? (int32_t)rk : -1;
+            if constexpr (RUNS) {
+                // folded rows and rows past the range touch no histogram word; a wave whose
+                // rows share a bucket (a run of one key) reserves its ranks with one atomic
+                rank[r] = wave_rank(hist, t, take);
+            } else {
+                const uint32_t rk = atomicAdd(&hist[take ? t : P], 1u);
+                rank[r] = take ? (int32_t)rk : -1;
+            }
         }
     };
     uint32_t novf = 0;
@@ -1390,9 +1396,13 @@ __global__ __launch_bounds__(256) void k_ha_first(const K *keys, uint64_t nrow, 
     uint32_t newly = 0, heads = 0, lost = 0;
     const uint64_t nvec = nrow / V, stride = (uint64_t)gridDim.x * 256;
     const int lane = threadIdx.x & 63;
+    // every wave runs both loops with a wave-uniform trip count (lanes past nvec are guarded,
+    // not retired): the neighbour shuffle below needs lane - 1 to hold vector v - 1 in the
+    // same call
     auto vec = [&](uint64_t v, const Vec &x) {
         // the row before this lane's first is the previous lane's last (lane 0: a load)
         K prev = __shfl_up(x.k[V - 1], 1, 64);
+        if (v >= nvec) return;
         const bool has_prev = base + v * V > 0;
         if (lane == 0 && has_prev) prev = keys[v * V - 1];
 #pragma unroll
@@ -1404,13 +1414,18 @@ __global__ __launch_bounds__(256) void k_ha_first(const K *keys, uint64_t nrow, 
             }
         }
     };
-    uint64_t v = blockIdx.x * 256ull + threadIdx.x;
-    for (; v + stride < nvec; v += 2 * stride) {
-        const Vec a = src[v], b = src[v + stride];
-        vec(v, a);
-        vec(v + stride, b);
+    const Vec none{};
+    uint64_t w = blockIdx.x * 256ull + (threadIdx.x & ~63u);  // the wave's first vector
+    for (; w + stride < nvec; w += 2 * stride) {
+        const uint64_t va = w + lane, vb = va + stride;
+        const Vec a = va < nvec ? src[va] : none, b = vb < nvec ? src[vb] : none;
+        vec(va, a);
+        vec(vb, b);
     }
-    for (; v < nvec; v += stride) vec(v, src[v]);
+    for (; w < nvec; w += stride) {
+        const uint64_t va = w + lane;
+        vec(va, va < nvec ? src[va] : none);
+    }
     // the last nrow % V rows
     for (uint64_t i = nvec * V + blockIdx.x * 256ull + threadIdx.x; i < nrow; i += stride) {
         const K k = keys[i];

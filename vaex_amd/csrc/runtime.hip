@@ -31,12 +31,16 @@ static std::map<int, int> g_cus;
 // The process's GPU (one process per GPU): vh_set_device records it, and every other thread
 // adopts it on its first library call -- HIP's current device is per thread, so a task run
 // from a worker thread (the executor allows that) would otherwise land on device 0.
+// A thread re-adopts after every vh_set_device (generation counter), so a thread that called
+// the library before the device was chosen (a pool created before comm init) follows it too.
 static int g_default_device = -1;
-static thread_local bool t_device_adopted = false;
+static int g_device_gen = 0;
+static thread_local int t_device_gen = 0;
 
 int current_device() {
-    if (!t_device_adopted) {
-        t_device_adopted = true;
+    const int gen = __atomic_load_n(&g_device_gen, __ATOMIC_ACQUIRE);
+    if (t_device_gen != gen) {
+        t_device_gen = gen;
         const int want = __atomic_load_n(&g_default_device, __ATOMIC_ACQUIRE);
         if (want >= 0) VH_HIP(hipSetDevice(want));
     }
@@ -55,7 +59,8 @@ DeviceScope::~DeviceScope() {
 // ---- device block cache (common.hpp) ---------------------------------------------------
 namespace {
 // Freed device blocks are kept for reuse (exact sizes, 1 MiB granularity): at most 1/8 of
-// the device's memory, blocks of up to 1/16 of it.  Large blocks matter: a 1e9-row query
+// the device's memory (VAEX_AMD_DEVICE_CACHE_MB overrides it per process, 0 disables the
+// cache), blocks of up to 1/16 of it.  Large blocks matter: a 1e9-row query
 // allocates multi-GB temporaries (h2o q10's 8 GB combined key column), and a fresh hipMalloc
 // of 8 GB stalled for 5.7 s every few queries on a device holding ~60 GB.  A failed
 // allocation drops the cache and retries.
@@ -63,9 +68,10 @@ struct BlockCache {
     std::multimap<uint64_t, void *> free;
     uint64_t cached = 0;
     uint64_t max_bytes = 0, max_block = 0;
+    bool limits_set = false;
 };
 void cache_limits(BlockCache &c) {
-    if (c.max_bytes) return;
+    if (c.limits_set) return;
     size_t fr = 0, total = 0;
     if (hipMemGetInfo(&fr, &total) != hipSuccess || total == 0) {
         (void)hipGetLastError();
@@ -73,6 +79,12 @@ void cache_limits(BlockCache &c) {
     }
     c.max_bytes = total / 8;
     c.max_block = total / 16;
+    if (const char *e = getenv("VAEX_AMD_DEVICE_CACHE_MB")) {
+        c.max_bytes = (uint64_t)strtoull(e, nullptr, 10) << 20;
+        c.max_block = std::min(c.max_block, c.max_bytes);
+    }
+    if (!c.max_bytes) c.max_block = 0;
+    c.limits_set = true;
 }
 std::mutex g_cache_mu;
 std::map<int, BlockCache> g_cache;
@@ -532,8 +544,8 @@ int vh_device_count(int *count) {
 int vh_set_device(int device) {
     VH_API_BEGIN
     VH_HIP(hipSetDevice(device));
-    t_device_adopted = true;
     __atomic_store_n(&g_default_device, device, __ATOMIC_RELEASE);
+    t_device_gen = __atomic_add_fetch(&g_device_gen, 1, __ATOMIC_ACQ_REL);
     VH_API_END
 }
 
@@ -613,11 +625,17 @@ int vh_device_cache_trim(void) {
     VH_API_BEGIN
     VH_HIP(hipStreamSynchronize(stream()));
     dense_rank_scratch_release();
+    // every device with cached blocks (a process may have run work on several)
     std::lock_guard<std::mutex> lk(g_cache_mu);
-    BlockCache &c = g_cache[current_device()];
-    for (auto &kv : c.free) (void)hipFree(kv.second);
-    c.free.clear();
-    c.cached = 0;
+    for (auto &dc : g_cache) {
+        BlockCache &c = dc.second;
+        if (c.free.empty()) continue;
+        DeviceScope ds(dc.first);
+        VH_HIP(hipStreamSynchronize(stream()));
+        for (auto &kv : c.free) (void)hipFree(kv.second);
+        c.free.clear();
+        c.cached = 0;
+    }
     VH_API_END
 }
 

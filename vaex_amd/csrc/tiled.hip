@@ -432,23 +432,8 @@ __device__ inline void lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
-// rank of a row in its tile's LDS histogram.  Every lane of the wave calls it (no exec
-// divergence).  When all taking lanes share one tile (sorted or clustered rows) one atomic
-// reserves the wave's ranks and each lane takes its position among them -- 64 same-address
-// LDS atomics would serialise; otherwise one atomic per lane.
-__device__ __forceinline__ int32_t tile_rank(uint32_t *hist, uint32_t t, bool take) {
-    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-    const uint64_t act = __ballot(take);
-    if (__ballot(take && t != t0) == 0) {
-        if (!act) return -1;
-        const int lane = threadIdx.x & 63, lead = __builtin_ctzll(act);
-        uint32_t base = 0;
-        if (lane == lead) base = atomicAdd(&hist[t0], (uint32_t)__builtin_popcountll(act));
-        base = (uint32_t)__shfl((int)base, lead, 64);
-        return take ? (int32_t)(base + (uint32_t)__builtin_popcountll(act & ((1ull << lane) - 1))) : -1;
-    }
-    return take ? (int32_t)atomicAdd(&hist[t], 1u) : -1;
-}
+// rank of a row in its tile's LDS histogram (common.hpp wave_rank)
+__device__ __forceinline__ int32_t tile_rank(uint32_t *hist, uint32_t t, bool take) { return wave_rank(hist, t, take); }
 
 // exclusive scan of in[0..T) into out[0..T), returns the total (all threads)
 __device__ inline uint32_t block_exclusive_scan(const uint32_t *in, uint32_t *out, uint32_t T, uint32_t *wave_sums) {

@@ -596,8 +596,13 @@ class DataFrame:
         if agg is None:  # df.groupby(by).agg(...): the same routes as groupby(by, agg=...)
             return GroupByDeferred(self, by, sort=sort, assume_sparse=assume_sparse, row_limit=row_limit)
         dense_ranges = {}
-        if agg is not None and assume_sparse != True and isinstance(by, (list, tuple)) and len(by) > 1:  # noqa: E712
-            res = groupby_multikey(self, by, agg, sort=sort, row_limit=row_limit)
+        multikey = isinstance(by, (list, tuple)) and len(by) > 1
+        if multikey:
+            # assume_sparse is the reference's combine flag (dataframe.py:6679 ->
+            # GroupBy(combine=assume_sparse), groupby.py:313-333): True combines the keys into
+            # one grouper, 'auto' when rows / cells < 10, False bins the cartesian grid
+            combine = True if assume_sparse is True else (False if assume_sparse is False else "auto")
+            res = groupby_multikey(self, by, agg, sort=sort, row_limit=row_limit, combine=combine)
             if res is not None:
                 return res
         if agg is not None and assume_sparse != True:  # noqa: E712
@@ -615,7 +620,7 @@ class DataFrame:
                                       row_limit=row_limit)
                     if res is not None:
                         return res
-        if agg is not None and assume_sparse == True:  # noqa: E712
+        if agg is not None and assume_sparse == True and not multikey:  # noqa: E712
             # the ordered_set grouper's result (groups in first-appearance order, or sorted)
             # for count / sum / mean of an integer key: one hash-partitioned pass, then the
             # groups ordered by the row their key first appears at (hashagg.order_first)
@@ -624,7 +629,8 @@ class DataFrame:
                               first_order=not sort)
             if res is not None:
                 return res
-        groupby = GroupBy(self, by=by, sort=sort, row_limit=row_limit, dense=assume_sparse != True,  # noqa: E712
+        groupby = GroupBy(self, by=by, sort=sort, row_limit=row_limit,
+                          dense=assume_sparse != True or multikey,  # noqa: E712
                           dense_ranges=dense_ranges)
         try:
             return groupby.agg(agg)

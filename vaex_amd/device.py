@@ -98,11 +98,6 @@ class DeviceArray:
         a = self.to_numpy()
         return a if dtype is None else a.astype(dtype)
 
-    @property
-    def __cuda_array_interface__(self):
-        # lets torch.as_tensor(...) alias the HBM buffer (used by the RCCL grid reduce)
-        return {"shape": (self.length,), "typestr": self.dtype.str, "data": (self.ptr, False), "version": 2}
-
     def __del__(self):
         if getattr(self, "_owns", False) and self.ptr:
             try:

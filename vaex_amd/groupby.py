@@ -246,45 +246,123 @@ def _key_ranges(df, by):
     return out
 
 
-def groupby_multikey(df, by, agg, sort=False, row_limit=None):
-    """Multi-key ``groupby(by=[k1, k2, ...], agg=...)`` over integer keys (groupby.py:248-333).
+def groupby_multikey(df, by, agg, sort=False, row_limit=None, combine="auto"):
+    """Multi-key ``groupby(by=[k1, k2, ...], agg=...)`` (groupby.py:248-333).
 
-    With enough rows per cell (rows / prod(spans) >= 10, the reference's ``combine='auto'``
-    test) every key becomes a dense grouper and the cartesian grid is binned directly.
-    Otherwise the keys are combined on the GPU into one int64 key, the cartesian ordinal
-    ``sum_j (k_j - min_j) * prod(span_{j+1..})`` (``vh_combine_keys``, first key most
-    significant), which takes the single-key routes (dense grid, fused hash pass, or the
-    set grouper for other aggregators); the labels are decoded back per key.  The
-    reference combines the per-key set ordinals instead of value offsets; both give the
-    lexicographic order of ``sort=True``.  Returns None when the keys do not qualify
-    (non-integer, masked, filtered frame, spans whose product reaches 2**62)."""
-    import ctypes
-    from . import _lib
-    from .device import DeviceArray
+    ``combine`` is the reference's ``assume_sparse`` (dataframe.py:6679 passes it as
+    ``GroupBy(combine=...)``, groupby.py:313-333): ``True`` always combines the keys into
+    one grouper, ``'auto'`` combines when rows / cells < 10, ``False`` never does (the
+    caller bins the cartesian grid; this returns None).
+
+    Integer keys: with enough rows per cell (``'auto'``) every key becomes a dense grouper
+    and the cartesian grid is binned directly.  Otherwise the keys are combined on the GPU
+    into one int64 key, the cartesian ordinal ``sum_j (k_j - min_j) * prod(span_{j+1..})``
+    (``vh_combine_keys``, first key most significant), which takes the single-key routes
+    (dense grid, fused hash pass, or the set grouper for other aggregators); the labels are
+    decoded back per key.  The reference combines the per-key set ordinals instead of value
+    offsets; both give the lexicographic order of ``sort=True``.  Keys that are not plain
+    integer columns (floats, masked, filtered frames) are combined through their GPU set
+    ordinals exactly as the reference does (:func:`_groupby_combine_sets`).
+
+    Group order without ``sort``: ``'auto'`` returns the lexicographic order; ``True``
+    returns the combined grouper's set order, i.e. the order in which each key combination
+    first appears (GrouperCombined over an ordered_set, what the reference produces with
+    one thread), as the single-key ``assume_sparse=True`` route does.
+
+    Returns None when the query is not taken here (``combine=False``, or ``'auto'`` with
+    keys that do not qualify): the caller takes the grouper-built cartesian GroupBy."""
+    if combine is False:
+        return None
     ranges = _key_ranges(df, by)
     if ranges is None:
-        return None
+        return _groupby_combine_sets(df, by, agg, sort=sort, row_limit=row_limit, combine=combine)
     spans = [vmax - vmin + 1 for _, vmin, vmax in ranges]
     cells = 1
     for sp in spans:
         cells *= sp
-    if cells >= 2 ** 62:
-        return _groupby_recombine(df, ranges, agg, sort=sort, row_limit=row_limit)
-    n = df.length_unfiltered()
     names = [name for name, _, _ in ranges]
-    if n / cells >= COMBINE_OCCUPANCY and all(sp <= DENSE_KEY_MAX for sp in spans):
+    first_order = combine is True and not sort
+    if cells >= 2 ** 62:
+        return _groupby_recombine(df, ranges, agg, sort=sort, row_limit=row_limit, combine=combine)
+    n = df.length_unfiltered()
+    if combine == "auto" and n / cells >= COMBINE_OCCUPANCY and all(sp <= DENSE_KEY_MAX for sp in spans):
         dense_ranges = {name: (vmin, vmax) for name, vmin, vmax in ranges}
         return GroupBy(df, by=names, sort=sort, row_limit=row_limit, dense_ranges=dense_ranges).agg(agg)
+    return _groupby_combined(df, ranges, agg, names, sort=sort, row_limit=row_limit, first_order=first_order)
+
+
+def _groupby_combined(df, ranges, agg, key_names, sort=False, row_limit=None, first_order=False):
+    """Combine the integer key columns of ``ranges`` [(name, min, max)] into one int64 key
+    and group by it: the single-key routes, in first-appearance order with ``first_order``
+    (the ``assume_sparse=True`` single-key route), else sorted by combined key =
+    lexicographic.  Returns {key name: labels (decoded per key), aggregate columns...}."""
     combined, mults = _combine_columns(df, ranges)
     # the aggregators are named against the original frame (callables expand over its
     # non-key columns), then evaluated on a copy that also holds the combined key
-    actions = [(name, a) for name, a in parse_actions(df, agg, names)]
+    actions = [(name, a) for name, a in parse_actions(df, agg, key_names)]
     tmp = df.copy()
     tmp.add_column(COMBINED_KEY, combined)
-    res = tmp.groupby(COMBINED_KEY, agg=actions, sort=sort, row_limit=row_limit)
+    res = tmp.groupby(COMBINED_KEY, agg=actions, sort=sort, row_limit=row_limit,
+                      assume_sparse=True if first_order else "auto")
     columns = _decode_labels(df, res.columns[COMBINED_KEY], None, ranges, mults)
     for name, values in res.columns.items():
         if name != COMBINED_KEY:
+            columns[name] = values
+    return DataFrame(columns)
+
+
+ORDINAL_KEY = "__vaex_amd_ordinal_{}"
+
+
+def _groupby_combine_sets(df, by, agg, sort=False, row_limit=None, combine=True):
+    """``_combine`` over per-key set groupers (groupby.py:248-288, GroupByBase combine=True
+    :313-315): each key gets its GPU ordered_set (Grouper, ``sort`` orders it), every row's
+    ordinal into it (``map_ordinal`` on the device for HBM columns; masked rows take the
+    set's null ordinal, NaN its NaN ordinal), and the ordinal columns are combined like
+    integer keys of range [0, N - 1].  Labels are the sets' keys at the decoded ordinals.
+    For keys the integer route does not take (floating point, masked, filtered frames).
+    ``combine='auto'`` decides from the set sizes, as the reference does (rows / cells < 10
+    combines; otherwise the cartesian grid of these groupers).  Returns None for categorical
+    or binner keys (the caller's cartesian GroupBy)."""
+    from .device import DeviceArray
+    if any(isinstance(b, BinnerBase) or not isinstance(b, (str, Expression)) or df.is_category(b) for b in by):
+        return None
+    names = [str(b) for b in by]
+    n = df.length_unfiltered()
+    work = df.copy()
+    groupers, ranges = [], []
+    for name in names:
+        groupers.append(Grouper(work[name], df=work, sort=sort, row_limit=row_limit, df_original=df))
+    cells = 1
+    for g in groupers:
+        cells *= g.N
+    if any(g.N == 0 for g in groupers) or (combine == "auto" and n / max(cells, 1) >= COMBINE_OCCUPANCY):
+        return GroupBy(work, by=groupers, sort=sort, row_limit=row_limit).agg(agg)
+    for i, (name, g) in enumerate(zip(names, groupers)):
+        col = df._eval_host(name, 0, n)
+        mask = np.ma.getmaskarray(col) if np.ma.isMaskedArray(col) else None
+        if np.ma.isMaskedArray(col):
+            col = col.data
+        ords = g.set.map_ordinal(col if isinstance(col, DeviceArray) else np.ascontiguousarray(col))
+        if mask is not None and mask.any():
+            ords = np.array(ords, copy=True)
+            ords[mask] = g.null_value
+        key = ORDINAL_KEY.format(i)
+        work.add_column(key, ords)
+        ranges.append((key, 0, g.N - 1))
+    actions = [(name, a) for name, a in parse_actions(df, agg, names)]
+    if cells >= 2 ** 62:
+        res = _groupby_recombine(work, ranges, actions, sort=sort, row_limit=row_limit, combine=True,
+                                 key_names=names)
+    else:
+        res = _groupby_combined(work, ranges, actions, names, sort=sort, row_limit=row_limit, first_order=not sort)
+    columns = {}
+    for name, g, (key, _, _) in zip(names, groupers, ranges):
+        ords = res.columns[key]
+        ords = ords.to_numpy() if isinstance(ords, DeviceArray) else np.asarray(ords)
+        columns[name] = np.asarray(g.bin_values)[ords.astype(np.int64)]
+    for name, values in res.columns.items():
+        if not name.startswith("__vaex_amd_ordinal_"):
             columns[name] = values
     return DataFrame(columns)
 
@@ -349,7 +427,7 @@ def _decode_labels(df, ck, table, ranges, mults):
 RECOMBINED_KEY = "__vaex_amd_recombined_key_{}"
 
 
-def _groupby_recombine(df, ranges, agg, sort=False, row_limit=None):
+def _groupby_recombine(df, ranges, agg, sort=False, row_limit=None, combine="auto", key_names=None):
     """Multi-key groupby whose cartesian span reaches 2**62: the reference's ``_combine``
     recursion (groupby.py:248-288).  The leading keys whose span product stays below 2**62
     are combined on the GPU into one int64 value, that value is replaced by its dense rank
@@ -369,7 +447,7 @@ def _groupby_recombine(df, ranges, agg, sort=False, row_limit=None):
     if take < 2:
         return None  # two keys alone overflow 62 bits: not combinable here
     head, rest = ranges[:take], ranges[take:]
-    names = [name for name, _, _ in ranges]
+    names = key_names or [name for name, _, _ in ranges]
     actions = [(name, a) for name, a in parse_actions(df, agg, names)]
     combined, mults = _combine_columns(df, head)
     n = len(combined)
@@ -385,7 +463,7 @@ def _groupby_recombine(df, ranges, agg, sort=False, row_limit=None):
     tmp = df.copy()
     tmp.add_column(key, ordinal)
     by = [key] + [name for name, _, _ in rest]
-    res = tmp.groupby(by, agg=actions, sort=sort, row_limit=row_limit)
+    res = tmp.groupby(by, agg=actions, sort=sort, row_limit=row_limit, assume_sparse=combine)
     columns = _decode_labels(df, res.columns[key], distinct_dev, head, mults)
     del distinct_dev
     for name, values in res.columns.items():
