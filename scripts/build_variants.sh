@@ -7,7 +7,7 @@ SRC=${SRC:-tiled}
 cd "$(dirname "$0")/../vaex_amd/csrc"
 make -s
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -munsafe-fp-atomics"
-OBJS="runtime binning tiled hashset hashagg expr nunique comm"
+OBJS="runtime binning tiled first hashset hashagg expr nunique comm"
 for v in "$@"; do
   name=${v%%:*}; fl=${v#*:}
   mkdir -p build/var_$name

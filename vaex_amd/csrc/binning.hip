@@ -472,22 +472,7 @@ __global__ __launch_bounds__(256) void k_small_fused(SmallAggs sa, const uint16_
 // AggFirst (superagg.cpp:481-505).  Per chunk: (A) min order key per cell,
 // (B) lowest row holding that key, (C) per cell: take it if strictly smaller
 // than the grid's order -- ties go to the earliest row, as a serial pass does.
-template <typename T> __device__ inline uint64_t order_key(T v) {
-    if constexpr (is_float_t<T>::value) {
-        double d = (double)v;
-        if (d == 0.0) d = 0.0;
-        uint64_t u;
-        __builtin_memcpy(&u, &d, 8);
-        return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
-    } else if constexpr (is_signed_int_t<T>::value) {
-        return (uint64_t)(int64_t)v ^ 0x8000000000000000ULL;
-    } else if constexpr (std::is_same<T, vbool>::value) {
-        return v.v;
-    } else {
-        return (uint64_t)v;
-    }
-}
-
+// (order_key: common.hpp; the tile path, tiled.hip, fills the same (A)/(B) scratch.)
 template <typename T>
 __global__ __launch_bounds__(256) void k_first_a(AggDev a, const uint64_t *idx, uint64_t n) {
     for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n;
@@ -1651,6 +1636,15 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
             // small grids: LDS sub-grid per workgroup for every kind but AggFirst / AggNUnique
             const bool small = L * 8 <= LDS_AGG_MAX_BYTES;
             auto lds_ok = [&](int kind) { return small && kind != VH_AGG_FIRST && kind != VH_AGG_NUNIQUE; };
+            // AggFirst over a large grid: the tile-partitioned engine (first.hip) fills its
+            // s_key / s_row scratch without per-row global atomics; k_first_c merges as below
+            for (int k = 0; k < naggs; k++) {
+                if (tdone[k] || ads[k].kind != VH_AGG_FIRST || small) continue;
+                if (!try_tiled_first(plan, ads[k], len, L, row0, scalar_f64_dims(g))) continue;
+                VH_DISPATCH_DTYPE(ads[k].dtype, T, hipLaunchKernelGGL(k_first_c<T>, dim3(blocks_for(L, 256)), dim3(256), 0, stream(), ads[k], L, row0));
+                VH_HIP(hipGetLastError());
+                tdone[k] = 1;
+            }
             // binners the cell kernels handle (scalar / ordinal); set-ordinal binners keep
             // the per-row plan_index of k_agg_lds
             bool cells_ok = small && L <= 65536;

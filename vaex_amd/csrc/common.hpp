@@ -201,6 +201,25 @@ template <typename T> __device__ inline bool is_nan_v(T v) {
     else return false;
 }
 
+// AggFirst's order value as an order-preserving u64 (floats: -0.0 == 0.0, as `<` compares
+// them; signed: offset binary) -- min over it = the reference's strict `<` minimum
+template <typename T> __device__ inline uint64_t order_key(T v) {
+    if constexpr (is_float_t<T>::value) {
+        double d = (double)v;
+        if (d == 0.0) d = 0.0;
+        uint64_t u;
+        __builtin_memcpy(&u, &d, 8);
+        return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
+    } else if constexpr (is_signed_int_t<T>::value) {
+        return (uint64_t)(int64_t)v ^ 0x8000000000000000ULL;
+    } else if constexpr (std::is_same<T, vbool>::value) {
+        return v.v;
+    } else {
+        return (uint64_t)v;
+    }
+}
+
+
 // ---- runtime ---------------------------------------------------------------
 hipStream_t stream();
 hipStream_t copy_stream();  // H2D staging copies (overlap the compute stream)

@@ -183,6 +183,11 @@ bool try_tiled(const BinPlan &plan, const FusedAggs &fa, uint64_t n, uint64_t ce
 uint64_t stat_tile_overflow(bool reset);
 uint64_t stat_hashagg_overflow(bool reset);
 uint64_t stat_set_overflow(bool reset);
+// AggFirst over a grid too large for LDS through the tile-partitioned exchange (first.hip):
+// fills the aggregator's s_key / s_row scratch for rows [0, n) of this chunk (global rows
+// row0 + j); false when not eligible or when its resolve list overflowed (scratch reset)
+bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t cells, uint64_t row0, int nd_f64);
+uint64_t stat_first_tiled(bool reset);  // chunks binned by try_tiled_first
 // a set-ordinal grid (one set-ordinal binner over an integer key) with count / float64 sum
 // aggregators through the fused hash aggregation (hashagg.hip); false when not eligible
 bool hashagg_bin_set_ordinal(const BinPlan &plan, const FusedAggs &fa, uint64_t n);

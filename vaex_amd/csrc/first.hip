@@ -1,0 +1,566 @@
+// AggFirst on the tile-partitioned path (superagg.cpp:436-511): first(v, order=o,
+// binby=...) over a grid too large for one workgroup's LDS, with no per-row global atomics.
+//
+// AggFirst keeps, per cell, the value at the row whose order value is smallest (strict `<`:
+// among equal order values the row a serial pass meets first, i.e. the lowest row), over
+// rows whose value and order are both non-NaN (masks are ignored, as the reference's
+// "TODO: masked support").  The generic path (binning.hip k_first_a/b/c) finds, per chunk,
+// the minimum order key of every cell (s_key) and the lowest row holding it (s_row) with two
+// passes of scattered 64-bit global atomics, then k_first_c merges them into the grid.  This
+// engine fills the same s_key / s_row scratch through the partition exchange instead:
+//
+//   sample  -- per-tile row fractions from ~1M evenly spaced rows (4096 cells per tile)
+//   pass A  -- batches of 4096 rows dealt round-robin to the workgroups; a row's cell, its
+//              order key (order_key: order-preserving u64) and its row are ranked per tile in
+//              LDS, counting-sorted, and streamed as runs into per-(XCD, tile) streams: each
+//              run is reserved with one atomic per (tile, batch) by the tile's rank-0 row, so
+//              the runs of all workgroups of one XCD abut and their partial lines meet in that
+//              XCD's L2 (scripts/bw_probe4.hip: 3.77 ms against 4.70 for private per-workgroup
+//              regions at 256 tiles).  2 + 8 + 4 bytes per row.
+//   pass B  -- unit = (tile, XCD stream, slice) + a slice of the tile's spill area: per
+//              8192-entry step, phase 1 lowers the LDS order key of each cell (a row that
+//              lowers it resets the cell's row), phase 2 lowers the cell's row among entries
+//              equal to the key; the unit's (key, row) per touched cell is merged with a global
+//              atomicMin of s_key, and appended to a resolve list when it may win.
+//   resolve -- list entries whose key equals the final s_key lower s_row (global rows).
+// Rows past a stream and its spill area (sampling miss) go to s_key + the list directly; a
+// full list sets a flag and the chunk is redone by the generic path (s_key / s_row reset).
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "binner_dev.hpp"
+#include "common.hpp"
+#include "engine.hpp"
+
+namespace vh {
+
+constexpr int TF_THREADS = 512;
+constexpr int TF_RPT = 8;
+constexpr int TF_BATCH = TF_THREADS * TF_RPT;  // 4096 rows per batch
+constexpr int TFB_THREADS = 1024;
+constexpr uint32_t TF_S_LOG2 = 12;  // 4096 cells per tile: pass B LDS 8-B key + 4-B row = 48 KB
+constexpr uint32_t TF_MAX_TILES = 2048;
+constexpr int TF_SAMPLE_BLOCKS = 512;
+
+struct FirstParams {
+    uint32_t T, NX, s_log2, pad;
+    uint64_t n, cells;
+    const uint32_t *cap;          // [T] stream capacity of (xcd, t), the same for every xcd; multiple of 8
+    const uint32_t *toff;         // [T] stream offset inside an xcd block; multiple of 8
+    uint64_t xstride;             // entries of one xcd block
+    uint32_t *sfill;              // [NX * T] entries reserved (may exceed cap)
+    uint32_t *spill_fill;         // [T]
+    const uint32_t *spill_cap;    // [T]
+    const uint64_t *spill_start;  // [T] relative to spill_base
+    uint64_t spill_base;
+    uint16_t *ecell;
+    unsigned long long *eokey;
+    uint32_t *erow;
+    unsigned long long *s_key, *s_row;  // the aggregator's per-cell scratch (AggDev)
+    uint4 *list;                        // (cell, row, key lo, key hi)
+    unsigned long long *list_fill;
+    uint64_t list_cap;
+    unsigned *flag;  // list overflow: the host redoes the chunk on the generic path
+};
+
+template <int ND> __device__ __forceinline__ uint64_t tf_cell(const BinPlan &p, uint64_t i) {
+    if constexpr (ND == 0) {
+        return plan_index(p, i);
+    } else {
+        uint64_t c = 0;
+#pragma unroll
+        for (int d = 0; d < ND; d++) c += scalar_index<double>(p.b[d], i) * p.b[d].stride;
+        return c;
+    }
+}
+
+__device__ inline void tf_lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+__device__ inline void tf_list_push(const FirstParams &fp, uint64_t slot, uint32_t cell, uint32_t row, uint64_t key) {
+    if (slot < fp.list_cap) fp.list[slot] = make_uint4(cell, row, (uint32_t)key, (uint32_t)(key >> 32));
+    else atomicOr(fp.flag, 1u);
+}
+
+// per-tile histogram of TF_SAMPLE_BLOCKS evenly spaced batch-sized row blocks (count and
+// square: the block-to-block spread tells clustered rows)
+template <int ND>
+__global__ __launch_bounds__(TF_THREADS) void k_first_sample(BinPlan p, uint64_t n, uint32_t s_log2, uint32_t T,
+                                                             uint64_t block_stride, unsigned long long *hist) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    uint32_t *h = reinterpret_cast<uint32_t *>(lds_raw);
+    for (uint32_t t = threadIdx.x; t < T; t += TF_THREADS) h[t] = 0;
+    __syncthreads();
+    const uint64_t r0 = blockIdx.x * block_stride;
+    for (uint64_t r = threadIdx.x; r < TF_BATCH && r0 + r < n; r += TF_THREADS)
+        atomicAdd(&h[(uint32_t)(tf_cell<ND>(p, r0 + r) >> s_log2)], 1u);
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < T; t += TF_THREADS)
+        if (h[t]) {
+            atomicAdd(&hist[t], (unsigned long long)h[t]);
+            atomicAdd(&hist[T + t], (unsigned long long)h[t] * h[t]);
+        }
+}
+
+// pass A (see the file comment).  LDS: staged keys u32 | order keys u64 | rows u32 (one batch)
+// | per tile: hist, hcnt, boff, sbase, soff, cap, toff
+template <int ND, typename T>
+__global__ __launch_bounds__(TF_THREADS) void k_first_scatter(BinPlan p, AggDev a, FirstParams fp) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    __shared__ uint32_t s_tot;
+    const uint32_t NT = fp.T;
+    unsigned long long *sokey = reinterpret_cast<unsigned long long *>(lds_raw);
+    uint32_t *skey = reinterpret_cast<uint32_t *>(sokey + TF_BATCH);
+    uint32_t *srow = skey + TF_BATCH;
+    uint32_t *hist = srow + TF_BATCH;
+    uint32_t *hcnt = hist + NT, *boff = hcnt + NT, *sbase = boff + NT, *soff = sbase + NT, *cap = soff + NT, *toff = cap + NT;
+    for (uint32_t t = threadIdx.x; t < NT; t += TF_THREADS) {
+        hist[t] = 0;
+        cap[t] = fp.cap[t];
+        toff[t] = fp.toff[t];
+    }
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const uint32_t x = xcc % fp.NX;
+    const uint64_t xblock = (uint64_t)x * fp.xstride;
+    uint32_t *sfill = fp.sfill + (uint64_t)x * NT;
+    const uint32_t smask = (1u << fp.s_log2) - 1;
+    const int lane = threadIdx.x & 63;
+    __syncthreads();
+    const uint64_t n = fp.n;
+    // batches w, w + W, w + 2W, ...: every workgroup's rows spread over the whole range; the
+    // trip count is uniform within the workgroup (every thread meets every barrier)
+    for (uint64_t b0 = (uint64_t)blockIdx.x * TF_BATCH; b0 < n; b0 += (uint64_t)gridDim.x * TF_BATCH) {
+        uint32_t key[TF_RPT];
+        int32_t rank[TF_RPT];
+        unsigned long long ok[TF_RPT];
+#pragma unroll
+        for (int r = 0; r < TF_RPT; r++) {
+            const uint64_t i = b0 + (uint64_t)r * TF_THREADS + threadIdx.x;
+            const bool in = i < n;
+            uint64_t c = 0;
+            bool keep = false;
+            ok[r] = 0;
+            if (in) {
+                c = tf_cell<ND>(p, i);
+                const T v = load_v<T>(a.data, i, a.flip), o = load_v<T>(a.data2, i, a.flip);
+                keep = !is_nan_v(v) && !is_nan_v(o);
+                ok[r] = order_key(o);
+            }
+            const uint32_t t = (uint32_t)(c >> fp.s_log2);
+            key[r] = (t << 16) | ((uint32_t)c & smask);
+            rank[r] = wave_rank(hist, t, keep);
+        }
+        // B1: every rank taken -> wave 0 scans the histogram (and clears it for the next batch)
+        tf_lds_barrier();
+        if (threadIdx.x < 64) {
+            const uint32_t per = (NT + 63) / 64, t0 = lane * per;
+            uint32_t s = 0;
+            for (uint32_t t = t0; t < t0 + per && t < NT; t++) s += hist[t];
+            uint32_t inc = s;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(inc, off, 64);
+                if (lane >= off) inc += y;
+            }
+            uint32_t acc = inc - s;
+            for (uint32_t t = t0; t < t0 + per && t < NT; t++) {
+                const uint32_t h = hist[t];
+                boff[t] = acc;
+                hcnt[t] = h;
+                hist[t] = 0;
+                acc += h;
+            }
+            if (lane == 63) s_tot = inc;
+        }
+        // B2: rows stage at their sorted positions; a tile's rank-0 row reserves the tile's run
+        // in this XCD's stream (and past its capacity, in the tile's spill area)
+        tf_lds_barrier();
+#pragma unroll
+        for (int r = 0; r < TF_RPT; r++) {
+            if (rank[r] < 0) continue;
+            const uint32_t t = key[r] >> 16;
+            const uint32_t pos = boff[t] + (uint32_t)rank[r];
+            skey[pos] = key[r];
+            sokey[pos] = ok[r];
+            srow[pos] = (uint32_t)(b0 + (uint64_t)r * TF_THREADS + threadIdx.x);
+            if (rank[r] == 0) {
+                const uint32_t h = hcnt[t], c = cap[t];
+                const uint32_t old = atomicAdd(&sfill[t], h);
+                sbase[t] = old;
+                if (old + h > c) {
+                    const uint32_t first = max(old, c);
+                    soff[t] = atomicAdd(&fp.spill_fill[t], old + h - first) - first;
+                }
+            }
+        }
+        // B3: the sorted runs stream out
+        tf_lds_barrier();
+        const uint32_t tot = s_tot;
+        for (uint32_t k = threadIdx.x; k < tot; k += TF_THREADS) {
+            const uint32_t kk = skey[k];
+            const uint32_t t = kk >> 16;
+            const uint32_t d = sbase[t] + (k - boff[t]);
+            uint64_t e;
+            if (d < cap[t]) {
+                e = xblock + toff[t] + d;
+            } else {
+                const uint32_t si = d + soff[t];
+                if (si >= fp.spill_cap[t]) {
+                    // past the stream and the spill area: straight to s_key and the list
+                    const uint32_t c = (t << fp.s_log2) | (kk & 0xffffu);
+                    atomicMin(&fp.s_key[c], sokey[k]);
+                    tf_list_push(fp, atomicAdd(fp.list_fill, 1ull), c, srow[k], sokey[k]);
+                    continue;
+                }
+                e = fp.spill_base + fp.spill_start[t] + si;
+            }
+            fp.ecell[e] = (uint16_t)kk;
+            fp.eokey[e] = sokey[k];
+            fp.erow[e] = srow[k];
+        }
+    }
+}
+
+struct FirstUnit {
+    uint32_t tile, xcd, part, parts;
+};
+
+// pass B (see the file comment)
+__global__ __launch_bounds__(TFB_THREADS) void k_first_reduce(FirstParams fp, const FirstUnit *units) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    __shared__ uint32_t s_w[TFB_THREADS / 64];
+    __shared__ unsigned long long s_base;
+    const uint32_t S = 1u << fp.s_log2;
+    unsigned long long *lkey = reinterpret_cast<unsigned long long *>(lds_raw);
+    uint32_t *lrow = reinterpret_cast<uint32_t *>(lkey + S);
+    const FirstUnit u = units[blockIdx.x];
+    const uint32_t t = u.tile;
+    for (uint32_t i = threadIdx.x; i < S; i += TFB_THREADS) {
+        lkey[i] = ~0ull;
+        lrow[i] = ~0u;
+    }
+    // this unit: slice `part` of `parts` of stream (xcd, t), and slice xcd * parts + part of
+    // NX * parts of the tile's spill area (slice bounds at multiples of 8 entries)
+    const uint32_t F = min(fp.sfill[(uint64_t)u.xcd * fp.T + t], fp.cap[t]);
+    const uint32_t a0 = u.part == 0 ? 0u : (uint32_t)((uint64_t)F * u.part / u.parts) & ~7u;
+    const uint32_t a1 = u.part + 1 == u.parts ? F : (uint32_t)((uint64_t)F * (u.part + 1) / u.parts) & ~7u;
+    const uint32_t SF = min(fp.spill_fill[t], fp.spill_cap[t]);
+    const uint32_t P = fp.NX * u.parts, idx = u.xcd * u.parts + u.part;
+    const uint32_t q0 = idx == 0 ? 0u : (uint32_t)((uint64_t)SF * idx / P) & ~7u;
+    const uint32_t q1 = idx + 1 == P ? SF : (uint32_t)((uint64_t)SF * (idx + 1) / P) & ~7u;
+    const uint64_t eA = (uint64_t)u.xcd * fp.xstride + fp.toff[t] + a0, eB = fp.spill_base + fp.spill_start[t] + q0;
+    const uint32_t nA = a1 > a0 ? a1 - a0 : 0u, nB = q1 > q0 ? q1 - q0 : 0u;
+    const uint32_t CA = (nA + 7) / 8, C = CA + (nB + 7) / 8;
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < C; c0 += TFB_THREADS) {  // uniform trip count: barriers inside
+        const uint32_t c = c0 + threadIdx.x;
+        uint32_t rem = 0;
+        uint64_t e = 0;
+        if (c < CA) {
+            e = eA + 8ull * c;
+            rem = min(8u, nA - 8 * c);
+        } else if (c < C) {
+            e = eB + 8ull * (c - CA);
+            rem = min(8u, nB - 8 * (c - CA));
+        }
+        uint4 cw = make_uint4(0, 0, 0, 0), r0 = cw, r1 = cw;
+        ulonglong2 k[4] = {};
+        if (rem) {
+            cw = *reinterpret_cast<const uint4 *>(fp.ecell + e);
+#pragma unroll
+            for (int h = 0; h < 4; h++) k[h] = *reinterpret_cast<const ulonglong2 *>(fp.eokey + e + 2 * h);
+            r0 = *reinterpret_cast<const uint4 *>(fp.erow + e);
+            r1 = *reinterpret_cast<const uint4 *>(fp.erow + e + 4);
+        }
+        const uint32_t cws[4] = {cw.x, cw.y, cw.z, cw.w};
+        const uint32_t rows[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+        // phase 1: lower the cell's order key; the row that lowers it clears the cell's row
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if ((uint32_t)j >= rem) continue;
+            const uint32_t cl = (cws[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+            const unsigned long long kj = (j & 1) ? k[j >> 1].y : k[j >> 1].x;
+            const unsigned long long old = atomicMin(&lkey[cl], kj);
+            if (kj < old) lrow[cl] = ~0u;
+        }
+        __syncthreads();
+        // phase 2: the lowest row among the entries holding the cell's key
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if ((uint32_t)j >= rem) continue;
+            const uint32_t cl = (cws[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+            const unsigned long long kj = (j & 1) ? k[j >> 1].y : k[j >> 1].x;
+            if (kj == lkey[cl]) atomicMin(&lrow[cl], rows[j]);
+        }
+        __syncthreads();
+    }
+    // merge: global minimum key per cell, and the candidates for its row into the list (one
+    // list reservation per workgroup)
+    const uint64_t cbase = (uint64_t)t << fp.s_log2;
+    constexpr int PER = 8;  // S / TFB_THREADS cells per thread (S <= 8192)
+    uint32_t push = 0;
+    unsigned long long kept[PER];
+    uint32_t kc[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const uint32_t i = q * TFB_THREADS + threadIdx.x;
+        kept[q] = ~0ull;
+        kc[q] = 0;
+        if (i >= S || cbase + i >= fp.cells) continue;
+        const unsigned long long kk = lkey[i];
+        if (kk == ~0ull) continue;
+        const unsigned long long old = atomicMin(&fp.s_key[cbase + i], kk);
+        if (kk <= old) {
+            kept[q] = kk;
+            kc[q] = i;
+            push++;
+        }
+    }
+    const uint64_t base = block_reserve<TFB_THREADS>(push, s_w, &s_base, fp.list_fill);
+    uint64_t j = base;
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        if (kept[q] == ~0ull) continue;
+        tf_list_push(fp, j++, (uint32_t)(cbase + kc[q]), lrow[kc[q]], kept[q]);
+    }
+}
+
+// resolve: candidates holding the final key lower the cell's (global) row
+__global__ __launch_bounds__(256) void k_first_resolve(FirstParams fp, uint64_t row0) {
+    if (*fp.flag) return;
+    const uint64_t m = min(*fp.list_fill, fp.list_cap);
+    for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) {
+        const uint4 e = fp.list[j];
+        const unsigned long long kk = (unsigned long long)e.z | ((unsigned long long)e.w << 32);
+        if (kk == fp.s_key[e.x]) atomicMin(&fp.s_row[e.x], (unsigned long long)(row0 + e.y));
+    }
+}
+
+struct FirstScratch {
+    std::mutex mu;
+    DevBuf ecell, eokey, erow, meta, list;
+};
+
+static FirstScratch &first_scratch() {
+    static std::mutex g;
+    static std::map<int, std::unique_ptr<FirstScratch>> m;
+    std::lock_guard<std::mutex> lk(g);
+    auto &p = m[current_device()];
+    if (!p) p = std::make_unique<FirstScratch>();
+    return *p;
+}
+
+template <int ND> static void tf_launch_a(int dtype, unsigned grid, size_t lds, const BinPlan &plan, const AggDev &ad,
+                                          const FirstParams &fp) {
+    VH_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((k_first_scatter<ND, T>), dim3(grid), dim3(TF_THREADS), lds, stream(), plan, ad, fp));
+}
+
+template <int ND> static int tf_blocks_per_cu(int dtype, size_t lds) {
+    int nb = 1;
+    VH_DISPATCH_DTYPE(dtype, T, VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_first_scatter<ND, T>, TF_THREADS, lds)));
+    return nb;
+}
+
+static uint64_t g_first_tiled_chunks = 0;  // chunks the engine binned (vh_stat_read("first_tiled_chunks"))
+
+uint64_t stat_first_tiled(bool reset) {
+    return reset ? __atomic_exchange_n(&g_first_tiled_chunks, 0ull, __ATOMIC_RELAXED)
+                 : __atomic_load_n(&g_first_tiled_chunks, __ATOMIC_RELAXED);
+}
+
+bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t cells, uint64_t row0, int nd_f64) {
+    if (n < (1u << 20) || n >= (1ull << 32) || !ad.data || !ad.data2 || !ad.s_key || !ad.s_row) return false;
+    const uint32_t s_log2 = TF_S_LOG2;
+    const uint64_t S = 1ull << s_log2;
+    const uint64_t T64 = (cells + S - 1) / S;
+    if (T64 < 2 || T64 > TF_MAX_TILES) return false;
+    const uint32_t T = (uint32_t)T64;
+    const uint32_t NX = (uint32_t)std::max(1, std::min(8, cu_count() / 32));
+    const int nd = nd_f64 >= 1 && nd_f64 <= 3 ? nd_f64 : 0;
+    FirstScratch &ws = first_scratch();
+    std::lock_guard<std::mutex> lock(ws.mu);
+    hipStream_t st = stream();
+    const size_t lds_a = (size_t)16 * TF_BATCH + (size_t)7 * 4 * T + 64;
+    if (lds_a > 160 * 1024) return false;
+    int bpc = 1;
+    {
+        static std::mutex mu;
+        static std::map<std::tuple<int, int, int, size_t>, int> cache;
+        std::lock_guard<std::mutex> lk(mu);
+        const auto key = std::make_tuple(current_device(), nd, ad.dtype, lds_a);
+        auto it = cache.find(key);
+        if (it == cache.end()) {
+            int v = nd == 1 ? tf_blocks_per_cu<1>(ad.dtype, lds_a) : nd == 2 ? tf_blocks_per_cu<2>(ad.dtype, lds_a)
+                    : nd == 3 ? tf_blocks_per_cu<3>(ad.dtype, lds_a) : tf_blocks_per_cu<0>(ad.dtype, lds_a);
+            it = cache.emplace(key, std::max(1, std::min(v, 4))).first;
+        }
+        bpc = it->second;
+    }
+    const uint32_t W = (uint32_t)cu_count() * (uint32_t)bpc;
+    // meta: hist (2T u64) | cap | toff | spill_cap (T u32 each) | spill_start (T u64) | sfill
+    // (NX T u32) | spill_fill (T u32) | list_fill | flag | units
+    const uint64_t nb = (n + TF_BATCH - 1) / TF_BATCH;
+    const uint64_t sblocks = std::min<uint64_t>(nb, TF_SAMPLE_BLOCKS);
+    const uint64_t bstride = std::max<uint64_t>(TF_BATCH, n / sblocks);
+    const double target = std::max(1.0, (double)n / ((double)cu_count() * 4));
+    const uint64_t max_units = (uint64_t)NX * T * 64 + 64;
+    const uint64_t meta_bytes = 16 * (uint64_t)T + 4 * 3 * (uint64_t)T + 8 * (uint64_t)T + 4 * (uint64_t)NX * T +
+                                4 * (uint64_t)T + 64 + sizeof(FirstUnit) * max_units + 1024;
+    ws.meta.ensure(meta_bytes);
+    char *mb = ws.meta.as<char>();
+    auto carve = [&](uint64_t bytes) {
+        char *p = mb;
+        mb += (bytes + 255) & ~uint64_t(255);
+        return p;
+    };
+    auto *d_hist = reinterpret_cast<unsigned long long *>(carve(16 * (uint64_t)T));
+    auto *d_cap = reinterpret_cast<uint32_t *>(carve(4 * (uint64_t)T));
+    auto *d_toff = reinterpret_cast<uint32_t *>(carve(4 * (uint64_t)T));
+    auto *d_scap = reinterpret_cast<uint32_t *>(carve(4 * (uint64_t)T));
+    auto *d_sstart = reinterpret_cast<uint64_t *>(carve(8 * (uint64_t)T));
+    auto *d_sfill = reinterpret_cast<uint32_t *>(carve(4 * (uint64_t)NX * T));
+    auto *d_spfill = reinterpret_cast<uint32_t *>(carve(4 * (uint64_t)T));
+    auto *d_misc = reinterpret_cast<unsigned long long *>(carve(64));  // [0] list fill, [1] flag
+    auto *d_units = reinterpret_cast<FirstUnit *>(carve(sizeof(FirstUnit) * max_units));
+    (void)mb;
+    VH_HIP(hipMemsetAsync(d_hist, 0, 16 * (uint64_t)T, st));
+    {
+        TimedScope ts("first_sample");
+        const size_t lds = 4 * (size_t)T;
+        switch (nd) {
+        case 1: hipLaunchKernelGGL(k_first_sample<1>, dim3(sblocks), dim3(TF_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist); break;
+        case 2: hipLaunchKernelGGL(k_first_sample<2>, dim3(sblocks), dim3(TF_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist); break;
+        case 3: hipLaunchKernelGGL(k_first_sample<3>, dim3(sblocks), dim3(TF_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist); break;
+        default: hipLaunchKernelGGL(k_first_sample<0>, dim3(sblocks), dim3(TF_THREADS), lds, st, plan, n, s_log2, T, bstride, d_hist);
+        }
+        VH_HIP(hipGetLastError());
+    }
+    thread_local PinnedBuf stage;
+    const uint64_t up_bytes = 4 * 3 * (uint64_t)T + 8 * (uint64_t)T + sizeof(FirstUnit) * max_units + 256;
+    stage.ensure(16 * (uint64_t)T + up_bytes + 256);
+    VH_HIP(hipMemcpyAsync(stage.ptr, d_hist, 16 * (uint64_t)T, hipMemcpyDeviceToHost, st));
+    VH_HIP(hipStreamSynchronize(st));
+    const unsigned long long *hist = stage.as<unsigned long long>();
+    uint64_t sampled = 0;
+    for (uint32_t t = 0; t < T; t++) sampled += hist[t];
+    if (!sampled) return false;
+    // stream capacities per (XCD, tile), sized for the rows one XCD's workgroups take (an
+    // even share plus a batch per workgroup) with Poisson room, one batch of slack (sorted
+    // columns: a tile's batches are dealt over the XCDs +-1), and for clustered tiles (whole
+    // batch-sized blocks in or out, per the sample's spread) four standard deviations of the
+    // XCD's batch count; past a stream, the tile's spill area
+    const double rows_x = (double)n / NX + (double)(W / NX + 1) * TF_BATCH;
+    const double batches_x = rows_x / TF_BATCH;
+    std::vector<uint32_t> cap(T), toff(T), scap(T);
+    std::vector<uint64_t> sstart(T);
+    uint64_t xstride = 0, stotal = 0;
+    for (uint32_t t = 0; t < T; t++) {
+        const double p = (double)hist[t] / (double)sampled;
+        const double m = (double)hist[t] / (double)sblocks, var_b = std::max(0.0, (double)hist[T + t] / (double)sblocks - m * m);
+        const bool clustered = var_b > 4.0 * m + 1.0;
+        const double e = rows_x * p;
+        double c = e * 1.04 + 6.0 * std::sqrt(e + 1.0) + TF_BATCH;
+        if (clustered) c += 4.0 * std::sqrt(batches_x * p + 1.0) * TF_BATCH;
+        const uint64_t ci = std::min<uint64_t>(((uint64_t)c + 7) & ~uint64_t(7), ((uint64_t)rows_x + 7) & ~uint64_t(7));
+        cap[t] = (uint32_t)ci;
+        toff[t] = (uint32_t)xstride;
+        xstride += ci;
+        double sc = 0.02 * (double)n * p + 2.0 * TF_BATCH;
+        if (clustered) sc += 0.25 * (double)n * p;
+        if (hist[t] == 0) sc = std::min<double>((double)n, (double)bstride) + 2.0 * TF_BATCH;  // a tile the sample missed
+        scap[t] = (uint32_t)std::min<uint64_t>(((uint64_t)sc + 7) & ~uint64_t(7), (n + 7) & ~uint64_t(7));
+        sstart[t] = stotal;
+        stotal += scap[t];
+    }
+    if (xstride >= (1ull << 32) - TF_BATCH) return false;
+    const uint64_t total = (uint64_t)NX * xstride + stotal + 16;
+    // pass-B units: each (XCD stream, tile) split by its expected entries
+    std::vector<FirstUnit> units;
+    for (uint32_t t = 0; t < T; t++) {
+        const double e = (double)n * (double)hist[t] / (double)sampled / NX;
+        const uint32_t g = (uint32_t)std::min(64.0, std::max(1.0, std::ceil(e / target)));
+        for (uint32_t x = 0; x < NX; x++)
+            for (uint32_t k = 0; k < g; k++) units.push_back({t, x, k, g});
+    }
+    if (units.size() > max_units) return false;
+    const uint64_t list_cap = (uint64_t)units.size() * S + (1u << 20);
+    ws.ecell.ensure(total * 2);
+    ws.eokey.ensure(total * 8);
+    ws.erow.ensure(total * 4);
+    ws.list.ensure(list_cap * 16);
+    char *upl = stage.as<char>() + 16 * (uint64_t)T;
+    auto upload = [&](void *dst, const void *src, uint64_t bytes) {
+        memcpy(upl, src, bytes);
+        VH_HIP(hipMemcpyAsync(dst, upl, bytes, hipMemcpyHostToDevice, st));
+        upl += (bytes + 15) & ~uint64_t(15);
+    };
+    upload(d_cap, cap.data(), 4 * (uint64_t)T);
+    upload(d_toff, toff.data(), 4 * (uint64_t)T);
+    upload(d_scap, scap.data(), 4 * (uint64_t)T);
+    upload(d_sstart, sstart.data(), 8 * (uint64_t)T);
+    upload(d_units, units.data(), sizeof(FirstUnit) * units.size());
+    VH_HIP(hipMemsetAsync(d_sfill, 0, 4 * (uint64_t)NX * T, st));
+    VH_HIP(hipMemsetAsync(d_spfill, 0, 4 * (uint64_t)T, st));
+    VH_HIP(hipMemsetAsync(d_misc, 0, 64, st));
+    FirstParams fp{};
+    fp.T = T;
+    fp.NX = NX;
+    fp.s_log2 = s_log2;
+    fp.n = n;
+    fp.cells = cells;
+    fp.cap = d_cap;
+    fp.toff = d_toff;
+    fp.xstride = xstride;
+    fp.sfill = d_sfill;
+    fp.spill_fill = d_spfill;
+    fp.spill_cap = d_scap;
+    fp.spill_start = d_sstart;
+    fp.spill_base = (uint64_t)NX * xstride;
+    fp.ecell = ws.ecell.as<uint16_t>();
+    fp.eokey = ws.eokey.as<unsigned long long>();
+    fp.erow = ws.erow.as<uint32_t>();
+    fp.s_key = static_cast<unsigned long long *>(ad.s_key);
+    fp.s_row = static_cast<unsigned long long *>(ad.s_row);
+    fp.list = ws.list.as<uint4>();
+    fp.list_fill = d_misc;
+    fp.list_cap = list_cap;
+    fp.flag = reinterpret_cast<unsigned *>(d_misc + 1);
+    {
+        TimedScope ts("first_scatter");
+        switch (nd) {
+        case 1: tf_launch_a<1>(ad.dtype, W, lds_a, plan, ad, fp); break;
+        case 2: tf_launch_a<2>(ad.dtype, W, lds_a, plan, ad, fp); break;
+        case 3: tf_launch_a<3>(ad.dtype, W, lds_a, plan, ad, fp); break;
+        default: tf_launch_a<0>(ad.dtype, W, lds_a, plan, ad, fp);
+        }
+        VH_HIP(hipGetLastError());
+    }
+    {
+        TimedScope ts("first_reduce");
+        hipLaunchKernelGGL(k_first_reduce, dim3((unsigned)units.size()), dim3(TFB_THREADS), (size_t)12 * S, st, fp, d_units);
+        VH_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_first_resolve, dim3(blocks_for(list_cap, 256, 4)), dim3(256), 0, st, fp, row0);
+        VH_HIP(hipGetLastError());
+    }
+    unsigned long long *res = reinterpret_cast<unsigned long long *>(stage.as<char>());
+    VH_HIP(hipMemcpyAsync(res, d_misc, 16, hipMemcpyDeviceToHost, st));
+    VH_HIP(hipStreamSynchronize(st));
+    if ((unsigned)res[1]) {
+        // the resolve list overflowed: the generic path redoes this chunk from clean scratch
+        VH_HIP(hipMemsetAsync(ad.s_key, 0xff, cells * 8, st));
+        VH_HIP(hipMemsetAsync(ad.s_row, 0xff, cells * 8, st));
+        return false;
+    }
+    __atomic_add_fetch(&g_first_tiled_chunks, 1ull, __ATOMIC_RELAXED);
+    return true;
+}
+
+}  // namespace vh

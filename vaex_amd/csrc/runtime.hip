@@ -753,6 +753,7 @@ int vh_stat_read(const char *name, uint64_t *value, int reset) {
     if (n == "tile_overflow_rows") *value = stat_tile_overflow(reset != 0);
     else if (n == "hashagg_overflow_rows") *value = stat_hashagg_overflow(reset != 0);
     else if (n == "set_overflow_rows") *value = stat_set_overflow(reset != 0);
+    else if (n == "first_tiled_chunks") *value = stat_first_tiled(reset != 0);
     else fail(VH_ERR_ARG, "vh_stat_read: unknown statistic '" + n + "'");
     VH_API_END
 }

@@ -1207,7 +1207,12 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
             f = i < row_end ? f : 0u;
             const uint32_t t = c >> s_log2;
             key[r] = (t << 16) | (c & smask);
-            rank[r] = tile_rank(l.hist, t, f != 0);
+            if (DBG(tp.debug) & 64) {  // experiment: no ranking
+                asm volatile("" ::"v"(key[r]), "v"(f));
+                rank[r] = -1;
+            } else {
+                rank[r] = tile_rank(l.hist, t, f != 0);
+            }
         }
     };
     Regs cur, nxt;
@@ -1222,7 +1227,12 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
             rows(b0 + sb * bstep, cur, key + sb * TA_RPT, rank + sb * TA_RPT, vals + sb * TA_RPT);
             if (sb + 1 < SB || VH_TA_DRAIN) cur = nxt;
         }
-        batch_commit_fast<NV, SB * TA_RPT, VT>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
+        if (DBG(tp.debug) & 32) {  // experiment: no commit (loads, cell math, ranking only)
+#pragma unroll
+            for (int r = 0; r < SB * TA_RPT; r++) asm volatile("" ::"v"(key[r]), "v"(rank[r]));
+        } else {
+            batch_commit_fast<NV, SB * TA_RPT, VT>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
+        }
         if (!VH_TA_DRAIN) cur = nxt;
     }
     lds_barrier();

@@ -114,34 +114,16 @@ class GrouperDense(BinnerBase):
             self._bin_values = _label_range(self.min_value, self.N, self.value_dtype)
         return self._bin_values
 
-    def occupied_values(self, mask, all_set=False, first=0):
-        """Labels of the cells where mask is set (mask over the central cells from `first` on)."""
-        vmin = self.min_value + first
-        if all_set:
-            return _label_range(vmin, len(mask), self.value_dtype)
-        return (np.flatnonzero(mask) + vmin).astype(self.value_dtype)
-
-    def trim(self, counts_edges, mask):
-        """A speculative range: raise DenseRangeMiss when keys fell outside it (under/overflow
-        cells 1 and N + 2 of the count(*) grid), else the (first, last) occupied central cells,
-        with the label dtype taken from the keys that occur (what the exact range gives)."""
-        if counts_edges[1] or counts_edges[-1] or not mask.any():
-            raise DenseRangeMiss(self.expression)
-        first = int(np.argmax(mask))
-        last = len(mask) - 1 - int(np.argmax(mask[::-1]))
-        self.value_dtype = label_dtype(self.key_dtype, self.min_value + first, self.min_value + last)
-        return first, last
-
     def labels(self):
         return self.bin_values.tolist()
 
 
-def _label_range(vmin, n, dtype):
+def _label_range(vmin, n, dtype, threads=True):
     """min .. min + n - 1 as `dtype` (label_dtype chose it to hold them), built in that dtype
     directly (no int64 array and cast for a 1e6-group result)."""
     dtype = np.dtype(dtype)
     if dtype.kind in "iu":
-        return hostops.arange(vmin, n, dtype)
+        return hostops.arange(vmin, n, dtype, threads=threads)
     return np.arange(vmin, vmin + n, dtype=np.int64).astype(dtype)
 
 
@@ -583,6 +565,8 @@ class GroupBy(GroupByBase):
         counts = self.counts
         if has_non_existing_pairs and counts is None:
             counts = self.df._agg(vagg.count(edges=True), self.binners, delay=True)
+        if len(self.by) == 1 and isinstance(self.by[0], GrouperDense):
+            return self._agg_dense(arrays, counts)
         self.df.execute()
         arrays = {k: extract_central_part(np.asarray(v.get())) for k, v in arrays.items()}
         columns = {}
@@ -590,22 +574,13 @@ class GroupBy(GroupByBase):
             counts_edges = np.asarray(counts.get())
             counts = extract_central_part(counts_edges)
             mask = counts > 0
-            if len(self.by) == 1 and getattr(self.by[0], "speculative", False):
-                first, last = self.by[0].trim(counts_edges, mask)
-                mask = mask[first:last + 1]
-                arrays = {k: v[first:last + 1] for k, v in arrays.items()}
-            else:
-                first = 0
             if self.row_limit is not None and any(getattr(b, "dense", False) for b in self.by):
                 groups = int(np.count_nonzero(mask))
                 if groups > self.row_limit:  # what the set build of Grouper raises (groupby.py:125)
                     raise RowLimitException(f"Resulting grouper has {groups:,} unique combinations, which is "
                                             f"larger than the allowed row limit of {self.row_limit:,}")
-            every = bool(mask.all())  # every cell occupied (e.g. a dense key range): no compaction
-            if len(self.by) == 1 and isinstance(self.by[0], GrouperDense):
-                coords = [self.by[0].occupied_values(mask, all_set=every, first=first)]
-            else:
-                coords = [c[mask] for c in np.meshgrid(*[np.asarray(b.bin_values) for b in self.by], indexing="ij")]
+            every = bool(mask.all())  # every cell occupied: no compaction
+            coords = [c[mask] for c in np.meshgrid(*[np.asarray(b.bin_values) for b in self.by], indexing="ij")]
             for b, coord in zip(self.by, coords):
                 columns[b.label] = coord
             for k, v in arrays.items():
@@ -615,6 +590,51 @@ class GroupBy(GroupByBase):
             for k, v in arrays.items():
                 assert v.ndim == 1
                 columns[k] = v
+        return DataFrame(columns)
+
+
+    def _agg_dense(self, arrays, counts):
+        """One dense integer key (GrouperDense): the occupied range of the count(*) grid is
+        found by host threads (count_nonzero per chunk, no mask array when every cell of it is
+        occupied), and the label range is built on the host pool while the GPU bins (labels
+        sliced to the occupied cells afterwards) -- groupby.py:484-533's result: groups in key
+        order, empty cells dropped."""
+        g = self.by[0]
+        dtype0 = np.dtype(g.value_dtype)
+        # a range of up to 4 Mi labels is built while the GPU bins (larger ones only for the
+        # occupied cells, afterwards)
+        labels = hostops.submit(_label_range, g.min_value, g.N, dtype0, False) if g.N <= (1 << 22) else None
+        try:
+            self.df.execute()
+        finally:
+            labels = labels.result() if labels is not None else None
+        arrays = {k: extract_central_part(np.asarray(v.get())) for k, v in arrays.items()}
+        counts_edges = np.asarray(counts.get())
+        central = extract_central_part(counts_edges)
+        nnz, first, last = hostops.occupancy(central)
+        if g.speculative:
+            # keys outside the guessed range sit in the under / overflow cells
+            if counts_edges[1] or counts_edges[-1] or nnz == 0:
+                raise DenseRangeMiss(g.expression)
+            g.value_dtype = label_dtype(g.key_dtype, g.min_value + first, g.min_value + last)
+        if self.row_limit is not None and nnz > self.row_limit:  # what Grouper's set build raises (groupby.py:125)
+            raise RowLimitException(f"Resulting grouper has {nnz:,} unique combinations, which is "
+                                    f"larger than the allowed row limit of {self.row_limit:,}")
+        if nnz == 0:
+            first, last = 0, -1
+        sl = slice(first, last + 1)
+        every = nnz == last - first + 1  # the occupied range has no empty cell: no compaction
+        if every:
+            lab = labels[sl] if labels is not None and np.dtype(g.value_dtype) == dtype0 else \
+                _label_range(g.min_value + first, nnz, g.value_dtype)
+            columns = {g.label: lab}
+            for k, v in arrays.items():
+                columns[k] = v[sl]
+            return DataFrame(columns)
+        mask = central[sl] > 0
+        columns = {g.label: (np.flatnonzero(mask) + (g.min_value + first)).astype(g.value_dtype)}
+        for k, v in arrays.items():
+            columns[k] = v[sl][mask]
         return DataFrame(columns)
 
 

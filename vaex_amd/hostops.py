@@ -23,18 +23,29 @@ def _threads():
     return max(1, min(8, n, int(os.environ.get("OMP_NUM_THREADS", n))))
 
 
+def _get_pool():
+    global _pool
+    with _pool_lock:
+        if _pool is None:
+            _pool = ThreadPoolExecutor(_threads(), thread_name_prefix="vaex_amd_host")
+    return _pool
+
+
+def submit(fn, *args):
+    """fn(*args) on the host pool (a Future): host work overlapped with a GPU pass, which
+    releases the GIL while the library waits on the device."""
+    return _get_pool().submit(fn, *args)
+
+
 def _run(fn, n):
     """fn(i0, i1) over [0, n) in chunks, on the pool when n is large."""
-    global _pool
     k = min(_threads(), max(1, n // MIN_SPLIT))
     if k == 1:
         fn(0, n)
         return
-    with _pool_lock:
-        if _pool is None:
-            _pool = ThreadPoolExecutor(_threads(), thread_name_prefix="vaex_amd_host")
+    pool = _get_pool()
     b = [n * i // k for i in range(k + 1)]
-    for f in [_pool.submit(fn, b[i], b[i + 1]) for i in range(k)]:
+    for f in [pool.submit(fn, b[i], b[i + 1]) for i in range(k)]:
         f.result()
 
 
@@ -64,8 +75,9 @@ def true_divide(a, b):
     return out
 
 
-def arange(vmin, n, dtype):
-    """vmin .. vmin + n - 1 in `dtype` (every value representable in it)."""
+def arange(vmin, n, dtype, threads=True):
+    """vmin .. vmin + n - 1 in `dtype` (every value representable in it).  threads=False: on
+    the calling thread only (a job already running on the pool must not wait on it)."""
     dtype = np.dtype(dtype)
     if n < MIN_SPLIT:
         return np.arange(vmin, vmin + n, dtype=dtype)
@@ -74,7 +86,10 @@ def arange(vmin, n, dtype):
     def part(i0, i1):
         out[i0:i1] = np.arange(vmin + i0, vmin + i1, dtype=dtype)
 
-    _run(part, n)
+    if threads:
+        _run(part, n)
+    else:
+        part(0, n)
     return out
 
 
@@ -104,3 +119,32 @@ def minmax(a):
 
     _run(part, len(a))
     return min(v[0] for v in res.values()), max(v[1] for v in res.values())
+
+
+def occupancy(a):
+    """(nonzero count, first nonzero index, last nonzero index) of a 1-d array ((0, -1, -1)
+    when all are zero): count_nonzero per chunk on the host threads; the first / last index
+    is searched only inside chunks that are not fully occupied (a dense groupby's count grid
+    usually is)."""
+    a = np.asarray(a)
+    n = len(a)
+    res = {}
+
+    def part(i0, i1):
+        c = a[i0:i1]
+        nz = int(np.count_nonzero(c))
+        if nz == 0:
+            res[i0] = (0, -1, -1)
+        elif nz == i1 - i0:
+            res[i0] = (nz, i0, i1 - 1)
+        else:
+            idx = np.flatnonzero(c)
+            res[i0] = (nz, i0 + int(idx[0]), i0 + int(idx[-1]))
+
+    if n:
+        _run(part, n)
+    parts = [res[k] for k in sorted(res)]
+    nnz = sum(p[0] for p in parts)
+    firsts = [p[1] for p in parts if p[0]]
+    lasts = [p[2] for p in parts if p[0]]
+    return nnz, (firsts[0] if firsts else -1), (lasts[-1] if lasts else -1)
