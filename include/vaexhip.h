@@ -236,6 +236,14 @@ int vh_hashagg_read(vh_hashagg *h, int64_t *keys, int64_t *counts, void *const *
  * their total rows).  A prefix of the rows is scanned until every group has its first row
  * (run heads only); keys that first appear late fall back to an ordered_set over all rows. */
 int vh_hashagg_order_first(vh_hashagg *h, const void *keys, uint64_t n, int loc);
+/* the same first-appearance order for the groups of a dense integer key range (the grid
+ * route of groupby(key, assume_sparse=True)): labels[0..m) are the keys of the result groups
+ * (int64, host or HBM; every one occurs in `keys`, all within [vmin, vmin + span)), and
+ * perm[i] (host, int64) is the label index of the i-th group in the order the keys first
+ * appear in the key column (n rows, host or HBM) -- an ordered_set's ordinal order
+ * (hash_primitives.hpp:96-281).  A prefix of run heads is scanned until every label is seen. */
+int vh_dense_first_order(const void *keys, uint64_t n, int loc, int key_dtype, int64_t vmin, uint64_t span,
+                         const int64_t *labels, uint64_t m, int64_t *perm);
 /* ---- multi-GPU (comm.hip): RCCL bound by the library, one process per GPU ----------
  * The reference has no multi-process path; its ExecutorLocal reduces per-thread task
  * parts serially (execution.py:285, Aggregator::reduce superagg.cpp:160-167,205-212,

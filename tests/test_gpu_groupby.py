@@ -155,20 +155,26 @@ def test_dense_and_hash_groupers_agree(dense):
     np.testing.assert_allclose(dfg["v_sum"].to_numpy()[order], s, rtol=1e-6, atol=1e-9)
 
 
+@pytest.mark.parametrize("spread", [1, 1000])
 @pytest.mark.parametrize("kdtype", ["int8", "int16", "int32", "uint32", "int64"])
-def test_set_ordinal_grid_through_hash_aggregation(kdtype):
+def test_set_ordinal_grid_through_hash_aggregation(kdtype, spread):
     """assume_sparse=True with count / sum aggregators over >= 2^22 rows: the set-ordinal
     grid is filled by the fused hash aggregation (per-key totals added at each key's
     ordinal cell, hashagg_bin_set_ordinal) -- groups in first-appearance order, counts
     exact, sums within 1e-6, NaN values skipped by sum and count(v), keys of every width
-    including negative 1- and 2-byte keys (sign- vs zero-extended bits)."""
+    including negative 1- and 2-byte keys (sign- vs zero-extended bits).  spread 1: a dense
+    key range (the grid route + vh_dense_first_order); spread 1000 on >= 4-byte keys: a sparse
+    range (the hash aggregation + vh_hashagg_order_first)."""
     import vaex_amd
     from vaex_amd.device import DeviceArray
     rng = np.random.default_rng(21)
     n = (1 << 22) + 3
     info = np.iinfo(kdtype)
     lo, hi = max(info.min, -40_000), min(info.max, 60_000)
-    keys = rng.integers(lo, hi, n, endpoint=True).astype(kdtype)
+    keys = rng.integers(lo, hi, n, endpoint=True)
+    if np.dtype(kdtype).itemsize >= 4:
+        keys = keys * spread
+    keys = keys.astype(kdtype)
     v = rng.normal(size=n)
     v[rng.random(n) < 0.01] = np.nan
     df = vaex_amd.from_arrays(key=DeviceArray.from_numpy(keys), v=DeviceArray.from_numpy(v))
@@ -186,16 +192,18 @@ def test_set_ordinal_grid_through_hash_aggregation(kdtype):
     np.testing.assert_allclose(dfg["s"].to_numpy()[order], s, rtol=1e-6, atol=1e-9)
 
 
+@pytest.mark.parametrize("spread", [1, 1000])
 @pytest.mark.parametrize("vdtype", ["float64", "float32", "int32", "int64"])
-def test_set_ordinal_min_max_tile_path(vdtype):
+def test_set_ordinal_min_max_tile_path(vdtype, spread):
     """assume_sparse=True with min / max (+ count): the set-ordinal binner's fused LUT probe
     (k_tile_scatter_ord<SET = true>) feeding the tile path's min / max slots -- exact per-key
-    extrema (NaN skipped, as AggMin/AggMax do), groups in first-appearance order."""
+    extrema (NaN skipped, as AggMin/AggMax do), groups in first-appearance order.  spread 1:
+    a dense key range (BinnerOrdinal grid + vh_dense_first_order); spread 1000: the set route."""
     import vaex_amd
     from vaex_amd.device import DeviceArray
     rng = np.random.default_rng(33)
     n = (1 << 22) + 5
-    keys = rng.integers(-5_000, 200_000, n).astype(np.int32)
+    keys = (rng.integers(-5_000, 200_000, n) * spread).astype(np.int32)
     if vdtype.startswith("float"):
         v = rng.normal(size=n).astype(vdtype)
         v[rng.random(n) < 0.01] = np.nan

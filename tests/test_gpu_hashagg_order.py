@@ -143,11 +143,20 @@ def test_order_first_wave_straddling_the_grid_stride():
     keys[row(b) + 12:row(b) + 16] = K
     keys[row(b - 1 + S):row(b + S)] = K  # what the neighbour lane loaded last
     keys[row(b - 1 + S) + 4:row(b - 1 + S) + 8] = M
-    df = vaex_amd.from_arrays(key=DeviceArray.from_numpy(keys), v=DeviceArray.from_numpy(np.ones(n)))
-    got = df.groupby("key", agg={"n": vaex_amd.agg.count()}, assume_sparse=True)
+    dkeys = DeviceArray.from_numpy(keys)
     exp = _first_order(keys)
+    u, cnt = np.unique(keys, return_counts=True)
+    # the hash aggregation's scan (k_ha_first) ...
+    from vaex_amd.hashagg import HashAgg
+    ha = HashAgg(np.int32, [])
+    ha.update(dkeys, [])
+    hk, hc, _, _ = ha.finish(first_order_keys=dkeys)
+    np.testing.assert_array_equal(hk, exp)
+    np.testing.assert_array_equal(hc, cnt[np.searchsorted(u, exp)])
+    # ... and the dense-range grid route's (k_dense_first), through groupby(assume_sparse=True)
+    df = vaex_amd.from_arrays(key=dkeys, v=DeviceArray.from_numpy(np.ones(n)))
+    got = df.groupby("key", agg={"n": vaex_amd.agg.count()}, assume_sparse=True)
     np.testing.assert_array_equal(got["key"].to_numpy(), exp)
     gk = list(got["key"].to_numpy())
     assert gk.index(K) < gk.index(M)
-    u, cnt = np.unique(keys, return_counts=True)
     np.testing.assert_array_equal(got["n"].to_numpy(), cnt[np.searchsorted(u, exp)])

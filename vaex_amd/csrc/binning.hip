@@ -1519,9 +1519,11 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
     // tile pass per group over the same staged chunk)
     bool tile_generic = !all_fusable && L * 8 > LDS_AGG_MAX_BYTES;
     // (min / max too: LDS min / max cells in pass B; not of bool data)
+    // (and AggSumMoment of float data -- var / std: a moment cell beside the sum's in pass B)
     auto tile_kind = [](const vh_agg *a) {
         return (a->kind == VH_AGG_COUNT || (a->kind == VH_AGG_SUM && a->data.set) ||
-                ((a->kind == VH_AGG_MIN || a->kind == VH_AGG_MAX) && a->data.set && a->dtype != VH_BOOL)) &&
+                ((a->kind == VH_AGG_MIN || a->kind == VH_AGG_MAX) && a->data.set && a->dtype != VH_BOOL) ||
+                (a->kind == VH_AGG_SUM_MOMENT && a->data.set && (a->dtype == VH_F64 || a->dtype == VH_F32))) &&
                !a->mask.set && !a->flip;
     };
     for (int k = 0; k < naggs && tile_generic; k++) tile_generic = tile_kind(aggs[k]);
@@ -1603,6 +1605,7 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                            f.grid = ad.grid;
                            f.dtype = ad.dtype;
                            f.vint = ad.kind == VH_AGG_SUM && ad.dtype != VH_F64 && ad.dtype != VH_F32;
+                           f.moment = ad.moment;
                        }
                        // at most two carried value columns per group (sums, min, max of one
                        // column share one: same_value_slot)

@@ -122,7 +122,18 @@ struct FusedAgg {
     void *grid;           // int64 counts / upcast sums (float64, int64 or uint64), length1d cells
     int32_t dtype;        // data dtype code
     int32_t vint;         // the sum accumulates 64-bit integers (integer / bool data), not float64
+    uint32_t moment;      // AggSumMoment: the power summed (float data only on the tile path)
+    uint32_t pad;
 };
+
+// AggSumMoment's term of a non-NaN float value (superagg.cpp:400-433: pow(value, moment) in
+// double; moment 2 as value * value, which pow rounds identically)
+__device__ inline double moment_term(double v, uint32_t m) {
+    if (m == 0) return 1.0;
+    if (m == 1) return v;
+    if (m == 2) return v * v;
+    return pow(v, (double)m);
+}
 
 // two value-carrying aggregators (sum / min / max) read the same column the same way: the tile
 // path carries that column once per row for both

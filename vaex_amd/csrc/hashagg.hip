@@ -1470,6 +1470,77 @@ __global__ __launch_bounds__(256) void k_ha_permute(const int64_t *src, int64_t 
     }
 }
 
+// First row of every key of a dense key range [vmin, vmin + span): the run heads of rows
+// [0, nrow) of a chunk starting at global row `base` (16-B aligned keys, keys[-1] readable when
+// base > 0) lower first[key - vmin]; stats[0] += keys seen for the first time, stats[1] += run
+// heads.  Same wave-uniform loop as k_ha_first, with a direct index instead of a table probe.
+template <typename K>
+__global__ __launch_bounds__(256) void k_dense_first(const K *keys, uint64_t nrow, uint64_t base, int64_t vmin, uint64_t span,
+                                                     unsigned long long *first, unsigned long long *stats) {
+    constexpr int V = 16 / sizeof(K);
+    struct alignas(16) Vec { K k[V]; };
+    const Vec *src = reinterpret_cast<const Vec *>(keys);
+    uint32_t newly = 0, heads = 0;
+    const uint64_t nvec = nrow / V, stride = (uint64_t)gridDim.x * 256;
+    const int lane = threadIdx.x & 63;
+    auto row_head = [&](K k, uint64_t row) {
+        heads++;
+        const uint64_t off = (uint64_t)((int64_t)k - vmin);
+        if (off >= span) return;
+        unsigned long long *f = first + off;
+        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= row) return;
+        newly += atomicMin(f, (unsigned long long)row) == ~0ull;
+    };
+    auto vec = [&](uint64_t v, const Vec &x) {
+        K prev = __shfl_up(x.k[V - 1], 1, 64);
+        if (v >= nvec) return;
+        const bool has_prev = base + v * V > 0;
+        if (lane == 0 && has_prev) prev = keys[v * V - 1];
+#pragma unroll
+        for (int j = 0; j < V; j++)
+            if (j ? x.k[j] != x.k[j - 1] : (!has_prev || x.k[0] != prev)) row_head(x.k[j], base + v * V + j);
+    };
+    const Vec none{};
+    uint64_t w = blockIdx.x * 256ull + (threadIdx.x & ~63u);
+    for (; w + stride < nvec; w += 2 * stride) {
+        const uint64_t va = w + lane, vb = va + stride;
+        const Vec a = va < nvec ? src[va] : none, b = vb < nvec ? src[vb] : none;
+        vec(va, a);
+        vec(vb, b);
+    }
+    for (; w < nvec; w += stride) {
+        const uint64_t va = w + lane;
+        vec(va, va < nvec ? src[va] : none);
+    }
+    for (uint64_t i = nvec * V + blockIdx.x * 256ull + threadIdx.x; i < nrow; i += stride) {
+        const K k = keys[i];
+        if (base + i > 0 && keys[i - 1] == k) continue;
+        row_head(k, base + i);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        newly += __shfl_xor(newly, off, 64);
+        heads += __shfl_xor(heads, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (newly) atomicAdd(&stats[0], (unsigned long long)newly);
+        if (heads) atomicAdd(&stats[1], (unsigned long long)heads);
+    }
+}
+
+// fr[j] = first row of labels[j] (sort key), idx[j] = j
+__global__ __launch_bounds__(256) void k_dense_first_gather(const int64_t *labels, uint64_t m, int64_t vmin,
+                                                            const unsigned long long *first, unsigned long long *fr, uint32_t *idx) {
+    for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) {
+        fr[j] = first[(uint64_t)(labels[j] - vmin)];
+        idx[j] = (uint32_t)j;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_widen_u32(const uint32_t *src, uint64_t m, int64_t *dst) {
+    for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) dst[j] = src[j];
+}
+
 // combined key of a multi-key groupby: sum_j (key_j - min_j) * mult_j as int64
 // (groupby.py:248-288 _combine: the cartesian ordinal, first key most significant)
 constexpr int HC_MAX_KEYS = 8;
@@ -2406,6 +2477,84 @@ int vh_hashagg_order_first(vh_hashagg *h, const void *keys, uint64_t n, int loc)
     VH_HIP(hipGetLastError());
     VH_HIP(hipStreamSynchronize(st));
     h->res = reinterpret_cast<const char *>(dst);
+    VH_API_END
+}
+
+/* first-appearance order of the groups of a dense key range (vh_dense_first_order; see
+ * vaexhip.h) */
+int vh_dense_first_order(const void *keys, uint64_t n, int loc, int key_dtype, int64_t vmin, uint64_t span,
+                         const int64_t *labels, uint64_t m, int64_t *perm) {
+    VH_API_BEGIN
+    if (!key_dtype_ok(key_dtype)) fail(VH_ERR_ARG, "dense_first_order: integer keys only");
+    if (m == 0) return VH_OK;
+    if (span == 0 || m > span || m >= (1ull << 32)) fail(VH_ERR_ARG, "dense_first_order: bad key range");
+    loc = resolve_loc(keys, loc);
+    hipStream_t st = stream();
+    const int kisz = dtype_itemsize(key_dtype);
+    size_t tmp_bytes = 0;
+    VH_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
+                                     (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)m, 0, 64, st));
+    const uint64_t af = (8 * span + 255) & ~255ull, a8 = (8 * m + 255) & ~255ull, a4 = (4 * m + 255) & ~255ull;
+    DevBuf work;
+    work.ensure(af + 3 * a8 + 2 * a4 + 256 + tmp_bytes + 256);
+    char *wb = work.as<char>();
+    auto *first = reinterpret_cast<unsigned long long *>(wb);
+    auto *fr = reinterpret_cast<unsigned long long *>(wb + af);
+    auto *fr2 = reinterpret_cast<unsigned long long *>(wb + af + a8);
+    auto *dlab = reinterpret_cast<int64_t *>(wb + af + 2 * a8);
+    auto *idx = reinterpret_cast<uint32_t *>(wb + af + 3 * a8);
+    auto *idx2 = reinterpret_cast<uint32_t *>(wb + af + 3 * a8 + a4);
+    auto *stats = reinterpret_cast<unsigned long long *>(wb + af + 3 * a8 + 2 * a4);
+    void *tmp = wb + af + 3 * a8 + 2 * a4 + 256;
+    VH_HIP(hipMemsetAsync(first, 0xff, 8 * span, st));
+    VH_HIP(hipMemsetAsync(stats, 0, 16, st));
+    VH_HIP(hipMemcpyAsync(dlab, labels, 8 * m, hipMemcpyDefault, st));
+    thread_local PinnedBuf res_buf;
+    res_buf.ensure(64);
+    auto *hstats = res_buf.as<unsigned long long>();
+    {
+        TimedScope ts("dense_first");
+        HaScratch &S = scratch();
+        std::lock_guard<std::mutex> lk(S.mu);
+        // prefix scan of run heads in growing chunks until every group has its first row
+        uint64_t r0 = 0, chunk = std::max<uint64_t>(1u << 20, 4 * m);
+        const bool aligned = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
+        while (r0 < n) {
+            const uint64_t r1 = std::min(n, r0 + (chunk & ~uint64_t(1023)));
+            const void *kp = static_cast<const char *>(keys) + r0 * kisz;
+            if (loc == VH_LOC_HOST || !aligned) {
+                const uint64_t lead = std::min<uint64_t>(r0, 16 / kisz);
+                S.stage.ensure((r1 - r0) * kisz + 64);
+                char *d = S.stage.as<char>() + 16;
+                VH_HIP(hipMemcpyAsync(d - lead * kisz, static_cast<const char *>(keys) + (r0 - lead) * kisz,
+                                      (r1 - r0 + lead) * kisz, hipMemcpyDefault, st));
+                kp = d;
+            }
+            VH_DISPATCH_DTYPE(key_dtype, K, {
+                if constexpr (std::is_integral_v<K>) {
+                    hipLaunchKernelGGL(k_dense_first<K>, dim3(blocks_for((r1 - r0) / (16 / sizeof(K)) + 1, 256, 8)), dim3(256),
+                                       0, st, static_cast<const K *>(kp), r1 - r0, r0, vmin, span, first, stats);
+                }
+            });
+            VH_HIP(hipGetLastError());
+            VH_HIP(hipMemcpyAsync(hstats, stats, 16, hipMemcpyDeviceToHost, st));
+            VH_HIP(hipStreamSynchronize(st));
+            r0 = r1;
+            if (hstats[0] >= m) break;
+            chunk = hstats[1] * 16 > r0 ? chunk + chunk / 2 : chunk * 4;
+        }
+        if (hstats[0] < m) fail(VH_ERR_ARG, "dense_first_order: a label's key does not occur in the column");
+    }
+    hipLaunchKernelGGL(k_dense_first_gather, dim3(blocks_for(m, 256, 8)), dim3(256), 0, st, dlab, m, vmin, first, fr, idx);
+    VH_HIP(hipGetLastError());
+    size_t tb = tmp_bytes;
+    VH_HIP(rocprim::radix_sort_pairs(tmp, tb, fr, fr2, idx, idx2, (size_t)m, 0, 64, st));
+    // perm as int64 (into the first-row scratch, then one copy to the caller's buffer)
+    auto *p64 = reinterpret_cast<int64_t *>(first);
+    hipLaunchKernelGGL(k_widen_u32, dim3(blocks_for(m, 256, 8)), dim3(256), 0, st, idx2, m, p64);
+    VH_HIP(hipGetLastError());
+    copy_to_host(perm, p64, 8 * m, st);
+    VH_HIP(hipStreamSynchronize(st));
     VH_API_END
 }
 

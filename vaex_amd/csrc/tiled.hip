@@ -610,7 +610,9 @@ __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, co
                                 __builtin_bit_cast(uint64_t, l.sv[tp.val_slot[a] * TA_BATCH + k]), false);
                 } else if constexpr (NV > 0) {
                     const double v = l.sv[tp.val_slot[a] * TA_BATCH + k];
-                    if (fa.a[a].vint)
+                    if (fa.a[a].kind == VH_AGG_SUM_MOMENT) {
+                        if (v == v) atomicAdd(reinterpret_cast<double *>(fa.a[a].grid) + c, moment_term(v, fa.a[a].moment));
+                    } else if (fa.a[a].vint)
                         atomicAdd(reinterpret_cast<unsigned long long *>(fa.a[a].grid) + c,
                                   __builtin_bit_cast(unsigned long long, v));
                     else
@@ -742,7 +744,9 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
                                 __builtin_bit_cast(uint64_t, vt_wide<VT>(sv[tp.val_slot[a] * CAP + k], tp, tp.val_slot[a])), false);
                 } else if constexpr (NV > 0) {
                     const double v = vt_wide<VT>(sv[tp.val_slot[a] * CAP + k], tp, tp.val_slot[a]);
-                    if (fa.a[a].vint)
+                    if (fa.a[a].kind == VH_AGG_SUM_MOMENT) {
+                        if (v == v) atomicAdd(reinterpret_cast<double *>(fa.a[a].grid) + c, moment_term(v, fa.a[a].moment));
+                    } else if (fa.a[a].vint)
                         atomicAdd(reinterpret_cast<unsigned long long *>(fa.a[a].grid) + c, __builtin_bit_cast(unsigned long long, v));
                     else
                         atomicAdd(reinterpret_cast<double *>(fa.a[a].grid) + c, v);
@@ -1267,6 +1271,12 @@ __device__ inline void reduce_entry(const FusedAggs &fa, const TileParams &tp, u
                 else
                     mm_lds(reinterpret_cast<uint64_t *>(lds + fa.a[k].lds_off) + local, fa.a[k].dtype, fa.a[k].kind == VH_AGG_MAX, v[s]);
             }
+        } else if (fa.a[k].kind == VH_AGG_SUM_MOMENT) {
+            if constexpr (!MM) continue;
+#pragma unroll
+            for (int s = 0; s < NV; s++)
+                if (s == tp.val_slot[k] && v[s] == v[s])
+                    atomicAdd(reinterpret_cast<double *>(lds + fa.a[k].lds_off) + local, moment_term(v[s], fa.a[k].moment));
         } else {
 #pragma unroll
             for (int s = 0; s < NV; s++) {
@@ -2093,8 +2103,9 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     // ---- pass B
     {
         TimedScope ts("tile_reduce");
+        // MM: the per-entry pass B (min / max cells, moment terms) instead of the run form
         bool mm = false;
-        for (int k = 0; k < fa.na; k++) mm = mm || is_minmax(fa.a[k].kind);
+        for (int k = 0; k < fa.na; k++) mm = mm || is_minmax(fa.a[k].kind) || fa.a[k].kind == VH_AGG_SUM_MOMENT;
         uint64_t mm_bytes = 0;
         for (int k = 0; k < fa.na; k++)
             if (is_minmax(fa.a[k].kind)) mm_bytes += ((cells * (mm_cell32(fa.a[k].dtype) ? 4 : 8)) + 255) & ~uint64_t(255);

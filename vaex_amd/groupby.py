@@ -189,6 +189,35 @@ def _dense_range(df, expression, speculative=False):
     return int(vmin), int(vmax)
 
 
+def first_appearance_order(df, key, res):
+    """The key-sorted groups of a dense-range groupby result ``res`` reordered by the row each
+    key first appears at in ``df[key]`` -- the ordinal order of an ordered_set built over the
+    key column (hash_primitives.hpp:96-281), i.e. the Grouper route's group order
+    (groupby.py:97-168) -- on the device (vh_dense_first_order: run-head prefix scan, radix
+    sort of the first rows), the columns permuted by host threads."""
+    import ctypes
+    from . import _lib
+    from .device import DeviceArray
+    labels = np.asarray(res.columns[key])
+    m = len(labels)
+    if m < 2:
+        return res
+    col = df.columns[key]
+    lab64 = hostops.astype(labels, np.int64)
+    perm = _lib.pinned_empty(m, np.int64)
+    if isinstance(col, DeviceArray):
+        ptr, loc = col.ptr, _lib.LOC_DEVICE
+    else:
+        col = np.ascontiguousarray(col)
+        ptr, loc = col.ctypes.data, _lib.LOC_HOST
+    code, _ = _lib.dtype_code(np.dtype(col.dtype))
+    vmin = int(lab64[0])
+    span = int(lab64[-1]) - vmin + 1
+    _lib.call("vh_dense_first_order", ptr, df.length_unfiltered(), loc, code, ctypes.c_int64(vmin), span,
+              lab64.ctypes.data, m, perm.ctypes.data)
+    return DataFrame({name: hostops.take(v, perm) for name, v in res.columns.items()})
+
+
 COMBINE_OCCUPANCY = 10  # groupby.py:329-333: combine when rows / cells < 10
 COMBINED_KEY = "__vaex_amd_combined_key"
 

@@ -107,6 +107,20 @@ def astype(a, dtype):
     return out
 
 
+def take(a, idx):
+    """a[idx] for a 1-d array and an int64 index array (numpy take, split over the threads)."""
+    a, idx = np.asarray(a), np.asarray(idx)
+    if a.ndim != 1 or len(idx) < MIN_SPLIT:
+        return np.take(a, idx)
+    out = _empty(len(idx), a.dtype)
+
+    def part(i0, i1):
+        np.take(a, idx[i0:i1], out=out[i0:i1])
+
+    _run(part, len(idx))
+    return out
+
+
 def minmax(a):
     """(a.min(), a.max()) of a non-empty 1-d integer array."""
     a = np.asarray(a)
