@@ -50,6 +50,8 @@ def parse():
                    help="rows of the C4 leg (2D mean streamed from a memory-mapped HDF5 file); 0 = skip")
     p.add_argument("--check", action="store_true", help="verify size-independent properties")
     p.add_argument("--breakdown", action="store_true", help="print host-side timing of one step")
+    p.add_argument("--no-aggs", action="store_true", help="skip the first / var legs on the C2 grid")
+    p.add_argument("--no-set", action="store_true", help="skip the ordered_set.update leg")
     return p.parse_args()
 
 
@@ -201,6 +203,10 @@ def main():
             extra["groupby_sorted_keys"] = bench_groupby(int(args.groupby_rows), args, layout="sorted")
     if rank == 0 and world == 1 and not args.no_count_only:
         extra["count_only"] = bench_count_only(x, y, n, bins, args)
+    if rank == 0 and world == 1 and not args.no_aggs:
+        extra["aggs"] = bench_other_aggs(x, y, w, n, bins, args, ms_per_step)
+    if rank == 0 and world == 1 and not args.no_set:
+        extra["ordered_set"] = bench_ordered_set(int(args.groupby_rows), args)
     if rank == 0 and world == 1 and args.host_rows > 0:
         extra["host_columns"] = bench_host_columns(x, y, w, int(min(args.host_rows, n)), bins)
     if rank == 0 and world == 1 and args.c4_rows > 0:
@@ -305,6 +311,94 @@ def bench_count_only(x, y, n, bins, args):
             "kernel_frac": round(16 * n / (per[dom] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if dom else None,
             "pipeline_GBps": round(16 * n / (pipe * 1e-3) / 1e9, 1) if pipe else None,
             "pipeline_frac": round(16 * n / (pipe * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if pipe else None}
+
+
+def bench_other_aggs(x, y, w, n, bins, args, c2_ms):
+    """Other aggregators on the C2 grid (1027^2 cells, 1e9 rows resident), end to end with the
+    grids read back, median of the steps:
+      first -- first(w, order=o, binby=[x, y]) (AggFirst, superagg.cpp:436-511) with a fourth
+               column o ~ U[0, 1): the tile-partitioned engine (first.hip); algorithmic bytes
+               32 per row (x, y, w, o);
+      var   -- var(w, binby=[x, y]) (agg.py:191-229: AggSumMoment(2) + sum + count of w in
+               one tile pass); 24 B per row.
+    ratio_to_c2 = ms / the headline count+sum step."""
+    import vaex_amd
+    from vaex_amd import _lib
+    from vaex_amd.device import DeviceArray
+    o = DeviceArray.random(n, "uniform", seed=9)
+    df = vaex_amd.from_arrays(x=x, y=y, w=w, o=o)
+    lim = [[-4.0, 4.0], [-4.0, 4.0]]
+    out = {}
+    legs = (("first", lambda: df.first("w", "o", binby=["x", "y"], limits=lim, shape=bins), 32,
+             ["first_sample", "first_scatter", "first_reduce", "bin_indices", "bin_aggregate"]),
+            ("var", lambda: df.var("w", binby=["x", "y"], limits=lim, shape=bins), 24,
+             TILE_KERNELS + ["bin_indices", "bin_aggregate"]))
+    for name, f, bpr, kernels in legs:
+        r = f()
+        _lib.synchronize()
+        ts = []
+        _lib.timing_reset()
+        _lib.timing_enable(True)
+        for _ in range(max(3, args.steps // 2)):
+            t0 = time.perf_counter()
+            r = f()
+            ts.append(time.perf_counter() - t0)
+        _lib.synchronize()
+        _lib.timing_enable(False)
+        per = {}
+        for k in kernels:
+            c, ms = _lib.timing_read(k)
+            if c:
+                per[k] = ms / c
+        t = float(np.median(ts))
+        dom = max(per, key=per.get) if per else None
+        out[name] = {"ms": round(t * 1e3, 3), "rows_per_s": n / t, "ratio_to_c2": round(t * 1e3 / c2_ms, 3),
+                     "algorithmic_bytes_per_row": bpr, "per_kernel_ms": {k: round(v, 4) for k, v in per.items()},
+                     "kernel": dom,
+                     "kernel_frac": round(bpr * n / (per[dom] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if dom else None,
+                     "finite_cells": int(np.isfinite(np.asarray(r)).sum())}
+    c = df.count(binby=["x", "y"], limits=lim, shape=bins)
+    out["var"]["cells_with_rows"] = int((np.asarray(c) > 0).sum())
+    del df, o
+    return out
+
+
+def bench_ordered_set(n, args):
+    """ordered_set_int32.update over the C3 keys (1e9 int32 rows, 1e6 distinct; random and
+    sorted layouts): the standalone set build of df._set / Grouper (hash_primitives.hpp:96-281),
+    median of 3, with the set kernels' HIP-event times; algorithmic bytes 4 per row."""
+    from vaex_amd import _lib, superutils
+    from vaex_amd.device import DeviceArray
+    out = {"rows": n, "algorithmic_bytes_per_row": 4}
+    names = ["set_sample", "set_insert", "set_reduce", "set_rank", "set_direct"]
+    for layout in ("random", "sorted"):
+        if layout == "sorted":
+            keys = DeviceArray.random(n, "sorted_int", a=5, b=5 + 1_000_000, dtype="int32")
+        else:
+            keys = DeviceArray.random(n, "randint", seed=5, a=5, b=5 + 1_000_000, dtype="int32")
+        s = superutils.ordered_set_int32()
+        s.update(keys)
+        _lib.synchronize()
+        ts = []
+        _lib.timing_reset()
+        _lib.timing_enable(True)
+        for _ in range(3):
+            s = superutils.ordered_set_int32()
+            t0 = time.perf_counter()
+            s.update(keys)
+            m = len(s)
+            ts.append(time.perf_counter() - t0)
+        _lib.timing_enable(False)
+        per = {}
+        for k in names:
+            c, ms = _lib.timing_read(k)
+            if c:
+                per[k] = round(ms / 3, 4)
+        t = float(np.median(ts))
+        out[layout] = {"ms": round(t * 1e3, 3), "rows_per_s": n / t, "keys": m, "keys_ok": m == 1_000_000,
+                       "per_kernel_ms": per}
+        del keys, s
+    return out
 
 
 def bench_zero_d(w, n, args):
@@ -531,8 +625,9 @@ def bench_groupby(n, args, layout="random"):
       fused -- the one-pass hash-partitioned aggregation (hashagg.hip) the frame takes for
                sparse int keys, run on the same columns through its API;
       hash  -- assume_sparse=True: the ordered_set grouper's result (groups in the order their
-               keys first appear): the fused hash aggregation + vh_hashagg_order_first (a
-               run-head prefix scan for each group's first row, a radix sort of the groups).
+               keys first appear): for this dense key range the grid route + vh_dense_first_order
+               (a run-head prefix scan for each group's first row, a radix sort of the groups);
+      hash_minmax -- the same with min + max + sum + count(*) of v (one carried value slot).
     Per-kernel milliseconds from HIP events on the library stream."""
     from vaex_amd import _lib
     from vaex_amd.device import DeviceArray
@@ -546,8 +641,8 @@ def bench_groupby(n, args, layout="random"):
     df = vaex_amd.from_arrays(key=keys, v=v)
     out = {"rows": n, "algorithmic_bytes_per_row": 12, "layout": layout}
     names = ["minmax", "tile_sample", "tile_scatter", "tile_scatter_ord", "tile_scatter_set", "tile_reduce", "ha_sample",
-             "ha_scatter", "ha_scatter_f64", "ha_reduce", "ha_finish", "ha_first", "set_sample", "set_insert", "set_reduce", "set_rank",
-             "bin_fused_global"]
+             "ha_scatter", "ha_scatter_f64", "ha_reduce", "ha_finish", "ha_first", "dense_first", "set_sample", "set_insert",
+             "set_reduce", "set_rank", "bin_fused_global"]
 
     def run(mode):
         if mode == "fused":
@@ -555,13 +650,16 @@ def bench_groupby(n, args, layout="random"):
             ha.update(keys, [v])
             k, c, s, _ = ha.finish()
             return k, c, s[0]
+        if mode == "hash_minmax":  # assume_sparse=True with min + max + sum (+ count(*))
+            dfg = df.groupby("key", agg={"v": ["sum", "count", "min", "max"]}, assume_sparse=True)
+            return dfg["key"].to_numpy(), dfg["v"].to_numpy(), dfg["v_sum"].to_numpy()
         dfg = df.groupby("key", agg={"v": ["sum", "count"]}, assume_sparse="auto" if mode == "auto" else True)
         # {"v": ["sum", "count"]} names the count(*) column "v" (groupby.py:345-402)
         return dfg["key"].to_numpy(), dfg["v"].to_numpy(), dfg["v_sum"].to_numpy()
 
     v_total = float(vaex_amd.from_arrays(v=v).sum("v"))  # independent 0-d reduction
     ref_groups = None
-    for mode in ("auto", "fused", "hash"):
+    for mode in ("auto", "fused", "hash", "hash_minmax"):
         run(mode)  # warm-up
         _lib.trace_report()
         _lib.synchronize()
