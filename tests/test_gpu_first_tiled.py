@@ -166,3 +166,45 @@ def test_first_dataframe_api_matches_generic_small_grid():
         [oracle.Binner("scalar", x, vmin=-4, vmax=4, bins=1024), oracle.Binner("scalar", y, vmin=-4, vmax=4, bins=1024)],
         "first", data=w, data2=o))
     np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.parametrize("dtype", ["float64", "int32", "float32"])
+@pytest.mark.parametrize("order", ["ties", "descending"])
+def test_first_small_grid_lds(dtype, order):
+    """Small grids (12 B of LDS per cell fit a workgroup): per-workgroup LDS (key, row) cells
+    + a fold of the partials (k_first_small) instead of per-row global atomics on few cells;
+    bit-exact with ties, NaN and max-valued orders."""
+    rng = np.random.default_rng(31)
+    n = 3_000_007
+    x = rng.normal(size=n)
+    dt = np.dtype(dtype)
+    if dt.kind == "f":
+        v = rng.normal(size=n).astype(dt)
+        o = (rng.integers(0, 4, n) if order == "ties" else np.arange(n, 0, -1)).astype(dt)
+        v[::19] = np.nan
+        o[5::23] = np.nan
+        o[::29] = np.finfo(dt).max
+    else:
+        v = rng.integers(-(1 << 30), 1 << 30, n).astype(dt)
+        o = (rng.integers(0, 4, n) if order == "ties" else np.arange(n, 0, -1)).astype(dt)
+        o[::29] = np.iinfo(dt).max
+    specs = [("BinnerScalar_float64", x, -3.0, 3.0, 256)]
+    gv, go, _ = _run(specs, v, o)
+    ev, eo = _oracle_first([oracle.Binner("scalar", x, vmin=-3, vmax=3, bins=256)], v, o)
+    np.testing.assert_array_equal(go.view(f"u{dt.itemsize}"), eo.view(f"u{dt.itemsize}"))
+    np.testing.assert_array_equal(gv.view(f"u{dt.itemsize}"), ev.view(f"u{dt.itemsize}"))
+
+
+def test_first_small_grid_host_chunks():
+    """Host columns in several pipeline chunks on a small 2-d grid: row offsets per chunk."""
+    rng = np.random.default_rng(32)
+    n = (1 << 24) + 12345
+    x, y = rng.normal(size=n), rng.normal(size=n)
+    v = rng.normal(size=n)
+    o = rng.integers(0, 2, n).astype(np.float64)
+    specs = [("BinnerScalar_float64", x, -3.0, 3.0, 40), ("BinnerScalar_float64", y, -3.0, 3.0, 50)]
+    gv, go, _ = _run(specs, v, o, device=False)
+    ev, eo = _oracle_first([oracle.Binner("scalar", x, vmin=-3, vmax=3, bins=40),
+                            oracle.Binner("scalar", y, vmin=-3, vmax=3, bins=50)], v, o)
+    np.testing.assert_array_equal(go, eo)
+    np.testing.assert_array_equal(gv, ev)

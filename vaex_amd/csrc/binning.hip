@@ -517,6 +517,102 @@ __global__ __launch_bounds__(256) void k_first_c(AggDev a, uint64_t cells, uint6
     }
 }
 
+// AggFirst on a small grid (L cells of 12 B of LDS each fit a workgroup): each workgroup
+// keeps, per cell, the smallest order key of its rows and the lowest row holding it -- per
+// 2048-row step, phase 1 lowers the key (a row that lowers it clears the cell's row), phase 2
+// lowers the row among rows holding the key -- and writes its (key, row) cells as partials;
+// k_first_small_fold folds the partials per cell into s_key / s_row (global rows) for
+// k_first_c.  No per-row global atomics (the generic k_first_a/b contend on few cells).
+constexpr int FS_THREADS = 256, FS_RPT = 8;
+template <typename T>
+__global__ __launch_bounds__(FS_THREADS) void k_first_small(AggDev a, const uint16_t *cells, uint64_t n, uint32_t L,
+                                                            unsigned long long *pkey, uint32_t *prow) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    unsigned long long *lkey = reinterpret_cast<unsigned long long *>(lds_raw);
+    uint32_t *lrow = reinterpret_cast<uint32_t *>(lkey + L);
+    for (uint32_t c = threadIdx.x; c < L; c += FS_THREADS) {
+        lkey[c] = ~0ull;
+        lrow[c] = ~0u;
+    }
+    __syncthreads();
+    // workgroup w takes steps w, w + W, ... of FS_THREADS * FS_RPT rows (uniform trip count)
+    constexpr uint64_t STEP = (uint64_t)FS_THREADS * FS_RPT;
+    for (uint64_t b0 = blockIdx.x * STEP; b0 < n; b0 += (uint64_t)gridDim.x * STEP) {
+        uint32_t cl[FS_RPT];
+        unsigned long long kk[FS_RPT];
+        bool take[FS_RPT];
+#pragma unroll
+        for (int r = 0; r < FS_RPT; r++) {
+            const uint64_t i = b0 + (uint64_t)r * FS_THREADS + threadIdx.x;
+            take[r] = false;
+            cl[r] = 0;
+            kk[r] = ~0ull;
+            if (i < n) {
+                const T v = load_v<T>(a.data, i, a.flip), o = load_v<T>(a.data2, i, a.flip);
+                take[r] = !is_nan_v(v) && !is_nan_v(o);
+                cl[r] = cells[i];
+                kk[r] = order_key(o);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < FS_RPT; r++)
+            if (take[r] && atomicMin(&lkey[cl[r]], kk[r]) > kk[r]) lrow[cl[r]] = ~0u;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < FS_RPT; r++)
+            if (take[r] && kk[r] == lkey[cl[r]]) atomicMin(&lrow[cl[r]], (uint32_t)(b0 + (uint64_t)r * FS_THREADS + threadIdx.x));
+        __syncthreads();
+    }
+    for (uint32_t c = threadIdx.x; c < L; c += FS_THREADS) {
+        pkey[(uint64_t)blockIdx.x * L + c] = lkey[c];
+        prow[(uint64_t)blockIdx.x * L + c] = lrow[c];
+    }
+}
+
+// one workgroup per cell: the lexicographic (key, row) minimum over the W partials
+__global__ __launch_bounds__(256) void k_first_small_fold(const unsigned long long *pkey, const uint32_t *prow, uint32_t W,
+                                                          uint32_t L, uint64_t row0, unsigned long long *s_key,
+                                                          unsigned long long *s_row) {
+    __shared__ unsigned long long sk[4];
+    __shared__ uint32_t sr[4];
+    const uint32_t c = blockIdx.x;
+    unsigned long long bk = ~0ull;
+    uint32_t br = ~0u;
+    for (uint32_t w = threadIdx.x; w < W; w += 256) {
+        const unsigned long long k = pkey[(uint64_t)w * L + c];
+        const uint32_t r = prow[(uint64_t)w * L + c];
+        if (k < bk || (k == bk && r < br)) {
+            bk = k;
+            br = r;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long k = __shfl_xor(bk, off, 64);
+        const uint32_t r = (uint32_t)__shfl_xor((int)br, off, 64);
+        if (k < bk || (k == bk && r < br)) {
+            bk = k;
+            br = r;
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+        sk[threadIdx.x >> 6] = bk;
+        sr[threadIdx.x >> 6] = br;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int q = 1; q < 4; q++)
+            if (sk[q] < bk || (sk[q] == bk && sr[q] < br)) {
+                bk = sk[q];
+                br = sr[q];
+            }
+        if (bk != ~0ull) {
+            s_key[c] = bk;
+            s_row[c] = row0 + br;
+        }
+    }
+}
+
 // ============================================================================
 // device: grid fill / reduce (Aggregator::reduce)
 // ============================================================================
@@ -1654,8 +1750,10 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
             for (int d = 0; d < plan.nb; d++) cells_ok = cells_ok && (plan.b[d].kind == 0 || plan.b[d].kind == 1);
             uint16_t *cells = nullptr;
             uint64_t *idx = nullptr;
+            // AggFirst on a small grid takes the LDS kernels below (no indices)
+            const bool first_lds = cells_ok && len && len < (1ull << 32) && 12 * L <= 96 * 1024;
             for (int k = 0; k < naggs && !idx; k++) {
-                if (tdone[k] || lds_ok(ads[k].kind)) continue;
+                if (tdone[k] || lds_ok(ads[k].kind) || (first_lds && ads[k].kind == VH_AGG_FIRST)) continue;
                 g->ws.idx.ensure(len * 8);
                 idx = g->ws.idx.as<uint64_t>();
                 TimedScope ts("bin_indices");
@@ -1760,6 +1858,32 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
                         for (size_t q = i; q < j; q++) done[pend[q]] = 1;
                     }
                     i = j;
+                }
+            }
+            // AggFirst on a small grid: per-workgroup LDS (key, row) cells + a fold of the
+            // partials (k_first_small / k_first_small_fold), then the usual merge
+            const uint64_t fs_lds = 12 * L;
+            if (first_lds) {
+                for (int k = 0; k < naggs; k++) {
+                    AggDev &ad = ads[k];
+                    if (done[k] || ad.kind != VH_AGG_FIRST) continue;
+                    make_cells();
+                    TimedScope ts("bin_first_lds");
+                    const unsigned W = std::max(1u, std::min<unsigned>(blocks_for(len, FS_THREADS * FS_RPT, 4),
+                                                                       (unsigned)((64ull << 20) / (12 * L))));
+                    g->ws.first_part.ensure((uint64_t)W * L * 12 + 256);
+                    auto *pkey = g->ws.first_part.as<unsigned long long>();
+                    auto *prow = reinterpret_cast<uint32_t *>(pkey + (uint64_t)W * L);
+                    VH_DISPATCH_DTYPE(ad.dtype, T, {
+                        hipLaunchKernelGGL(k_first_small<T>, dim3(W), dim3(FS_THREADS), (size_t)fs_lds, stream(), ad, cells, len,
+                                           (uint32_t)L, pkey, prow);
+                        hipLaunchKernelGGL(k_first_small_fold, dim3((unsigned)L), dim3(256), 0, stream(), pkey, prow, W,
+                                           (uint32_t)L, row0, static_cast<unsigned long long *>(ad.s_key),
+                                           static_cast<unsigned long long *>(ad.s_row));
+                        hipLaunchKernelGGL(k_first_c<T>, dim3(blocks_for(L, 256)), dim3(256), 0, stream(), ad, L, row0);
+                    });
+                    VH_HIP(hipGetLastError());
+                    done[k] = 1;
                 }
             }
             for (int k = 0; k < naggs; k++) {

@@ -179,6 +179,7 @@ struct HostPipe {
 struct Workspace {
     DevBuf idx;                                   // generic path indices1d
     DevBuf cells;                                 // small-grid path: u16 cell per row
+    DevBuf first_part;                            // small-grid AggFirst: per-workgroup (key, row) partials
     HostPipe pipe;                                // host-column staging
     DevBuf tile_entries, tile_values, tile_meta;  // tiled path
     ~Workspace();
