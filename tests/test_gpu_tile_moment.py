@@ -44,10 +44,18 @@ def test_var_std_c2_grid_tile_path(dtype, stat):
     got, timers = _timed(lambda: np.asarray(getattr(df, stat)("w", binby=["x", "y"], limits=lim, shape=1024)))
     assert timers["tile_reduce"] >= 1 and timers["bin_aggregate"] == 0, timers
     bs = [oracle.Binner("scalar", x, vmin=-4, vmax=4, bins=1024), oracle.Binner("scalar", y, vmin=-4, vmax=4, bins=1024)]
-    exp = oracle.extract_central_part(oracle.var_grid(bs, w))
-    if stat == "std":
-        exp = exp ** 0.5
-    np.testing.assert_allclose(got, exp, rtol=1e-6, atol=1e-12, equal_nan=True)
+    var = oracle.extract_central_part(oracle.var_grid(bs, w))
+    if stat == "var":
+        np.testing.assert_allclose(got, var, rtol=1e-6, atol=1e-12, equal_nan=True)
+        return
+    # std = sqrt(m2 / n - mean^2): where the variance is ~0 (one-row cells, equal values) its
+    # rounding residue has either sign, so sqrt is NaN or tiny depending on the summation
+    # order; compare std where the variance is well above the residue
+    ok = np.isfinite(var) & (var > 1e-9)
+    np.testing.assert_allclose(got[ok], var[ok] ** 0.5, rtol=1e-6, atol=1e-12)
+    tiny = np.isfinite(var) & ~ok
+    assert np.all(~np.isfinite(got[tiny]) | (np.abs(got[tiny]) < 1e-4))
+    np.testing.assert_array_equal(np.isnan(var), np.isnan(got) & ~tiny)
 
 
 def test_sum_moment_with_count_sum_and_min_max():
