@@ -1639,7 +1639,14 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
             return;
         }
     }
-    const uint64_t chunk_max = any_host ? (uint64_t(1) << 24) : ((all_fusable || tile_generic) ? length : (uint64_t(1) << 26));
+    // AggFirst alone needs no per-row index buffer (tiled engine on large grids, LDS kernels on
+    // small ones): HBM columns in one chunk, like the tile path (< 2^32 rows per launch)
+    bool first_only = naggs > 0;
+    for (int k = 0; k < naggs; k++) first_only = first_only && aggs[k]->kind == VH_AGG_FIRST;
+    const uint64_t chunk_max = any_host ? (uint64_t(1) << 24)
+                               : (all_fusable || tile_generic) ? length
+                               : first_only ? std::min<uint64_t>(length, (uint64_t(1) << 32) - 4096)
+                                            : (uint64_t(1) << 26);
     HostPipe &pipe = g->ws.pipe;
     if (any_host) {
         pipe.cols.clear();

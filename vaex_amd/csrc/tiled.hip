@@ -1343,6 +1343,98 @@ template <int NV> struct TileRun {
     }
 };
 
+// The per-entry pass B's run form (plans with min / max / moment aggregators): a run of
+// entries of one LDS cell is folded in registers -- per aggregator its count, float sum,
+// integer sum, moment sum, or min / max slot value -- and flushed with one LDS atomic per
+// aggregator, as reduce_entry would apply its entries one by one (same results: counts and
+// integer sums exact, min / max exact, float sums / moments in another association order).
+template <int NV> struct MixRun {
+    uint64_t acc[MAX_FUSED_AGGS];  // count | double sum | uint64 sum | min / max slot bits
+    uint32_t has;                  // bit k: aggregator k took an entry of the run
+    __device__ void clear() {
+        has = 0;
+#pragma unroll
+        for (int k = 0; k < MAX_FUSED_AGGS; k++) acc[k] = 0;
+    }
+    __device__ void add(const FusedAggs &fa, const TileParams &tp, uint32_t fl, const double *v) {
+#pragma unroll
+        for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+            if (k >= fa.na) break;
+            const int kind = fa.a[k].kind;
+            if (kind == VH_AGG_COUNT) {
+                const int cs = tp.cnt_slot[k];
+                bool take = cs == CNT_ALWAYS || (cs == CNT_FLAG && ((fl >> k) & 1));
+#pragma unroll
+                for (int s = 0; s < NV; s++)
+                    if (s == cs) take = v[s] == v[s];
+                if (take) {
+                    acc[k]++;
+                    has |= 1u << k;
+                }
+                continue;
+            }
+            double x = 0.0;
+#pragma unroll
+            for (int s = 0; s < NV; s++)
+                if (s == tp.val_slot[k]) x = v[s];
+            if (kind == VH_AGG_SUM && fa.a[k].vint) {
+                acc[k] += __builtin_bit_cast(uint64_t, x);
+                has |= 1u << k;
+                continue;
+            }
+            const int dt = fa.a[k].dtype;
+            if ((kind == VH_AGG_SUM || kind == VH_AGG_SUM_MOMENT || dt_float(dt)) && x != x) continue;  // NaN
+            if (kind == VH_AGG_SUM || kind == VH_AGG_SUM_MOMENT) {
+                const double t = kind == VH_AGG_SUM ? x : moment_term(x, fa.a[k].moment);
+                acc[k] = __builtin_bit_cast(uint64_t, __builtin_bit_cast(double, acc[k]) + t);
+                has |= 1u << k;
+                continue;
+            }
+            // min / max: keep the better slot value (float as double, signed as int64,
+            // unsigned as uint64 bits)
+            const bool mx = kind == VH_AGG_MAX;
+            const uint64_t xb = __builtin_bit_cast(uint64_t, x);
+            if (!((has >> k) & 1)) {
+                acc[k] = xb;
+            } else {
+                bool better;
+                if (dt_float(dt)) {
+                    const double cur = __builtin_bit_cast(double, acc[k]);
+                    better = mx ? x > cur : x < cur;
+                } else if (dt_signed(dt)) {
+                    better = mx ? (int64_t)xb > (int64_t)acc[k] : (int64_t)xb < (int64_t)acc[k];
+                } else {
+                    better = mx ? xb > acc[k] : xb < acc[k];
+                }
+                if (better) acc[k] = xb;
+            }
+            has |= 1u << k;
+        }
+    }
+    __device__ void flush(const FusedAggs &fa, unsigned char *lds, uint32_t local) const {
+#pragma unroll
+        for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+            if (k >= fa.na) break;
+            if (!((has >> k) & 1)) continue;
+            const int kind = fa.a[k].kind;
+            unsigned char *cell = lds + fa.a[k].lds_off;
+            if (kind == VH_AGG_COUNT) {
+                atomicAdd(reinterpret_cast<uint32_t *>(cell) + local, (uint32_t)acc[k]);
+            } else if (kind == VH_AGG_SUM && fa.a[k].vint) {
+                atomicAdd(reinterpret_cast<unsigned long long *>(cell) + local, (unsigned long long)acc[k]);
+            } else if (kind == VH_AGG_SUM || kind == VH_AGG_SUM_MOMENT) {
+                atomicAdd(reinterpret_cast<double *>(cell) + local, __builtin_bit_cast(double, acc[k]));
+            } else {
+                const double x = __builtin_bit_cast(double, acc[k]);
+                if (mm_cell32(fa.a[k].dtype))
+                    mm_lds32(reinterpret_cast<uint32_t *>(cell) + local, fa.a[k].dtype, kind == VH_AGG_MAX, x);
+                else
+                    mm_lds(reinterpret_cast<uint64_t *>(cell) + local, fa.a[k].dtype, kind == VH_AGG_MAX, x);
+            }
+        }
+    }
+};
+
 constexpr int TB_UNROLL = 8;
 #ifndef VH_TB_VU
 #define VH_TB_VU 0  // 8-entry chunks per lane per step (0 = by NV)
@@ -1499,6 +1591,11 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                 auto chunk = [&](auto jc) {
                     constexpr int j = decltype(jc)::value;
                     const uint32_t words[4] = {ev[j].x, ev[j].y, ev[j].z, ev[j].w};
+                    // runs of one cell (sorted / clustered rows) folded in registers: one LDS
+                    // atomic per aggregator and run (same-address atomics serialise)
+                    MixRun<NV> run;
+                    run.clear();
+                    uint32_t cur = ~0u;
 #pragma unroll
                     for (int x = 0; x < 8; x++) {
                         // a guard, not a break: the loop stays unrolled and vv in registers
@@ -1507,10 +1604,19 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
 #pragma unroll
                             for (int s = 0; s < NV; s++) v[s] = (x & 1) ? vv[j][s][x >> 1].y : vv[j][s][x >> 1].x;
                             const uint32_t local = (words[x >> 1] >> (16 * (x & 1))) & 0xffffu;
-                            if (DBG(tp.debug) & 8) asm volatile("" :: "v"(local));
-                            else reduce_entry<NV, MM>(fa, tp, lds_raw, local, 0xfu, v);
+                            if (DBG(tp.debug) & 8) {
+                                asm volatile("" :: "v"(local));
+                                continue;
+                            }
+                            if (local != cur) {
+                                if (cur != ~0u) run.flush(fa, lds_raw, cur);
+                                cur = local;
+                                run.clear();
+                            }
+                            run.add(fa, tp, 0xfu, v);
                         }
                     }
+                    if (cur != ~0u) run.flush(fa, lds_raw, cur);
                 };
                 static_assert(VU <= 8, "chunks per step");
                 chunk(std::integral_constant<int, 0>{});
