@@ -37,9 +37,9 @@ def submit(fn, *args):
     return _get_pool().submit(fn, *args)
 
 
-def _run(fn, n):
+def _run(fn, n, min_split=MIN_SPLIT):
     """fn(i0, i1) over [0, n) in chunks, on the pool when n is large."""
-    k = min(_threads(), max(1, n // MIN_SPLIT))
+    k = min(_threads(), max(1, n // min_split))
     if k == 1:
         fn(0, n)
         return
@@ -115,9 +115,11 @@ def take(a, idx):
     out = _empty(len(idx), a.dtype)
 
     def part(i0, i1):
-        np.take(a, idx[i0:i1], out=out[i0:i1])
+        # mode 'clip': numpy buffers `out` under the default mode='raise' (the indices are a
+        # permutation, in range)
+        np.take(a, idx[i0:i1], out=out[i0:i1], mode="clip")
 
-    _run(part, len(idx))
+    _run(part, len(idx), MIN_SPLIT // 8)  # random gathers: latency-bound, every thread helps
     return out
 
 
