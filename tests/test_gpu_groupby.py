@@ -162,9 +162,8 @@ def test_set_ordinal_grid_through_hash_aggregation(kdtype, spread):
     grid is filled by the fused hash aggregation (per-key totals added at each key's
     ordinal cell, hashagg_bin_set_ordinal) -- groups in first-appearance order, counts
     exact, sums within 1e-6, NaN values skipped by sum and count(v), keys of every width
-    including negative 1- and 2-byte keys (sign- vs zero-extended bits).  spread 1: a dense
-    key range (the grid route + vh_dense_first_order); spread 1000 on >= 4-byte keys: a sparse
-    range (the hash aggregation + vh_hashagg_order_first)."""
+    including negative 1- and 2-byte keys (sign- vs zero-extended bits); dense (spread 1) and
+    sparse (spread 1000, >= 4-byte keys) key ranges."""
     import vaex_amd
     from vaex_amd.device import DeviceArray
     rng = np.random.default_rng(21)

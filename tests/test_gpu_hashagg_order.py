@@ -154,8 +154,9 @@ def test_order_first_wave_straddling_the_grid_stride():
     np.testing.assert_array_equal(hk, exp)
     np.testing.assert_array_equal(hc, cnt[np.searchsorted(u, exp)])
     # ... and the dense-range grid route's (k_dense_first), through groupby(assume_sparse=True)
+    # with an aggregator the hash aggregation does not carry (min)
     df = vaex_amd.from_arrays(key=dkeys, v=DeviceArray.from_numpy(np.ones(n)))
-    got = df.groupby("key", agg={"n": vaex_amd.agg.count()}, assume_sparse=True)
+    got = df.groupby("key", agg={"n": vaex_amd.agg.count(), "lo": vaex_amd.agg.min("v")}, assume_sparse=True)
     np.testing.assert_array_equal(got["key"].to_numpy(), exp)
     gk = list(got["key"].to_numpy())
     assert gk.index(K) < gk.index(M)

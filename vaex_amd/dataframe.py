@@ -622,12 +622,16 @@ class DataFrame:
                         return res
         if agg is not None and assume_sparse == True and not multikey:  # noqa: E712
             # the ordered_set grouper's result (groups in first-appearance order, or sorted).
-            # An integer key over a dense value range: the BinnerOrdinal grid (any aggregator,
-            # tile path), then the groups ordered by the row their key first appears at
-            # (vh_dense_first_order); otherwise count / sum / mean: one hash-partitioned pass
-            # and the same ordering (hashagg.order_first)
+            # count / sum / mean of an integer key: one hash-partitioned pass, the groups
+            # ordered by the row their key first appears at (hashagg.order_first); other
+            # aggregators over a dense key range: the BinnerOrdinal grid (tile path), then the
+            # same ordering (vh_dense_first_order)
             from .groupby import first_appearance_order
             from .hashagg import eligible_key, try_groupby
+            res = try_groupby(self, by, agg, lambda a, g: parse_actions(self, a, g), sort=sort, row_limit=row_limit,
+                              first_order=not sort)
+            if res is not None:
+                return res
             key = eligible_key(self, by)
             if key is not None and getattr(self.executor, "world", 1) == 1:
                 rng = _dense_range(self, key, speculative=_speculate)
@@ -638,10 +642,6 @@ class DataFrame:
                         return self.groupby(by, agg=agg, sort=sort, assume_sparse=assume_sparse, row_limit=row_limit,
                                             _speculate=False)
                     return res if sort else first_appearance_order(self, key, res)
-            res = try_groupby(self, by, agg, lambda a, g: parse_actions(self, a, g), sort=sort, row_limit=row_limit,
-                              first_order=not sort)
-            if res is not None:
-                return res
         groupby = GroupBy(self, by=by, sort=sort, row_limit=row_limit,
                           dense=assume_sparse != True or multikey,  # noqa: E712
                           dense_ranges=dense_ranges)
