@@ -1512,7 +1512,7 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
         __syncthreads();
     }
     if (!tp.flags_mode) {
-        constexpr int VU = tb_vu<NV>();
+        constexpr int VU = MM ? 1 : tb_vu<NV>();  // the run form of min / max / moment plans: one chunk per lane (128 VGPRs at 1024 threads)
         const uint32_t C = s_pre[nw];
         const uint16_t *ent16 = reinterpret_cast<const uint16_t *>(tp.entries);
         const uint64_t toff_t = tp.toff[t];
