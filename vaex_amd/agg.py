@@ -205,12 +205,10 @@ class AggregatorDescriptorVar(AggregatorDescriptorMulti):
 
         @delayed
         def finish(sum_moment, sum, count):
-            sum = np.array(sum, dtype=np.float64)
-            with np.errstate(divide="ignore", invalid="ignore"):
-                mean = sum / count
-                raw_moments2 = np.asarray(sum_moment, dtype=np.float64) / count
-                variance = raw_moments2 - mean ** 2
-            return self.finish(variance)
+            # sum_moment / count - (sum / count) ** 2 element-wise over host threads (the
+            # reference's numpy expression, agg.py:207-213, bit for bit)
+            from . import hostops
+            return self.finish(hostops.variance(sum_moment, sum, count))
 
         return [task_sum_moment, task_sum, task_count], finish(task_sum_moment, task_sum, task_count)
 

@@ -12,16 +12,17 @@
 //   sample  -- per-tile row fractions from ~1M evenly spaced rows (4096 cells per tile)
 //   pass A  -- batches of 4096 rows dealt round-robin to the workgroups; a row's cell, its
 //              order key (order_key: order-preserving u64) and its row are ranked per tile in
-//              LDS, counting-sorted, and streamed as runs into per-(XCD, tile) streams: each
-//              run is reserved with one atomic per (tile, batch) by the tile's rank-0 row, so
-//              the runs of all workgroups of one XCD abut and their partial lines meet in that
-//              XCD's L2 (scripts/bw_probe4.hip: 3.77 ms against 4.70 for private per-workgroup
-//              regions at 256 tiles).  2 + 8 + 4 bytes per row.
-//   pass B  -- unit = (tile, XCD stream, slice) + a slice of the tile's spill area: per
-//              8192-entry step, phase 1 lowers the LDS order key of each cell (a row that
-//              lowers it resets the cell's row), phase 2 lowers the cell's row among entries
-//              equal to the key; the unit's (key, row) per touched cell is merged with a global
-//              atomicMin of s_key, and appended to a resolve list when it may win.
+//              LDS, counting-sorted, and streamed as runs into per-(workgroup, tile) regions
+//              sized from the sample (tiled.hip's layout; a run past its region reserves the
+//              tile's spill area).  2 + 8 + 4 bytes per row.  (Per-(XCD, tile) streams with
+//              one reservation atomic per tile and batch were tried: the returning atomics
+//              cost 4.5 of 17 ms of pass A at 1e9 rows.)
+//   pass B  -- unit = (tile, range of pass-A workgroups) + a slice of the tile's spill area,
+//              read as one stream of 8-entry chunks: per 8192-entry step, phase 1 lowers the
+//              LDS order key of each cell (a row that lowers it resets the cell's row), phase
+//              2 lowers the cell's row among entries equal to the key; the unit's (key, row)
+//              per touched cell is merged with a global atomicMin of s_key, and appended to a
+//              resolve list when it may win.
 //   resolve -- list entries whose key equals the final s_key lower s_row (global rows).
 // Rows past a stream and its spill area (sampling miss) go to s_key + the list directly; a
 // full list sets a flag and the chunk is redone by the generic path (s_key / s_row reset).
@@ -47,12 +48,12 @@ constexpr uint32_t TF_MAX_TILES = 2048;
 constexpr int TF_SAMPLE_BLOCKS = 512;
 
 struct FirstParams {
-    uint32_t T, NX, s_log2, pad;
+    uint32_t T, W, s_log2, pad;
     uint64_t n, cells;
-    const uint32_t *cap;          // [T] stream capacity of (xcd, t), the same for every xcd; multiple of 8
-    const uint32_t *toff;         // [T] stream offset inside an xcd block; multiple of 8
-    uint64_t xstride;             // entries of one xcd block
-    uint32_t *sfill;              // [NX * T] entries reserved (may exceed cap)
+    const uint32_t *cap;          // [T] region capacity of (workgroup, t), the same for every workgroup; multiple of 8
+    const uint32_t *toff;         // [T] region offset inside a workgroup's block; multiple of 8
+    uint64_t xstride;             // entries of one workgroup's block
+    uint32_t *sfill;              // [W * T] entries produced per (workgroup, tile) (may exceed cap)
     uint32_t *spill_fill;         // [T]
     const uint32_t *spill_cap;    // [T]
     const uint64_t *spill_start;  // [T] relative to spill_base
@@ -65,6 +66,7 @@ struct FirstParams {
     unsigned long long *list_fill;
     uint64_t list_cap;
     unsigned *flag;  // list overflow: the host redoes the chunk on the generic path
+    uint32_t debug;  // ablation build only (VH_FIRST_DEBUG): 1 = no stream reservation atomics
 };
 
 template <int ND> __device__ __forceinline__ uint64_t tf_cell(const BinPlan &p, uint64_t i) {
@@ -110,7 +112,7 @@ __global__ __launch_bounds__(TF_THREADS) void k_first_sample(BinPlan p, uint64_t
 }
 
 // pass A (see the file comment).  LDS: staged keys u32 | order keys u64 | rows u32 (one batch)
-// | per tile: hist, hcnt, boff, sbase, soff, cap, toff
+// | per tile: hist, boff, sbase, soff, fill, cap, toff
 template <int ND, typename T>
 __global__ __launch_bounds__(TF_THREADS) void k_first_scatter(BinPlan p, AggDev a, FirstParams fp) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
@@ -120,17 +122,14 @@ __global__ __launch_bounds__(TF_THREADS) void k_first_scatter(BinPlan p, AggDev 
     uint32_t *skey = reinterpret_cast<uint32_t *>(sokey + TF_BATCH);
     uint32_t *srow = skey + TF_BATCH;
     uint32_t *hist = srow + TF_BATCH;
-    uint32_t *hcnt = hist + NT, *boff = hcnt + NT, *sbase = boff + NT, *soff = sbase + NT, *cap = soff + NT, *toff = cap + NT;
+    uint32_t *boff = hist + NT, *sbase = boff + NT, *soff = sbase + NT, *fill = soff + NT, *cap = fill + NT, *toff = cap + NT;
     for (uint32_t t = threadIdx.x; t < NT; t += TF_THREADS) {
         hist[t] = 0;
+        fill[t] = 0;
         cap[t] = fp.cap[t];
         toff[t] = fp.toff[t];
     }
-    unsigned xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    const uint32_t x = xcc % fp.NX;
-    const uint64_t xblock = (uint64_t)x * fp.xstride;
-    uint32_t *sfill = fp.sfill + (uint64_t)x * NT;
+    const uint64_t wblock = (uint64_t)blockIdx.x * fp.xstride;
     const uint32_t smask = (1u << fp.s_log2) - 1;
     const int lane = threadIdx.x & 63;
     __syncthreads();
@@ -158,7 +157,9 @@ __global__ __launch_bounds__(TF_THREADS) void k_first_scatter(BinPlan p, AggDev 
             key[r] = (t << 16) | ((uint32_t)c & smask);
             rank[r] = wave_rank(hist, t, keep);
         }
-        // B1: every rank taken -> wave 0 scans the histogram (and clears it for the next batch)
+        // B1: every rank taken -> wave 0 scans the histogram (clearing it for the next batch)
+        // and advances this workgroup's regions; a run past a region's capacity reserves the
+        // excess in the tile's spill area
         tf_lds_barrier();
         if (threadIdx.x < 64) {
             const uint32_t per = (NT + 63) / 64, t0 = lane * per;
@@ -172,36 +173,30 @@ __global__ __launch_bounds__(TF_THREADS) void k_first_scatter(BinPlan p, AggDev 
             }
             uint32_t acc = inc - s;
             for (uint32_t t = t0; t < t0 + per && t < NT; t++) {
-                const uint32_t h = hist[t];
+                const uint32_t h = hist[t], b = fill[t], c = cap[t];
                 boff[t] = acc;
-                hcnt[t] = h;
+                sbase[t] = b;
+                fill[t] = b + h;
                 hist[t] = 0;
                 acc += h;
+                if (b + h > c) {
+                    const uint32_t first = max(b, c);
+                    soff[t] = atomicAdd(&fp.spill_fill[t], b + h - first) - first;
+                }
             }
             if (lane == 63) s_tot = inc;
         }
-        // B2: rows stage at their sorted positions; a tile's rank-0 row reserves the tile's run
-        // in this XCD's stream (and past its capacity, in the tile's spill area)
+        // B2: rows stage at their sorted positions
         tf_lds_barrier();
 #pragma unroll
         for (int r = 0; r < TF_RPT; r++) {
             if (rank[r] < 0) continue;
-            const uint32_t t = key[r] >> 16;
-            const uint32_t pos = boff[t] + (uint32_t)rank[r];
+            const uint32_t pos = boff[key[r] >> 16] + (uint32_t)rank[r];
             skey[pos] = key[r];
             sokey[pos] = ok[r];
             srow[pos] = (uint32_t)(b0 + (uint64_t)r * TF_THREADS + threadIdx.x);
-            if (rank[r] == 0) {
-                const uint32_t h = hcnt[t], c = cap[t];
-                const uint32_t old = atomicAdd(&sfill[t], h);
-                sbase[t] = old;
-                if (old + h > c) {
-                    const uint32_t first = max(old, c);
-                    soff[t] = atomicAdd(&fp.spill_fill[t], old + h - first) - first;
-                }
-            }
         }
-        // B3: the sorted runs stream out
+        // B3: the sorted runs stream out to the regions
         tf_lds_barrier();
         const uint32_t tot = s_tot;
         for (uint32_t k = threadIdx.x; k < tot; k += TF_THREADS) {
@@ -210,11 +205,11 @@ __global__ __launch_bounds__(TF_THREADS) void k_first_scatter(BinPlan p, AggDev 
             const uint32_t d = sbase[t] + (k - boff[t]);
             uint64_t e;
             if (d < cap[t]) {
-                e = xblock + toff[t] + d;
+                e = wblock + toff[t] + d;
             } else {
                 const uint32_t si = d + soff[t];
                 if (si >= fp.spill_cap[t]) {
-                    // past the stream and the spill area: straight to s_key and the list
+                    // past the region and the spill area: straight to s_key and the list
                     const uint32_t c = (t << fp.s_log2) | (kk & 0xffffu);
                     atomicMin(&fp.s_key[c], sokey[k]);
                     tf_list_push(fp, atomicAdd(fp.list_fill, 1ull), c, srow[k], sokey[k]);
@@ -227,17 +222,23 @@ __global__ __launch_bounds__(TF_THREADS) void k_first_scatter(BinPlan p, AggDev 
             fp.erow[e] = srow[k];
         }
     }
+    tf_lds_barrier();
+    for (uint32_t t = threadIdx.x; t < NT; t += TF_THREADS) fp.sfill[(uint64_t)blockIdx.x * NT + t] = fill[t];
 }
 
 struct FirstUnit {
-    uint32_t tile, xcd, part, parts;
+    uint32_t tile, w0, w1, parts;  // parts: slice (low 16 bits) of parts (high 16) of the spill area
 };
 
-// pass B (see the file comment)
+// pass B (see the file comment): the unit's regions (pass-A workgroups w0 .. w1 - 1) and its
+// slice of the tile's spill area, read as one flat stream of 8-entry chunks (prefix sums of
+// the region fills in LDS)
 __global__ __launch_bounds__(TFB_THREADS) void k_first_reduce(FirstParams fp, const FirstUnit *units) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
     __shared__ uint32_t s_w[TFB_THREADS / 64];
     __shared__ unsigned long long s_base;
+    __shared__ uint32_t s_fill[1024 + 1];
+    __shared__ uint32_t s_pre[1024 + 2];
     const uint32_t S = 1u << fp.s_log2;
     unsigned long long *lkey = reinterpret_cast<unsigned long long *>(lds_raw);
     uint32_t *lrow = reinterpret_cast<uint32_t *>(lkey + S);
@@ -247,29 +248,45 @@ __global__ __launch_bounds__(TFB_THREADS) void k_first_reduce(FirstParams fp, co
         lkey[i] = ~0ull;
         lrow[i] = ~0u;
     }
-    // this unit: slice `part` of `parts` of stream (xcd, t), and slice xcd * parts + part of
-    // NX * parts of the tile's spill area (slice bounds at multiples of 8 entries)
-    const uint32_t F = min(fp.sfill[(uint64_t)u.xcd * fp.T + t], fp.cap[t]);
-    const uint32_t a0 = u.part == 0 ? 0u : (uint32_t)((uint64_t)F * u.part / u.parts) & ~7u;
-    const uint32_t a1 = u.part + 1 == u.parts ? F : (uint32_t)((uint64_t)F * (u.part + 1) / u.parts) & ~7u;
+    const uint32_t part = u.parts & 0xffffu, parts = u.parts >> 16;
     const uint32_t SF = min(fp.spill_fill[t], fp.spill_cap[t]);
-    const uint32_t P = fp.NX * u.parts, idx = u.xcd * u.parts + u.part;
-    const uint32_t q0 = idx == 0 ? 0u : (uint32_t)((uint64_t)SF * idx / P) & ~7u;
-    const uint32_t q1 = idx + 1 == P ? SF : (uint32_t)((uint64_t)SF * (idx + 1) / P) & ~7u;
-    const uint64_t eA = (uint64_t)u.xcd * fp.xstride + fp.toff[t] + a0, eB = fp.spill_base + fp.spill_start[t] + q0;
-    const uint32_t nA = a1 > a0 ? a1 - a0 : 0u, nB = q1 > q0 ? q1 - q0 : 0u;
-    const uint32_t CA = (nA + 7) / 8, C = CA + (nB + 7) / 8;
+    const uint32_t q0 = part == 0 ? 0u : (uint32_t)((uint64_t)SF * part / parts) & ~7u;
+    const uint32_t q1 = part + 1 >= parts ? SF : (uint32_t)((uint64_t)SF * (part + 1) / parts) & ~7u;
+    const uint64_t eB = fp.spill_base + fp.spill_start[t] + q0;
+    const uint32_t nwr = u.w1 - u.w0, nw = nwr + 1, cap_t = fp.cap[t];
+    for (uint32_t k = threadIdx.x; k < nw; k += TFB_THREADS)
+        s_fill[k] = k < nwr ? min(fp.sfill[(uint64_t)(u.w0 + k) * fp.T + t], cap_t) : (q1 > q0 ? q1 - q0 : 0u);
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of the chunk counts
+        const uint32_t lane = threadIdx.x, per = (nw + 63) / 64, k0 = lane * per;
+        uint32_t sum = 0;
+        for (uint32_t k = k0; k < k0 + per && k < nw; k++) sum += (s_fill[k] + 7) >> 3;
+        uint32_t inc = sum;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(inc, off, 64);
+            if ((int)lane >= off) inc += y;
+        }
+        uint32_t acc = inc - sum;
+        for (uint32_t k = k0; k < k0 + per && k < nw; k++) {
+            s_pre[k] = acc;
+            acc += (s_fill[k] + 7) >> 3;
+        }
+        if (lane == 63) s_pre[nw] = inc;
+    }
+    __syncthreads();
+    const uint32_t C = s_pre[nw];
+    const uint64_t toff_t = fp.toff[t];
+    uint32_t kk = 0;  // region of this lane's current chunk (chunk indices of a lane only grow)
     __syncthreads();
     for (uint32_t c0 = 0; c0 < C; c0 += TFB_THREADS) {  // uniform trip count: barriers inside
         const uint32_t c = c0 + threadIdx.x;
         uint32_t rem = 0;
         uint64_t e = 0;
-        if (c < CA) {
-            e = eA + 8ull * c;
-            rem = min(8u, nA - 8 * c);
-        } else if (c < C) {
-            e = eB + 8ull * (c - CA);
-            rem = min(8u, nB - 8 * (c - CA));
+        if (c < C) {
+            while (s_pre[kk + 1] <= c) kk++;
+            const uint32_t q = (c - s_pre[kk]) * 8;
+            e = kk < nwr ? (uint64_t)(u.w0 + kk) * fp.xstride + toff_t + q : eB + q;
+            rem = min(8u, s_fill[kk] - q);
         }
         uint4 cw = make_uint4(0, 0, 0, 0), r0 = cw, r1 = cw;
         ulonglong2 k[4] = {};
@@ -383,7 +400,6 @@ bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t
     const uint64_t T64 = (cells + S - 1) / S;
     if (T64 < 2 || T64 > TF_MAX_TILES) return false;
     const uint32_t T = (uint32_t)T64;
-    const uint32_t NX = (uint32_t)std::max(1, std::min(8, cu_count() / 32));
     const int nd = nd_f64 >= 1 && nd_f64 <= 3 ? nd_f64 : 0;
     FirstScratch &ws = first_scratch();
     std::lock_guard<std::mutex> lock(ws.mu);
@@ -404,16 +420,16 @@ bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t
         }
         bpc = it->second;
     }
-    const uint32_t W = (uint32_t)cu_count() * (uint32_t)bpc;
-    // meta: hist (2T u64) | cap | toff | spill_cap (T u32 each) | spill_start (T u64) | sfill
-    // (NX T u32) | spill_fill (T u32) | list_fill | flag | units
+    const uint32_t W = std::min<uint32_t>(1024, (uint32_t)cu_count() * (uint32_t)bpc);
+    // meta: hist (2T u64) | cap | toff | spill_cap (T u32 each) | spill_start (T u64) | fills
+    // (W T u32) | spill_fill (T u32) | list_fill | flag | units
     const uint64_t nb = (n + TF_BATCH - 1) / TF_BATCH;
     const uint64_t sblocks = std::min<uint64_t>(nb, TF_SAMPLE_BLOCKS);
     const uint64_t bstride = std::max<uint64_t>(TF_BATCH, n / sblocks);
     const double target = std::max(1.0, (double)n / ((double)cu_count() * 4));
-    const uint64_t max_units = (uint64_t)NX * T * 64 + 64;
-    const uint64_t meta_bytes = 16 * (uint64_t)T + 4 * 3 * (uint64_t)T + 8 * (uint64_t)T + 4 * (uint64_t)NX * T +
-                                4 * (uint64_t)T + 64 + sizeof(FirstUnit) * max_units + 1024;
+    const uint64_t max_units = (uint64_t)T + 4 * (uint64_t)cu_count() + 16;
+    const uint64_t meta_bytes = 16 * (uint64_t)T + 4 * 3 * (uint64_t)T + 8 * (uint64_t)T + 4 * (uint64_t)W * T +
+                                4 * (uint64_t)T + 64 + sizeof(FirstUnit) * max_units + 4096;
     ws.meta.ensure(meta_bytes);
     char *mb = ws.meta.as<char>();
     auto carve = [&](uint64_t bytes) {
@@ -426,7 +442,7 @@ bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t
     auto *d_toff = reinterpret_cast<uint32_t *>(carve(4 * (uint64_t)T));
     auto *d_scap = reinterpret_cast<uint32_t *>(carve(4 * (uint64_t)T));
     auto *d_sstart = reinterpret_cast<uint64_t *>(carve(8 * (uint64_t)T));
-    auto *d_sfill = reinterpret_cast<uint32_t *>(carve(4 * (uint64_t)NX * T));
+    auto *d_sfill = reinterpret_cast<uint32_t *>(carve(4 * (uint64_t)W * T));
     auto *d_spfill = reinterpret_cast<uint32_t *>(carve(4 * (uint64_t)T));
     auto *d_misc = reinterpret_cast<unsigned long long *>(carve(64));  // [0] list fill, [1] flag
     auto *d_units = reinterpret_cast<FirstUnit *>(carve(sizeof(FirstUnit) * max_units));
@@ -452,13 +468,13 @@ bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t
     uint64_t sampled = 0;
     for (uint32_t t = 0; t < T; t++) sampled += hist[t];
     if (!sampled) return false;
-    // stream capacities per (XCD, tile), sized for the rows one XCD's workgroups take (an
-    // even share plus a batch per workgroup) with Poisson room, one batch of slack (sorted
-    // columns: a tile's batches are dealt over the XCDs +-1), and for clustered tiles (whole
-    // batch-sized blocks in or out, per the sample's spread) four standard deviations of the
-    // XCD's batch count; past a stream, the tile's spill area
-    const double rows_x = (double)n / NX + (double)(W / NX + 1) * TF_BATCH;
-    const double batches_x = rows_x / TF_BATCH;
+    // region capacities per (workgroup, tile) (tiled.hip's plan): workgroup w takes batches
+    // w, w + W, ... so its tile distribution is the global one; Poisson room for shuffled rows,
+    // one batch of slack for clustered tiles (whole batch-sized blocks in or out, per the
+    // sample's spread); past a region, the tile's spill area (for clustered tiles the expected
+    // excess of a workgroup's Poisson batch count over its region, for all workgroups)
+    const uint64_t kbat = (nb + W - 1) / W;
+    const double rows_w = (double)kbat * TF_BATCH;
     std::vector<uint32_t> cap(T), toff(T), scap(T);
     std::vector<uint64_t> sstart(T);
     uint64_t xstride = 0, stotal = 0;
@@ -466,29 +482,38 @@ bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t
         const double p = (double)hist[t] / (double)sampled;
         const double m = (double)hist[t] / (double)sblocks, var_b = std::max(0.0, (double)hist[T + t] / (double)sblocks - m * m);
         const bool clustered = var_b > 4.0 * m + 1.0;
-        const double e = rows_x * p;
-        double c = e * 1.04 + 6.0 * std::sqrt(e + 1.0) + TF_BATCH;
-        if (clustered) c += 4.0 * std::sqrt(batches_x * p + 1.0) * TF_BATCH;
-        const uint64_t ci = std::min<uint64_t>(((uint64_t)c + 7) & ~uint64_t(7), ((uint64_t)rows_x + 7) & ~uint64_t(7));
+        const double e = rows_w * p;
+        const double c = e * 1.04 + 6.0 * std::sqrt(e + 1.0) + 32 + (clustered ? TF_BATCH : 0);
+        const uint64_t ci = std::min<uint64_t>(((uint64_t)c + 7) & ~uint64_t(7), ((uint64_t)rows_w + 15) & ~uint64_t(7));
         cap[t] = (uint32_t)ci;
         toff[t] = (uint32_t)xstride;
         xstride += ci;
-        double sc = 0.02 * (double)n * p + 2.0 * TF_BATCH;
-        if (clustered) sc += 0.25 * (double)n * p;
+        double sc = 0.02 * (double)n * p + TF_BATCH;
+        if (clustered) {
+            const double p_hi = std::min(1.0, p + 2.0 * std::sqrt(p * (1.0 - p) / (double)sblocks));
+            const double lam = (double)kbat * p_hi;
+            double excess = 0.0, pk = std::exp(-lam);
+            for (uint64_t x = 0; x <= kbat && (double)x <= lam + 12.0 * std::sqrt(lam) + 12.0; x++) {
+                if (x) pk *= lam / (double)x;
+                excess += pk * std::max(0.0, (double)x * TF_BATCH - (double)ci);
+            }
+            sc = std::min(1.25 * (double)n * p_hi, 2.0 * (double)W * excess) + 4.0 * TF_BATCH;
+        }
         if (hist[t] == 0) sc = std::min<double>((double)n, (double)bstride) + 2.0 * TF_BATCH;  // a tile the sample missed
-        scap[t] = (uint32_t)std::min<uint64_t>(((uint64_t)sc + 7) & ~uint64_t(7), (n + 7) & ~uint64_t(7));
+        scap[t] = (uint32_t)std::min<uint64_t>(((uint64_t)sc + 7) & ~uint64_t(7), (n + 15) & ~uint64_t(7));
         sstart[t] = stotal;
         stotal += scap[t];
     }
-    if (xstride >= (1ull << 32) - TF_BATCH) return false;
-    const uint64_t total = (uint64_t)NX * xstride + stotal + 16;
-    // pass-B units: each (XCD stream, tile) split by its expected entries
+    if (xstride >= (1ull << 32) - TF_BATCH || stotal >= (1ull << 32)) return false;
+    const uint64_t total = (uint64_t)W * xstride + stotal + 16;
+    // pass-B units: tiles split over ranges of pass-A workgroups by expected entries; unit k
+    // of g of a tile also reads slice k of g of the tile's spill area
     std::vector<FirstUnit> units;
     for (uint32_t t = 0; t < T; t++) {
-        const double e = (double)n * (double)hist[t] / (double)sampled / NX;
-        const uint32_t g = (uint32_t)std::min(64.0, std::max(1.0, std::ceil(e / target)));
-        for (uint32_t x = 0; x < NX; x++)
-            for (uint32_t k = 0; k < g; k++) units.push_back({t, x, k, g});
+        const double e = (double)n * (double)hist[t] / (double)sampled;
+        const uint32_t g = (uint32_t)std::min<double>(W, std::max(1.0, std::ceil(e / target)));
+        for (uint32_t k = 0; k < g; k++)
+            units.push_back({t, (uint32_t)((uint64_t)W * k / g), (uint32_t)((uint64_t)W * (k + 1) / g), k | (g << 16)});
     }
     if (units.size() > max_units) return false;
     const uint64_t list_cap = (uint64_t)units.size() * S + (1u << 20);
@@ -507,12 +532,12 @@ bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t
     upload(d_scap, scap.data(), 4 * (uint64_t)T);
     upload(d_sstart, sstart.data(), 8 * (uint64_t)T);
     upload(d_units, units.data(), sizeof(FirstUnit) * units.size());
-    VH_HIP(hipMemsetAsync(d_sfill, 0, 4 * (uint64_t)NX * T, st));
+    VH_HIP(hipMemsetAsync(d_sfill, 0, 4 * (uint64_t)W * T, st));
     VH_HIP(hipMemsetAsync(d_spfill, 0, 4 * (uint64_t)T, st));
     VH_HIP(hipMemsetAsync(d_misc, 0, 64, st));
     FirstParams fp{};
     fp.T = T;
-    fp.NX = NX;
+    fp.W = W;
     fp.s_log2 = s_log2;
     fp.n = n;
     fp.cells = cells;
@@ -523,7 +548,7 @@ bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t
     fp.spill_fill = d_spfill;
     fp.spill_cap = d_scap;
     fp.spill_start = d_sstart;
-    fp.spill_base = (uint64_t)NX * xstride;
+    fp.spill_base = (uint64_t)W * xstride;
     fp.ecell = ws.ecell.as<uint16_t>();
     fp.eokey = ws.eokey.as<unsigned long long>();
     fp.erow = ws.erow.as<uint32_t>();
@@ -533,6 +558,9 @@ bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t
     fp.list_fill = d_misc;
     fp.list_cap = list_cap;
     fp.flag = reinterpret_cast<unsigned *>(d_misc + 1);
+#ifdef VH_ABLATION
+    if (const char *dbg = getenv("VH_FIRST_DEBUG")) fp.debug = (uint32_t)atoi(dbg);
+#endif
     {
         TimedScope ts("first_scatter");
         switch (nd) {

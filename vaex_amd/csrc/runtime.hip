@@ -639,6 +639,31 @@ int vh_device_cache_trim(void) {
     VH_API_END
 }
 
+/* dst[i] = src[idx[i]] for i < n items of `itemsize` bytes, on up to `threads` host threads
+ * (the permutation of a groupby's result columns into first-appearance order; numpy's take
+ * holds the interpreter lock) */
+int vh_host_take(void *dst, const void *src, const int64_t *idx, uint64_t n, int itemsize, int threads) {
+    VH_API_BEGIN
+    if (itemsize != 1 && itemsize != 2 && itemsize != 4 && itemsize != 8) fail(VH_ERR_ARG, "vh_host_take: itemsize");
+    auto part = [=](uint64_t i0, uint64_t i1) {
+        switch (itemsize) {
+        case 8: for (uint64_t i = i0; i < i1; i++) static_cast<uint64_t *>(dst)[i] = static_cast<const uint64_t *>(src)[idx[i]]; break;
+        case 4: for (uint64_t i = i0; i < i1; i++) static_cast<uint32_t *>(dst)[i] = static_cast<const uint32_t *>(src)[idx[i]]; break;
+        case 2: for (uint64_t i = i0; i < i1; i++) static_cast<uint16_t *>(dst)[i] = static_cast<const uint16_t *>(src)[idx[i]]; break;
+        default: for (uint64_t i = i0; i < i1; i++) static_cast<uint8_t *>(dst)[i] = static_cast<const uint8_t *>(src)[idx[i]];
+        }
+    };
+    const int t = (int)std::min<uint64_t>((uint64_t)std::max(1, threads), std::max<uint64_t>(1, n / 65536));
+    if (t <= 1) {
+        part(0, n);
+    } else {
+        std::vector<std::thread> pool;
+        for (int k = 0; k < t; k++) pool.emplace_back(part, n * k / t, n * (k + 1) / t);
+        for (auto &th : pool) th.join();
+    }
+    VH_API_END
+}
+
 int vh_host_register(void *ptr, uint64_t bytes) {
     VH_API_BEGIN
     if (!ptr || !bytes) fail(VH_ERR_ARG, "vh_host_register: empty range");

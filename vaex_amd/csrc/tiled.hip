@@ -109,6 +109,9 @@ struct TileParams {
     // typed grid afterwards by k_mm_merge (a CAS per cell on 1- and 2-byte grids serialised
     // on the shared words)
     void *mmtmp[MAX_FUSED_AGGS];
+    // run form of pass B with min / max / moment: per value slot its min / max encoding (2 bits:
+    // 0 float, 1 signed, 2 unsigned); mgeneric: a moment other than 2 (per-entry form)
+    uint32_t skind, mgeneric;
 };
 
 // value of row h (0/1) of a loaded pair of a column of dtype dt, as the 8-byte slot pass A
@@ -1293,10 +1296,15 @@ __device__ inline void reduce_entry(const FusedAggs &fa, const TileParams &tp, u
 
 // a run of entries of one LDS cell (count / sum aggregators): entries, and per value slot
 // the non-NaN count, the float sum of non-NaN values and the 64-bit integer sum
-template <int NV> struct TileRun {
+// X: the plan also has min / max and moment-2 aggregators (var / std): per value slot the
+// run's sum of squares and min / max in an order-preserving u64 form (float: ord_bits, NaN
+// skipped; signed: bits ^ 2^63; unsigned: bits) -- skind packs each slot's form (2 bits)
+template <int NV, bool X = false> struct TileRun {
     uint32_t cnt, nn[NV > 0 ? NV : 1];
     double sum[NV > 0 ? NV : 1];
     unsigned long long isum[NV > 0 ? NV : 1];
+    double sum2[X && NV > 0 ? NV : 1];
+    uint64_t mn[X && NV > 0 ? NV : 1], mx[X && NV > 0 ? NV : 1];
     __device__ void clear() {
         cnt = 0;
 #pragma unroll
@@ -1304,9 +1312,14 @@ template <int NV> struct TileRun {
             nn[s] = 0;
             sum[s] = 0.0;
             isum[s] = 0;
+            if constexpr (X) {
+                sum2[s] = 0.0;
+                mn[s] = ~0ull;
+                mx[s] = 0;
+            }
         }
     }
-    __device__ void add(const TileParams &, const double *v) {
+    __device__ void add(const TileParams &tp, const double *v) {
         cnt++;
 #pragma unroll
         for (int s = 0; s < NV; s++) {
@@ -1314,6 +1327,15 @@ template <int NV> struct TileRun {
             if (v[s] == v[s]) {
                 nn[s]++;
                 sum[s] += v[s];
+                if constexpr (X) sum2[s] += v[s] * v[s];
+            }
+            if constexpr (X) {
+                const uint32_t code = (tp.skind >> (2 * s)) & 3u;
+                const uint64_t b = __builtin_bit_cast(uint64_t, v[s]);
+                if (code == 0 && v[s] != v[s]) continue;
+                const uint64_t e = code == 0 ? ord_bits(v[s]) : code == 1 ? b ^ (1ull << 63) : b;
+                mn[s] = e < mn[s] ? e : mn[s];
+                mx[s] = e > mx[s] ? e : mx[s];
             }
         }
     }
@@ -1322,114 +1344,41 @@ template <int NV> struct TileRun {
 #pragma unroll
         for (int k = 0; k < MAX_FUSED_AGGS; k++) {
             if (k >= fa.na) break;
-            if (fa.a[k].kind == VH_AGG_COUNT) {
+            const int kind = fa.a[k].kind;
+            if (kind == VH_AGG_COUNT) {
                 const int cs = tp.cnt_slot[k];
                 uint32_t c = cs == CNT_ALWAYS || cs == CNT_FLAG ? cnt : 0u;
 #pragma unroll
                 for (int s = 0; s < NV; s++)
                     if (s == cs) c = nn[s];
                 if (c) atomicAdd(reinterpret_cast<uint32_t *>(lds + fa.a[k].lds_off) + local, c);
-            } else {
-#pragma unroll
-                for (int s = 0; s < NV; s++) {
-                    if (s != tp.val_slot[k]) continue;
-                    if (fa.a[k].vint)
-                        atomicAdd(reinterpret_cast<unsigned long long *>(lds + fa.a[k].lds_off) + local, isum[s]);
-                    else if (nn[s])
-                        atomicAdd(reinterpret_cast<double *>(lds + fa.a[k].lds_off) + local, sum[s]);
-                }
-            }
-        }
-    }
-};
-
-// The per-entry pass B's run form (plans with min / max / moment aggregators): a run of
-// entries of one LDS cell is folded in registers -- per aggregator its count, float sum,
-// integer sum, moment sum, or min / max slot value -- and flushed with one LDS atomic per
-// aggregator, as reduce_entry would apply its entries one by one (same results: counts and
-// integer sums exact, min / max exact, float sums / moments in another association order).
-template <int NV> struct MixRun {
-    uint64_t acc[MAX_FUSED_AGGS];  // count | double sum | uint64 sum | min / max slot bits
-    uint32_t has;                  // bit k: aggregator k took an entry of the run
-    __device__ void clear() {
-        has = 0;
-#pragma unroll
-        for (int k = 0; k < MAX_FUSED_AGGS; k++) acc[k] = 0;
-    }
-    __device__ void add(const FusedAggs &fa, const TileParams &tp, uint32_t fl, const double *v) {
-#pragma unroll
-        for (int k = 0; k < MAX_FUSED_AGGS; k++) {
-            if (k >= fa.na) break;
-            const int kind = fa.a[k].kind;
-            if (kind == VH_AGG_COUNT) {
-                const int cs = tp.cnt_slot[k];
-                bool take = cs == CNT_ALWAYS || (cs == CNT_FLAG && ((fl >> k) & 1));
-#pragma unroll
-                for (int s = 0; s < NV; s++)
-                    if (s == cs) take = v[s] == v[s];
-                if (take) {
-                    acc[k]++;
-                    has |= 1u << k;
-                }
                 continue;
             }
-            double x = 0.0;
 #pragma unroll
-            for (int s = 0; s < NV; s++)
-                if (s == tp.val_slot[k]) x = v[s];
-            if (kind == VH_AGG_SUM && fa.a[k].vint) {
-                acc[k] += __builtin_bit_cast(uint64_t, x);
-                has |= 1u << k;
-                continue;
-            }
-            const int dt = fa.a[k].dtype;
-            if ((kind == VH_AGG_SUM || kind == VH_AGG_SUM_MOMENT || dt_float(dt)) && x != x) continue;  // NaN
-            if (kind == VH_AGG_SUM || kind == VH_AGG_SUM_MOMENT) {
-                const double t = kind == VH_AGG_SUM ? x : moment_term(x, fa.a[k].moment);
-                acc[k] = __builtin_bit_cast(uint64_t, __builtin_bit_cast(double, acc[k]) + t);
-                has |= 1u << k;
-                continue;
-            }
-            // min / max: keep the better slot value (float as double, signed as int64,
-            // unsigned as uint64 bits)
-            const bool mx = kind == VH_AGG_MAX;
-            const uint64_t xb = __builtin_bit_cast(uint64_t, x);
-            if (!((has >> k) & 1)) {
-                acc[k] = xb;
-            } else {
-                bool better;
-                if (dt_float(dt)) {
-                    const double cur = __builtin_bit_cast(double, acc[k]);
-                    better = mx ? x > cur : x < cur;
-                } else if (dt_signed(dt)) {
-                    better = mx ? (int64_t)xb > (int64_t)acc[k] : (int64_t)xb < (int64_t)acc[k];
-                } else {
-                    better = mx ? xb > acc[k] : xb < acc[k];
+            for (int s = 0; s < NV; s++) {
+                if (s != tp.val_slot[k]) continue;
+                if constexpr (X) {
+                    if (kind == VH_AGG_SUM_MOMENT) {
+                        if (nn[s]) atomicAdd(reinterpret_cast<double *>(lds + fa.a[k].lds_off) + local, sum2[s]);
+                        continue;
+                    }
+                    if (is_minmax(kind)) {
+                        const uint32_t code = (tp.skind >> (2 * s)) & 3u;
+                        if (code == 0 ? nn[s] == 0 : cnt == 0) continue;
+                        const bool m = kind == VH_AGG_MAX;
+                        const uint64_t e = m ? mx[s] : mn[s];
+                        const double x = code == 0 ? unord_bits(e) : __builtin_bit_cast(double, code == 1 ? e ^ (1ull << 63) : e);
+                        if (mm_cell32(fa.a[k].dtype))
+                            mm_lds32(reinterpret_cast<uint32_t *>(lds + fa.a[k].lds_off) + local, fa.a[k].dtype, m, x);
+                        else
+                            mm_lds(reinterpret_cast<uint64_t *>(lds + fa.a[k].lds_off) + local, fa.a[k].dtype, m, x);
+                        continue;
+                    }
                 }
-                if (better) acc[k] = xb;
-            }
-            has |= 1u << k;
-        }
-    }
-    __device__ void flush(const FusedAggs &fa, unsigned char *lds, uint32_t local) const {
-#pragma unroll
-        for (int k = 0; k < MAX_FUSED_AGGS; k++) {
-            if (k >= fa.na) break;
-            if (!((has >> k) & 1)) continue;
-            const int kind = fa.a[k].kind;
-            unsigned char *cell = lds + fa.a[k].lds_off;
-            if (kind == VH_AGG_COUNT) {
-                atomicAdd(reinterpret_cast<uint32_t *>(cell) + local, (uint32_t)acc[k]);
-            } else if (kind == VH_AGG_SUM && fa.a[k].vint) {
-                atomicAdd(reinterpret_cast<unsigned long long *>(cell) + local, (unsigned long long)acc[k]);
-            } else if (kind == VH_AGG_SUM || kind == VH_AGG_SUM_MOMENT) {
-                atomicAdd(reinterpret_cast<double *>(cell) + local, __builtin_bit_cast(double, acc[k]));
-            } else {
-                const double x = __builtin_bit_cast(double, acc[k]);
-                if (mm_cell32(fa.a[k].dtype))
-                    mm_lds32(reinterpret_cast<uint32_t *>(cell) + local, fa.a[k].dtype, kind == VH_AGG_MAX, x);
-                else
-                    mm_lds(reinterpret_cast<uint64_t *>(cell) + local, fa.a[k].dtype, kind == VH_AGG_MAX, x);
+                if (fa.a[k].vint)
+                    atomicAdd(reinterpret_cast<unsigned long long *>(lds + fa.a[k].lds_off) + local, isum[s]);
+                else if (nn[s])
+                    atomicAdd(reinterpret_cast<double *>(lds + fa.a[k].lds_off) + local, sum[s]);
             }
         }
     }
@@ -1560,13 +1509,15 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                     }
                 }
             }
-            if (!any_mm) {
+            if (!any_mm || !tp.mgeneric) {
                 // consecutive entries of one cell (sorted / clustered rows) are added up in
-                // registers first: one LDS atomic per run of a chunk, not per entry
+                // registers first: one LDS atomic per run of a chunk, not per entry (min / max /
+                // moment-2 plans: the extended run); a moment other than 2 takes the per-entry
+                // form below
 #pragma unroll
                 for (int j = 0; j < VU; j++) {
                     const uint32_t words[4] = {ev[j].x, ev[j].y, ev[j].z, ev[j].w};
-                    TileRun<NV> run;
+                    TileRun<NV, MM> run;
                     uint32_t cur = ~0u;
 #pragma unroll
                     for (int x = 0; x < 8; x++) {
@@ -1591,11 +1542,6 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                 auto chunk = [&](auto jc) {
                     constexpr int j = decltype(jc)::value;
                     const uint32_t words[4] = {ev[j].x, ev[j].y, ev[j].z, ev[j].w};
-                    // runs of one cell (sorted / clustered rows) folded in registers: one LDS
-                    // atomic per aggregator and run (same-address atomics serialise)
-                    MixRun<NV> run;
-                    run.clear();
-                    uint32_t cur = ~0u;
 #pragma unroll
                     for (int x = 0; x < 8; x++) {
                         // a guard, not a break: the loop stays unrolled and vv in registers
@@ -1604,19 +1550,10 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
 #pragma unroll
                             for (int s = 0; s < NV; s++) v[s] = (x & 1) ? vv[j][s][x >> 1].y : vv[j][s][x >> 1].x;
                             const uint32_t local = (words[x >> 1] >> (16 * (x & 1))) & 0xffffu;
-                            if (DBG(tp.debug) & 8) {
-                                asm volatile("" :: "v"(local));
-                                continue;
-                            }
-                            if (local != cur) {
-                                if (cur != ~0u) run.flush(fa, lds_raw, cur);
-                                cur = local;
-                                run.clear();
-                            }
-                            run.add(fa, tp, 0xfu, v);
+                            if (DBG(tp.debug) & 8) asm volatile("" :: "v"(local));
+                            else reduce_entry<NV, MM>(fa, tp, lds_raw, local, 0xfu, v);
                         }
                     }
-                    if (cur != ~0u) run.flush(fa, lds_raw, cur);
                 };
                 static_assert(VU <= 8, "chunks per step");
                 chunk(std::integral_constant<int, 0>{});
@@ -2209,9 +2146,19 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     // ---- pass B
     {
         TimedScope ts("tile_reduce");
-        // MM: the per-entry pass B (min / max cells, moment terms) instead of the run form
+        // MM: min / max cells or moment terms in pass B (the extended run form; a moment
+        // other than 2 takes the per-entry form)
         bool mm = false;
-        for (int k = 0; k < fa.na; k++) mm = mm || is_minmax(fa.a[k].kind) || fa.a[k].kind == VH_AGG_SUM_MOMENT;
+        for (int k = 0; k < fa.na; k++) {
+            const FusedAgg &a = fa.a[k];
+            mm = mm || is_minmax(a.kind) || a.kind == VH_AGG_SUM_MOMENT;
+            if (a.kind == VH_AGG_SUM_MOMENT && a.moment != 2) tp.mgeneric = 1;
+            if (is_minmax(a.kind) && tp.val_slot[k] >= 0) {
+                const uint32_t code = (a.dtype == VH_F64 || a.dtype == VH_F32) ? 0u
+                                      : (a.dtype == VH_I64 || a.dtype == VH_I32 || a.dtype == VH_I16 || a.dtype == VH_I8) ? 1u : 2u;
+                tp.skind |= code << (2 * tp.val_slot[k]);
+            }
+        }
         uint64_t mm_bytes = 0;
         for (int k = 0; k < fa.na; k++)
             if (is_minmax(fa.a[k].kind)) mm_bytes += ((cells * (mm_cell32(fa.a[k].dtype) ? 4 : 8)) + 255) & ~uint64_t(255);

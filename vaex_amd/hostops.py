@@ -108,19 +108,43 @@ def astype(a, dtype):
 
 
 def take(a, idx):
-    """a[idx] for a 1-d array and an int64 index array (numpy take, split over the threads)."""
-    a, idx = np.asarray(a), np.asarray(idx)
-    if a.ndim != 1 or len(idx) < MIN_SPLIT:
+    """a[idx] for a 1-d array and an int64 index array (in range): the library's host gather
+    on the host threads (numpy's take holds the interpreter lock)."""
+    a, idx = np.asarray(a), np.ascontiguousarray(idx, dtype=np.int64)
+    if a.ndim != 1 or len(idx) < MIN_SPLIT or a.dtype.itemsize not in (1, 2, 4, 8) or a.dtype.hasobject:
         return np.take(a, idx)
+    a = np.ascontiguousarray(a)
     out = _empty(len(idx), a.dtype)
+    _lib.call("vh_host_take", out.ctypes.data, a.ctypes.data, idx.ctypes.data, len(idx), a.dtype.itemsize,
+              max(_threads(), 8))
+    return out
+
+
+def variance(sum_moment, sums, counts):
+    """agg.py:207-213's finish, element-wise in the same operations (bit-identical to the
+    numpy expression): mean = sum / count, m2 / count - mean ** 2, over the host threads."""
+    sm = np.asarray(sum_moment, dtype=np.float64)
+    s = np.asarray(sums, dtype=np.float64)
+    c = np.asarray(counts)
+    if sm.shape != s.shape or s.shape != c.shape or sm.size < MIN_SPLIT:
+        with np.errstate(divide="ignore", invalid="ignore"):
+            mean = s / c
+            return sm / c - mean ** 2
+    shape = sm.shape
+    sm, s, c = sm.reshape(-1, order="K"), s.reshape(-1, order="K"), c.reshape(-1, order="K")
+    if not (sm.flags.c_contiguous and s.flags.c_contiguous and c.flags.c_contiguous):
+        with np.errstate(divide="ignore", invalid="ignore"):
+            mean = s / c
+            return (sm / c - mean ** 2).reshape(shape)
+    out = _empty(sm.size, np.float64)
 
     def part(i0, i1):
-        # mode 'clip': numpy buffers `out` under the default mode='raise' (the indices are a
-        # permutation, in range)
-        np.take(a, idx[i0:i1], out=out[i0:i1], mode="clip")
+        with np.errstate(divide="ignore", invalid="ignore"):
+            mean = s[i0:i1] / c[i0:i1]
+            np.subtract(sm[i0:i1] / c[i0:i1], mean * mean, out=out[i0:i1])
 
-    _run(part, len(idx), MIN_SPLIT // 8)  # random gathers: latency-bound, every thread helps
-    return out
+    _run(part, sm.size)
+    return out.reshape(shape)
 
 
 def minmax(a):
