@@ -131,11 +131,16 @@ def variance(sum_moment, sums, counts):
             mean = s / c
             return sm / c - mean ** 2
     shape = sm.shape
-    sm, s, c = sm.reshape(-1, order="K"), s.reshape(-1, order="K"), c.reshape(-1, order="K")
-    if not (sm.flags.c_contiguous and s.flags.c_contiguous and c.flags.c_contiguous):
+    arrs = (sm, s, c)
+    if all(a.flags.c_contiguous for a in arrs):
+        order = "C"
+    elif all(a.flags.f_contiguous for a in arrs):
+        order = "F"
+    else:
         with np.errstate(divide="ignore", invalid="ignore"):
             mean = s / c
-            return (sm / c - mean ** 2).reshape(shape)
+            return sm / c - mean ** 2
+    sm, s, c = (a.reshape(-1, order=order) for a in arrs)  # views in memory order
     out = _empty(sm.size, np.float64)
 
     def part(i0, i1):
@@ -144,7 +149,7 @@ def variance(sum_moment, sums, counts):
             np.subtract(sm[i0:i1] / c[i0:i1], mean * mean, out=out[i0:i1])
 
     _run(part, sm.size)
-    return out.reshape(shape)
+    return out.reshape(shape, order=order)
 
 
 def minmax(a):
