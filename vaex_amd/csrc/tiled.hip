@@ -1863,8 +1863,11 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     };
     uint64_t per_cell = 0;
     for (int k = 0; k < fa_in.na; k++) per_cell += cell_bytes(fa_in.a[k]);
+    // pass B's LDS tile: 96 KB for count / sum plans; wider cells (min / max / moment) get up
+    // to 128 KB so their tiles keep 4096 cells (fewer tiles: longer pass-A runs per region)
+    const uint64_t budget = per_cell > 12 ? std::max<uint64_t>(TILE_LDS_BUDGET, 128 * 1024) : TILE_LDS_BUDGET;
     uint32_t s_log2 = 0;
-    while (s_log2 < 16 && ((uint64_t)2 << s_log2) * per_cell <= TILE_LDS_BUDGET) s_log2++;
+    while (s_log2 < 16 && ((uint64_t)2 << s_log2) * per_cell <= budget) s_log2++;
     const uint64_t S = 1ull << s_log2;
     const uint64_t T64 = (cells + S - 1) / S;
     if (T64 > TILE_MAX_TILES || T64 < 2) return false;

@@ -187,7 +187,7 @@ def occupancy(a):
             res[i0] = (nz, i0 + int(idx[0]), i0 + int(idx[-1]))
 
     if n:
-        _run(part, n)
+        _run(part, n, MIN_SPLIT // 8)  # a streaming count: every thread's memory bandwidth helps
     parts = [res[k] for k in sorted(res)]
     nnz = sum(p[0] for p in parts)
     firsts = [p[1] for p in parts if p[0]]
