@@ -21,7 +21,12 @@ df = vaex_amd.from_arrays(key=keys, v=v)
 
 
 def q():
-    r = df.groupby("key", agg={"v": ["sum", "count"]}, assume_sparse="auto" if mode == "auto" else True)
+    if mode == "hash_minmax":
+        r = df.groupby("key", agg={"v": ["sum", "count", "min", "max"]}, assume_sparse=True)
+    elif mode == "var":
+        return df.var("v", binby=["key"], limits=[5, 5 + 10 ** 6], shape=10 ** 6)
+    else:
+        r = df.groupby("key", agg={"v": ["sum", "count"]}, assume_sparse="auto" if mode == "auto" else True)
     return r["key"].to_numpy(), r["v"].to_numpy(), r["v_sum"].to_numpy()
 
 

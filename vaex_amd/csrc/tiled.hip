@@ -186,19 +186,24 @@ __device__ inline uint64_t mm_identity(int dt, bool mx) {
     if (dt_signed(dt)) return mx ? (uint64_t)INT64_MIN : (uint64_t)INT64_MAX;
     return mx ? 0ull : ~0ull;  // float (ordered bits) and unsigned
 }
-// one carried slot value into an LDS cell
+// one carried slot value into an LDS cell.  A plain read first: only a value that improves
+// on the cell pays the atomic (a stale read only sends a no-op atomic; a cell of many rows
+// improves ~ln(rows) times)
 __device__ inline void mm_lds(uint64_t *cell, int dt, bool mx, double v) {
     if (dt_float(dt)) {
         if (v != v) return;
-        const uint64_t o = ord_bits(v);
+        const uint64_t o = ord_bits(v), cur = *cell;
+        if (mx ? o <= cur : o >= cur) return;
         if (mx) atomicMax((unsigned long long *)cell, (unsigned long long)o);
         else atomicMin((unsigned long long *)cell, (unsigned long long)o);
     } else if (dt_signed(dt)) {
-        const long long x = (long long)__builtin_bit_cast(int64_t, v);
+        const long long x = (long long)__builtin_bit_cast(int64_t, v), cur = (long long)*cell;
+        if (mx ? x <= cur : x >= cur) return;
         if (mx) atomicMax((long long *)cell, x);
         else atomicMin((long long *)cell, x);
     } else {
-        const unsigned long long x = __builtin_bit_cast(unsigned long long, v);
+        const unsigned long long x = __builtin_bit_cast(unsigned long long, v), cur = *cell;
+        if (mx ? x <= cur : x >= cur) return;
         if (mx) atomicMax((unsigned long long *)cell, x);
         else atomicMin((unsigned long long *)cell, x);
     }
@@ -220,19 +225,23 @@ __device__ inline uint32_t ord_bits32(float f) {
 __device__ inline float unord_bits32(uint32_t o) {
     return __builtin_bit_cast(float, (o >> 31) ? (o & 0x7fffffffu) : ~o);
 }
-// one carried slot value (double: float data as a double, integers as int64 / uint64 bits)
+// one carried slot value (double: float data as a double, integers as int64 / uint64 bits),
+// with the same read-first filter
 __device__ inline void mm_lds32(uint32_t *cell, int dt, bool mx, double v) {
     if (dt_float(dt)) {
         if (v != v) return;
-        const uint32_t o = ord_bits32((float)v);
+        const uint32_t o = ord_bits32((float)v), cur = *cell;
+        if (mx ? o <= cur : o >= cur) return;
         if (mx) atomicMax(cell, o);
         else atomicMin(cell, o);
     } else if (dt_signed(dt)) {
-        const int x = (int)(int32_t)__builtin_bit_cast(int64_t, v);
+        const int x = (int)(int32_t)__builtin_bit_cast(int64_t, v), cur = (int)*cell;
+        if (mx ? x <= cur : x >= cur) return;
         if (mx) atomicMax(reinterpret_cast<int *>(cell), x);
         else atomicMin(reinterpret_cast<int *>(cell), x);
     } else {
-        const uint32_t x = (uint32_t)__builtin_bit_cast(uint64_t, v);
+        const uint32_t x = (uint32_t)__builtin_bit_cast(uint64_t, v), cur = *cell;
+        if (mx ? x <= cur : x >= cur) return;
         if (mx) atomicMax(cell, x);
         else atomicMin(cell, x);
     }
