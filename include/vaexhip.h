@@ -244,8 +244,10 @@ int vh_hashagg_order_first(vh_hashagg *h, const void *keys, uint64_t n, int loc)
  * (hash_primitives.hpp:96-281).  A prefix of run heads is scanned until every label is seen. */
 int vh_dense_first_order(const void *keys, uint64_t n, int loc, int key_dtype, int64_t vmin, uint64_t span,
                          const int64_t *labels, uint64_t m, int64_t *perm);
-/* host: dst[i] = src[idx[i]] (n items of itemsize 1/2/4/8 bytes) on up to `threads` threads */
-int vh_host_take(void *dst, const void *src, const int64_t *idx, uint64_t n, int itemsize, int threads);
+/* host: dsts[c][i] = srcs[c][idx[i]] for ncols columns of itemsizes[c] (1/2/4/8) bytes, i < n,
+ * on up to `threads` threads */
+int vh_host_take(int ncols, void *const *dsts, const void *const *srcs, const int *itemsizes, const int64_t *idx,
+                 uint64_t n, int threads);
 /* ---- multi-GPU (comm.hip): RCCL bound by the library, one process per GPU ----------
  * The reference has no multi-process path; its ExecutorLocal reduces per-thread task
  * parts serially (execution.py:285, Aggregator::reduce superagg.cpp:160-167,205-212,

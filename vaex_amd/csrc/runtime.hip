@@ -639,26 +639,39 @@ int vh_device_cache_trim(void) {
     VH_API_END
 }
 
-/* dst[i] = src[idx[i]] for i < n items of `itemsize` bytes, on up to `threads` host threads
- * (the permutation of a groupby's result columns into first-appearance order; numpy's take
- * holds the interpreter lock) */
-int vh_host_take(void *dst, const void *src, const int64_t *idx, uint64_t n, int itemsize, int threads) {
+/* dsts[c][i] = srcs[c][idx[i]] for ncols columns of itemsizes[c] (1/2/4/8) bytes, i < n, on up
+ * to `threads` host threads, each thread one index range over every column (the permutation
+ * of a groupby's result columns into first-appearance order; numpy's take holds the
+ * interpreter lock and would re-read the index per column) */
+int vh_host_take(int ncols, void *const *dsts, const void *const *srcs, const int *itemsizes, const int64_t *idx,
+                 uint64_t n, int threads) {
     VH_API_BEGIN
-    if (itemsize != 1 && itemsize != 2 && itemsize != 4 && itemsize != 8) fail(VH_ERR_ARG, "vh_host_take: itemsize");
-    auto part = [=](uint64_t i0, uint64_t i1) {
-        switch (itemsize) {
-        case 8: for (uint64_t i = i0; i < i1; i++) static_cast<uint64_t *>(dst)[i] = static_cast<const uint64_t *>(src)[idx[i]]; break;
-        case 4: for (uint64_t i = i0; i < i1; i++) static_cast<uint32_t *>(dst)[i] = static_cast<const uint32_t *>(src)[idx[i]]; break;
-        case 2: for (uint64_t i = i0; i < i1; i++) static_cast<uint16_t *>(dst)[i] = static_cast<const uint16_t *>(src)[idx[i]]; break;
-        default: for (uint64_t i = i0; i < i1; i++) static_cast<uint8_t *>(dst)[i] = static_cast<const uint8_t *>(src)[idx[i]];
+    for (int c = 0; c < ncols; c++)
+        if (itemsizes[c] != 1 && itemsizes[c] != 2 && itemsizes[c] != 4 && itemsizes[c] != 8)
+            fail(VH_ERR_ARG, "vh_host_take: itemsize");
+    std::vector<void *> d(dsts, dsts + ncols);
+    std::vector<const void *> sr(srcs, srcs + ncols);
+    std::vector<int> isz(itemsizes, itemsizes + ncols);
+    auto part = [&](uint64_t i0, uint64_t i1) {
+        for (uint64_t b = i0; b < i1; b += 4096) {  // blocks of the index: columns share its reads
+            const uint64_t e = std::min(i1, b + 4096);
+            for (int c = 0; c < ncols; c++) {
+                switch (isz[c]) {
+                case 8: for (uint64_t i = b; i < e; i++) static_cast<uint64_t *>(d[c])[i] = static_cast<const uint64_t *>(sr[c])[idx[i]]; break;
+                case 4: for (uint64_t i = b; i < e; i++) static_cast<uint32_t *>(d[c])[i] = static_cast<const uint32_t *>(sr[c])[idx[i]]; break;
+                case 2: for (uint64_t i = b; i < e; i++) static_cast<uint16_t *>(d[c])[i] = static_cast<const uint16_t *>(sr[c])[idx[i]]; break;
+                default: for (uint64_t i = b; i < e; i++) static_cast<uint8_t *>(d[c])[i] = static_cast<const uint8_t *>(sr[c])[idx[i]];
+                }
+            }
         }
     };
-    const int t = (int)std::min<uint64_t>((uint64_t)std::max(1, threads), std::max<uint64_t>(1, n / 65536));
+    const int t = (int)std::min<uint64_t>((uint64_t)std::max(1, threads), std::max<uint64_t>(1, n / 32768));
     if (t <= 1) {
         part(0, n);
     } else {
         std::vector<std::thread> pool;
-        for (int k = 0; k < t; k++) pool.emplace_back(part, n * k / t, n * (k + 1) / t);
+        for (int k = 1; k < t; k++) pool.emplace_back(part, n * k / t, n * (k + 1) / t);
+        part(0, n / t);
         for (auto &th : pool) th.join();
     }
     VH_API_END

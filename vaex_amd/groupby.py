@@ -215,7 +215,8 @@ def first_appearance_order(df, key, res):
     span = int(lab64[-1]) - vmin + 1
     _lib.call("vh_dense_first_order", ptr, df.length_unfiltered(), loc, code, ctypes.c_int64(vmin), span,
               lab64.ctypes.data, m, perm.ctypes.data)
-    return DataFrame({name: hostops.take(v, perm) for name, v in res.columns.items()})
+    names = list(res.columns)
+    return DataFrame(dict(zip(names, hostops.take_columns([res.columns[k] for k in names], perm))))
 
 
 COMBINE_OCCUPANCY = 10  # groupby.py:329-333: combine when rows / cells < 10

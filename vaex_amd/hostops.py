@@ -108,15 +108,33 @@ def astype(a, dtype):
 
 
 def take(a, idx):
-    """a[idx] for a 1-d array and an int64 index array (in range): the library's host gather
-    on the host threads (numpy's take holds the interpreter lock)."""
-    a, idx = np.asarray(a), np.ascontiguousarray(idx, dtype=np.int64)
-    if a.ndim != 1 or len(idx) < MIN_SPLIT or a.dtype.itemsize not in (1, 2, 4, 8) or a.dtype.hasobject:
-        return np.take(a, idx)
-    a = np.ascontiguousarray(a)
-    out = _empty(len(idx), a.dtype)
-    _lib.call("vh_host_take", out.ctypes.data, a.ctypes.data, idx.ctypes.data, len(idx), a.dtype.itemsize,
-              max(_threads(), 8))
+    """a[idx] for a 1-d array and an int64 index array (in range)."""
+    return take_columns([a], idx)[0]
+
+
+def take_columns(cols, idx):
+    """[c[idx] for c in cols] (1-d arrays, int64 indices in range): one call of the library's
+    host gather over the host threads, each thread one index range of every column (numpy's
+    take holds the interpreter lock)."""
+    import ctypes
+    idx = np.ascontiguousarray(idx, dtype=np.int64)
+    cols = [np.asarray(c) for c in cols]
+    fast = [c.ndim == 1 and c.dtype.itemsize in (1, 2, 4, 8) and not c.dtype.hasobject for c in cols]
+    out = [None] * len(cols)
+    if len(idx) >= MIN_SPLIT // 8:
+        todo = [i for i, f in enumerate(fast) if f]
+        srcs = [np.ascontiguousarray(cols[i]) for i in todo]
+        dsts = [_empty(len(idx), s.dtype) for s in srcs]
+        if todo:
+            k = len(todo)
+            _lib.call("vh_host_take", k, (ctypes.c_void_p * k)(*[d.ctypes.data for d in dsts]),
+                      (ctypes.c_void_p * k)(*[s.ctypes.data for s in srcs]), (ctypes.c_int * k)(*[s.dtype.itemsize for s in srcs]),
+                      idx.ctypes.data, len(idx), max(_threads(), 8))
+        for i, d in zip(todo, dsts):
+            out[i] = d
+    for i, c in enumerate(cols):
+        if out[i] is None:
+            out[i] = np.take(c, idx)
     return out
 
 
