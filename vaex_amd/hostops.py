@@ -140,34 +140,31 @@ def take_columns(cols, idx):
 
 def variance(sum_moment, sums, counts):
     """agg.py:207-213's finish, element-wise in the same operations (bit-identical to the
-    numpy expression): mean = sum / count, m2 / count - mean ** 2, over the host threads."""
+    numpy expression): mean = sum / count, m2 / count - mean ** 2, over the host threads (the
+    inputs may be strided views of the grids' host images; the work is split along the last
+    axis)."""
     sm = np.asarray(sum_moment, dtype=np.float64)
     s = np.asarray(sums, dtype=np.float64)
     c = np.asarray(counts)
-    if sm.shape != s.shape or s.shape != c.shape or sm.size < MIN_SPLIT:
+    if sm.shape != s.shape or s.shape != c.shape or sm.size < MIN_SPLIT or sm.ndim == 0:
         with np.errstate(divide="ignore", invalid="ignore"):
             mean = s / c
             return sm / c - mean ** 2
-    shape = sm.shape
-    arrs = (sm, s, c)
-    if all(a.flags.c_contiguous for a in arrs):
-        order = "C"
-    elif all(a.flags.f_contiguous for a in arrs):
-        order = "F"
-    else:
-        with np.errstate(divide="ignore", invalid="ignore"):
-            mean = s / c
-            return sm / c - mean ** 2
-    sm, s, c = (a.reshape(-1, order=order) for a in arrs)  # views in memory order
-    out = _empty(sm.size, np.float64)
+    order = "F" if sm.ndim > 1 and not sm.flags.c_contiguous else "C"
+    out = np.empty(sm.shape, np.float64, order=order)
 
     def part(i0, i1):
+        sl = (Ellipsis, slice(i0, i1))
         with np.errstate(divide="ignore", invalid="ignore"):
-            mean = s[i0:i1] / c[i0:i1]
-            np.subtract(sm[i0:i1] / c[i0:i1], mean * mean, out=out[i0:i1])
+            mean = s[sl] / c[sl]
+            np.subtract(sm[sl] / c[sl], mean * mean, out=out[sl])
 
-    _run(part, sm.size)
-    return out.reshape(shape, order=order)
+    last = sm.shape[-1]
+    if last >= 8:
+        _run(part, last, max(1, last // 8))
+    else:
+        part(0, last)
+    return out
 
 
 def minmax(a):

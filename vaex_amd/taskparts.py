@@ -160,11 +160,11 @@ class TaskPartAggregation:
             if dtype_out.kind in "mM" or result.dtype.itemsize == dtype_out.itemsize:
                 result = result.view(dtype_out.newbyteorder("=") if dtype_out.byteorder not in "<=|" else dtype_out)
             host = getattr(aggs[0], "_host", None) if len(aggs) == 1 and not selection_waslist else None
-            if host is not None and (result.flags.c_contiguous or result.flags.f_contiguous) and \
-                    np.may_share_memory(result, host):
+            if host is not None and np.may_share_memory(result, host):
                 # the part is done with its aggregator: hand its (page-locked) host image over
-                # instead of copying it (cpu.py:605 copies because its grids are reused; for an
-                # N-d grid that copy is a transpose into C order, ~2 ms per 1e6 cells)
+                # (the result may be a strided view of it: the grid's central part) instead of
+                # copying it (cpu.py:605 copies because its grids are reused; for an N-d grid
+                # that copy is a transpose into C order, ~2 ms per 1e6 cells)
                 aggs[0]._release_host()
                 results.append(result)
             else:
