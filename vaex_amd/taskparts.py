@@ -24,6 +24,18 @@ def parse_ordinal_values(expression):
     return (m.group(1).strip(), m.group(2)) if m else None
 
 
+def _rebase(view, host):
+    """``view`` (a view into the 1-d host image ``host``, whatever it is based on) rebuilt as
+    an array based on ``host`` alone; None when it does not lie inside ``host``."""
+    if not np.may_share_memory(view, host) or view.size == 0 or any(s < 0 for s in view.strides):
+        return None
+    offset = view.__array_interface__["data"][0] - host.ctypes.data
+    extent = sum((n - 1) * s for n, s in zip(view.shape, view.strides)) + view.itemsize
+    if offset < 0 or offset + extent > host.nbytes:
+        return None
+    return np.ndarray(view.shape, view.dtype, buffer=host, offset=offset, strides=view.strides)
+
+
 def create_binner(df, spec):
     """binner-cpu decode (cpu.py:40-51), plus the fused set-ordinal binner for groupby."""
     if spec.kind == "ordinal":
@@ -160,13 +172,16 @@ class TaskPartAggregation:
             if dtype_out.kind in "mM" or result.dtype.itemsize == dtype_out.itemsize:
                 result = result.view(dtype_out.newbyteorder("=") if dtype_out.byteorder not in "<=|" else dtype_out)
             host = getattr(aggs[0], "_host", None) if len(aggs) == 1 and not selection_waslist else None
-            if host is not None and np.may_share_memory(result, host):
+            rebased = _rebase(result, host) if host is not None else None
+            if rebased is not None:
                 # the part is done with its aggregator: hand its (page-locked) host image over
                 # (the result may be a strided view of it: the grid's central part) instead of
                 # copying it (cpu.py:605 copies because its grids are reused; for an N-d grid
-                # that copy is a transpose into C order, ~2 ms per 1e6 cells)
+                # that copy is a transpose into C order, ~2 ms per 1e6 cells).  The view is
+                # rebuilt over the image itself so it does not keep the aggregator (and the
+                # columns it references) alive.
                 aggs[0]._release_host()
-                results.append(result)
+                results.append(rebased)
             else:
                 results.append(result.copy())
         return results
