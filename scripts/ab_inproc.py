@@ -23,7 +23,7 @@ def main():
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--rows", type=float, default=1e9)
     ap.add_argument("--rounds", type=int, default=12)
-    ap.add_argument("--workloads", default="c2sum,c2count", help="c2sum,c2count,c3")
+    ap.add_argument("--workloads", default="c2sum,c2count", help="c2sum,c2count,c2mm,c2var,c3,c3mm,c3fused,c3set")
     a = ap.parse_args()
     libs = [_lib.load_library(os.path.abspath(p)) for p in a.libs]
     _lib._lib = libs[0]
@@ -41,6 +41,9 @@ def main():
         if wl == "c3":
             df3.groupby("key", agg={"v_sum": vaex_amd.agg.sum("v"), "v_count": vaex_amd.agg.count("v")})
             return
+        if wl == "c3mm":
+            df3.groupby("key", agg={"v": ["sum", "count", "min", "max"]}, assume_sparse=True)
+            return
         if wl in ("c3fused", "c3fused0"):  # c3fused0: no count(v) (count(*) only)
             from vaex_amd.hashagg import HashAgg
             ha = HashAgg(keys.dtype, [x.dtype], [wl == "c3fused"])
@@ -51,7 +54,7 @@ def main():
             from vaex_amd import superutils
             superutils.ordered_set_int32().update(keys)
             return
-        with_sum = wl == "c2sum"
+        with_sum = wl in ("c2sum", "c2mm", "c2var")
         bx = superagg.BinnerScalar_float64("x", -4.0, 4.0, 1024)
         by = superagg.BinnerScalar_float64("y", -4.0, 4.0, 1024)
         bx.set_data(x)
@@ -61,6 +64,12 @@ def main():
         if with_sum:
             aggs.append(superagg.AggSum_float64(grid))
             aggs[1].set_data(w, 0)
+        if wl == "c2mm":
+            aggs += [superagg.AggMin_float64(grid), superagg.AggMax_float64(grid)]
+        if wl == "c2var":
+            aggs.append(superagg.AggSumMoment_float64(grid, 2))
+        for ag in aggs[2:]:
+            ag.set_data(w, 0)
         grid.bin(aggs)
 
     res = {(i, wl): {k: [] for k in KERNELS} for i in range(len(libs)) for wl in workloads}

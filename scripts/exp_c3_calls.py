@@ -23,6 +23,7 @@ df = vaex_amd.from_arrays(key=keys, v=v)
 def q():
     if mode == "hash_minmax":
         r = df.groupby("key", agg={"v": ["sum", "count", "min", "max"]}, assume_sparse=True)
+        return [r[c].to_numpy() for c in r.get_column_names()]
     elif mode == "var":
         return df.var("v", binby=["key"], limits=[5, 5 + 10 ** 6], shape=10 ** 6)
     else:

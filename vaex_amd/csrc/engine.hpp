@@ -128,11 +128,14 @@ struct FusedAgg {
 
 // AggSumMoment's term of a non-NaN float value (superagg.cpp:400-433: pow(value, moment) in
 // double; moment 2 as value * value, which pow rounds identically)
+// pow out of line: inlined at every call site of an unrolled kernel it is ~7000 instructions
+// each, for a moment that is rarely above 2
+__device__ __noinline__ inline double moment_pow(double v, uint32_t m) { return pow(v, (double)m); }
 __device__ inline double moment_term(double v, uint32_t m) {
     if (m == 0) return 1.0;
     if (m == 1) return v;
     if (m == 2) return v * v;
-    return pow(v, (double)m);
+    return moment_pow(v, m);
 }
 
 // two value-carrying aggregators (sum / min / max) read the same column the same way: the tile

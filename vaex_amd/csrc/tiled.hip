@@ -112,6 +112,7 @@ struct TileParams {
     // run form of pass B with min / max / moment: per value slot its min / max encoding (2 bits:
     // 0 float, 1 signed, 2 unsigned); mgeneric: a moment other than 2 (per-entry form)
     uint32_t skind, mgeneric;
+    uint32_t mmk;  // bit k: aggregator k is a min / max (pass B reads its cells ahead of the run)
 };
 
 // value of row h (0/1) of a loaded pair of a column of dtype dt, as the 8-byte slot pass A
@@ -246,6 +247,36 @@ __device__ inline void mm_lds32(uint32_t *cell, int dt, bool mx, double v) {
         else atomicMin(cell, x);
     }
 }
+// a min / max LDS cell's bits (4-byte cells zero-extended), and whether v would improve on a
+// cell holding them (mm_lds / mm_lds32's filter, without the atomic)
+__device__ inline uint64_t mm_peek(const unsigned char *lds, const FusedAgg &a, uint32_t local) {
+    if (mm_cell32(a.dtype)) return reinterpret_cast<const uint32_t *>(lds + a.lds_off)[local];
+    return reinterpret_cast<const uint64_t *>(lds + a.lds_off)[local];
+}
+__device__ inline bool mm_improves(int dt, bool mx, uint64_t cur, double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    if (mm_cell32(dt)) {
+        if (dt_float(dt)) {
+            if (v != v) return false;
+            const uint32_t o = ord_bits32((float)v), c = (uint32_t)cur;
+            return mx ? o > c : o < c;
+        }
+        if (dt_signed(dt)) {
+            const int x = (int)(int32_t)(int64_t)b, c = (int)(uint32_t)cur;
+            return mx ? x > c : x < c;
+        }
+        const uint32_t x = (uint32_t)b, c = (uint32_t)cur;
+        return mx ? x > c : x < c;
+    }
+    if (dt_float(dt)) {
+        if (v != v) return false;
+        const uint64_t o = ord_bits(v);
+        return mx ? o > cur : o < cur;
+    }
+    if (dt_signed(dt)) return mx ? (long long)b > (long long)cur : (long long)b < (long long)cur;
+    return mx ? b > cur : b < cur;
+}
+
 // a 4-byte cell as the carried-slot bits mm_grid takes
 __device__ inline uint64_t mm_cell32_slot(int dt, uint32_t x) {
     if (dt_float(dt)) return __builtin_bit_cast(uint64_t, (double)unord_bits32(x));
@@ -1307,7 +1338,9 @@ __device__ inline void reduce_entry(const FusedAggs &fa, const TileParams &tp, u
 // the non-NaN count, the float sum of non-NaN values and the 64-bit integer sum
 // X: the plan also has min / max and moment-2 aggregators (var / std): per value slot the
 // run's sum of squares and min / max in an order-preserving u64 form (float: ord_bits, NaN
-// skipped; signed: bits ^ 2^63; unsigned: bits) -- skind packs each slot's form (2 bits)
+// skipped; signed: bits ^ 2^63; unsigned: bits) -- skind packs each slot's form (2 bits).
+// min / max take only the entries whose gate bits say they improve on the cell as read ahead
+// of the chunk (bit 2s: a min of slot s, bit 2s + 1: a max), so a run of none flushes nothing
 template <int NV, bool X = false> struct TileRun {
     uint32_t cnt, nn[NV > 0 ? NV : 1];
     double sum[NV > 0 ? NV : 1];
@@ -1328,7 +1361,7 @@ template <int NV, bool X = false> struct TileRun {
             }
         }
     }
-    __device__ void add(const TileParams &tp, const double *v) {
+    __device__ __attribute__((always_inline)) void add(const TileParams &tp, const double *v, uint32_t gate = 0) {
         cnt++;
 #pragma unroll
         for (int s = 0; s < NV; s++) {
@@ -1339,17 +1372,20 @@ template <int NV, bool X = false> struct TileRun {
                 if constexpr (X) sum2[s] += v[s] * v[s];
             }
             if constexpr (X) {
+                if (!((gate >> (2 * s)) & 3u)) continue;  // improves neither cell (NaN never does)
                 const uint32_t code = (tp.skind >> (2 * s)) & 3u;
                 const uint64_t b = __builtin_bit_cast(uint64_t, v[s]);
-                if (code == 0 && v[s] != v[s]) continue;
                 const uint64_t e = code == 0 ? ord_bits(v[s]) : code == 1 ? b ^ (1ull << 63) : b;
-                mn[s] = e < mn[s] ? e : mn[s];
-                mx[s] = e > mx[s] ? e : mx[s];
+                if ((gate >> (2 * s)) & 1u) mn[s] = e < mn[s] ? e : mn[s];
+                if ((gate >> (2 * s)) & 2u) mx[s] = e > mx[s] ? e : mx[s];
             }
         }
     }
     // the run into the LDS tile, as reduce_entry would add its entries one by one
-    __device__ void flush(const FusedAggs &fa, const TileParams &tp, unsigned char *lds, uint32_t local) const {
+    // add / flush always inlined: out of line they take fa / tp / the run by address, which
+    // puts all three in scratch memory (the two-slot min / max kernel did)
+    __device__ __attribute__((always_inline)) void flush(const FusedAggs &fa, const TileParams &tp, unsigned char *lds,
+                                                         uint32_t local) const {
 #pragma unroll
         for (int k = 0; k < MAX_FUSED_AGGS; k++) {
             if (k >= fa.na) break;
@@ -1373,9 +1409,10 @@ template <int NV, bool X = false> struct TileRun {
                     }
                     if (is_minmax(kind)) {
                         const uint32_t code = (tp.skind >> (2 * s)) & 3u;
-                        if (code == 0 ? nn[s] == 0 : cnt == 0) continue;
                         const bool m = kind == VH_AGG_MAX;
                         const uint64_t e = m ? mx[s] : mn[s];
+                        // no gated entry (an improving one never encodes as the identity)
+                        if (m ? e == 0 : e == ~0ull) continue;
                         const double x = code == 0 ? unord_bits(e) : __builtin_bit_cast(double, code == 1 ? e ^ (1ull << 63) : e);
                         if (mm_cell32(fa.a[k].dtype))
                             mm_lds32(reinterpret_cast<uint32_t *>(lds + fa.a[k].lds_off) + local, fa.a[k].dtype, m, x);
@@ -1405,7 +1442,9 @@ template <int NV> constexpr int tb_vu() { return VH_TB_VU ? VH_TB_VU : NV == 0 ?
 // short the regions are; a lane finds the region of its chunk by a forward scan (chunk
 // indices of a lane only grow).  Entries are reduced with LDS atomics, then the tile is
 // flushed with coalesced global atomics.
-template <int NV, bool NARROW = false, bool MM = false, bool PK = false>
+// MG: a moment other than 2 (per-entry form; its own instantiation, so the run form's
+// registers are not sized for it)
+template <int NV, bool NARROW = false, bool MM = false, bool PK = false, bool MG = false>
 __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TileParams tp, const WorkUnit *units) {
     static_assert(!PK || (NV == 2 && NARROW), "packed pairs of narrow slots");
     extern __shared__ __align__(16) unsigned char lds_raw[];
@@ -1451,7 +1490,6 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
     __syncthreads();
     // MM: the plan has min / max aggregators (a separate instantiation: their code would
     // raise the count / sum kernel's registers past the 1024-thread budget)
-    constexpr bool any_mm = MM;
     if constexpr (MM) {  // min / max cells start at the kind's identity (after the zero fill)
         const uint32_t ncells = 1u << tp.s_log2;
         #pragma unroll
@@ -1518,7 +1556,7 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                     }
                 }
             }
-            if (!any_mm || !tp.mgeneric) {
+            if constexpr (!MG) {
                 // consecutive entries of one cell (sorted / clustered rows) are added up in
                 // registers first: one LDS atomic per run of a chunk, not per entry (min / max /
                 // moment-2 plans: the extended run); a moment other than 2 takes the per-entry
@@ -1526,12 +1564,55 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
 #pragma unroll
                 for (int j = 0; j < VU; j++) {
                     const uint32_t words[4] = {ev[j].x, ev[j].y, ev[j].z, ev[j].w};
-                    TileRun<NV, MM> run;
-                    uint32_t cur = ~0u;
+                    if constexpr (MM) {
+                        // min / max: the chunk's 8 cells of each such aggregator are read in one
+                        // go and compared before any atomic (one LDS wait per aggregator, not a
+                        // read-then-atomic round trip per entry; a stale read only lets a no-op
+                        // atomic through, as cells only improve).  gate: 4 bits per entry (bit
+                        // 2s: improves a min of slot s, 2s + 1: a max)
+                        static_assert(NV <= 2, "4 gate bits per entry");
+                        uint32_t gate = 0;
 #pragma unroll
-                    for (int x = 0; x < 8; x++) {
-                        const uint32_t local = (words[x >> 1] >> (16 * (x & 1))) & 0xffffu;
-                        if ((uint32_t)x < rem[j]) {
+                        for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+                            if (!((tp.mmk >> k) & 1u)) continue;
+                            const FusedAgg &a = fa.a[k];
+                            const int vs = tp.val_slot[k];
+                            const bool m = a.kind == VH_AGG_MAX;
+                            uint64_t cell[8];
+#pragma unroll
+                            for (int x = 0; x < 8; x++) {
+                                const uint32_t local = (uint32_t)x < rem[j] ? (words[x >> 1] >> (16 * (x & 1))) & 0xffffu : 0u;
+                                cell[x] = mm_peek(lds_raw, a, local);
+                            }
+#pragma unroll
+                            for (int x = 0; x < 8; x++) {
+#pragma unroll
+                                for (int s = 0; s < NV; s++) {
+                                    if (s != vs) continue;
+                                    const double vx = (x & 1) ? vv[j][s][x >> 1].y : vv[j][s][x >> 1].x;
+                                    if ((uint32_t)x < rem[j] && mm_improves(a.dtype, m, cell[x], vx))
+                                        gate |= (m ? 2u : 1u) << (4 * x + 2 * s);
+                                }
+                            }
+                        }
+                        // the extended run's flush is large: one copy of the entry body in a
+                        // run-time loop that takes the head of shift registers (an unrolled loop
+                        // spills; a run-time index into the chunk's arrays -- selects included,
+                        // which the compiler folds into one -- goes through scratch memory)
+                        double sv[NV > 0 ? NV : 1][8];
+#pragma unroll
+                        for (int s = 0; s < NV; s++)
+#pragma unroll
+                            for (int h = 0; h < 4; h++) {
+                                sv[s][2 * h] = vv[j][s][h].x;
+                                sv[s][2 * h + 1] = vv[j][s][h].y;
+                            }
+                        uint32_t w0 = words[0], w1 = words[1], w2 = words[2], w3 = words[3];
+                        TileRun<NV, true> run;
+                        uint32_t cur = ~0u;
+#pragma unroll 1
+                        for (uint32_t x = 0; x < rem[j]; x++) {
+                            const uint32_t local = w0 & 0xffffu;
                             if (local != cur) {
                                 if (cur != ~0u) run.flush(fa, tp, lds_raw, cur);
                                 cur = local;
@@ -1539,11 +1620,39 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                             }
                             double v[NV > 0 ? NV : 1];
 #pragma unroll
-                            for (int s = 0; s < NV; s++) v[s] = (x & 1) ? vv[j][s][x >> 1].y : vv[j][s][x >> 1].x;
-                            run.add(tp, v);
+                            for (int s = 0; s < NV; s++) v[s] = sv[s][0];
+                            run.add(tp, v, gate & 0xfu);
+                            gate >>= 4;
+                            w0 = (w0 >> 16) | (w1 << 16);
+                            w1 = (w1 >> 16) | (w2 << 16);
+                            w2 = (w2 >> 16) | (w3 << 16);
+                            w3 >>= 16;
+#pragma unroll
+                            for (int s = 0; s < NV; s++)
+#pragma unroll
+                                for (int h = 0; h < 7; h++) sv[s][h] = sv[s][h + 1];
                         }
+                        if (cur != ~0u) run.flush(fa, tp, lds_raw, cur);
+                    } else {
+                        TileRun<NV, false> run;
+                        uint32_t cur = ~0u;
+#pragma unroll
+                        for (int x = 0; x < 8; x++) {
+                            const uint32_t local = (words[x >> 1] >> (16 * (x & 1))) & 0xffffu;
+                            if ((uint32_t)x < rem[j]) {
+                                if (local != cur) {
+                                    if (cur != ~0u) run.flush(fa, tp, lds_raw, cur);
+                                    cur = local;
+                                    run.clear();
+                                }
+                                double v[NV > 0 ? NV : 1];
+#pragma unroll
+                                for (int s = 0; s < NV; s++) v[s] = (x & 1) ? vv[j][s][x >> 1].y : vv[j][s][x >> 1].x;
+                                run.add(tp, v);
+                            }
+                        }
+                        if (cur != ~0u) run.flush(fa, tp, lds_raw, cur);
                     }
-                    if (cur != ~0u) run.flush(fa, tp, lds_raw, cur);
                 }
             } else {
                 // chunk j as a compile-time index (the unroller gave up on this body, and a
@@ -1579,11 +1688,14 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
         for (uint32_t k = 0; k < nw; k++) {
             const uint32_t cnt = s_fill[k];
             const uint64_t base = k < nwr ? (uint64_t)(u.w_begin + k) * tp.wg_stride + tp.toff[t] : spill0;
-            for (uint32_t q0 = 0; q0 < cnt; q0 += TB_THREADS * TB_UNROLL) {
-                uint32_t ent[TB_UNROLL];
-                double v[TB_UNROLL][NV > 0 ? NV : 1];
+            // min / max plans: fewer entries in flight (8 inlined reduce_entry bodies of two
+            // slots spill)
+            constexpr int UN = MM && NV > 1 ? 2 : TB_UNROLL;
+            for (uint32_t q0 = 0; q0 < cnt; q0 += TB_THREADS * UN) {
+                uint32_t ent[UN];
+                double v[UN][NV > 0 ? NV : 1];
 #pragma unroll
-                for (int j = 0; j < TB_UNROLL; j++) {
+                for (int j = 0; j < UN; j++) {
                     const uint32_t q = q0 + j * TB_THREADS + threadIdx.x;
                     if (q < cnt) {
                         const uint64_t e = base + q;
@@ -1599,7 +1711,7 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                     }
                 }
 #pragma unroll
-                for (int j = 0; j < TB_UNROLL; j++) {
+                for (int j = 0; j < UN; j++) {
                     const uint32_t q = q0 + j * TB_THREADS + threadIdx.x;
                     if (q < cnt) reduce_entry<NV, MM>(fa, tp, lds_raw, ent[j] & 0xffffu, ent[j] >> 16, v[j]);
                 }
@@ -2165,6 +2277,7 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
             const FusedAgg &a = fa.a[k];
             mm = mm || is_minmax(a.kind) || a.kind == VH_AGG_SUM_MOMENT;
             if (a.kind == VH_AGG_SUM_MOMENT && a.moment != 2) tp.mgeneric = 1;
+            if (is_minmax(a.kind)) tp.mmk |= 1u << k;
             if (is_minmax(a.kind) && tp.val_slot[k] >= 0) {
                 const uint32_t code = (a.dtype == VH_F64 || a.dtype == VH_F32) ? 0u
                                       : (a.dtype == VH_I64 || a.dtype == VH_I32 || a.dtype == VH_I16 || a.dtype == VH_I8) ? 1u : 2u;
@@ -2192,7 +2305,8 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         const unsigned g = (unsigned)units.size();
 #define VH_TB(NV_, NAR_)                                                                                      \
     do {                                                                                                      \
-        if (mm) hipLaunchKernelGGL((k_tile_reduce<NV_, NAR_, true>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units); \
+        if (mm && tp.mgeneric) hipLaunchKernelGGL((k_tile_reduce<NV_, NAR_, true, false, true>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units); \
+        else if (mm) hipLaunchKernelGGL((k_tile_reduce<NV_, NAR_, true>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units); \
         else hipLaunchKernelGGL((k_tile_reduce<NV_, NAR_, false>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units); \
     } while (0)
         switch (nv) {
@@ -2203,7 +2317,8 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
             break;
         default:
             if (tp.vpacked) {
-                if (mm) hipLaunchKernelGGL((k_tile_reduce<2, true, true, true>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
+                if (mm && tp.mgeneric) hipLaunchKernelGGL((k_tile_reduce<2, true, true, true, true>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
+                else if (mm) hipLaunchKernelGGL((k_tile_reduce<2, true, true, true>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
                 else hipLaunchKernelGGL((k_tile_reduce<2, true, false, true>), dim3(g), dim3(TB_THREADS), lds_b, st, fa, tp, d_units);
             } else if (vnarrow) {
                 VH_TB(2, true);
