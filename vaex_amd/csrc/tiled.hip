@@ -190,21 +190,23 @@ __device__ inline uint64_t mm_identity(int dt, bool mx) {
 // one carried slot value into an LDS cell.  A plain read first: only a value that improves
 // on the cell pays the atomic (a stale read only sends a no-op atomic; a cell of many rows
 // improves ~ln(rows) times)
+// (RF false: the caller has already compared against a read of the cell -- the atomic only)
+template <bool RF = true>
 __device__ inline void mm_lds(uint64_t *cell, int dt, bool mx, double v) {
     if (dt_float(dt)) {
         if (v != v) return;
-        const uint64_t o = ord_bits(v), cur = *cell;
-        if (mx ? o <= cur : o >= cur) return;
+        const uint64_t o = ord_bits(v), cur = RF ? *cell : 0;
+        if (RF && (mx ? o <= cur : o >= cur)) return;
         if (mx) atomicMax((unsigned long long *)cell, (unsigned long long)o);
         else atomicMin((unsigned long long *)cell, (unsigned long long)o);
     } else if (dt_signed(dt)) {
-        const long long x = (long long)__builtin_bit_cast(int64_t, v), cur = (long long)*cell;
-        if (mx ? x <= cur : x >= cur) return;
+        const long long x = (long long)__builtin_bit_cast(int64_t, v), cur = RF ? (long long)*cell : 0;
+        if (RF && (mx ? x <= cur : x >= cur)) return;
         if (mx) atomicMax((long long *)cell, x);
         else atomicMin((long long *)cell, x);
     } else {
-        const unsigned long long x = __builtin_bit_cast(unsigned long long, v), cur = *cell;
-        if (mx ? x <= cur : x >= cur) return;
+        const unsigned long long x = __builtin_bit_cast(unsigned long long, v), cur = RF ? *cell : 0;
+        if (RF && (mx ? x <= cur : x >= cur)) return;
         if (mx) atomicMax((unsigned long long *)cell, x);
         else atomicMin((unsigned long long *)cell, x);
     }
@@ -228,21 +230,22 @@ __device__ inline float unord_bits32(uint32_t o) {
 }
 // one carried slot value (double: float data as a double, integers as int64 / uint64 bits),
 // with the same read-first filter
+template <bool RF = true>
 __device__ inline void mm_lds32(uint32_t *cell, int dt, bool mx, double v) {
     if (dt_float(dt)) {
         if (v != v) return;
-        const uint32_t o = ord_bits32((float)v), cur = *cell;
-        if (mx ? o <= cur : o >= cur) return;
+        const uint32_t o = ord_bits32((float)v), cur = RF ? *cell : 0;
+        if (RF && (mx ? o <= cur : o >= cur)) return;
         if (mx) atomicMax(cell, o);
         else atomicMin(cell, o);
     } else if (dt_signed(dt)) {
-        const int x = (int)(int32_t)__builtin_bit_cast(int64_t, v), cur = (int)*cell;
-        if (mx ? x <= cur : x >= cur) return;
+        const int x = (int)(int32_t)__builtin_bit_cast(int64_t, v), cur = RF ? (int)*cell : 0;
+        if (RF && (mx ? x <= cur : x >= cur)) return;
         if (mx) atomicMax(reinterpret_cast<int *>(cell), x);
         else atomicMin(reinterpret_cast<int *>(cell), x);
     } else {
-        const uint32_t x = (uint32_t)__builtin_bit_cast(uint64_t, v), cur = *cell;
-        if (mx ? x <= cur : x >= cur) return;
+        const uint32_t x = (uint32_t)__builtin_bit_cast(uint64_t, v), cur = RF ? *cell : 0;
+        if (RF && (mx ? x <= cur : x >= cur)) return;
         if (mx) atomicMax(cell, x);
         else atomicMin(cell, x);
     }
@@ -1414,10 +1417,12 @@ template <int NV, bool X = false> struct TileRun {
                         // no gated entry (an improving one never encodes as the identity)
                         if (m ? e == 0 : e == ~0ull) continue;
                         const double x = code == 0 ? unord_bits(e) : __builtin_bit_cast(double, code == 1 ? e ^ (1ull << 63) : e);
+                        // gated entries improve on the cell as read ahead: the atomic only (no
+                        // second read and wait per run)
                         if (mm_cell32(fa.a[k].dtype))
-                            mm_lds32(reinterpret_cast<uint32_t *>(lds + fa.a[k].lds_off) + local, fa.a[k].dtype, m, x);
+                            mm_lds32<false>(reinterpret_cast<uint32_t *>(lds + fa.a[k].lds_off) + local, fa.a[k].dtype, m, x);
                         else
-                            mm_lds(reinterpret_cast<uint64_t *>(lds + fa.a[k].lds_off) + local, fa.a[k].dtype, m, x);
+                            mm_lds<false>(reinterpret_cast<uint64_t *>(lds + fa.a[k].lds_off) + local, fa.a[k].dtype, m, x);
                         continue;
                     }
                 }
