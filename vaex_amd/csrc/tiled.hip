@@ -109,10 +109,9 @@ struct TileParams {
     // typed grid afterwards by k_mm_merge (a CAS per cell on 1- and 2-byte grids serialised
     // on the shared words)
     void *mmtmp[MAX_FUSED_AGGS];
-    // run form of pass B with min / max / moment: per value slot its min / max encoding (2 bits:
-    // 0 float, 1 signed, 2 unsigned); mgeneric: a moment other than 2 (per-entry form)
-    uint32_t skind, mgeneric;
-    uint32_t mmk;  // bit k: aggregator k is a min / max (pass B reads its cells ahead of the run)
+    // pass B with min / max / moment: mgeneric, a moment other than 2 (per-entry form); mmk, bit
+    // k set when aggregator k is a min / max (its cells are read ahead of each chunk)
+    uint32_t mgeneric, mmk;
 };
 
 // value of row h (0/1) of a loaded pair of a column of dtype dt, as the 8-byte slot pass A
@@ -1340,16 +1339,12 @@ __device__ inline void reduce_entry(const FusedAggs &fa, const TileParams &tp, u
 // a run of entries of one LDS cell (count / sum aggregators): entries, and per value slot
 // the non-NaN count, the float sum of non-NaN values and the 64-bit integer sum
 // X: the plan also has min / max and moment-2 aggregators (var / std): per value slot the
-// run's sum of squares and min / max in an order-preserving u64 form (float: ord_bits, NaN
-// skipped; signed: bits ^ 2^63; unsigned: bits) -- skind packs each slot's form (2 bits).
-// min / max take only the entries whose gate bits say they improve on the cell as read ahead
-// of the chunk (bit 2s: a min of slot s, bit 2s + 1: a max), so a run of none flushes nothing
+// run's sum of squares (min / max entries are committed one by one, see k_tile_reduce)
 template <int NV, bool X = false> struct TileRun {
     uint32_t cnt, nn[NV > 0 ? NV : 1];
     double sum[NV > 0 ? NV : 1];
     unsigned long long isum[NV > 0 ? NV : 1];
     double sum2[X && NV > 0 ? NV : 1];
-    uint64_t mn[X && NV > 0 ? NV : 1], mx[X && NV > 0 ? NV : 1];
     __device__ void clear() {
         cnt = 0;
 #pragma unroll
@@ -1357,14 +1352,10 @@ template <int NV, bool X = false> struct TileRun {
             nn[s] = 0;
             sum[s] = 0.0;
             isum[s] = 0;
-            if constexpr (X) {
-                sum2[s] = 0.0;
-                mn[s] = ~0ull;
-                mx[s] = 0;
-            }
+            if constexpr (X) sum2[s] = 0.0;
         }
     }
-    __device__ __attribute__((always_inline)) void add(const TileParams &tp, const double *v, uint32_t gate = 0) {
+    __device__ __attribute__((always_inline)) void add(const TileParams &tp, const double *v) {
         cnt++;
 #pragma unroll
         for (int s = 0; s < NV; s++) {
@@ -1374,14 +1365,7 @@ template <int NV, bool X = false> struct TileRun {
                 sum[s] += v[s];
                 if constexpr (X) sum2[s] += v[s] * v[s];
             }
-            if constexpr (X) {
-                if (!((gate >> (2 * s)) & 3u)) continue;  // improves neither cell (NaN never does)
-                const uint32_t code = (tp.skind >> (2 * s)) & 3u;
-                const uint64_t b = __builtin_bit_cast(uint64_t, v[s]);
-                const uint64_t e = code == 0 ? ord_bits(v[s]) : code == 1 ? b ^ (1ull << 63) : b;
-                if ((gate >> (2 * s)) & 1u) mn[s] = e < mn[s] ? e : mn[s];
-                if ((gate >> (2 * s)) & 2u) mx[s] = e > mx[s] ? e : mx[s];
-            }
+
         }
     }
     // the run into the LDS tile, as reduce_entry would add its entries one by one
@@ -1410,21 +1394,7 @@ template <int NV, bool X = false> struct TileRun {
                         if (nn[s]) atomicAdd(reinterpret_cast<double *>(lds + fa.a[k].lds_off) + local, sum2[s]);
                         continue;
                     }
-                    if (is_minmax(kind)) {
-                        const uint32_t code = (tp.skind >> (2 * s)) & 3u;
-                        const bool m = kind == VH_AGG_MAX;
-                        const uint64_t e = m ? mx[s] : mn[s];
-                        // no gated entry (an improving one never encodes as the identity)
-                        if (m ? e == 0 : e == ~0ull) continue;
-                        const double x = code == 0 ? unord_bits(e) : __builtin_bit_cast(double, code == 1 ? e ^ (1ull << 63) : e);
-                        // gated entries improve on the cell as read ahead: the atomic only (no
-                        // second read and wait per run)
-                        if (mm_cell32(fa.a[k].dtype))
-                            mm_lds32<false>(reinterpret_cast<uint32_t *>(lds + fa.a[k].lds_off) + local, fa.a[k].dtype, m, x);
-                        else
-                            mm_lds<false>(reinterpret_cast<uint64_t *>(lds + fa.a[k].lds_off) + local, fa.a[k].dtype, m, x);
-                        continue;
-                    }
+                    if (is_minmax(kind)) continue;  // committed per entry by the caller
                 }
                 if (fa.a[k].vint)
                     atomicAdd(reinterpret_cast<unsigned long long *>(lds + fa.a[k].lds_off) + local, isum[s]);
@@ -1436,6 +1406,11 @@ template <int NV, bool X = false> struct TileRun {
 };
 
 constexpr int TB_UNROLL = 8;
+#ifndef VH_MM_PEEK
+// min / max in pass B: 1 = read the chunk's cells first and commit only improving entries;
+// 0 = a (non-returning) LDS atomic per entry
+#define VH_MM_PEEK 0
+#endif
 #ifndef VH_TB_VU
 #define VH_TB_VU 0  // 8-entry chunks per lane per step (0 = by NV)
 #endif
@@ -1579,25 +1554,33 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                         uint32_t gate = 0;
 #pragma unroll
                         for (int k = 0; k < MAX_FUSED_AGGS; k++) {
-                            if (!((tp.mmk >> k) & 1u)) continue;
+                            if (!((tp.mmk >> k) & 1u) || (DBG(tp.debug) & 256)) continue;  // 256: experiment, no min / max
                             const FusedAgg &a = fa.a[k];
                             const int vs = tp.val_slot[k];
                             const bool m = a.kind == VH_AGG_MAX;
-                            uint64_t cell[8];
+                            if constexpr (VH_MM_PEEK) {
+                                uint64_t cell[8];
 #pragma unroll
-                            for (int x = 0; x < 8; x++) {
-                                const uint32_t local = (uint32_t)x < rem[j] ? (words[x >> 1] >> (16 * (x & 1))) & 0xffffu : 0u;
-                                cell[x] = mm_peek(lds_raw, a, local);
-                            }
-#pragma unroll
-                            for (int x = 0; x < 8; x++) {
-#pragma unroll
-                                for (int s = 0; s < NV; s++) {
-                                    if (s != vs) continue;
-                                    const double vx = (x & 1) ? vv[j][s][x >> 1].y : vv[j][s][x >> 1].x;
-                                    if ((uint32_t)x < rem[j] && mm_improves(a.dtype, m, cell[x], vx))
-                                        gate |= (m ? 2u : 1u) << (4 * x + 2 * s);
+                                for (int x = 0; x < 8; x++) {
+                                    const uint32_t local = (uint32_t)x < rem[j] ? (words[x >> 1] >> (16 * (x & 1))) & 0xffffu : 0u;
+                                    cell[x] = mm_peek(lds_raw, a, local);
                                 }
+#pragma unroll
+                                for (int x = 0; x < 8; x++) {
+#pragma unroll
+                                    for (int s = 0; s < NV; s++) {
+                                        if (s != vs) continue;
+                                        const double vx = (x & 1) ? vv[j][s][x >> 1].y : vv[j][s][x >> 1].x;
+                                        if ((uint32_t)x < rem[j] && mm_improves(a.dtype, m, cell[x], vx))
+                                            gate |= (m ? 2u : 1u) << (4 * x + 2 * s);
+                                    }
+                                }
+                            } else {
+#pragma unroll
+                                for (int x = 0; x < 8; x++)
+#pragma unroll
+                                    for (int s = 0; s < NV; s++)
+                                        if (s == vs && (uint32_t)x < rem[j]) gate |= (m ? 2u : 1u) << (4 * x + 2 * s);
                             }
                         }
                         // the extended run's flush is large: one copy of the entry body in a
@@ -1626,8 +1609,28 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                             double v[NV > 0 ? NV : 1];
 #pragma unroll
                             for (int s = 0; s < NV; s++) v[s] = sv[s][0];
-                            run.add(tp, v, gate & 0xfu);
+                            run.add(tp, v);
+                            // min / max: only entries that improve on their cell as read ahead
+                            // commit (the atomic alone); a wave without one skips the block
+                            const uint32_t g = gate & 0xfu;
                             gate >>= 4;
+                            if (g) {
+#pragma unroll
+                                for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+                                    if (!((tp.mmk >> k) & 1u)) continue;
+                                    const FusedAgg &a = fa.a[k];
+                                    const int vs = tp.val_slot[k];
+                                    const bool m = a.kind == VH_AGG_MAX;
+#pragma unroll
+                                    for (int s = 0; s < NV; s++) {
+                                        if (s != vs || !((g >> (2 * s + (m ? 1 : 0))) & 1u)) continue;
+                                        if (mm_cell32(a.dtype))
+                                            mm_lds32<false>(reinterpret_cast<uint32_t *>(lds_raw + a.lds_off) + local, a.dtype, m, v[s]);
+                                        else
+                                            mm_lds<false>(reinterpret_cast<uint64_t *>(lds_raw + a.lds_off) + local, a.dtype, m, v[s]);
+                                    }
+                                }
+                            }
                             w0 = (w0 >> 16) | (w1 << 16);
                             w1 = (w1 >> 16) | (w2 << 16);
                             w2 = (w2 >> 16) | (w3 << 16);
@@ -2283,11 +2286,6 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
             mm = mm || is_minmax(a.kind) || a.kind == VH_AGG_SUM_MOMENT;
             if (a.kind == VH_AGG_SUM_MOMENT && a.moment != 2) tp.mgeneric = 1;
             if (is_minmax(a.kind)) tp.mmk |= 1u << k;
-            if (is_minmax(a.kind) && tp.val_slot[k] >= 0) {
-                const uint32_t code = (a.dtype == VH_F64 || a.dtype == VH_F32) ? 0u
-                                      : (a.dtype == VH_I64 || a.dtype == VH_I32 || a.dtype == VH_I16 || a.dtype == VH_I8) ? 1u : 2u;
-                tp.skind |= code << (2 * tp.val_slot[k]);
-            }
         }
         uint64_t mm_bytes = 0;
         for (int k = 0; k < fa.na; k++)
