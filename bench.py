@@ -52,14 +52,64 @@ def parse():
     p.add_argument("--breakdown", action="store_true", help="print host-side timing of one step")
     p.add_argument("--no-aggs", action="store_true", help="skip the first / var legs on the C2 grid")
     p.add_argument("--no-set", action="store_true", help="skip the ordered_set.update leg")
+    p.add_argument("--dry-launch", action="store_true",
+                   help="(launcher test) every rank prints its rank environment and exits before any GPU call")
+    p.add_argument("--dry-launch-fail-rank", type=int, default=-1,
+                   help="(launcher test) with --dry-launch, this rank exits with status 3")
     return p.parse_args()
+
+
+def launch_ranks(args, argv):
+    """``--gpus N`` (N > 1) without a launcher: start N rank processes of this script, one per
+    GPU, as torch.distributed.run would (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
+    MASTER_PORT in each child's environment), wait for all of them and return a non-zero
+    status when any fails (the others are then terminated: they would wait at the first
+    collective forever).  The children inherit stdout, so rank 0's JSON line is this
+    command's output.  Runs before anything imports vaex_amd or touches the GPU, and starts
+    children (never exec), so this process stays GPU-free.  Replaces the reference's thread
+    fan-out over chunks (execution.py:214-289) at process-per-GPU granularity."""
+    import socket
+    import subprocess
+    n = args.gpus
+    # two free ports: MASTER_PORT and the host channel's (vaex_amd.comm, VAEX_AMD_COMM_PORT)
+    with socket.socket() as s1, socket.socket() as s2:
+        s1.bind(("127.0.0.1", 0))
+        s2.bind(("127.0.0.1", 0))
+        port, comm_port = s1.getsockname()[1], s2.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), VAEX_AMD_COMM_PORT=str(comm_port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    alive = set(range(n))
+    while alive:
+        for r in sorted(alive):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            alive.discard(r)
+            if c != 0 and rc == 0:
+                print(f"bench.py: rank {r} exited with status {c}; stopping the other ranks", file=sys.stderr, flush=True)
+                rc = c if c > 0 else 1
+                for q in alive:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    return rc
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_launch:
+        print(json.dumps({"rank": rank, "local_rank": local_rank, "world": world, "gpus": args.gpus,
+                          "master_addr": os.environ.get("MASTER_ADDR"), "master_port": os.environ.get("MASTER_PORT"),
+                          "pid": os.getpid()}), flush=True)
+        sys.exit(3 if rank == args.dry_launch_fail_rank else 0)
     dist = None
     import vaex_amd
     from vaex_amd import _lib, superagg
@@ -72,6 +122,9 @@ def main():
     if world > 1 or os.environ.get("BENCH_FORCE_DIST"):
         from vaex_amd import comm as vcomm
         dist = vcomm.init("rccl")
+    # the world RCCL actually reduced over: an all-reduce of one per rank through the
+    # communicator (None without one)
+    rccl_ranks = int(dist.allreduce(np.ones(1, np.int64))[0]) if dist is not None else None
     n = int(args.rows)
     bins = args.bins
     # resident synthetic columns (each rank its own shard: seeds offset by rank)
@@ -221,7 +274,7 @@ def main():
             "metric": BASELINE_METRIC,
             "value": value,
             "unit": "rows/s",
-            "n_gpus": world,
+            "n_gpus": rccl_ranks if rccl_ranks is not None else world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
@@ -236,6 +289,7 @@ def main():
                 "rows_per_gpu": n,
                 "grid": [bins + 3, bins + 3],
                 "parallelism": f"row-shard x{world}" + (" + RCCL grid all-reduce" if world > 1 else ""),
+                "rccl_ranks": rccl_ranks,
             },
             "roofline": roofline,
             "cpu_baseline": cpu,

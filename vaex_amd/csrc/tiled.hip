@@ -112,7 +112,22 @@ struct TileParams {
     // pass B with min / max / moment: mgeneric, a moment other than 2 (per-entry form); mmk, bit
     // k set when aggregator k is a min / max (its cells are read ahead of each chunk)
     uint32_t mgeneric, mmk;
+    // wide stream-out of the fast kernels (batch_commit_fast): every (workgroup, tile) run of
+    // a commit is padded to a multiple of 8 entries with DUMMY_CELL entries, so runs start
+    // 8-aligned in the region and a lane stores 8 cells / 2 float64 values / 4 narrow slots
+    // per 16-byte store; pass B skips the dummies.  lds_cap: staged entries per value slot
+    uint32_t wide, lds_cap;
 };
+
+// local cell of a padding entry (tiles hold at most 2^15 cells when runs are padded)
+constexpr uint32_t DUMMY_CELL = 0xffffu;
+typedef unsigned int vh_u32x4 __attribute__((ext_vector_type(4)));
+typedef double vh_f64x2 __attribute__((ext_vector_type(2)));
+// a 16-byte region store, non-temporal when nt (wave-uniform)
+template <typename V> __device__ __forceinline__ void region_store(V *p, V v, bool nt) {
+    if (nt) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 
 // value of row h (0/1) of a loaded pair of a column of dtype dt, as the 8-byte slot pass A
 // carries (float data as double, integer / bool data as int64 / uint64 bits); `pr` holds
@@ -681,13 +696,17 @@ __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, co
 // The next batch's ranking may start while slower waves still stream: it only touches
 // hist, which the scan already cleared; boff/dbase/sp/sv are rewritten only after the next
 // B1, which every wave reaches after its stream-out.
+// Wide stream-out (tp.wide): a tile's staged run is padded to hp = roundup8(h) entries with
+// DUMMY_CELL keys, so boff, the region bases and dbase stay multiples of 8.
 __device__ inline void fast_scan(const ScatterLds &l, const TileParams &tp, uint32_t T) {
     if (threadIdx.x >= 64) return;
     const uint32_t lane = threadIdx.x;
     const uint32_t per = (T + 63) / 64;
     const uint32_t t0 = lane * per;
+    const uint32_t pad = tp.wide ? 7u : 0u;
+    uint32_t *sk = reinterpret_cast<uint32_t *>(l.sp);
     uint32_t s = 0;
-    for (uint32_t t = t0; t < t0 + per && t < T; t++) s += l.hist[t];
+    for (uint32_t t = t0; t < t0 + per && t < T; t++) s += (l.hist[t] + pad) & ~pad;
     uint32_t inc = s;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -696,11 +715,12 @@ __device__ inline void fast_scan(const ScatterLds &l, const TileParams &tp, uint
     }
     uint32_t acc = inc - s;
     for (uint32_t t = t0; t < t0 + per && t < T; t++) {
-        const uint32_t h = l.hist[t], b = l.base[t], lim = l.lim[t];
+        const uint32_t h0 = l.hist[t], h = (h0 + pad) & ~pad, b = l.base[t], lim = l.lim[t];
         l.boff[t] = acc;
         l.dbase[t] = b - acc;
         l.base[t] = b + h;
         l.hist[t] = 0;
+        for (uint32_t x = h0; x < h; x++) sk[acc + x] = (t << 16) | DUMMY_CELL;
         acc += h;
         if (b + h > lim) {  // rows past the region: reserve them in the tile's spill area
             const uint32_t first = max(b, lim);
@@ -723,7 +743,7 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
                                          uint64_t region0, const uint32_t *key, const int32_t *rank,
                                          const VT (*vals)[NV > 0 ? NV : 1], uint32_t count_mask,
                                          const uint32_t *keyed_slot_of) {
-    constexpr uint32_t CAP = R * TA_THREADS;
+    const uint32_t CAP = tp.lds_cap;  // staged entries per value slot (R * TA_THREADS, + 8 T when wide)
     uint32_t *sk = reinterpret_cast<uint32_t *>(l.sp);
     VT *sv = reinterpret_cast<VT *>(l.sv);
     lds_barrier();
@@ -739,8 +759,9 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
         for (int s = 0; s < NV; s++) sv[s * CAP + pos] = vals[r][s];
     }
     lds_barrier();
-    for (uint32_t k = threadIdx.x; k < tot; k += TA_THREADS) {
-        const uint32_t kk = sk[k];
+    // staged entry k to its region / spill slot, or (past both) to the grid with global
+    // atomics; padding entries (DUMMY_CELL) are stored like rows but never applied
+    auto entry = [&](uint32_t k, uint32_t kk) __attribute__((always_inline)) {
         const uint32_t t = kk >> 16;
         const uint32_t dest = l.dbase[t] + k;
         if (DBG(tp.debug) & 128) {  // experiment: no region stores
@@ -754,7 +775,7 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
                     uint32_t *vb = reinterpret_cast<uint32_t *>(tp.values[0]) + (e & ~uint64_t(7)) * 2 + (e & 7);
                     vb[0] = sv[k];
                     vb[8] = sv[CAP + k];
-                    continue;
+                    return;
                 }
             }
 #pragma unroll
@@ -766,7 +787,7 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
                 else
                     tp.values[s][e] = sv[s * CAP + k];
             }
-        } else {
+        } else if ((kk & 0xffffu) != DUMMY_CELL) {
             // past the region and the spill area: apply the staged row with global atomics
             const uint64_t c = ((uint64_t)t << tp.s_log2) | (kk & 0xffffu);
             atomicAdd(&d_tile_overflow_rows, 1ull);
@@ -797,6 +818,101 @@ __device__ inline void batch_commit_fast(const ScatterLds &l, const FusedAggs &f
                         atomicAdd(reinterpret_cast<double *>(fa.a[a].grid) + c, v);
                 }
             }
+        }
+    };
+    if (!tp.wide) {
+        for (uint32_t k = threadIdx.x; k < tot; k += TA_THREADS) entry(k, sk[k]);
+        return;
+    }
+    // Wide stream-out: runs are padded to 8 entries and start 8-aligned in their regions
+    // (tot, boff, dbase, region bases and region limits are multiples of 8), so an aligned
+    // group of 8 staged entries lies in one tile and wholly inside or wholly past its region.
+    // Cells: one 16-byte store of 8 u16 cells per group; groups past the region take the
+    // per-entry path (spill area / atomics), which also stores their values.
+    uint16_t *ent16 = reinterpret_cast<uint16_t *>(tp.entries);
+    const bool nt_cells = (tp.wide >> 1) & 1, nt_vals = (tp.wide >> 2) & 1;
+    for (uint32_t g = threadIdx.x; g < (tot >> 3); g += TA_THREADS) {
+        const uint32_t k = g << 3;
+        const uint4 a = *reinterpret_cast<const uint4 *>(sk + k), b = *reinterpret_cast<const uint4 *>(sk + k + 4);
+        const uint32_t t = a.x >> 16;
+        const uint32_t dest = l.dbase[t] + k;
+        if (DBG(tp.debug) & 128) {
+            asm volatile("" ::"v"(a.y), "v"(dest));
+        } else if (dest < l.lim[t]) {
+            vh_u32x4 c;
+            c.x = (a.x & 0xffffu) | (a.y << 16);
+            c.y = (a.z & 0xffffu) | (a.w << 16);
+            c.z = (b.x & 0xffffu) | (b.y << 16);
+            c.w = (b.z & 0xffffu) | (b.w << 16);
+            region_store(reinterpret_cast<vh_u32x4 *>(ent16 + region0 + dest), c, nt_cells);
+        } else {
+#pragma unroll 1
+            for (uint32_t x = 0; x < 8; x++) entry(k + x, sk[k + x]);
+        }
+    }
+    if constexpr (NV > 0) {
+        if (DBG(tp.debug) & 128) return;
+        if constexpr (sizeof(VT) == 8) {
+            if (!tp.vnarrow) {
+                // float64 slots: one 16-byte store of 2 values per pair of staged entries; UV
+                // pairs per lane and step, their LDS lookups (key -> tile -> region base)
+                // issued together
+                constexpr int UV = 4;
+                const uint32_t np = tot >> 1;
+                for (uint32_t q0 = threadIdx.x; q0 < np; q0 += UV * TA_THREADS) {
+                    uint32_t kk[UV], dst[UV];
+                    bool ok[UV];
+#pragma unroll
+                    for (int u = 0; u < UV; u++) kk[u] = sk[(q0 + u * TA_THREADS < np ? q0 + u * TA_THREADS : q0) << 1];
+#pragma unroll
+                    for (int u = 0; u < UV; u++) {
+                        const uint32_t t = kk[u] >> 16;
+                        dst[u] = l.dbase[t] + ((q0 + u * TA_THREADS) << 1);
+                        ok[u] = q0 + u * TA_THREADS < np && dst[u] < l.lim[t];  // else: the per-entry path
+                    }
+#pragma unroll
+                    for (int s = 0; s < NV; s++) {
+                        double2 v[UV];
+#pragma unroll
+                        for (int u = 0; u < UV; u++)
+                            v[u] = *reinterpret_cast<const double2 *>(sv + s * CAP + (ok[u] ? (q0 + u * TA_THREADS) << 1 : 0u));
+#pragma unroll
+                        for (int u = 0; u < UV; u++)
+                            if (ok[u]) region_store(reinterpret_cast<vh_f64x2 *>(tp.values[s] + region0 + dst[u]), vh_f64x2{v[u].x, v[u].y}, nt_vals);
+                    }
+                }
+                return;
+            }
+        }
+        // 4-byte slots: one 16-byte store of 4 slots per quad of staged entries
+        for (uint32_t q = threadIdx.x; q < (tot >> 2); q += TA_THREADS) {
+            const uint32_t k = q << 2;
+            const uint32_t t = sk[k] >> 16;
+            const uint32_t dest = l.dbase[t] + k;
+            if (dest >= l.lim[t]) continue;
+            const uint64_t e = region0 + dest;
+            vh_u32x4 w[NV];
+#pragma unroll
+            for (int s = 0; s < NV; s++) {
+                if constexpr (sizeof(VT) == 4) {
+                    const uint4 u = *reinterpret_cast<const uint4 *>(sv + s * CAP + k);
+                    w[s] = vh_u32x4{u.x, u.y, u.z, u.w};
+                } else {
+                    const bool fl = (tp.vfloat >> s) & 1;
+                    w[s] = vh_u32x4{slot_narrow(sv[s * CAP + k], fl), slot_narrow(sv[s * CAP + k + 1], fl),
+                                    slot_narrow(sv[s * CAP + k + 2], fl), slot_narrow(sv[s * CAP + k + 3], fl)};
+                }
+            }
+            if constexpr (sizeof(VT) == 4 && NV == 2) {
+                if (tp.vpacked) {  // [8 x slot 0 | 8 x slot 1] per 8 entries: e & 7 is 0 or 4
+                    uint32_t *vb = reinterpret_cast<uint32_t *>(tp.values[0]) + (e & ~uint64_t(7)) * 2 + (e & 7);
+                    region_store(reinterpret_cast<vh_u32x4 *>(vb), w[0], nt_vals);
+                    region_store(reinterpret_cast<vh_u32x4 *>(vb + 8), w[1], nt_vals);
+                    continue;
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < NV; s++) region_store(reinterpret_cast<vh_u32x4 *>(reinterpret_cast<uint32_t *>(tp.values[s]) + e), w[s], nt_vals);
         }
     }
 }
@@ -982,7 +1098,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan
     constexpr int PAIRS = TA_RPT / 2;
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const uint32_t T = tp.ntiles;
-    const ScatterLds l = fast_lds<NV>(lds_raw, T, SB * TA_BATCH);
+    const ScatterLds l = fast_lds<NV>(lds_raw, T, tp.lds_cap);
     scatter_lds_init(l, tp, T);
     __syncthreads();
     const double *col[NC];
@@ -1141,7 +1257,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
     using VT = std::conditional_t<VN, uint32_t, double>;
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const uint32_t T = tp.ntiles;
-    const ScatterLds l = fast_lds<NV>(lds_raw, T, SB * TA_BATCH, VN ? 4 : 8);
+    const ScatterLds l = fast_lds<NV>(lds_raw, T, tp.lds_cap, VN ? 4 : 8);
     scatter_lds_init(l, tp, T);
     __syncthreads();
     const int32_t *keys = reinterpret_cast<const int32_t *>(p.b[0].data);
@@ -1562,7 +1678,8 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                                 uint64_t cell[8];
 #pragma unroll
                                 for (int x = 0; x < 8; x++) {
-                                    const uint32_t local = (uint32_t)x < rem[j] ? (words[x >> 1] >> (16 * (x & 1))) & 0xffffu : 0u;
+                                    uint32_t local = (uint32_t)x < rem[j] ? (words[x >> 1] >> (16 * (x & 1))) & 0xffffu : 0u;
+                                    local = local == DUMMY_CELL ? 0u : local;
                                     cell[x] = mm_peek(lds_raw, a, local);
                                 }
 #pragma unroll
@@ -1601,7 +1718,12 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
 #pragma unroll 1
                         for (uint32_t x = 0; x < rem[j]; x++) {
                             const uint32_t local = w0 & 0xffffu;
-                            if (local != cur) {
+                            // min / max: only entries that improve on their cell as read ahead
+                            // commit (the atomic alone); a wave without one skips the block
+                            uint32_t g = gate & 0xfu;
+                            gate >>= 4;
+                            if (local == DUMMY_CELL) g = 0;  // run padding (wide pass A)
+                            else if (local != cur) {
                                 if (cur != ~0u) run.flush(fa, tp, lds_raw, cur);
                                 cur = local;
                                 run.clear();
@@ -1609,11 +1731,7 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                             double v[NV > 0 ? NV : 1];
 #pragma unroll
                             for (int s = 0; s < NV; s++) v[s] = sv[s][0];
-                            run.add(tp, v);
-                            // min / max: only entries that improve on their cell as read ahead
-                            // commit (the atomic alone); a wave without one skips the block
-                            const uint32_t g = gate & 0xfu;
-                            gate >>= 4;
+                            if (local != DUMMY_CELL) run.add(tp, v);
                             if (g) {
 #pragma unroll
                                 for (int k = 0; k < MAX_FUSED_AGGS; k++) {
@@ -1647,7 +1765,7 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
 #pragma unroll
                         for (int x = 0; x < 8; x++) {
                             const uint32_t local = (words[x >> 1] >> (16 * (x & 1))) & 0xffffu;
-                            if ((uint32_t)x < rem[j]) {
+                            if ((uint32_t)x < rem[j] && local != DUMMY_CELL) {
                                 if (local != cur) {
                                     if (cur != ~0u) run.flush(fa, tp, lds_raw, cur);
                                     cur = local;
@@ -1677,7 +1795,7 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                             for (int s = 0; s < NV; s++) v[s] = (x & 1) ? vv[j][s][x >> 1].y : vv[j][s][x >> 1].x;
                             const uint32_t local = (words[x >> 1] >> (16 * (x & 1))) & 0xffffu;
                             if (DBG(tp.debug) & 8) asm volatile("" :: "v"(local));
-                            else reduce_entry<NV, MM>(fa, tp, lds_raw, local, 0xfu, v);
+                            else if (local != DUMMY_CELL) reduce_entry<NV, MM>(fa, tp, lds_raw, local, 0xfu, v);
                         }
                     }
                 };
@@ -2053,10 +2171,19 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     const int fast_mode = !(fast || ord) ? 0
                           : narrow_ord  ? 3
                           : fast_lds_bytes(nv, T, (uint32_t)(fast_sb(nv) * TA_BATCH)) <= LDS_MAX_BYTES ? 2 : 1;
-    const size_t lds_a = fast_mode == 3   ? fast_lds_bytes(nv, T, (uint32_t)(fast_sb_narrow(nv) * TA_BATCH), 4)
-                         : fast_mode == 2 ? fast_lds_bytes(nv, T, (uint32_t)(fast_sb(nv) * TA_BATCH))
-                         : fast_mode == 1 ? fast_lds_bytes(nv, T, (uint32_t)TA_BATCH)
-                                          : scatter_lds_bytes(nv, T);
+    // wide stream-out (batch_commit_fast): runs padded to 8 entries, 16-byte region stores;
+    // needs 8 T more staged entries of LDS and tiles below 2^16 - 1 cells (DUMMY_CELL).
+    // VH_TILE_WIDE: bit 0 wide, bit 1 non-temporal cell stores, bit 2 non-temporal value stores
+    const int sb_k = fast_mode == 3 ? fast_sb_narrow(nv) : fast_mode == 2 ? fast_sb(nv) : 1;
+    const uint32_t cap0 = (uint32_t)(sb_k * TA_BATCH);
+    const int vbytes = fast_mode == 3 ? 4 : 8;
+    uint32_t wide_mode = 7;
+    if (const char *e = getenv("VH_TILE_WIDE")) wide_mode = (uint32_t)atoi(e);
+    const bool wide = (wide_mode & 1) && fast_mode != 0 && !flags_mode && S < DUMMY_CELL &&
+                      fast_lds_bytes(nv, T, cap0 + 8 * T, vbytes) <= LDS_MAX_BYTES;
+    tp.wide = wide ? wide_mode : 0u;
+    tp.lds_cap = wide ? cap0 + 8 * T : cap0;
+    const size_t lds_a = fast_mode != 0 ? fast_lds_bytes(nv, T, tp.lds_cap, vbytes) : scatter_lds_bytes(nv, T);
     if (lds_a > LDS_MAX_BYTES) return false;  // very many tiles: the global-atomic path
     int bpc;
     {
@@ -2149,6 +2276,8 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     // a tile) -- half the tile's expected rows when the rows are clustered.
     const uint64_t kbat = (nb + W - 1) / W;  // batches per workgroup (at most)
     const uint64_t rows_per_wg = kbat * TA_BATCH;
+    // wide stream-out: up to 7 padding entries per (workgroup, tile) and commit
+    const uint64_t pad_wg = wide ? 7 * ((kbat + sb_k - 1) / sb_k) : 0;
     std::vector<uint32_t> cap(T), scap(T);
     std::vector<uint64_t> toff(T), sstart(T);
     uint64_t stride = 0, stotal = 0;
@@ -2166,8 +2295,8 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         const bool clustered = var_b > 4.0 * m + 1.0;
         // a clustered tile gets one batch of slack: a workgroup's evenly spaced batches meet a
         // sorted column's tile floor or ceil of K p_t times
-        uint64_t c = (uint64_t)(e * 1.04 + 6.0 * std::sqrt(e + 1.0)) + 32 + (clustered ? TA_BATCH : 0);
-        c = std::min<uint64_t>((c + 7) & ~uint64_t(7), rows_per_wg + 8);
+        uint64_t c = (uint64_t)(e * 1.04 + 6.0 * std::sqrt(e + 1.0)) + 32 + (clustered ? TA_BATCH : 0) + pad_wg;
+        c = std::min<uint64_t>((c + 7) & ~uint64_t(7), rows_per_wg + pad_wg + 8);
         cap[t] = (uint32_t)c;
         toff[t] = stride;
         stride += c;
@@ -2188,13 +2317,14 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
             }
             sc = (uint64_t)std::min(1.25 * (double)n * p_hi, 2.0 * (double)W * excess) + 4 * TA_BATCH;
         }
-        scap[t] = (uint32_t)std::min<uint64_t>((sc + 7) & ~uint64_t(7), (uint64_t)n + 8);
+        if (wide) sc += sc / 4 + 8 * (uint64_t)W;  // padding of the spilled runs
+        scap[t] = (uint32_t)std::min<uint64_t>((sc + 7) & ~uint64_t(7), (uint64_t)n + 8 * (uint64_t)W + 8);
         sstart[t] = stotal;
         stotal += scap[t];
     }
     // pass A keeps region positions in u32 (destination | overflow bit), spill entries below
     // DEST_SPILL
-    if (stride + rows_per_wg >= (uint64_t)DEST_SPILL) return false;
+    if (stride + rows_per_wg + pad_wg >= (uint64_t)DEST_SPILL) return false;
     if (stotal >= (uint64_t)DEST_SPILL) {  // very large launches: shrink the spill areas
         const double f = (double)(DEST_SPILL - 8 * (uint64_t)T) / (double)stotal;
         stotal = 0;
