@@ -172,6 +172,10 @@ int vh_agg_info(const vh_agg *agg, uint64_t *bytes, int *grid_dtype, uint64_t *i
 int vh_agg_download(vh_agg *agg, void *host, uint64_t bytes);
 int vh_agg_upload(vh_agg *agg, const void *host, uint64_t bytes);
 int vh_agg_download_order(vh_agg *agg, void *host, uint64_t bytes); /* AggFirst order grid */
+/* Nonzero cells of grid items [begin, end): out3 = {count, first index, last index} relative to
+ * begin ({0, -1, -1} when none) -- the occupied range of a dense groupby's count(*) grid, found
+ * on the device (groupby.py:484-533 keeps the cells with count > 0). */
+int vh_agg_occupancy(vh_agg *agg, uint64_t begin, uint64_t end, int64_t *out3);
 int vh_agg_upload_order(vh_agg *agg, const void *host, uint64_t bytes);   /* (new) combine across ranks */
 int vh_agg_device_ptr(vh_agg *agg, void **grid_dptr, void **grid2_dptr);
 /* Aggregator.reduce(list) superagg.cpp:160-167, 205-212, 252-259, 354-361, 470-480 */

@@ -209,3 +209,24 @@ def test_first_small_grid_host_chunks():
                             oracle.Binner("scalar", y, vmin=-3, vmax=3, bins=50)], v, o)
     np.testing.assert_array_equal(go, eo)
     np.testing.assert_array_equal(gv, ev)
+
+
+def test_first_large_chunk_index_path_pieces():
+    """An AggFirst-only bin of more than 2^26 HBM rows on a grid neither the tiled engine
+    (grids of <= 12288 cells count as small) nor the LDS kernels (12 B per cell > 96 KB past
+    8192 cells) take: the index path runs in 2^26-row pieces (the chunk itself may be up to
+    2^32 rows); values, order ties across the pieces (earliest row) and NaN orders bit-exact."""
+    rng = np.random.default_rng(31)
+    n = (1 << 26) + 12345
+    x = rng.random(n)
+    y = rng.random(n)
+    v = rng.random(n)
+    o = rng.integers(0, 50, n).astype(np.float64)  # many ties per cell, across the pieces
+    o[::97] = np.nan
+    specs = [("BinnerScalar_float64", x, 0.0, 1.0, 100), ("BinnerScalar_float64", y, 0.0, 1.0, 100)]
+    from vaex_amd import superagg, _lib  # noqa: F401
+    gv, go, _ = _run(specs, v, o)
+    bs = [oracle.Binner("scalar", x, vmin=0.0, vmax=1.0, bins=100), oracle.Binner("scalar", y, vmin=0.0, vmax=1.0, bins=100)]
+    ev, eo = _oracle_first(bs, v, o)
+    np.testing.assert_array_equal(go.view("u8"), eo.ravel(order="F").view("u8"))
+    np.testing.assert_array_equal(gv.view("u8"), ev.ravel(order="F").view("u8"))

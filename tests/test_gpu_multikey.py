@@ -81,7 +81,8 @@ def test_sparse_keys_combine_into_fused_hash(monkeypatch, device):
     res = df.groupby(["k0", "k1"], agg=_agg())
     assert "vh_combine_keys" in calls and "vh_hashagg_create" in calls
     assert res.get_column_names()[:2] == ["k0", "k1"]
-    _check([k0, k1], v, res)
+    _check([k0, k1], v, res, sort_result=True)
+    _check_first_appearance([k0, k1], res, ["k0", "k1"])
 
 
 def test_combined_dense_range_takes_grid_path(monkeypatch):
@@ -95,9 +96,15 @@ def test_combined_dense_range_takes_grid_path(monkeypatch):
     df = _frame([k0, k1], v, True)
     calls = _spy(monkeypatch)
     res = df.groupby(["k0", "k1"], agg=_agg())
+    assert "vh_combine_keys" in calls
+    _check([k0, k1], v, res, sort_result=True)
+    _check_first_appearance([k0, k1], res, ["k0", "k1"])
+    assert res["k0"].to_numpy().dtype == np.int16 and res["k1"].to_numpy().dtype == np.uint32
+    # sort=True: lexicographic (the dense combined range bins as a BinnerOrdinal grid)
+    calls.clear()
+    res = df.groupby(["k0", "k1"], agg=_agg(), sort=True)
     assert "vh_combine_keys" in calls and "vh_hashagg_create" not in calls
     _check([k0, k1], v, res)
-    assert res["k0"].to_numpy().dtype == np.int16 and res["k1"].to_numpy().dtype == np.uint32
 
 
 def test_high_occupancy_keeps_cartesian_grid(monkeypatch):
@@ -147,6 +154,14 @@ def _first_appearance_order(keys):
         combined = combined.astype(np.int64).ravel()
     _, first = np.unique(combined, return_index=True)
     return np.sort(first)
+
+
+def _check_first_appearance(keys, res, names):
+    """Without sort, combined keys ('auto' below the occupancy, or True) come out in the order
+    each combination first appears: GrouperCombined over an ordered_set (groupby.py:313-333)."""
+    first = _first_appearance_order(keys)
+    for nm, k in zip(names, keys):
+        np.testing.assert_array_equal(res[nm].to_numpy(), k[first])
 
 
 def _check_combined(keys, v, res, names, sort):
@@ -349,3 +364,35 @@ def test_aliased_key_columns_share_one_minmax(n, monkeypatch):
     np.testing.assert_array_equal(got["n"].to_numpy(), cnt)
     np.testing.assert_array_equal(got["c"].to_numpy(), c)
     np.testing.assert_allclose(got["s"].to_numpy(), s, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("assume_sparse", [True, "auto"])
+def test_masked_integer_keys_combine_with_null_labels(assume_sparse):
+    """Masked integer keys take the set-ordinal combine (_groupby_combine_sets): a masked row
+    is its key's null group, whose label is masked (None in Grouper.labels, groupby.py:
+    158-168), never the raw value under the mask.  sort=True puts the null group last per
+    key; checked against oracle.groupby_agg(combine=True) on the keys with masked rows
+    replaced by a value above every key (which sorts the same way)."""
+    import vaex_amd
+    rng = np.random.default_rng(81)
+    n = 120_000
+    k0 = rng.integers(0, 700, n).astype(np.int32)
+    k1 = rng.integers(-40, 40, n).astype(np.int32)
+    m0 = np.zeros(n, bool)
+    m0[::13] = True
+    k0_raw = k0.copy()
+    k0_raw[m0] = 5  # the value under the mask must not become a label
+    v = rng.normal(size=n)
+    df = vaex_amd.from_arrays(k0=np.ma.masked_array(k0_raw, mask=m0), k1=k1, v=v)
+    res = df.groupby(["k0", "k1"], agg=_agg(), sort=True, assume_sparse=assume_sparse)
+    sentinel = np.int32(10_000)
+    k0s = np.where(m0, sentinel, k0)
+    exp = oracle.groupby_agg({"k0": k0s, "k1": k1, "v": v}, ["k0", "k1"],
+                             [("n", "count", None), ("v_sum", "sum", "v")], combine=True)
+    g0 = res["k0"].to_numpy()
+    null = exp["k0"] == sentinel
+    assert np.ma.isMaskedArray(g0) and np.array_equal(np.ma.getmaskarray(g0), null)
+    np.testing.assert_array_equal(np.asarray(g0)[~null], exp["k0"][~null])
+    np.testing.assert_array_equal(res["k1"].to_numpy(), exp["k1"])
+    np.testing.assert_array_equal(res["n"].to_numpy(), exp["n"])
+    np.testing.assert_allclose(res["v_sum"].to_numpy(), exp["v_sum"], rtol=1e-6, atol=1e-9)

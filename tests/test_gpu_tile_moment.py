@@ -48,14 +48,24 @@ def test_var_std_c2_grid_tile_path(dtype, stat):
     if stat == "var":
         np.testing.assert_allclose(got, var, rtol=1e-6, atol=1e-12, equal_nan=True)
         return
-    # std = sqrt(m2 / n - mean^2): where the variance is ~0 (one-row cells, equal values) its
-    # rounding residue has either sign, so sqrt is NaN or tiny depending on the summation
-    # order; compare std where the variance is well above the residue
-    ok = np.isfinite(var) & (var > 1e-9)
-    np.testing.assert_allclose(got[ok], var[ok] ** 0.5, rtol=1e-6, atol=1e-12)
-    tiny = np.isfinite(var) & ~ok
-    assert np.all(~np.isfinite(got[tiny]) | (np.abs(got[tiny]) < 1e-4))
-    np.testing.assert_array_equal(np.isnan(var), np.isnan(got) & ~tiny)
+    # std = sqrt(m2 / n - mean^2), checked per class of cell:
+    cnt = oracle.extract_central_part(oracle.compute_grid(bs, "count", data=w.astype(np.float64)))
+    empty, one, many = cnt == 0, cnt == 1, cnt >= 2
+    # empty cells: 0 / 0 on both sides
+    assert np.isnan(got[empty]).all() and np.isnan(var[empty]).all()
+    # one-row cells: the moment is v * v here, so m2 / 1 - (v / 1)^2 is exactly 0 and std is
+    # exactly 0.0; the reference adds pow(v, 2) (superagg.cpp:420,429), which glibc may round one
+    # ulp away from v * v, leaving a +-1-ulp residue there -- a negative one is NaN std
+    np.testing.assert_array_equal(got[one], 0.0)
+    residue = var[one]
+    ulp = np.spacing(np.square(w.astype(np.float64)).max())
+    assert np.all(np.abs(residue) <= ulp), "oracle residue beyond one ulp of v^2"
+    negative = np.flatnonzero(one.ravel() & (var.ravel() < 0))  # the reference's NaN std cells
+    assert np.all(got.ravel()[negative] == 0.0) and np.all(np.isnan(var.ravel()[negative] ** 0.5))
+    # several rows: the variance is far above its rounding residue (w in [1, 4) has no
+    # repeated values within a cell here), rtol 1e-6
+    assert np.all(var[many] > 1e-9)
+    np.testing.assert_allclose(got[many], var[many] ** 0.5, rtol=1e-6, atol=0)
 
 
 def test_sum_moment_with_count_sum_and_min_max():

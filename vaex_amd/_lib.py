@@ -74,6 +74,7 @@ SIGNATURES = {
     "vh_agg_download": (_i32, [_vp, _vp, _u64]),
     "vh_agg_upload": (_i32, [_vp, _vp, _u64]),
     "vh_agg_download_order": (_i32, [_vp, _vp, _u64]),
+    "vh_agg_occupancy": (_i32, [_vp, _u64, _u64, _vp]),
     "vh_agg_upload_order": (_i32, [_vp, _vp, _u64]),
     "vh_agg_device_ptr": (_i32, [_vp, _p(_vp), _p(_vp)]),
     "vh_agg_reduce": (_i32, [_vp, _p(_vp), _i32]),

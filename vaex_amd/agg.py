@@ -105,7 +105,10 @@ class AggregatorDescriptorBasic(AggregatorDescriptor):
         return agg_op_type(grid, *self.agg_args)
 
     def get_result(self, agg_operation):
-        """agg.py:116-120."""
+        """agg.py:116-120.  ``want_occupancy`` (set by a dense groupby on its count(*)): the
+        occupied range of the 1-d grid's central part is found on the device first."""
+        if getattr(self, "want_occupancy", False) and agg_operation.grid.dimensions == 1:
+            self.occupancy = agg_operation.occupancy(2, agg_operation.grid.length1d - 1)
         grid = np.asarray(agg_operation)
         if not self.edges:
             grid = extract_central_part(grid)

@@ -1205,6 +1205,35 @@ void HostPipe::mark_consumed(int b) {
 // ============================================================================
 // C ABI
 // ============================================================================
+namespace {
+// nonzero cells of grid words [begin, end): count, first and last index (+1) -- the occupied
+// range of a dense groupby's count(*) grid (groupby.py:484-533 keeps the cells with count > 0)
+template <typename W>
+__global__ __launch_bounds__(256) void k_occupancy(const W *g, uint64_t begin, uint64_t end, unsigned long long *out) {
+    unsigned long long nnz = 0, first = ~0ull, last = 0;
+    for (uint64_t i = begin + blockIdx.x * 256ull + threadIdx.x; i < end; i += (uint64_t)gridDim.x * 256) {
+        if (g[i] != 0) {
+            nnz++;
+            first = first < i - begin ? first : i - begin;
+            last = i - begin + 1;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        nnz += __shfl_down(nnz, off, 64);
+        const unsigned long long f = __shfl_down(first, off, 64), l = __shfl_down(last, off, 64);
+        first = f < first ? f : first;
+        last = l > last ? l : last;
+    }
+    if ((threadIdx.x & 63) == 0 && nnz) {
+        atomicAdd(&out[0], nnz);
+        atomicMin(&out[1], first);
+        atomicMax(&out[2], last);
+    }
+}
+
+}  // namespace
+
 extern "C" {
 
 int vh_binner_scalar_create(const char *expression, int dtype, int flip, double vmin, double vmax,
@@ -1429,6 +1458,39 @@ int vh_agg_download(vh_agg *a, void *host, uint64_t bytes) {
         copy_to_host(host, a->g.ptr, bytes, stream());
         VH_HIP(hipStreamSynchronize(stream()));
     }
+    VH_API_END
+}
+
+int vh_agg_occupancy(vh_agg *a, uint64_t begin, uint64_t end, int64_t *out3) {
+    VH_API_BEGIN
+    std::lock_guard<std::mutex> lk(a->grid->mu);
+    if (begin > end || end > a->grid->length1d) fail(VH_ERR_ARG, "occupancy range outside the grid");
+    nunique_finalize(a);
+    DevBuf &dres = a->grid->ws.stat;
+    thread_local PinnedBuf hres;
+    dres.ensure(64);
+    hres.ensure(64);
+    auto *d = dres.as<unsigned long long>();
+    const unsigned long long init[3] = {0ull, ~0ull, 0ull};
+    memcpy(hres.ptr, init, sizeof init);
+    VH_HIP(hipMemcpyAsync(d, hres.ptr, sizeof init, hipMemcpyHostToDevice, stream()));
+    const uint64_t n = end - begin;
+    if (n) {
+        const dim3 grd(std::max(1u, std::min(blocks_for(n, 256, 4), 4096u))), blk(256);
+        switch (a->grid_isz) {
+        case 1: hipLaunchKernelGGL(k_occupancy<uint8_t>, grd, blk, 0, stream(), static_cast<const uint8_t *>(a->g.ptr), begin, end, d); break;
+        case 2: hipLaunchKernelGGL(k_occupancy<uint16_t>, grd, blk, 0, stream(), static_cast<const uint16_t *>(a->g.ptr), begin, end, d); break;
+        case 4: hipLaunchKernelGGL(k_occupancy<uint32_t>, grd, blk, 0, stream(), static_cast<const uint32_t *>(a->g.ptr), begin, end, d); break;
+        default: hipLaunchKernelGGL(k_occupancy<uint64_t>, grd, blk, 0, stream(), static_cast<const uint64_t *>(a->g.ptr), begin, end, d);
+        }
+        VH_HIP(hipGetLastError());
+    }
+    VH_HIP(hipMemcpyAsync(hres.ptr, d, sizeof init, hipMemcpyDeviceToHost, stream()));
+    VH_HIP(hipStreamSynchronize(stream()));
+    const auto *r = hres.as<unsigned long long>();
+    out3[0] = (int64_t)r[0];
+    out3[1] = r[0] ? (int64_t)r[1] : -1;
+    out3[2] = r[0] ? (int64_t)r[2] - 1 : -1;
     VH_API_END
 }
 
@@ -1759,29 +1821,66 @@ void run_bin(vh_grid *g, vh_agg *const *aggs, int naggs, uint64_t length) {
             uint64_t *idx = nullptr;
             // AggFirst on a small grid takes the LDS kernels below (no indices)
             const bool first_lds = cells_ok && len && len < (1ull << 32) && 12 * L <= 96 * 1024;
-            for (int k = 0; k < naggs && !idx; k++) {
-                if (tdone[k] || lds_ok(ads[k].kind) || (first_lds && ads[k].kind == VH_AGG_FIRST)) continue;
-                g->ws.idx.ensure(len * 8);
-                idx = g->ws.idx.as<uint64_t>();
+            // per-row grid indices of `n` rows of plan `p` into `out`
+            auto compute_idx = [&](const BinPlan &p, uint64_t n, uint64_t *out) {
                 TimedScope ts("bin_indices");
-                bool hoist = plan.nb > 0;
-                for (int d = 0; d < plan.nb; d++) hoist = hoist && (plan.b[d].kind == 0 || plan.b[d].kind == 1);
+                bool hoist = p.nb > 0;
+                for (int d = 0; d < p.nb; d++) hoist = hoist && (p.b[d].kind == 0 || p.b[d].kind == 1);
                 if (hoist) {
-                    const dim3 cg(blocks_for(len, 256, 8)), cb(256);
-                    for (int d = 0; d < plan.nb; d++) {
-                        const BinnerDev &b = plan.b[d];
+                    const dim3 cg(blocks_for(n, 256, 8)), cb(256);
+                    for (int d = 0; d < p.nb; d++) {
+                        const BinnerDev &b = p.b[d];
                         const int first = d == 0 ? 1 : 0;
                         if (b.kind == 0) {
-                            VH_DISPATCH_DTYPE(b.dtype, T, hipLaunchKernelGGL((k_idx_dim<0, T>), cg, cb, 0, stream(), b, len, idx, first));
+                            VH_DISPATCH_DTYPE(b.dtype, T, hipLaunchKernelGGL((k_idx_dim<0, T>), cg, cb, 0, stream(), b, n, out, first));
                         } else {
-                            VH_DISPATCH_DTYPE(b.dtype, T, hipLaunchKernelGGL((k_idx_dim<1, T>), cg, cb, 0, stream(), b, len, idx, first));
+                            VH_DISPATCH_DTYPE(b.dtype, T, hipLaunchKernelGGL((k_idx_dim<1, T>), cg, cb, 0, stream(), b, n, out, first));
                         }
                         VH_HIP(hipGetLastError());
                     }
                 } else {
-                    hipLaunchKernelGGL(k_indices, dim3(blocks_for(len, 256)), dim3(256), 0, stream(), plan, len, idx);
+                    hipLaunchKernelGGL(k_indices, dim3(blocks_for(n, 256)), dim3(256), 0, stream(), p, n, out);
                     VH_HIP(hipGetLastError());
                 }
+            };
+            // AggFirst-only chunks of HBM columns run up to 2^32 rows (the engines above need no
+            // index buffer); one the engines refused takes the index path in IDX_ROWS pieces, so
+            // its index buffer stays 512 MB (rows numbered from each piece's first row)
+            constexpr uint64_t IDX_ROWS = uint64_t(1) << 26;
+            if (first_only && len > IDX_ROWS) {
+                for (uint64_t s0 = 0; s0 < len; s0 += IDX_ROWS) {
+                    const uint64_t sl = std::min(IDX_ROWS, len - s0);
+                    Stager ss{g->ws, row0 + s0, sl, buf};
+                    BinPlan sp{};
+                    sp.nb = plan.nb;
+                    for (int d = 0; d < sp.nb; d++) sp.b[d] = binner_dev(g->binners[d], g->strides[d], ss);
+                    g->ws.idx.ensure(sl * 8);
+                    uint64_t *sidx = g->ws.idx.as<uint64_t>();
+                    bool any = false;
+                    for (int k = 0; k < naggs; k++) {
+                        if (tdone[k] || first_lds) continue;
+                        if (!any) compute_idx(sp, sl, sidx);
+                        any = true;
+                        const AggDev sad = agg_dev(aggs[k], ss);
+                        TimedScope ts("bin_aggregate");
+                        const dim3 grd(blocks_for(sl, 256)), blk(256);
+                        VH_DISPATCH_DTYPE(sad.dtype, T, {
+                            hipLaunchKernelGGL(k_first_a<T>, grd, blk, 0, stream(), sad, sidx, sl);
+                            hipLaunchKernelGGL(k_first_b<T>, grd, blk, 0, stream(), sad, sidx, sl, row0 + s0);
+                            hipLaunchKernelGGL(k_first_c<T>, dim3(blocks_for(L, 256)), blk, 0, stream(), sad, L, row0 + s0);
+                        });
+                        VH_HIP(hipGetLastError());
+                    }
+                    if (!any) break;
+                }
+                if (!first_lds)
+                    for (int k = 0; k < naggs; k++) tdone[k] = 1;
+            }
+            for (int k = 0; k < naggs && !idx; k++) {
+                if (tdone[k] || lds_ok(ads[k].kind) || (first_lds && ads[k].kind == VH_AGG_FIRST)) continue;
+                g->ws.idx.ensure(len * 8);
+                idx = g->ws.idx.as<uint64_t>();
+                compute_idx(plan, len, idx);
             }
             auto make_cells = [&]() {
                 if (cells) return;

@@ -111,11 +111,13 @@ inline int upcast_dtype(int dtype) {
 // them -- 64 same-address LDS atomics would serialise; otherwise one atomic per taking lane,
 // and rows that do not take (past the range, folded) touch nothing.
 __device__ __forceinline__ int32_t wave_rank(uint32_t *hist, uint32_t t, bool take) {
-    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
     const uint64_t act = __ballot(take);
+    if (!act) return -1;
+    // the bin of the first TAKING lane (lane 0 may be a folded row or past the range)
+    const int lead = __builtin_ctzll(act);
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)t, lead);
     if (__ballot(take && t != t0) == 0) {
-        if (!act) return -1;
-        const int lane = threadIdx.x & 63, lead = __builtin_ctzll(act);
+        const int lane = threadIdx.x & 63;
         uint32_t base = 0;
         if (lane == lead) base = atomicAdd(&hist[t0], (uint32_t)__builtin_popcountll(act));
         base = (uint32_t)__shfl((int)base, lead, 64);

@@ -264,34 +264,16 @@ __device__ inline void mm_lds32(uint32_t *cell, int dt, bool mx, double v) {
         else atomicMin(cell, x);
     }
 }
-// a min / max LDS cell's bits (4-byte cells zero-extended), and whether v would improve on a
-// cell holding them (mm_lds / mm_lds32's filter, without the atomic)
-__device__ inline uint64_t mm_peek(const unsigned char *lds, const FusedAgg &a, uint32_t local) {
-    if (mm_cell32(a.dtype)) return reinterpret_cast<const uint32_t *>(lds + a.lds_off)[local];
-    return reinterpret_cast<const uint64_t *>(lds + a.lds_off)[local];
-}
-__device__ inline bool mm_improves(int dt, bool mx, uint64_t cur, double v) {
+// a carried slot value as an order-preserving u64 (float data: ord_bits; signed: the sign bit
+// flipped; unsigned: the bits) and back, for folding runs of min / max values in registers
+__device__ inline uint64_t mm_okey(int dt, double v) {
     const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    if (mm_cell32(dt)) {
-        if (dt_float(dt)) {
-            if (v != v) return false;
-            const uint32_t o = ord_bits32((float)v), c = (uint32_t)cur;
-            return mx ? o > c : o < c;
-        }
-        if (dt_signed(dt)) {
-            const int x = (int)(int32_t)(int64_t)b, c = (int)(uint32_t)cur;
-            return mx ? x > c : x < c;
-        }
-        const uint32_t x = (uint32_t)b, c = (uint32_t)cur;
-        return mx ? x > c : x < c;
-    }
-    if (dt_float(dt)) {
-        if (v != v) return false;
-        const uint64_t o = ord_bits(v);
-        return mx ? o > cur : o < cur;
-    }
-    if (dt_signed(dt)) return mx ? (long long)b > (long long)cur : (long long)b < (long long)cur;
-    return mx ? b > cur : b < cur;
+    if (dt_float(dt)) return ord_bits(v);
+    return dt_signed(dt) ? b ^ (1ull << 63) : b;
+}
+__device__ inline double mm_unokey(int dt, uint64_t o) {
+    if (dt_float(dt)) return unord_bits(o);
+    return __builtin_bit_cast(double, dt_signed(dt) ? o ^ (1ull << 63) : o);
 }
 
 // a 4-byte cell as the carried-slot bits mm_grid takes
@@ -1522,11 +1504,6 @@ template <int NV, bool X = false> struct TileRun {
 };
 
 constexpr int TB_UNROLL = 8;
-#ifndef VH_MM_PEEK
-// min / max in pass B: 1 = read the chunk's cells first and commit only improving entries;
-// 0 = a (non-returning) LDS atomic per entry
-#define VH_MM_PEEK 0
-#endif
 #ifndef VH_TB_VU
 #define VH_TB_VU 0  // 8-entry chunks per lane per step (0 = by NV)
 #endif
@@ -1603,6 +1580,15 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
         }
         __syncthreads();
     }
+    // per value slot: the dtype of a min / max aggregator on it (-1: none)
+    int mmdt[NV > 0 ? NV : 1];
+#pragma unroll
+    for (int s = 0; s < NV; s++) {
+        mmdt[s] = -1;
+#pragma unroll
+        for (int k = 0; k < MAX_FUSED_AGGS; k++)
+            if (k < fa.na && ((tp.mmk >> k) & 1u) && tp.val_slot[k] == s) mmdt[s] = fa.a[k].dtype;
+    }
     if (!tp.flags_mode) {
         constexpr int VU = MM ? 1 : tb_vu<NV>();  // the run form of min / max / moment plans: one chunk per lane (128 VGPRs at 1024 threads)
         const uint32_t C = s_pre[nw];
@@ -1661,49 +1647,15 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                 for (int j = 0; j < VU; j++) {
                     const uint32_t words[4] = {ev[j].x, ev[j].y, ev[j].z, ev[j].w};
                     if constexpr (MM) {
-                        // min / max: the chunk's 8 cells of each such aggregator are read in one
-                        // go and compared before any atomic (one LDS wait per aggregator, not a
-                        // read-then-atomic round trip per entry; a stale read only lets a no-op
-                        // atomic through, as cells only improve).  gate: 4 bits per entry (bit
-                        // 2s: improves a min of slot s, 2s + 1: a max)
-                        static_assert(NV <= 2, "4 gate bits per entry");
-                        uint32_t gate = 0;
-#pragma unroll
-                        for (int k = 0; k < MAX_FUSED_AGGS; k++) {
-                            if (!((tp.mmk >> k) & 1u) || (DBG(tp.debug) & 256)) continue;  // 256: experiment, no min / max
-                            const FusedAgg &a = fa.a[k];
-                            const int vs = tp.val_slot[k];
-                            const bool m = a.kind == VH_AGG_MAX;
-                            if constexpr (VH_MM_PEEK) {
-                                uint64_t cell[8];
-#pragma unroll
-                                for (int x = 0; x < 8; x++) {
-                                    uint32_t local = (uint32_t)x < rem[j] ? (words[x >> 1] >> (16 * (x & 1))) & 0xffffu : 0u;
-                                    local = local == DUMMY_CELL ? 0u : local;
-                                    cell[x] = mm_peek(lds_raw, a, local);
-                                }
-#pragma unroll
-                                for (int x = 0; x < 8; x++) {
-#pragma unroll
-                                    for (int s = 0; s < NV; s++) {
-                                        if (s != vs) continue;
-                                        const double vx = (x & 1) ? vv[j][s][x >> 1].y : vv[j][s][x >> 1].x;
-                                        if ((uint32_t)x < rem[j] && mm_improves(a.dtype, m, cell[x], vx))
-                                            gate |= (m ? 2u : 1u) << (4 * x + 2 * s);
-                                    }
-                                }
-                            } else {
-#pragma unroll
-                                for (int x = 0; x < 8; x++)
-#pragma unroll
-                                    for (int s = 0; s < NV; s++)
-                                        if (s == vs && (uint32_t)x < rem[j]) gate |= (m ? 2u : 1u) << (4 * x + 2 * s);
-                            }
-                        }
-                        // the extended run's flush is large: one copy of the entry body in a
-                        // run-time loop that takes the head of shift registers (an unrolled loop
-                        // spills; a run-time index into the chunk's arrays -- selects included,
-                        // which the compiler folds into one -- goes through scratch memory)
+                        // min / max: a lane folds each run of one cell in its chunk (an entry
+                        // whose successor is another cell, or the chunk's last, ends the run) in
+                        // an order-preserving u64 form per value slot, and commits the run's
+                        // min / max with one non-returning LDS atomic per aggregator: sorted /
+                        // clustered rows stop paying an atomic per entry on one address, random
+                        // rows (runs of one) pay what a per-entry atomic did.  The extended
+                        // run's flush is large: one copy of the entry body in a run-time loop
+                        // that takes the head of shift registers (an unrolled loop spills; a
+                        // run-time index into the chunk's arrays goes through scratch memory)
                         double sv[NV > 0 ? NV : 1][8];
 #pragma unroll
                         for (int s = 0; s < NV; s++)
@@ -1715,37 +1667,55 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                         uint32_t w0 = words[0], w1 = words[1], w2 = words[2], w3 = words[3];
                         TileRun<NV, true> run;
                         uint32_t cur = ~0u;
+                        uint64_t lo[NV > 0 ? NV : 1], hi[NV > 0 ? NV : 1];
+#pragma unroll
+                        for (int s = 0; s < NV; s++) {
+                            lo[s] = ~0ull;
+                            hi[s] = 0;
+                        }
 #pragma unroll 1
                         for (uint32_t x = 0; x < rem[j]; x++) {
-                            const uint32_t local = w0 & 0xffffu;
-                            // min / max: only entries that improve on their cell as read ahead
-                            // commit (the atomic alone); a wave without one skips the block
-                            uint32_t g = gate & 0xfu;
-                            gate >>= 4;
-                            if (local == DUMMY_CELL) g = 0;  // run padding (wide pass A)
-                            else if (local != cur) {
-                                if (cur != ~0u) run.flush(fa, tp, lds_raw, cur);
-                                cur = local;
-                                run.clear();
-                            }
+                            const uint32_t local = w0 & 0xffffu, next = (w0 >> 16) & 0xffffu;
                             double v[NV > 0 ? NV : 1];
 #pragma unroll
                             for (int s = 0; s < NV; s++) v[s] = sv[s][0];
-                            if (local != DUMMY_CELL) run.add(tp, v);
-                            if (g) {
+                            if (local != DUMMY_CELL) {  // (DUMMY_CELL: run padding of the wide pass A)
+                                if (local != cur) {
+                                    if (cur != ~0u) run.flush(fa, tp, lds_raw, cur);
+                                    cur = local;
+                                    run.clear();
+                                }
+                                run.add(tp, v);
 #pragma unroll
-                                for (int k = 0; k < MAX_FUSED_AGGS; k++) {
-                                    if (!((tp.mmk >> k) & 1u)) continue;
-                                    const FusedAgg &a = fa.a[k];
-                                    const int vs = tp.val_slot[k];
-                                    const bool m = a.kind == VH_AGG_MAX;
+                                for (int s = 0; s < NV; s++) {
+                                    if (mmdt[s] < 0) continue;
+                                    const bool ok = !dt_float(mmdt[s]) || v[s] == v[s];  // NaN never enters
+                                    const uint64_t o = mm_okey(mmdt[s], v[s]);
+                                    lo[s] = ok && o < lo[s] ? o : lo[s];
+                                    hi[s] = ok && o > hi[s] ? o : hi[s];
+                                }
+                                if (x + 1 >= rem[j] || next != local) {
+#pragma unroll
+                                    for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+                                        if (!((tp.mmk >> k) & 1u)) continue;
+                                        const FusedAgg &a = fa.a[k];
+                                        const bool m = a.kind == VH_AGG_MAX;
+#pragma unroll
+                                        for (int s = 0; s < NV; s++) {
+                                            if (s != tp.val_slot[k]) continue;
+                                            const uint64_t o = m ? hi[s] : lo[s];
+                                            if (o == (m ? 0ull : ~0ull)) continue;  // the cell's identity: a no-op
+                                            const double r = mm_unokey(a.dtype, o);
+                                            if (mm_cell32(a.dtype))
+                                                mm_lds32<false>(reinterpret_cast<uint32_t *>(lds_raw + a.lds_off) + local, a.dtype, m, r);
+                                            else
+                                                mm_lds<false>(reinterpret_cast<uint64_t *>(lds_raw + a.lds_off) + local, a.dtype, m, r);
+                                        }
+                                    }
 #pragma unroll
                                     for (int s = 0; s < NV; s++) {
-                                        if (s != vs || !((g >> (2 * s + (m ? 1 : 0))) & 1u)) continue;
-                                        if (mm_cell32(a.dtype))
-                                            mm_lds32<false>(reinterpret_cast<uint32_t *>(lds_raw + a.lds_off) + local, a.dtype, m, v[s]);
-                                        else
-                                            mm_lds<false>(reinterpret_cast<uint64_t *>(lds_raw + a.lds_off) + local, a.dtype, m, v[s]);
+                                        lo[s] = ~0ull;
+                                        hi[s] = 0;
                                     }
                                 }
                             }

@@ -130,7 +130,9 @@ class Expression:
 
     def to_numpy(self):
         v = self.values
-        return v.to_numpy() if isinstance(v, DeviceArray) else np.asarray(v)
+        if isinstance(v, DeviceArray):
+            return v.to_numpy()
+        return v if np.ma.isMaskedArray(v) else np.asarray(v)  # masked columns stay masked
 
     def tolist(self):
         return self.to_numpy().tolist()

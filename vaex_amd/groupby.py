@@ -276,10 +276,11 @@ def groupby_multikey(df, by, agg, sort=False, row_limit=None, combine="auto"):
     integer columns (floats, masked, filtered frames) are combined through their GPU set
     ordinals exactly as the reference does (:func:`_groupby_combine_sets`).
 
-    Group order without ``sort``: ``'auto'`` returns the lexicographic order; ``True``
-    returns the combined grouper's set order, i.e. the order in which each key combination
-    first appears (GrouperCombined over an ordered_set, what the reference produces with
-    one thread), as the single-key ``assume_sparse=True`` route does.
+    Group order without ``sort``: whenever the keys are combined (``True``, or ``'auto'``
+    below the occupancy) the combined grouper's set order, i.e. the order in which each key
+    combination first appears (GrouperCombined over an ordered_set, what the reference
+    produces with one thread), as the single-key ``assume_sparse=True`` route does; the
+    dense cartesian route of ``'auto'`` (enough rows per cell) is sorted per key.
 
     Returns None when the query is not taken here (``combine=False``, or ``'auto'`` with
     keys that do not qualify): the caller takes the grouper-built cartesian GroupBy."""
@@ -293,7 +294,9 @@ def groupby_multikey(df, by, agg, sort=False, row_limit=None, combine="auto"):
     for sp in spans:
         cells *= sp
     names = [name for name, _, _ in ranges]
-    first_order = combine is True and not sort
+    # combined keys (True, or 'auto' below the occupancy): the combined grouper's set order
+    # without sort, as GrouperCombined over an ordered_set gives (groupby.py:313-333)
+    first_order = not sort
     if cells >= 2 ** 62:
         return _groupby_recombine(df, ranges, agg, sort=sort, row_limit=row_limit, combine=combine)
     n = df.length_unfiltered()
@@ -372,7 +375,11 @@ def _groupby_combine_sets(df, by, agg, sort=False, row_limit=None, combine=True)
     for name, g, (key, _, _) in zip(names, groupers, ranges):
         ords = res.columns[key]
         ords = ords.to_numpy() if isinstance(ords, DeviceArray) else np.asarray(ords)
-        columns[name] = np.asarray(g.bin_values)[ords.astype(np.int64)]
+        ords = ords.astype(np.int64)
+        vals = np.asarray(g.bin_values)[ords]
+        if getattr(g, "has_null", False):  # the null group's label is masked (Grouper.labels: None)
+            vals = np.ma.masked_array(vals, mask=ords == g.null_value)
+        columns[name] = vals
     for name, values in res.columns.items():
         if not name.startswith("__vaex_amd_ordinal_"):
             columns[name] = values
@@ -536,12 +543,18 @@ class GroupByBase:
         df = self.df
         grids = {}
         self.counts = None
+        self.count_desc = None
+        dense1 = len(self.by) == 1 and isinstance(self.by[0], GrouperDense)
         for column_name, aggregate in parse_actions(df, actions, self.groupby_expression):
             aggregate.edges = True
+            is_count = isinstance(aggregate, vagg.AggregatorDescriptorBasic) and aggregate.name == "AggCount" \
+                and aggregate.expression == "*" and aggregate.selection in (None, False)
+            if is_count and dense1 and self.counts is None:
+                aggregate.want_occupancy = True  # the occupied range, found on the device
+                self.count_desc = aggregate
             values = df._agg(aggregate, self.binners, delay=True)
             grids[column_name] = values
-            if isinstance(aggregate, vagg.AggregatorDescriptorBasic) and aggregate.name == "AggCount" \
-                    and aggregate.expression == "*" and aggregate.selection in (None, False):
+            if is_count:
                 self.counts = values
         return grids
 
@@ -594,7 +607,11 @@ class GroupBy(GroupByBase):
         has_non_existing_pairs = len(self.by) > 1 or any(getattr(b, "dense", False) for b in self.by)
         counts = self.counts
         if has_non_existing_pairs and counts is None:
-            counts = self.df._agg(vagg.count(edges=True), self.binners, delay=True)
+            desc = vagg.count(edges=True)
+            if len(self.by) == 1 and isinstance(self.by[0], GrouperDense):
+                desc.want_occupancy = True
+                self.count_desc = desc
+            counts = self.df._agg(desc, self.binners, delay=True)
         if len(self.by) == 1 and isinstance(self.by[0], GrouperDense):
             return self._agg_dense(arrays, counts)
         self.df.execute()
@@ -641,7 +658,8 @@ class GroupBy(GroupByBase):
         arrays = {k: extract_central_part(np.asarray(v.get())) for k, v in arrays.items()}
         counts_edges = np.asarray(counts.get())
         central = extract_central_part(counts_edges)
-        nnz, first, last = hostops.occupancy(central)
+        occ = getattr(self.count_desc, "occupancy", None)
+        nnz, first, last = occ if occ is not None else hostops.occupancy(central)
         if g.speculative:
             # keys outside the guessed range sit in the under / overflow cells
             if counts_edges[1] or counts_edges[-1] or nnz == 0:

@@ -129,7 +129,7 @@ def take_columns(cols, idx):
             k = len(todo)
             _lib.call("vh_host_take", k, (ctypes.c_void_p * k)(*[d.ctypes.data for d in dsts]),
                       (ctypes.c_void_p * k)(*[s.ctypes.data for s in srcs]), (ctypes.c_int * k)(*[s.dtype.itemsize for s in srcs]),
-                      idx.ctypes.data, len(idx), max(_threads(), 8))
+                      idx.ctypes.data, len(idx), _threads())
         for i, d in zip(todo, dsts):
             out[i] = d
     for i, c in enumerate(cols):

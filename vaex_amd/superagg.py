@@ -318,6 +318,16 @@ class Aggregator:
         _lib.call("vh_agg_device_ptr", self._handle, ctypes.byref(p), ctypes.byref(p2))
         return p.value
 
+    def occupancy(self, begin=0, end=None):
+        """(nonzero count, first, last) of grid items [begin, end) relative to begin, found on
+        the device ((0, -1, -1) when none): a dense groupby's occupied cells without a scan of
+        the host image."""
+        end = self._grid.length1d if end is None else end
+        self._before_device_use()
+        out = (ctypes.c_int64 * 3)()
+        _lib.call("vh_agg_occupancy", self._handle, int(begin), int(end), out)
+        return int(out[0]), int(out[1]), int(out[2])
+
     def device_order_ptr(self):
         """HBM address of AggFirst's order grid."""
         p, p2 = ctypes.c_void_p(), ctypes.c_void_p()
