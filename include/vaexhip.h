@@ -248,6 +248,15 @@ int vh_hashagg_order_first(vh_hashagg *h, const void *keys, uint64_t n, int loc)
  * (hash_primitives.hpp:96-281).  A prefix of run heads is scanned until every label is seen. */
 int vh_dense_first_order(const void *keys, uint64_t n, int loc, int key_dtype, int64_t vmin, uint64_t span,
                          const int64_t *labels, uint64_t m, int64_t *perm);
+/* groupby(int key, assume_sparse=True) over a dense key range, finished on the device: the
+ * occupied cells of the count(*) grid slice `counts` (range cells, count_isz-byte integers;
+ * cell j is key vmin + j; m of them occupied), ordered by the row each key first appears at
+ * (the ordered_set grouper's order, groupby.py:97-168), each of ncols device columns src[c]
+ * (the aggregators' grid slices, isz[c]-byte items) gathered in that order into the host
+ * buffer dst[c] (m items), and the keys written to labels (m items of label_isz bytes). */
+int vh_dense_first_take(const void *keys, uint64_t n, int loc, int key_dtype, int64_t vmin, uint64_t range,
+                        const void *counts, int count_isz, uint64_t m, int ncols, const void *const *src,
+                        const int *isz, void *const *dst, int label_isz, void *labels);
 /* host: dsts[c][i] = srcs[c][idx[i]] for ncols columns of itemsizes[c] (1/2/4/8) bytes, i < n,
  * on up to `threads` threads */
 int vh_host_take(int ncols, void *const *dsts, const void *const *srcs, const int *itemsizes, const int64_t *idx,

@@ -30,7 +30,7 @@ for layout in layouts:
         _lib.synchronize()
         _lib.timing_enable(False)
         per = {}
-        for name in ("ha_sample", "ha_scatter", "ha_reduce", "ha_finish"):
+        for name in ("ha_sample", "ha_scatter", "ha_scatter_f64", "ha_reduce", "ha_finish"):
             cnt, ms = _lib.timing_read(name)
             if cnt:
                 per[name] = round(ms / cnt, 3)

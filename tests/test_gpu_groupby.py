@@ -361,3 +361,43 @@ def test_small_grid_wide_cells_beyond_fused_budget():
     by = oracle.Binner("scalar", y, vmin=-3, vmax=3, bins=100)
     exp = oracle.extract_central_part(oracle.compute_grid([bx, by], "sum", data=f32))
     np.testing.assert_allclose(got, exp, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("layout", ["holes", "outliers", "host_key"])
+def test_dense_first_order_device_finish(layout):
+    """assume_sparse=True with min / max / sum / count over a dense key range: the grids stay in
+    HBM and vh_dense_first_take gathers the occupied cells in first-appearance order before the
+    read-back (groupby.py:97-168 ordered_set order).  holes: only even keys occur (the
+    occupied cells are compacted on the device); outliers: keys outside the sampled range
+    (the speculative range misses, the exact range reruns); host_key: the key column in host
+    memory (staged for the first-row scan).  Against numpy per key."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(91)
+    n = (1 << 22) + 3
+    keys = rng.integers(0, 150_000, n).astype(np.int32)
+    if layout == "holes":
+        keys = keys * 2
+    out_rows = rng.integers(0, n, 7)
+    if layout == "outliers":
+        keys[out_rows] = np.array([-40_000, -39_999, 400_000, 400_001, 399_000, -1, 150_001], np.int32)
+    v = rng.normal(size=n)
+    v[::29] = np.nan
+    v[out_rows] = 1.5  # one-row groups: not NaN (an all-NaN group keeps the min / max fill)
+    kcol = keys if layout == "host_key" else DeviceArray.from_numpy(keys)
+    df = vaex_amd.from_arrays(key=kcol, v=DeviceArray.from_numpy(v))
+    got = df.groupby("key", agg={"lo": vaex_amd.agg.min("v"), "hi": vaex_amd.agg.max("v"), "s": vaex_amd.agg.sum("v"),
+                                 "n": vaex_amd.agg.count()}, assume_sparse=True)
+    u, first, inv = np.unique(keys, return_index=True, return_inverse=True)
+    order = np.argsort(first)
+    np.testing.assert_array_equal(got["key"].to_numpy(), u[order])
+    assert got["key"].to_numpy().dtype == np.int32
+    lo = np.full(len(u), np.inf)
+    hi = np.full(len(u), -np.inf)
+    np.fmin.at(lo, inv, v)
+    np.fmax.at(hi, inv, v)
+    s = np.bincount(inv, weights=np.nan_to_num(v), minlength=len(u))
+    np.testing.assert_array_equal(got["lo"].to_numpy(), lo[order])
+    np.testing.assert_array_equal(got["hi"].to_numpy(), hi[order])
+    np.testing.assert_array_equal(got["n"].to_numpy(), np.bincount(inv, minlength=len(u))[order])
+    np.testing.assert_allclose(got["s"].to_numpy(), s[order], rtol=1e-6, atol=1e-9)

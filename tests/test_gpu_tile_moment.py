@@ -58,14 +58,24 @@ def test_var_std_c2_grid_tile_path(dtype, stat):
     # ulp away from v * v, leaving a +-1-ulp residue there -- a negative one is NaN std
     np.testing.assert_array_equal(got[one], 0.0)
     residue = var[one]
-    ulp = np.spacing(np.square(w.astype(np.float64)).max())
+    ulp = np.spacing(np.nanmax(np.square(w.astype(np.float64))))
     assert np.all(np.abs(residue) <= ulp), "oracle residue beyond one ulp of v^2"
     negative = np.flatnonzero(one.ravel() & (var.ravel() < 0))  # the reference's NaN std cells
-    assert np.all(got.ravel()[negative] == 0.0) and np.all(np.isnan(var.ravel()[negative] ** 0.5))
-    # several rows: the variance is far above its rounding residue (w in [1, 4) has no
-    # repeated values within a cell here), rtol 1e-6
-    assert np.all(var[many] > 1e-9)
-    np.testing.assert_allclose(got[many], var[many] ** 0.5, rtol=1e-6, atol=0)
+    assert np.all(got.ravel()[negative] == 0.0) and np.all(var.ravel()[negative] < 0)
+    # several rows: m2 / n - mean^2 subtracts two numbers of size m2 / n, so its rounding
+    # residue is a few ulps of m2 / n whatever the summation order; the GPU's variance
+    # (got^2) must match the oracle's within rtol 1e-6 plus that residue, and where the
+    # variance itself is inside the residue (two nearly equal values in a cell) the sign is
+    # the summation order's: std is NaN or below sqrt(residue) -- those cells are few
+    m2n = oracle.extract_central_part(oracle.compute_grid(bs, "sum_moment", data=w.astype(np.float64), moment=2)) / np.maximum(cnt, 1)
+    resid = 16 * np.finfo(np.float64).eps * m2n
+    inside = many & (np.abs(var) <= resid)
+    clear = many & ~inside
+    assert inside.sum() <= 1e-3 * many.sum(), int(inside.sum())
+    np.testing.assert_array_less(np.abs(got[clear] ** 2 - var[clear]), 1e-6 * var[clear] + resid[clear])
+    assert np.all(np.isfinite(got[clear]))
+    g_in = got[inside]
+    assert np.all(np.isnan(g_in) | (g_in ** 2 <= 2 * resid[inside]))
 
 
 def test_sum_moment_with_count_sum_and_min_max():

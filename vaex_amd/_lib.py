@@ -95,6 +95,7 @@ SIGNATURES = {
     "vh_hashagg_read": (_i32, [_vp, _vp, _vp, _p(_vp), _p(_vp)]),
     "vh_hashagg_order_first": (_i32, [_vp, _vp, _u64, _i32]),
     "vh_dense_first_order": (_i32, [_vp, _u64, _i32, _i32, _i64, _u64, _vp, _u64, _vp]),
+    "vh_dense_first_take": (_i32, [_vp, _u64, _i32, _i32, _i64, _u64, _vp, _i32, _u64, _i32, _vp, _vp, _vp, _i32, _vp]),
     "vh_host_take": (_i32, [_i32, _vp, _vp, _vp, _vp, _u64, _i32]),
     "vh_combine_keys": (_i32, [_u64, _i32, _p(_vp), _p(_i32), _p(_i64), _p(_i64), _vp]),
     "vh_dense_rank_i64": (_i32, [_u64, _vp, _vp, _vp, _p(_u64)]),

@@ -185,7 +185,6 @@ struct Workspace {
     DevBuf first_part;                            // small-grid AggFirst: per-workgroup (key, row) partials
     HostPipe pipe;                                // host-column staging
     DevBuf tile_entries, tile_values, tile_meta;  // tiled path
-    DevBuf stat;                                  // small device results (vh_agg_occupancy)
     ~Workspace();
 };
 

@@ -1541,6 +1541,50 @@ __global__ __launch_bounds__(256) void k_widen_u32(const uint32_t *src, uint64_t
     for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) dst[j] = src[j];
 }
 
+// occupied cells of a count grid slice (any integer item size): flag[j] = count[j] != 0
+__global__ __launch_bounds__(256) void k_nz_flags(const void *counts, int isz, uint64_t range, uint32_t *flag) {
+    for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < range; j += (uint64_t)gridDim.x * 256) {
+        uint64_t c;
+        switch (isz) {
+        case 1: c = static_cast<const uint8_t *>(counts)[j]; break;
+        case 2: c = static_cast<const uint16_t *>(counts)[j]; break;
+        case 4: c = static_cast<const uint32_t *>(counts)[j]; break;
+        default: c = static_cast<const uint64_t *>(counts)[j];
+        }
+        flag[j] = c != 0;
+    }
+}
+// gidx[pos[j]] = j for the flagged cells; the group's first row and its index for the sort
+__global__ __launch_bounds__(256) void k_nz_compact(const uint32_t *flag, const uint32_t *pos, uint64_t range,
+                                                    const unsigned long long *first, uint32_t *gidx,
+                                                    unsigned long long *fr, uint32_t *idx) {
+    for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < range; j += (uint64_t)gridDim.x * 256) {
+        if (!flag[j]) continue;
+        const uint32_t g = pos[j];
+        gidx[g] = (uint32_t)j;
+        fr[g] = first[j];
+        idx[g] = g;
+    }
+}
+// out[i] = src[gidx[perm[i]]] (items of isz bytes); labels: out[i] = vmin + gidx[perm[i]] as isz bytes
+__global__ __launch_bounds__(256) void k_take_items(const void *src, int isz, const uint32_t *gidx, const uint32_t *perm,
+                                                    uint64_t m, void *out, int labels, int64_t vmin) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t j = gidx[perm[i]];
+        const uint64_t v = labels ? (uint64_t)(vmin + (int64_t)j)
+                         : isz == 8 ? static_cast<const uint64_t *>(src)[j]
+                         : isz == 4 ? static_cast<const uint32_t *>(src)[j]
+                         : isz == 2 ? static_cast<const uint16_t *>(src)[j]
+                                    : static_cast<const uint8_t *>(src)[j];
+        switch (isz) {
+        case 1: static_cast<uint8_t *>(out)[i] = (uint8_t)v; break;
+        case 2: static_cast<uint16_t *>(out)[i] = (uint16_t)v; break;
+        case 4: static_cast<uint32_t *>(out)[i] = (uint32_t)v; break;
+        default: static_cast<uint64_t *>(out)[i] = v;
+        }
+    }
+}
+
 // combined key of a multi-key groupby: sum_j (key_j - min_j) * mult_j as int64
 // (groupby.py:248-288 _combine: the cartesian ordinal, first key most significant)
 constexpr int HC_MAX_KEYS = 8;
@@ -1762,7 +1806,8 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     for (uint32_t i = 0; i < FINE; i++) sampled += fh[i];
     const double ds = (double)fh[FINE], f1 = (double)fh[FINE + 1], f2 = (double)fh[FINE + 2];
     // clustered keys: most sampled rows equal their next row (a sorted key column)
-    const bool runs = sampled > 0 && (double)fh[FINE + 3] > 0.5 * (double)sampled;
+    bool runs = sampled > 0 && (double)fh[FINE + 3] > 0.5 * (double)sampled;
+    if (const char *e = getenv("VH_HA_RUNS")) runs = atoi(e) != 0;  // A/B: same results either way
     double dest;
     if (sampled >= n) dest = ds;  // every row sampled: exact
     else dest = f2 > 0 ? ds + f1 * f1 / (2 * f2) : ds + f1 * (f1 - 1) / 2;  // Chao1
@@ -2554,6 +2599,103 @@ int vh_dense_first_order(const void *keys, uint64_t n, int loc, int key_dtype, i
     hipLaunchKernelGGL(k_widen_u32, dim3(blocks_for(m, 256, 8)), dim3(256), 0, st, idx2, m, p64);
     VH_HIP(hipGetLastError());
     copy_to_host(perm, p64, 8 * m, st);
+    VH_HIP(hipStreamSynchronize(st));
+    VH_API_END
+}
+
+int vh_dense_first_take(const void *keys, uint64_t n, int loc, int key_dtype, int64_t vmin, uint64_t range,
+                        const void *counts, int count_isz, uint64_t m, int ncols, const void *const *src, const int *isz,
+                        void *const *dst, int label_isz, void *labels) {
+    VH_API_BEGIN
+    if (!key_dtype_ok(key_dtype)) fail(VH_ERR_ARG, "dense_first_take: integer keys only");
+    if (m == 0) return VH_OK;
+    if (range == 0 || m > range || range >= (1ull << 32)) fail(VH_ERR_ARG, "dense_first_take: bad key range");
+    if (resolve_loc(counts, VH_LOC_AUTO) != VH_LOC_DEVICE) fail(VH_ERR_ARG, "dense_first_take: device count grid only");
+    for (int c = 0; c < ncols; c++) {
+        if (resolve_loc(src[c], VH_LOC_AUTO) != VH_LOC_DEVICE) fail(VH_ERR_ARG, "dense_first_take: device columns only");
+        if (isz[c] != 1 && isz[c] != 2 && isz[c] != 4 && isz[c] != 8) fail(VH_ERR_ARG, "dense_first_take: item size");
+    }
+    if (label_isz != 1 && label_isz != 2 && label_isz != 4 && label_isz != 8) fail(VH_ERR_ARG, "dense_first_take: label size");
+    loc = resolve_loc(keys, loc);
+    hipStream_t st = stream();
+    const int kisz = dtype_itemsize(key_dtype);
+    size_t sort_bytes = 0, scan_bytes = 0;
+    VH_HIP(rocprim::radix_sort_pairs(nullptr, sort_bytes, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
+                                     (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)m, 0, 64, st));
+    VH_HIP(rocprim::exclusive_scan(nullptr, scan_bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)range,
+                                   rocprim::plus<uint32_t>(), st));
+    const uint64_t af = (8 * range + 255) & ~255ull, a4r = (4 * range + 255) & ~255ull, a8 = (8 * m + 255) & ~255ull,
+                   a4 = (4 * m + 255) & ~255ull, tb = std::max(sort_bytes, scan_bytes);
+    DevBuf work;
+    work.ensure(af + 2 * a4r + 3 * a8 + 3 * a4 + 256 + tb + 256);
+    char *wb = work.as<char>();
+    auto *first = reinterpret_cast<unsigned long long *>(wb);
+    auto *flag = reinterpret_cast<uint32_t *>(wb + af);
+    auto *pos = reinterpret_cast<uint32_t *>(wb + af + a4r);
+    auto *fr = reinterpret_cast<unsigned long long *>(wb + af + 2 * a4r);
+    auto *fr2 = reinterpret_cast<unsigned long long *>(wb + af + 2 * a4r + a8);
+    void *out = wb + af + 2 * a4r + 2 * a8;  // one gathered column at a time (<= 8 bytes per item)
+    auto *gidx = reinterpret_cast<uint32_t *>(wb + af + 2 * a4r + 3 * a8);
+    auto *idx = reinterpret_cast<uint32_t *>(wb + af + 2 * a4r + 3 * a8 + a4);
+    auto *idx2 = reinterpret_cast<uint32_t *>(wb + af + 2 * a4r + 3 * a8 + 2 * a4);
+    auto *stats = reinterpret_cast<unsigned long long *>(wb + af + 2 * a4r + 3 * a8 + 3 * a4);
+    void *tmp = wb + af + 2 * a4r + 3 * a8 + 3 * a4 + 256;
+    VH_HIP(hipMemsetAsync(first, 0xff, 8 * range, st));
+    VH_HIP(hipMemsetAsync(stats, 0, 16, st));
+    thread_local PinnedBuf res_buf;
+    res_buf.ensure(64);
+    auto *hstats = res_buf.as<unsigned long long>();
+    {
+        TimedScope ts("dense_first");
+        HaScratch &S = scratch();
+        std::lock_guard<std::mutex> lk(S.mu);
+        // every group's first row: the prefix scan of run heads of vh_dense_first_order
+        uint64_t r0 = 0, chunk = std::max<uint64_t>(1u << 20, 4 * m);
+        const bool aligned = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
+        while (r0 < n) {
+            const uint64_t r1 = std::min(n, r0 + (chunk & ~uint64_t(1023)));
+            const void *kp = static_cast<const char *>(keys) + r0 * kisz;
+            if (loc == VH_LOC_HOST || !aligned) {
+                const uint64_t lead = std::min<uint64_t>(r0, 16 / kisz);
+                S.stage.ensure((r1 - r0) * kisz + 64);
+                char *d = S.stage.as<char>() + 16;
+                VH_HIP(hipMemcpyAsync(d - lead * kisz, static_cast<const char *>(keys) + (r0 - lead) * kisz,
+                                      (r1 - r0 + lead) * kisz, hipMemcpyDefault, st));
+                kp = d;
+            }
+            VH_DISPATCH_DTYPE(key_dtype, K, {
+                if constexpr (std::is_integral_v<K>) {
+                    hipLaunchKernelGGL(k_dense_first<K>, dim3(blocks_for((r1 - r0) / (16 / sizeof(K)) + 1, 256, 8)), dim3(256),
+                                       0, st, static_cast<const K *>(kp), r1 - r0, r0, vmin, range, first, stats);
+                }
+            });
+            VH_HIP(hipGetLastError());
+            VH_HIP(hipMemcpyAsync(hstats, stats, 16, hipMemcpyDeviceToHost, st));
+            VH_HIP(hipStreamSynchronize(st));
+            r0 = r1;
+            if (hstats[0] >= m) break;
+            chunk = hstats[1] * 16 > r0 ? chunk + chunk / 2 : chunk * 4;
+        }
+        if (hstats[0] < m) fail(VH_ERR_ARG, "dense_first_take: an occupied cell's key does not occur in the column");
+    }
+    // the occupied cells in key order (flags, exclusive scan, compaction), sorted by first row
+    hipLaunchKernelGGL(k_nz_flags, dim3(blocks_for(range, 256, 8)), dim3(256), 0, st, counts, count_isz, range, flag);
+    size_t sb = scan_bytes;
+    VH_HIP(rocprim::exclusive_scan(tmp, sb, flag, pos, 0u, (size_t)range, rocprim::plus<uint32_t>(), st));
+    hipLaunchKernelGGL(k_nz_compact, dim3(blocks_for(range, 256, 8)), dim3(256), 0, st, flag, pos, range, first, gidx, fr, idx);
+    VH_HIP(hipGetLastError());
+    size_t tbs = sort_bytes;
+    VH_HIP(rocprim::radix_sort_pairs(tmp, tbs, fr, fr2, idx, idx2, (size_t)m, 0, 64, st));
+    // gather every column (and the labels) in that order, read back into the caller's buffers
+    for (int c = 0; c <= ncols; c++) {
+        const bool lab = c == ncols;
+        if (lab && !labels) break;
+        const int z = lab ? label_isz : isz[c];
+        hipLaunchKernelGGL(k_take_items, dim3(blocks_for(m, 256, 8)), dim3(256), 0, st, lab ? nullptr : src[c], z, gidx, idx2, m,
+                           out, lab ? 1 : 0, vmin);
+        VH_HIP(hipGetLastError());
+        copy_to_host(lab ? labels : dst[c], out, (uint64_t)z * m, st);
+    }
     VH_HIP(hipStreamSynchronize(st));
     VH_API_END
 }

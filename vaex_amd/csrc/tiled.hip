@@ -542,6 +542,11 @@ template <int NV> __device__ inline ScatterLds scatter_lds(unsigned char *raw, u
 #define VH_TA_SB0 2  // count-only commits (same-process A/B: 1 -> 2 is 3.99 -> 3.87 ms, 3 is 4.08)
 #endif
 __host__ __device__ constexpr int fast_sb(int nv) { return nv == 0 ? VH_TA_SB0 : nv == 1 ? VH_TA_SB : (VH_TA_SB < 2 ? VH_TA_SB : 2); }
+// the 3-d f64 pass A carries a third binner column: fewer batches per commit keep its
+// registers out of scratch memory (three batches of one value slot spilled 17 VGPRs)
+__host__ __device__ constexpr int fast_sb_nd(int nv, int nd) {
+    return nd < 3 ? fast_sb(nv) : nv >= 2 ? 1 : (fast_sb(nv) < 2 ? fast_sb(nv) : 2);
+}
 // narrow (4-byte) value slots staged as 4 bytes: two carried columns still fit three batches
 __host__ __device__ constexpr int fast_sb_narrow(int nv) { return nv == 0 ? VH_TA_SB0 : VH_TA_SB; }
 
@@ -1668,11 +1673,7 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                         TileRun<NV, true> run;
                         uint32_t cur = ~0u;
                         uint64_t lo[NV > 0 ? NV : 1], hi[NV > 0 ? NV : 1];
-#pragma unroll
-                        for (int s = 0; s < NV; s++) {
-                            lo[s] = ~0ull;
-                            hi[s] = 0;
-                        }
+                        bool open = false;  // a fold of two or more entries is in progress
 #pragma unroll 1
                         for (uint32_t x = 0; x < rem[j]; x++) {
                             const uint32_t local = w0 & 0xffffu, next = (w0 >> 16) & 0xffffu;
@@ -1686,15 +1687,10 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                                     run.clear();
                                 }
                                 run.add(tp, v);
-#pragma unroll
-                                for (int s = 0; s < NV; s++) {
-                                    if (mmdt[s] < 0) continue;
-                                    const bool ok = !dt_float(mmdt[s]) || v[s] == v[s];  // NaN never enters
-                                    const uint64_t o = mm_okey(mmdt[s], v[s]);
-                                    lo[s] = ok && o < lo[s] ? o : lo[s];
-                                    hi[s] = ok && o > hi[s] ? o : hi[s];
-                                }
-                                if (x + 1 >= rem[j] || next != local) {
+                                const bool end = x + 1 >= rem[j] || next != local;
+                                if (!open && end) {
+                                    // a run of one entry (random rows): its value goes straight
+                                    // to the cells, one non-returning atomic per aggregator
 #pragma unroll
                                     for (int k = 0; k < MAX_FUSED_AGGS; k++) {
                                         if (!((tp.mmk >> k) & 1u)) continue;
@@ -1703,19 +1699,42 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
 #pragma unroll
                                         for (int s = 0; s < NV; s++) {
                                             if (s != tp.val_slot[k]) continue;
-                                            const uint64_t o = m ? hi[s] : lo[s];
-                                            if (o == (m ? 0ull : ~0ull)) continue;  // the cell's identity: a no-op
-                                            const double r = mm_unokey(a.dtype, o);
                                             if (mm_cell32(a.dtype))
-                                                mm_lds32<false>(reinterpret_cast<uint32_t *>(lds_raw + a.lds_off) + local, a.dtype, m, r);
+                                                mm_lds32<false>(reinterpret_cast<uint32_t *>(lds_raw + a.lds_off) + local, a.dtype, m, v[s]);
                                             else
-                                                mm_lds<false>(reinterpret_cast<uint64_t *>(lds_raw + a.lds_off) + local, a.dtype, m, r);
+                                                mm_lds<false>(reinterpret_cast<uint64_t *>(lds_raw + a.lds_off) + local, a.dtype, m, v[s]);
                                         }
                                     }
+                                } else {
+                                    // a longer run: folded in registers, committed at its end
 #pragma unroll
                                     for (int s = 0; s < NV; s++) {
-                                        lo[s] = ~0ull;
-                                        hi[s] = 0;
+                                        if (mmdt[s] < 0) continue;
+                                        const bool ok = !dt_float(mmdt[s]) || v[s] == v[s];  // NaN never enters
+                                        const uint64_t o = mm_okey(mmdt[s], v[s]);
+                                        const uint64_t l0 = open ? lo[s] : ~0ull, h0 = open ? hi[s] : 0ull;
+                                        lo[s] = ok && o < l0 ? o : l0;
+                                        hi[s] = ok && o > h0 ? o : h0;
+                                    }
+                                    open = !end;
+                                    if (end) {
+#pragma unroll
+                                        for (int k = 0; k < MAX_FUSED_AGGS; k++) {
+                                            if (!((tp.mmk >> k) & 1u)) continue;
+                                            const FusedAgg &a = fa.a[k];
+                                            const bool m = a.kind == VH_AGG_MAX;
+#pragma unroll
+                                            for (int s = 0; s < NV; s++) {
+                                                if (s != tp.val_slot[k]) continue;
+                                                const uint64_t o = m ? hi[s] : lo[s];
+                                                if (o == (m ? 0ull : ~0ull)) continue;  // the cell's identity: a no-op
+                                                const double r = mm_unokey(a.dtype, o);
+                                                if (mm_cell32(a.dtype))
+                                                    mm_lds32<false>(reinterpret_cast<uint32_t *>(lds_raw + a.lds_off) + local, a.dtype, m, r);
+                                                else
+                                                    mm_lds<false>(reinterpret_cast<uint64_t *>(lds_raw + a.lds_off) + local, a.dtype, m, r);
+                                            }
+                                        }
                                     }
                                 }
                             }
@@ -1865,7 +1884,7 @@ static void launch_scatter(int fast, unsigned grid, size_t lds, const BinPlan &p
                            const TileParams &tp, uint64_t n) {
     if constexpr (ND > 0) {
         if (fast == 2) {
-            hipLaunchKernelGGL((k_tile_scatter_f64<ND, NV, fast_sb(NV)>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
+            hipLaunchKernelGGL((k_tile_scatter_f64<ND, NV, fast_sb_nd(NV, ND)>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
             return;
         }
         if (fast == 1) {
@@ -1894,7 +1913,7 @@ template <int ND, int NV> static int scatter_blocks_per_cu(int fast, size_t lds)
     int nb = 0;
     if constexpr (ND > 0) {
         if (fast == 2) {
-            VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter_f64<ND, NV, fast_sb(NV)>, TA_THREADS, lds));
+            VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter_f64<ND, NV, fast_sb_nd(NV, ND)>, TA_THREADS, lds));
             return nb;
         }
         if (fast == 1) {
@@ -2140,11 +2159,11 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
                             fast_lds_bytes(nv, T, (uint32_t)(fast_sb_narrow(nv) * TA_BATCH), 4) <= LDS_MAX_BYTES;
     const int fast_mode = !(fast || ord) ? 0
                           : narrow_ord  ? 3
-                          : fast_lds_bytes(nv, T, (uint32_t)(fast_sb(nv) * TA_BATCH)) <= LDS_MAX_BYTES ? 2 : 1;
+                          : fast_lds_bytes(nv, T, (uint32_t)(fast_sb_nd(nv, fast ? nd_f64 : 1) * TA_BATCH)) <= LDS_MAX_BYTES ? 2 : 1;
     // wide stream-out (batch_commit_fast): runs padded to 8 entries, 16-byte region stores;
     // needs 8 T more staged entries of LDS and tiles below 2^16 - 1 cells (DUMMY_CELL).
     // VH_TILE_WIDE: bit 0 wide, bit 1 non-temporal cell stores, bit 2 non-temporal value stores
-    const int sb_k = fast_mode == 3 ? fast_sb_narrow(nv) : fast_mode == 2 ? fast_sb(nv) : 1;
+    const int sb_k = fast_mode == 3 ? fast_sb_narrow(nv) : fast_mode == 2 ? fast_sb_nd(nv, fast ? nd_f64 : 1) : 1;
     const uint32_t cap0 = (uint32_t)(sb_k * TA_BATCH);
     const int vbytes = fast_mode == 3 ? 4 : 8;
     uint32_t wide_mode = 7;

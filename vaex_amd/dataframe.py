@@ -639,11 +639,12 @@ class DataFrame:
                 rng = _dense_range(self, key, speculative=_speculate)
                 if rng is not None:
                     try:
-                        res = GroupBy(self, by=by, sort=sort, row_limit=row_limit, dense_ranges={key: rng}).agg(agg)
+                        gb = GroupBy(self, by=by, sort=sort, row_limit=row_limit, dense_ranges={key: rng}, first_order=not sort)
+                        res = gb.agg(agg)
                     except DenseRangeMiss:
                         return self.groupby(by, agg=agg, sort=sort, assume_sparse=assume_sparse, row_limit=row_limit,
                                             _speculate=False)
-                    return res if sort else first_appearance_order(self, key, res)
+                    return res if sort or gb.device_finish else first_appearance_order(self, key, res)
         groupby = GroupBy(self, by=by, sort=sort, row_limit=row_limit,
                           dense=assume_sparse != True or multikey,  # noqa: E712
                           dense_ranges=dense_ranges)

@@ -513,11 +513,15 @@ class GrouperCategory(BinnerBase):
 
 
 class GroupByBase:
-    def __init__(self, df, by, sort=False, row_limit=None, dense=True, dense_ranges=None):
+    def __init__(self, df, by, sort=False, row_limit=None, dense=True, dense_ranges=None, first_order=False):
         df_original = df
         df = df.copy()
         self.df = df
         self.sort = sort
+        # groups in the order their keys first appear (the ordered_set grouper's order without
+        # sort): a dense single key finishes on the device (vh_dense_first_take)
+        self.first_order = first_order
+        self.key_df = df_original
         self.row_limit = row_limit
         if not isinstance(by, (list, tuple)):
             by = [by]
@@ -545,8 +549,18 @@ class GroupByBase:
         self.counts = None
         self.count_desc = None
         dense1 = len(self.by) == 1 and isinstance(self.by[0], GrouperDense)
-        for column_name, aggregate in parse_actions(df, actions, self.groupby_expression):
+        parsed = parse_actions(df, actions, self.groupby_expression)
+        # first-appearance order on the device: every aggregate a plain superagg grid (count /
+        # sum / min / max of a native column, no selection), so its HBM grid is gathered in
+        # that order and read back once (instead of the whole grid plus a host gather)
+        key_col = self.key_df.columns.get(str(self.by[0].expression)) if dense1 else None
+        self.device_finish = self.first_order and dense1 and key_col is not None and \
+            not np.ma.isMaskedArray(key_col) and np.dtype(key_col.dtype).kind in "iu" and all(
+            type(a) is vagg.AggregatorDescriptorBasic and a.name in ("AggCount", "AggSum", "AggMin", "AggMax")
+            and a.selection in (None, False) for _, a in parsed)
+        for column_name, aggregate in parsed:
             aggregate.edges = True
+            aggregate.keep_device = self.device_finish
             is_count = isinstance(aggregate, vagg.AggregatorDescriptorBasic) and aggregate.name == "AggCount" \
                 and aggregate.expression == "*" and aggregate.selection in (None, False)
             if is_count and dense1 and self.counts is None:
@@ -610,6 +624,7 @@ class GroupBy(GroupByBase):
             desc = vagg.count(edges=True)
             if len(self.by) == 1 and isinstance(self.by[0], GrouperDense):
                 desc.want_occupancy = True
+                desc.keep_device = self.device_finish
                 self.count_desc = desc
             counts = self.df._agg(desc, self.binners, delay=True)
         if len(self.by) == 1 and isinstance(self.by[0], GrouperDense):
@@ -655,6 +670,8 @@ class GroupBy(GroupByBase):
             self.df.execute()
         finally:
             labels = labels.result() if labels is not None else None
+        if self.device_finish:
+            return self._agg_dense_device(arrays, counts)
         arrays = {k: extract_central_part(np.asarray(v.get())) for k, v in arrays.items()}
         counts_edges = np.asarray(counts.get())
         central = extract_central_part(counts_edges)
@@ -683,6 +700,57 @@ class GroupBy(GroupByBase):
         columns = {g.label: (np.flatnonzero(mask) + (g.min_value + first)).astype(g.value_dtype)}
         for k, v in arrays.items():
             columns[k] = v[sl][mask]
+        return DataFrame(columns)
+
+
+    def _agg_dense_device(self, arrays, counts):
+        """_agg_dense for the first-appearance order with the grids still in HBM: the occupied
+        range from the device occupancy of the count(*) grid, then vh_dense_first_take gathers
+        every grid's occupied cells in the order their keys first appear in the key column and
+        reads them back (the result of Grouper(sort=False)'s ordered_set order, groupby.py:
+        97-168, 484-533)."""
+        import ctypes
+        from . import _lib
+        from .device import DeviceArray
+        g = self.by[0]
+        aggs = {k: v.get().agg for k, v in arrays.items()}
+        cagg = counts.get().agg
+        L = cagg.grid.length1d
+        nnz, first, last = self.count_desc.occupancy
+        if g.speculative:
+            # keys outside the guessed range sit in the under / overflow cells
+            if cagg.occupancy(1, 2)[0] or cagg.occupancy(L - 1, L)[0] or nnz == 0:
+                raise DenseRangeMiss(g.expression)
+            g.value_dtype = label_dtype(g.key_dtype, g.min_value + first, g.min_value + last)
+        if self.row_limit is not None and nnz > self.row_limit:
+            raise RowLimitException(f"Resulting grouper has {nnz:,} unique combinations, which is "
+                                    f"larger than the allowed row limit of {self.row_limit:,}")
+        label_dt = np.dtype(g.value_dtype)
+        if nnz == 0:
+            columns = {g.label: np.empty(0, label_dt)}
+            for k, a in aggs.items():
+                columns[k] = np.empty(0, a._grid_dtype)
+            return DataFrame(columns)
+        names = list(aggs)
+        outs = [_lib.pinned_empty(nnz, aggs[k]._grid_dtype) for k in names]
+        lab = _lib.pinned_empty(nnz, label_dt)
+        off = 2 + first  # central part starts at cell 2 (extract_central_part)
+        srcs = [aggs[k].device_grid_ptr() + off * aggs[k]._grid_dtype.itemsize for k in names]
+        cisz = cagg._grid_dtype.itemsize
+        key = self.key_df.columns[g.expression]
+        if isinstance(key, DeviceArray):
+            kptr, kloc = key.ptr, _lib.LOC_DEVICE
+        else:
+            key = np.ascontiguousarray(key)
+            kptr, kloc = key.ctypes.data, _lib.LOC_HOST
+        k = len(names)
+        _lib.call("vh_dense_first_take", kptr, self.key_df.length_unfiltered(), kloc, _lib.dtype_code(np.dtype(key.dtype))[0],
+                  ctypes.c_int64(g.min_value + first), last - first + 1, cagg.device_grid_ptr() + off * cisz, cisz, nnz, k,
+                  (ctypes.c_void_p * max(k, 1))(*srcs), (ctypes.c_int * max(k, 1))(*[aggs[n]._grid_dtype.itemsize for n in names]),
+                  (ctypes.c_void_p * max(k, 1))(*[o.ctypes.data for o in outs]), label_dt.itemsize, lab.ctypes.data)
+        columns = {g.label: lab}
+        for name, o in zip(names, outs):
+            columns[name] = o
         return DataFrame(columns)
 
 

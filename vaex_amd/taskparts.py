@@ -73,6 +73,18 @@ def _prepare(block):
     return block
 
 
+class DeviceResult:
+    """An aggregation result left in HBM: the aggregator (its grid, Fortran order with edges).
+    ``np.asarray`` reads the grid back like a plain result."""
+
+    def __init__(self, agg):
+        self.agg = agg
+
+    def __array__(self, dtype=None, copy=None):
+        a = np.asarray(self.agg)
+        return a if dtype is None else a.astype(dtype)
+
+
 class TaskPartAggregation:
     snake_name = "aggregations"
 
@@ -166,6 +178,13 @@ class TaskPartAggregation:
         """cpu.py:592-605."""
         results = []
         for desc, selections, aggs, selection_waslist in self.aggregations:
+            if getattr(desc, "keep_device", False) and len(aggs) == 1 and not selection_waslist:
+                # the caller finishes on the device (a dense groupby in first-appearance order):
+                # the aggregator itself is the result, its grid still in HBM (no read-back)
+                if getattr(desc, "want_occupancy", False) and aggs[0].grid.dimensions == 1:
+                    desc.occupancy = aggs[0].occupancy(2, aggs[0].grid.length1d - 1)
+                results.append(DeviceResult(aggs[0]))
+                continue
             grids = [desc.get_result(agg) for agg in aggs]
             result = np.asarray(grids) if selection_waslist else grids[0]
             dtype_out = np.dtype(desc.dtype_out)
