@@ -14,9 +14,14 @@
 //              order key (order_key: order-preserving u64) and its row are ranked per tile in
 //              LDS, counting-sorted, and streamed as runs into per-(workgroup, tile) regions
 //              sized from the sample (tiled.hip's layout; a run past its region reserves the
-//              tile's spill area).  2 + 8 + 4 bytes per row.  (Per-(XCD, tile) streams with
-//              one reservation atomic per tile and batch were tried: the returning atomics
-//              cost 4.5 of 17 ms of pass A at 1e9 rows.)
+//              tile's spill area).  4 + 8 bytes per row: the order key and one u32 packing
+//              the cell (12 bits), the row's offset in its 4096-row batch (12 bits) and the
+//              low 8 bits of the workgroup's commit index; the row is implied by the region
+//              (workgroup w), the commit index k and the offset: (k W + w) 4096 + offset, with
+//              k's high bits from the region positions where k crossed a multiple of 256
+//              (recorded per (workgroup, tile)).  Spill-area entries also store their row.
+//              (Per-(XCD, tile) streams with one reservation atomic per tile and batch were
+//              tried: the returning atomics cost 4.5 of 17 ms of pass A at 1e9 rows.)
 //   pass B  -- unit = (tile, range of pass-A workgroups) + a slice of the tile's spill area,
 //              read as one stream of 8-entry chunks: per 8192-entry step, phase 1 lowers the
 //              LDS order key of each cell (a row that lowers it resets the cell's row), phase
@@ -58,9 +63,11 @@ struct FirstParams {
     const uint32_t *spill_cap;    // [T]
     const uint64_t *spill_start;  // [T] relative to spill_base
     uint64_t spill_base;
-    uint16_t *ecell;
+    uint32_t *epack;  // cell | batch offset << 12 | commit index (low 8 bits) << 24
     unsigned long long *eokey;
-    uint32_t *erow;
+    uint32_t *erow;   // spill-area entries only: the chunk row
+    uint32_t *kbound; // [W][T][kh]: region position where the commit index reached 256 (j + 1)
+    uint32_t kh;
     unsigned long long *s_key, *s_row;  // the aggregator's per-cell scratch (AggDev)
     uint4 *list;                        // (cell, row, key lo, key hi)
     unsigned long long *list_fill;
@@ -136,7 +143,9 @@ __global__ __launch_bounds__(TF_THREADS) void k_first_scatter(BinPlan p, AggDev 
     const uint64_t n = fp.n;
     // batches w, w + W, w + 2W, ...: every workgroup's rows spread over the whole range; the
     // trip count is uniform within the workgroup (every thread meets every barrier)
-    for (uint64_t b0 = (uint64_t)blockIdx.x * TF_BATCH; b0 < n; b0 += (uint64_t)gridDim.x * TF_BATCH) {
+    static_assert(TF_S_LOG2 <= 12 && TF_BATCH <= 4096, "12-bit cells and batch offsets");
+    uint32_t kc = 0;  // this workgroup's commit index: batch b0 = (kc W + w) TF_BATCH
+    for (uint64_t b0 = (uint64_t)blockIdx.x * TF_BATCH; b0 < n; b0 += (uint64_t)gridDim.x * TF_BATCH, kc++) {
         uint32_t key[TF_RPT];
         int32_t rank[TF_RPT];
         unsigned long long ok[TF_RPT];
@@ -172,8 +181,10 @@ __global__ __launch_bounds__(TF_THREADS) void k_first_scatter(BinPlan p, AggDev 
                 if (lane >= off) inc += y;
             }
             uint32_t acc = inc - s;
+            const bool kb = kc && !(kc & 255u) && (kc >> 8) <= fp.kh;  // k crosses a multiple of 256
             for (uint32_t t = t0; t < t0 + per && t < NT; t++) {
                 const uint32_t h = hist[t], b = fill[t], c = cap[t];
+                if (kb) fp.kbound[((uint64_t)blockIdx.x * NT + t) * fp.kh + (kc >> 8) - 1] = b;
                 boff[t] = acc;
                 sbase[t] = b;
                 fill[t] = b + h;
@@ -194,15 +205,18 @@ __global__ __launch_bounds__(TF_THREADS) void k_first_scatter(BinPlan p, AggDev 
             const uint32_t pos = boff[key[r] >> 16] + (uint32_t)rank[r];
             skey[pos] = key[r];
             sokey[pos] = ok[r];
-            srow[pos] = (uint32_t)(b0 + (uint64_t)r * TF_THREADS + threadIdx.x);
+            srow[pos] = (uint32_t)r * TF_THREADS + threadIdx.x;  // offset in the batch
         }
         // B3: the sorted runs stream out to the regions
         tf_lds_barrier();
         const uint32_t tot = s_tot;
+        const uint32_t packk = (kc & 255u) << 24;
         for (uint32_t k = threadIdx.x; k < tot; k += TF_THREADS) {
             const uint32_t kk = skey[k];
             const uint32_t t = kk >> 16;
             const uint32_t d = sbase[t] + (k - boff[t]);
+            const uint32_t off = srow[k];
+            const uint32_t row = (uint32_t)b0 + off;  // chunk row (< 2^32)
             uint64_t e;
             if (d < cap[t]) {
                 e = wblock + toff[t] + d;
@@ -212,14 +226,14 @@ __global__ __launch_bounds__(TF_THREADS) void k_first_scatter(BinPlan p, AggDev 
                     // past the region and the spill area: straight to s_key and the list
                     const uint32_t c = (t << fp.s_log2) | (kk & 0xffffu);
                     atomicMin(&fp.s_key[c], sokey[k]);
-                    tf_list_push(fp, atomicAdd(fp.list_fill, 1ull), c, srow[k], sokey[k]);
+                    tf_list_push(fp, atomicAdd(fp.list_fill, 1ull), c, row, sokey[k]);
                     continue;
                 }
                 e = fp.spill_base + fp.spill_start[t] + si;
+                fp.erow[e] = row;  // spill entries carry their row (any workgroup, any commit)
             }
-            fp.ecell[e] = (uint16_t)kk;
+            fp.epack[e] = (kk & 0xfffu) | (off << 12) | packk;
             fp.eokey[e] = sokey[k];
-            fp.erow[e] = srow[k];
         }
     }
     tf_lds_barrier();
@@ -288,22 +302,39 @@ __global__ __launch_bounds__(TFB_THREADS) void k_first_reduce(FirstParams fp, co
             e = kk < nwr ? (uint64_t)(u.w0 + kk) * fp.xstride + toff_t + q : eB + q;
             rem = min(8u, s_fill[kk] - q);
         }
-        uint4 cw = make_uint4(0, 0, 0, 0), r0 = cw, r1 = cw;
+        uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, r0 = p0, r1 = p0;
         ulonglong2 k[4] = {};
+        const bool spill = kk >= nwr;
         if (rem) {
-            cw = *reinterpret_cast<const uint4 *>(fp.ecell + e);
+            p0 = *reinterpret_cast<const uint4 *>(fp.epack + e);
+            p1 = *reinterpret_cast<const uint4 *>(fp.epack + e + 4);
 #pragma unroll
             for (int h = 0; h < 4; h++) k[h] = *reinterpret_cast<const ulonglong2 *>(fp.eokey + e + 2 * h);
-            r0 = *reinterpret_cast<const uint4 *>(fp.erow + e);
-            r1 = *reinterpret_cast<const uint4 *>(fp.erow + e + 4);
+            if (spill) {
+                r0 = *reinterpret_cast<const uint4 *>(fp.erow + e);
+                r1 = *reinterpret_cast<const uint4 *>(fp.erow + e + 4);
+            }
         }
-        const uint32_t cws[4] = {cw.x, cw.y, cw.z, cw.w};
-        const uint32_t rows[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+        const uint32_t pk[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+        uint32_t rows[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+        if (rem && !spill) {
+            // region entries: row = (k W + w) TF_BATCH + offset, k's high bits from the region
+            // positions where the commit index crossed multiples of 256
+            const uint32_t w = u.w0 + kk, q0 = (c - s_pre[kk]) * 8;
+            const uint32_t *kb = fp.kbound + ((uint64_t)w * fp.T + t) * fp.kh;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                uint32_t hi = 0;
+                for (uint32_t h = 0; h < fp.kh; h++) hi += q0 + j >= kb[h];
+                const uint32_t kcj = (hi << 8) | (pk[j] >> 24);
+                rows[j] = (kcj * fp.W + w) * (uint32_t)TF_BATCH + ((pk[j] >> 12) & 0xfffu);
+            }
+        }
         // phase 1: lower the cell's order key; the row that lowers it clears the cell's row
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             if ((uint32_t)j >= rem) continue;
-            const uint32_t cl = (cws[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+            const uint32_t cl = pk[j] & 0xfffu;
             const unsigned long long kj = (j & 1) ? k[j >> 1].y : k[j >> 1].x;
             const unsigned long long old = atomicMin(&lkey[cl], kj);
             if (kj < old) lrow[cl] = ~0u;
@@ -313,7 +344,7 @@ __global__ __launch_bounds__(TFB_THREADS) void k_first_reduce(FirstParams fp, co
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             if ((uint32_t)j >= rem) continue;
-            const uint32_t cl = (cws[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+            const uint32_t cl = pk[j] & 0xfffu;
             const unsigned long long kj = (j & 1) ? k[j >> 1].y : k[j >> 1].x;
             if (kj == lkey[cl]) atomicMin(&lrow[cl], rows[j]);
         }
@@ -363,7 +394,7 @@ __global__ __launch_bounds__(256) void k_first_resolve(FirstParams fp, uint64_t 
 
 struct FirstScratch {
     std::mutex mu;
-    DevBuf ecell, eokey, erow, meta, list;
+    DevBuf epack, eokey, erow, meta, list;
 };
 
 static FirstScratch &first_scratch() {
@@ -428,8 +459,10 @@ bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t
     const uint64_t bstride = std::max<uint64_t>(TF_BATCH, n / sblocks);
     const double target = std::max(1.0, (double)n / ((double)cu_count() * 4));
     const uint64_t max_units = (uint64_t)T + 4 * (uint64_t)cu_count() + 16;
+    const uint64_t kbat0 = (nb + W - 1) / W;                   // commits per workgroup (at most)
+    const uint32_t kh = (uint32_t)std::max<uint64_t>(1, (kbat0 + 255) / 256);  // commit-index high parts
     const uint64_t meta_bytes = 16 * (uint64_t)T + 4 * 3 * (uint64_t)T + 8 * (uint64_t)T + 4 * (uint64_t)W * T +
-                                4 * (uint64_t)T + 64 + sizeof(FirstUnit) * max_units + 4096;
+                                4 * (uint64_t)T + 64 + sizeof(FirstUnit) * max_units + 4 * (uint64_t)W * T * kh + 4096;
     ws.meta.ensure(meta_bytes);
     char *mb = ws.meta.as<char>();
     auto carve = [&](uint64_t bytes) {
@@ -446,6 +479,7 @@ bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t
     auto *d_spfill = reinterpret_cast<uint32_t *>(carve(4 * (uint64_t)T));
     auto *d_misc = reinterpret_cast<unsigned long long *>(carve(64));  // [0] list fill, [1] flag
     auto *d_units = reinterpret_cast<FirstUnit *>(carve(sizeof(FirstUnit) * max_units));
+    auto *d_kbound = reinterpret_cast<uint32_t *>(carve(4 * (uint64_t)W * T * kh));
     (void)mb;
     VH_HIP(hipMemsetAsync(d_hist, 0, 16 * (uint64_t)T, st));
     {
@@ -517,9 +551,9 @@ bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t
     }
     if (units.size() > max_units) return false;
     const uint64_t list_cap = (uint64_t)units.size() * S + (1u << 20);
-    ws.ecell.ensure(total * 2);
+    ws.epack.ensure(total * 4);
     ws.eokey.ensure(total * 8);
-    ws.erow.ensure(total * 4);
+    ws.erow.ensure(total * 4);  // spill-area entries only
     ws.list.ensure(list_cap * 16);
     char *upl = stage.as<char>() + 16 * (uint64_t)T;
     auto upload = [&](void *dst, const void *src, uint64_t bytes) {
@@ -535,6 +569,7 @@ bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t
     VH_HIP(hipMemsetAsync(d_sfill, 0, 4 * (uint64_t)W * T, st));
     VH_HIP(hipMemsetAsync(d_spfill, 0, 4 * (uint64_t)T, st));
     VH_HIP(hipMemsetAsync(d_misc, 0, 64, st));
+    VH_HIP(hipMemsetAsync(d_kbound, 0xff, 4 * (uint64_t)W * T * kh, st));  // boundaries never reached: none
     FirstParams fp{};
     fp.T = T;
     fp.W = W;
@@ -549,9 +584,11 @@ bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t
     fp.spill_cap = d_scap;
     fp.spill_start = d_sstart;
     fp.spill_base = (uint64_t)W * xstride;
-    fp.ecell = ws.ecell.as<uint16_t>();
+    fp.epack = ws.epack.as<uint32_t>();
     fp.eokey = ws.eokey.as<unsigned long long>();
     fp.erow = ws.erow.as<uint32_t>();
+    fp.kbound = d_kbound;
+    fp.kh = kh;
     fp.s_key = static_cast<unsigned long long *>(ad.s_key);
     fp.s_row = static_cast<unsigned long long *>(ad.s_row);
     fp.list = ws.list.as<uint4>();

@@ -1522,8 +1522,8 @@ template <int NV> constexpr int tb_vu() { return VH_TB_VU ? VH_TB_VU : NV == 0 ?
 // flushed with coalesced global atomics.
 // MG: a moment other than 2 (per-entry form; its own instantiation, so the run form's
 // registers are not sized for it)
-template <int NV, bool NARROW = false, bool MM = false, bool PK = false, bool MG = false>
-__global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TileParams tp, const WorkUnit *units) {
+template <int NV, bool NARROW = false, bool MM = false, bool PK = false, bool MG = false, int TBT = TB_THREADS>
+__global__ __launch_bounds__(TBT) void k_tile_reduce(FusedAggs fa, TileParams tp, const WorkUnit *units) {
     static_assert(!PK || (NV == 2 && NARROW), "packed pairs of narrow slots");
     extern __shared__ __align__(16) unsigned char lds_raw[];
     __shared__ uint32_t s_fill[1024 + 1];
@@ -1540,14 +1540,14 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
     const uint32_t s1 = part + 1 >= parts ? F : min(F, (uint32_t)((uint64_t)F * (part + 1) / parts) & ~7u);
     const uint64_t spill0 = tp.spill_base + tp.spill_start[t] + s0;  // first entry of the slice
     bool any = false;
-    for (uint32_t k = threadIdx.x; k < nw; k += TB_THREADS) {
+    for (uint32_t k = threadIdx.x; k < nw; k += TBT) {
         const uint32_t f = k < nwr ? min(tp.fills[(uint64_t)t * tp.W + u.w_begin + k], cap) : (s1 > s0 ? s1 - s0 : 0u);
         s_fill[k] = f;
         any |= f != 0;
     }
     if (!__syncthreads_or(any)) return;
     uint32_t *lw = reinterpret_cast<uint32_t *>(lds_raw);
-    for (uint32_t i = threadIdx.x; i < fa.lds_words; i += TB_THREADS) lw[i] = 0;
+    for (uint32_t i = threadIdx.x; i < fa.lds_words; i += TBT) lw[i] = 0;
     if (!tp.flags_mode && threadIdx.x < 64) {
         // exclusive scan of the chunk counts by the first wave (per regions per lane)
         const uint32_t lane = threadIdx.x, per = (nw + 63) / 64, k0 = lane * per;
@@ -1576,12 +1576,12 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
             if (mm_cell32(fa.a[k].dtype)) {
                 uint32_t *cells = reinterpret_cast<uint32_t *>(lds_raw + fa.a[k].lds_off);
                 const uint32_t id = mm_identity32(fa.a[k].dtype, fa.a[k].kind == VH_AGG_MAX);
-                for (uint32_t i = threadIdx.x; i < ncells; i += TB_THREADS) cells[i] = id;
+                for (uint32_t i = threadIdx.x; i < ncells; i += TBT) cells[i] = id;
                 continue;
             }
             uint64_t *cells = reinterpret_cast<uint64_t *>(lds_raw + fa.a[k].lds_off);
             const uint64_t id = mm_identity(fa.a[k].dtype, fa.a[k].kind == VH_AGG_MAX);
-            for (uint32_t i = threadIdx.x; i < ncells; i += TB_THREADS) cells[i] = id;
+            for (uint32_t i = threadIdx.x; i < ncells; i += TBT) cells[i] = id;
         }
         __syncthreads();
     }
@@ -1595,18 +1595,21 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
             if (k < fa.na && ((tp.mmk >> k) & 1u) && tp.val_slot[k] == s) mmdt[s] = fa.a[k].dtype;
     }
     if (!tp.flags_mode) {
-        constexpr int VU = MM ? 1 : tb_vu<NV>();  // the run form of min / max / moment plans: one chunk per lane (128 VGPRs at 1024 threads)
+        // the run form of min / max / moment plans: one chunk per lane (128 VGPRs at 1024
+        // threads; a 512-thread form with two chunks and the entry loop unrolled kept 176 B per
+        // lane in scratch memory and ran pass B at 10.6 against 5.5 ms)
+        constexpr int VU = MM ? 1 : tb_vu<NV>();
         const uint32_t C = s_pre[nw];
         const uint16_t *ent16 = reinterpret_cast<const uint16_t *>(tp.entries);
         const uint64_t toff_t = tp.toff[t];
         uint32_t kk = 0;  // region of this lane's current chunk
-        for (uint32_t c0 = 0; c0 < C; c0 += TB_THREADS * VU) {
+        for (uint32_t c0 = 0; c0 < C; c0 += TBT * VU) {
             uint4 ev[VU];
             double2 vv[VU][NV > 0 ? NV : 1][4];
             uint32_t rem[VU];
 #pragma unroll
             for (int j = 0; j < VU; j++) {
-                const uint32_t c = c0 + j * TB_THREADS + threadIdx.x;
+                const uint32_t c = c0 + j * TBT + threadIdx.x;
                 const uint32_t cc = c < C ? c : C - 1;
                 while (s_pre[kk + 1] <= cc) kk++;
                 const uint32_t q = (cc - s_pre[kk]) * 8;
@@ -1674,8 +1677,7 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                         uint32_t cur = ~0u;
                         uint64_t lo[NV > 0 ? NV : 1], hi[NV > 0 ? NV : 1];
                         bool open = false;  // a fold of two or more entries is in progress
-#pragma unroll 1
-                        for (uint32_t x = 0; x < rem[j]; x++) {
+                        auto entry = [&](uint32_t x) __attribute__((always_inline)) {
                             const uint32_t local = w0 & 0xffffu, next = (w0 >> 16) & 0xffffu;
                             double v[NV > 0 ? NV : 1];
 #pragma unroll
@@ -1746,7 +1748,9 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                             for (int s = 0; s < NV; s++)
 #pragma unroll
                                 for (int h = 0; h < 7; h++) sv[s][h] = sv[s][h + 1];
-                        }
+                        };
+#pragma unroll 1
+                        for (uint32_t x = 0; x < rem[j]; x++) entry(x);
                         if (cur != ~0u) run.flush(fa, tp, lds_raw, cur);
                     } else {
                         TileRun<NV, false> run;
@@ -1806,12 +1810,12 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
             // min / max plans: fewer entries in flight (8 inlined reduce_entry bodies of two
             // slots spill)
             constexpr int UN = MM && NV > 1 ? 2 : TB_UNROLL;
-            for (uint32_t q0 = 0; q0 < cnt; q0 += TB_THREADS * UN) {
+            for (uint32_t q0 = 0; q0 < cnt; q0 += TBT * UN) {
                 uint32_t ent[UN];
                 double v[UN][NV > 0 ? NV : 1];
 #pragma unroll
                 for (int j = 0; j < UN; j++) {
-                    const uint32_t q = q0 + j * TB_THREADS + threadIdx.x;
+                    const uint32_t q = q0 + j * TBT + threadIdx.x;
                     if (q < cnt) {
                         const uint64_t e = base + q;
                         ent[j] = reinterpret_cast<const uint32_t *>(tp.entries)[e];
@@ -1827,7 +1831,7 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
                 }
 #pragma unroll
                 for (int j = 0; j < UN; j++) {
-                    const uint32_t q = q0 + j * TB_THREADS + threadIdx.x;
+                    const uint32_t q = q0 + j * TBT + threadIdx.x;
                     if (q < cnt) reduce_entry<NV, MM>(fa, tp, lds_raw, ent[j] & 0xffffu, ent[j] >> 16, v[j]);
                 }
             }
@@ -1840,7 +1844,7 @@ __global__ __launch_bounds__(TB_THREADS) void k_tile_reduce(FusedAggs fa, TilePa
     #pragma unroll
     for (int k = 0; k < MAX_FUSED_AGGS; k++) {
         if (k >= fa.na) break;
-        for (uint32_t i = threadIdx.x; i < ncell; i += TB_THREADS) {
+        for (uint32_t i = threadIdx.x; i < ncell; i += TBT) {
             if (fa.a[k].kind == VH_AGG_COUNT) {
                 const uint32_t v = reinterpret_cast<const uint32_t *>(lds_raw + fa.a[k].lds_off)[i];
                 if (v) atomicAdd((unsigned long long *)fa.a[k].grid + c0 + i, (unsigned long long)v);
