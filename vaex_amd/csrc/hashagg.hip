@@ -855,6 +855,20 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTab
                 const uint64_t heads = __builtin_popcountll(__ballot(!cin)) + __builtin_popcountll(__ballot(!same));
                 const bool all_in = __ballot(i0 >= row_end) == 0;
                 if (!all_in || heads > 16) continue;  // wave-uniform
+                if (__ballot(!same || (lane > 0 && !cin)) == 0) {
+                    // the wave's 128 rows hold one key (a long run of a sorted column): a plain
+                    // wave reduction instead of the segmented scan, one HBM-table update
+                    double sv = 0.0;
+                    if constexpr (NV > 0) sv = (v0 == v0 ? v0 : 0.0) + (v1 == v1 ? v1 : 0.0);
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) sv += __shfl_xor(sv, off, 64);
+                    HaRun r{128u, 0u, sv};
+                    if constexpr (NV > 0)
+                        r.nn = (uint32_t)(__builtin_popcountll(__ballot(v0 == v0)) + __builtin_popcountll(__ballot(v1 == v1)));
+                    if (lane == 63) ha_global_run<NV>(g, (uint64_t)k1, r, &s_new);
+                    folded[q] = true;
+                    continue;
+                }
                 // segmented inclusive scan of the run through row 2l+1 (flag: starts in this lane)
                 HaRun a = same ? ha_run_add(ha_run_of(v0), ha_run_of(v1)) : ha_run_of(v1);
                 bool f = !(same && cin);

@@ -117,6 +117,12 @@ struct TileParams {
     // 8-aligned in the region and a lane stores 8 cells / 2 float64 values / 4 narrow slots
     // per 16-byte store; pass B skips the dummies.  lds_cap: staged entries per value slot
     uint32_t wide, lds_cap;
+    // min / max pass B on one float64 value slot with at most one count, sum, min and max
+    // aggregator of it (no moments, no integer sums): a branch-light entry loop (mm_simple);
+    // LDS byte offsets of the count / sum / min / max cells (-1: absent), the count keyed on
+    // the slot's non-NaN values (mm_cnt_nn) or on every entry
+    uint32_t mm_simple, mm_cnt_nn;
+    int32_t mm_off[4];
 };
 
 // local cell of a padding entry (tiles hold at most 2^15 cells when runs are padded)
@@ -1654,6 +1660,52 @@ __global__ __launch_bounds__(TBT) void k_tile_reduce(FusedAggs fa, TileParams tp
 #pragma unroll
                 for (int j = 0; j < VU; j++) {
                     const uint32_t words[4] = {ev[j].x, ev[j].y, ev[j].z, ev[j].w};
+                    if constexpr (MM && NV == 1 && !NARROW) {
+                        if (tp.mm_simple) {
+                            // one float64 slot, count / sum / min / max of it: the run of one
+                            // cell folds all four in registers (min / max as order-preserving
+                            // bits) and commits with one LDS atomic per aggregator at its end
+                            const double vx[8] = {vv[j][0][0].x, vv[j][0][0].y, vv[j][0][1].x, vv[j][0][1].y,
+                                                  vv[j][0][2].x, vv[j][0][2].y, vv[j][0][3].x, vv[j][0][3].y};
+                            const int oc = tp.mm_off[0], osm = tp.mm_off[1], omn = tp.mm_off[2], omx = tp.mm_off[3];
+                            const bool cnn = tp.mm_cnt_nn;
+                            uint32_t cur = ~0u, rc = 0, rn = 0;
+                            double rs = 0.0;
+                            uint64_t rlo = ~0ull, rhi = 0;
+                            auto commit = [&]() __attribute__((always_inline)) {
+                                if (oc >= 0 && (cnn ? rn : rc)) atomicAdd(reinterpret_cast<uint32_t *>(lds_raw + oc) + cur, cnn ? rn : rc);
+                                if (rn) {
+                                    if (osm >= 0) atomicAdd(reinterpret_cast<double *>(lds_raw + osm) + cur, rs);
+                                    if (omn >= 0) atomicMin(reinterpret_cast<unsigned long long *>(lds_raw + omn) + cur, (unsigned long long)rlo);
+                                    if (omx >= 0) atomicMax(reinterpret_cast<unsigned long long *>(lds_raw + omx) + cur, (unsigned long long)rhi);
+                                }
+                            };
+#pragma unroll
+                            for (int x = 0; x < 8; x++) {
+                                const uint32_t local = (words[x >> 1] >> (16 * (x & 1))) & 0xffffu;
+                                if ((uint32_t)x >= rem[j] || local == DUMMY_CELL) continue;
+                                if (local != cur) {
+                                    if (cur != ~0u) commit();
+                                    cur = local;
+                                    rc = rn = 0;
+                                    rs = 0.0;
+                                    rlo = ~0ull;
+                                    rhi = 0;
+                                }
+                                const double v = vx[x];
+                                rc++;
+                                if (v == v) {
+                                    const uint64_t o = ord_bits(v);
+                                    rn++;
+                                    rs += v;
+                                    rlo = o < rlo ? o : rlo;
+                                    rhi = o > rhi ? o : rhi;
+                                }
+                            }
+                            if (cur != ~0u) commit();
+                            continue;
+                        }
+                    }
                     if constexpr (MM) {
                         // min / max: a lane folds each run of one cell in its chunk (an entry
                         // whose successor is another cell, or the chunk's last, ends the run) in
@@ -2409,6 +2461,33 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
             mm = mm || is_minmax(a.kind) || a.kind == VH_AGG_SUM_MOMENT;
             if (a.kind == VH_AGG_SUM_MOMENT && a.moment != 2) tp.mgeneric = 1;
             if (is_minmax(a.kind)) tp.mmk |= 1u << k;
+        }
+        // the branch-light form: one float64 value slot (8-byte), at most one count, sum, min and
+        // max of it, count(*) or the count of its non-NaN values
+        {
+            bool simple = mm && !tp.mgeneric && nv == 1 && !vnarrow && !flags_mode;
+            int off[4] = {-1, -1, -1, -1};
+            uint32_t cnn = 0;
+            for (int k = 0; k < fa.na && simple; k++) {
+                const FusedAgg &a = fa.a[k];
+                const int slot = a.kind == VH_AGG_COUNT ? -1 : tp.val_slot[k];
+                int r = -1;
+                if (a.kind == VH_AGG_COUNT) {
+                    r = 0;
+                    if (tp.cnt_slot[k] == 0) cnn = 1;
+                    else if (tp.cnt_slot[k] != CNT_ALWAYS) simple = false;
+                } else if (a.kind == VH_AGG_SUM && !a.vint && a.dtype == VH_F64 && slot == 0) r = 1;
+                else if (a.kind == VH_AGG_MIN && a.dtype == VH_F64 && slot == 0) r = 2;
+                else if (a.kind == VH_AGG_MAX && a.dtype == VH_F64 && slot == 0) r = 3;
+                else simple = false;
+                if (r >= 0) {
+                    if (off[r] >= 0) simple = false;  // two of one kind
+                    else off[r] = (int)a.lds_off;
+                }
+            }
+            tp.mm_simple = simple ? 1u : 0u;
+            tp.mm_cnt_nn = cnn;
+            for (int r = 0; r < 4; r++) tp.mm_off[r] = off[r];
         }
         uint64_t mm_bytes = 0;
         for (int k = 0; k < fa.na; k++)
