@@ -844,6 +844,9 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTab
 #pragma unroll
         for (int q = 0; q < PAIRS; q++) folded[q] = false;
         if constexpr (RUNS) {
+            bool pend = false;  // a run of uniform groups not yet in the HBM table
+            uint32_t pkey = 0;
+            HaRun prun{0u, 0u, 0.0};
 #pragma unroll
             for (int q = 0; q < PAIRS; q++) {
                 const uint64_t i0 = b0 + 2 * ((uint64_t)q * HA_THREADS + threadIdx.x);
@@ -857,7 +860,8 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTab
                 if (!all_in || heads > 16) continue;  // wave-uniform
                 if (__ballot(!same || (lane > 0 && !cin)) == 0) {
                     // the wave's 128 rows hold one key (a long run of a sorted column): a plain
-                    // wave reduction instead of the segmented scan, one HBM-table update
+                    // wave reduction instead of the segmented scan; consecutive such groups of
+                    // one key add up in (wave-uniform) registers, one HBM-table update per key
                     double sv = 0.0;
                     if constexpr (NV > 0) sv = (v0 == v0 ? v0 : 0.0) + (v1 == v1 ? v1 : 0.0);
 #pragma unroll
@@ -865,7 +869,15 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTab
                     HaRun r{128u, 0u, sv};
                     if constexpr (NV > 0)
                         r.nn = (uint32_t)(__builtin_popcountll(__ballot(v0 == v0)) + __builtin_popcountll(__ballot(v1 == v1)));
-                    if (lane == 63) ha_global_run<NV>(g, (uint64_t)k1, r, &s_new);
+                    const uint32_t ku = (uint32_t)__builtin_amdgcn_readfirstlane((int)k1);
+                    if (pend && pkey == ku) {
+                        prun = ha_run_add(prun, r);
+                    } else {
+                        if (pend && lane == 63) ha_global_run<NV>(g, (uint64_t)pkey, prun, &s_new);
+                        pend = true;
+                        pkey = ku;
+                        prun = r;
+                    }
                     folded[q] = true;
                     continue;
                 }
@@ -890,6 +902,7 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTab
                 if (!cin_next) ha_global_run<NV>(g, (uint64_t)k1, a, &s_new);
                 folded[q] = true;
             }
+            if (pend && lane == 63) ha_global_run<NV>(g, (uint64_t)pkey, prun, &s_new);
         }
 #pragma unroll
         for (int r = 0; r < HA_RPT; r++) {
@@ -922,8 +935,17 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTab
             rows(b0 + (uint64_t)sb * bstep, cur, kb + sb * HA_RPT, rank + sb * HA_RPT, vals + sb * HA_RPT);
             cur = nxt;
         }
-        // B1: every rank taken -> wave 0 scans the histogram
-        ha_lds_barrier();
+        // B1: every rank taken -> wave 0 scans the histogram.  A commit whose rows were all
+        // folded into runs (sorted keys) has nothing to partition: the scan, staging and
+        // stream-out are skipped
+        bool took = false;
+        if constexpr (RUNS) {
+#pragma unroll
+            for (int r = 0; r < SB * HA_RPT; r++) took = took || rank[r] >= 0;
+            if (!__syncthreads_or(took)) continue;
+        } else {
+            ha_lds_barrier();
+        }
         if (threadIdx.x < 64) {
             const uint32_t per = (P + 63) / 64;
             const uint32_t t0 = lane * per;
