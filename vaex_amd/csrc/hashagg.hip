@@ -844,9 +844,17 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTab
 #pragma unroll
         for (int q = 0; q < PAIRS; q++) folded[q] = false;
         if constexpr (RUNS) {
-            bool pend = false;  // a run of uniform groups not yet in the HBM table
-            uint32_t pkey = 0;
-            HaRun prun{0u, 0u, 0.0};
+            // a run of uniform groups not yet in the HBM table: its key, row and non-NaN counts
+            // (wave-uniform) and each lane's partial sum -- reduced over the wave once per run
+            bool pend = false;
+            uint32_t pkey = 0, pcnt = 0, pnn = 0;
+            double psum = 0.0;
+            auto flush = [&]() __attribute__((always_inline)) {
+                double t = psum;
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+                if (lane == 63) ha_global_run<NV>(g, (uint64_t)pkey, HaRun{pcnt, pnn, t}, &s_new);
+            };
 #pragma unroll
             for (int q = 0; q < PAIRS; q++) {
                 const uint64_t i0 = b0 + 2 * ((uint64_t)q * HA_THREADS + threadIdx.x);
@@ -859,24 +867,27 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTab
                 const bool all_in = __ballot(i0 >= row_end) == 0;
                 if (!all_in || heads > 16) continue;  // wave-uniform
                 if (__ballot(!same || (lane > 0 && !cin)) == 0) {
-                    // the wave's 128 rows hold one key (a long run of a sorted column): a plain
-                    // wave reduction instead of the segmented scan; consecutive such groups of
-                    // one key add up in (wave-uniform) registers, one HBM-table update per key
-                    double sv = 0.0;
-                    if constexpr (NV > 0) sv = (v0 == v0 ? v0 : 0.0) + (v1 == v1 ? v1 : 0.0);
-#pragma unroll
-                    for (int off = 32; off > 0; off >>= 1) sv += __shfl_xor(sv, off, 64);
-                    HaRun r{128u, 0u, sv};
-                    if constexpr (NV > 0)
-                        r.nn = (uint32_t)(__builtin_popcountll(__ballot(v0 == v0)) + __builtin_popcountll(__ballot(v1 == v1)));
+                    // the wave's 128 rows hold one key (a long run of a sorted column): no
+                    // segmented scan; consecutive such groups of one key add up (counts in
+                    // wave-uniform registers, sums per lane), one HBM-table update per key
+                    double sl = 0.0;
+                    uint32_t nn = 0;
+                    if constexpr (NV > 0) {
+                        sl = (v0 == v0 ? v0 : 0.0) + (v1 == v1 ? v1 : 0.0);
+                        nn = (uint32_t)(__builtin_popcountll(__ballot(v0 == v0)) + __builtin_popcountll(__ballot(v1 == v1)));
+                    }
                     const uint32_t ku = (uint32_t)__builtin_amdgcn_readfirstlane((int)k1);
                     if (pend && pkey == ku) {
-                        prun = ha_run_add(prun, r);
+                        pcnt += 128u;
+                        pnn += nn;
+                        psum += sl;
                     } else {
-                        if (pend && lane == 63) ha_global_run<NV>(g, (uint64_t)pkey, prun, &s_new);
+                        if (pend) flush();
                         pend = true;
                         pkey = ku;
-                        prun = r;
+                        pcnt = 128u;
+                        pnn = nn;
+                        psum = sl;
                     }
                     folded[q] = true;
                     continue;
@@ -902,7 +913,7 @@ __global__ __launch_bounds__(HA_THREADS) void k_ha_scatter_k4(HaParams hp, HaTab
                 if (!cin_next) ha_global_run<NV>(g, (uint64_t)k1, a, &s_new);
                 folded[q] = true;
             }
-            if (pend && lane == 63) ha_global_run<NV>(g, (uint64_t)pkey, prun, &s_new);
+            if (pend) flush();
         }
 #pragma unroll
         for (int r = 0; r < HA_RPT; r++) {
@@ -1914,6 +1925,9 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     const int kisz = dtype_itemsize(h->key_dtype);
     bool fast = (kisz == 4 || kisz == 8) && aligned16(keys) && n >= 8;
     for (int v = 0; v < nv; v++) fast = fast && h->vdtype[v] == VH_F64 && aligned16(vals[v]);
+#ifndef VH_HA_RUNS_SB_DEFAULT
+#define VH_HA_RUNS_SB_DEFAULT 1
+#endif
 #ifndef VH_HA_K4_DEFAULT
 #define VH_HA_K4_DEFAULT 1
 #endif
@@ -1923,9 +1937,17 @@ static void update_device(vh_hashagg *h, HaScratch &S, const void *keys, const v
     }();
     const bool k4 = fast && k4_on && kisz == 4 && nv <= 1;
     int sb = 0;
-    if (k4)
-        for (sb = 3; sb > 1 && ha_fast_lds_bytes(nv, sb, P) > 160 * 1024; sb--) {
+    if (k4) {
+        // clustered keys (RUNS) fold most groups before the partition: fewer batches per commit
+        // keep the registers of one commit's rows low (VH_HA_RUNS_SB: A/B)
+        int sb_max = 3;
+        if (runs) {
+            sb_max = VH_HA_RUNS_SB_DEFAULT;
+            if (const char *e = getenv("VH_HA_RUNS_SB")) sb_max = std::max(1, std::min(3, atoi(e)));
         }
+        for (sb = sb_max; sb > 1 && ha_fast_lds_bytes(nv, sb, P) > 160 * 1024; sb--) {
+        }
+    }
     const size_t lds_a = k4 ? ha_fast_lds_bytes(nv, sb, P) : ha_scatter_lds_bytes(nv, kbs, P);
     int bpc = 1;
     auto k4_kernel = [&](auto kc, auto nvc, auto sbc) {
