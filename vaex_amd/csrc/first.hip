@@ -44,7 +44,10 @@
 
 namespace vh {
 
-constexpr int TF_THREADS = 512;
+#ifndef VH_TF_THREADS
+#define VH_TF_THREADS 512
+#endif
+constexpr int TF_THREADS = VH_TF_THREADS;
 constexpr int TF_RPT = 8;
 constexpr int TF_BATCH = TF_THREADS * TF_RPT;  // 4096 rows per batch
 constexpr int TFB_THREADS = 1024;
