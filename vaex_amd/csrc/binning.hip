@@ -1210,7 +1210,7 @@ namespace {
 // nonzero cells of grid words [begin, end): count, first and last index (+1) -- the occupied
 // range of a dense groupby's count(*) grid (groupby.py:484-533 keeps the cells with count > 0)
 template <typename W>
-__global__ __launch_bounds__(256) void k_occupancy(const W *g, uint64_t begin, uint64_t end, unsigned long long *out) {
+__global__ __launch_bounds__(256) void k_occupancy(const W *g, uint64_t begin, uint64_t end, unsigned long long *part) {
     unsigned long long nnz = 0, first = ~0ull, last = 0;
     for (uint64_t i = begin + blockIdx.x * 256ull + threadIdx.x; i < end; i += (uint64_t)gridDim.x * 256) {
         if (g[i] != 0) {
@@ -1226,7 +1226,7 @@ __global__ __launch_bounds__(256) void k_occupancy(const W *g, uint64_t begin, u
         first = f < first ? f : first;
         last = l > last ? l : last;
     }
-    // one atomic set per workgroup (per-wave atomics on three addresses serialised: 0.17 ms)
+    // one partial per workgroup (no atomics: nothing to initialise, k_occupancy_fin reduces)
     __shared__ unsigned long long s_n[4], s_f[4], s_l[4];
     const int wv = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
@@ -1241,11 +1241,45 @@ __global__ __launch_bounds__(256) void k_occupancy(const W *g, uint64_t begin, u
             first = s_f[k] < first ? s_f[k] : first;
             last = s_l[k] > last ? s_l[k] : last;
         }
-        if (nnz) {
-            atomicAdd(&out[0], nnz);
-            atomicMin(&out[1], first);
-            atomicMax(&out[2], last);
+        part[3 * blockIdx.x] = nnz;
+        part[3 * blockIdx.x + 1] = first;
+        part[3 * blockIdx.x + 2] = last;
+    }
+}
+
+// the workgroup partials (at most 256) into the caller's page-locked result, written through
+// its device mapping (read on the host after a stream sync: no copy calls)
+__global__ __launch_bounds__(256) void k_occupancy_fin(const unsigned long long *part, uint32_t nb, unsigned long long *out) {
+    unsigned long long nnz = 0, first = ~0ull, last = 0;
+    if (threadIdx.x < nb) {
+        nnz = part[3 * threadIdx.x];
+        first = part[3 * threadIdx.x + 1];
+        last = part[3 * threadIdx.x + 2];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        nnz += __shfl_down(nnz, off, 64);
+        const unsigned long long f = __shfl_down(first, off, 64), l = __shfl_down(last, off, 64);
+        first = f < first ? f : first;
+        last = l > last ? l : last;
+    }
+    __shared__ unsigned long long s_n[4], s_f[4], s_l[4];
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_n[wv] = nnz;
+        s_f[wv] = first;
+        s_l[wv] = last;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < 4; k++) {
+            nnz += s_n[k];
+            first = s_f[k] < first ? s_f[k] : first;
+            last = s_l[k] > last ? s_l[k] : last;
         }
+        out[0] = nnz;
+        out[1] = first;
+        out[2] = last;
     }
 }
 
@@ -1483,35 +1517,39 @@ int vh_agg_occupancy(vh_agg *a, uint64_t begin, uint64_t end, int64_t *out3) {
     std::lock_guard<std::mutex> lk(a->grid->mu);
     if (begin > end || end > a->grid->length1d) fail(VH_ERR_ARG, "occupancy range outside the grid");
     nunique_finalize(a);
-    // one small result buffer per device (a grid lives for one query: a buffer of its own
-    // would be allocated per query)
+    // per-device workgroup partials (a grid lives for one query: a buffer of its own would be
+    // allocated per query) and a per-thread page-locked result the final kernel writes
     static std::mutex occ_mu;
     static std::map<int, std::unique_ptr<DevBuf>> occ_bufs;
     std::lock_guard<std::mutex> olk(occ_mu);
     auto &slot = occ_bufs[current_device()];
     if (!slot) slot = std::make_unique<DevBuf>();
-    DevBuf &dres = *slot;
+    DevBuf &dpart = *slot;
     thread_local PinnedBuf hres;
-    dres.ensure(64);
-    hres.ensure(64);
-    auto *d = dres.as<unsigned long long>();
-    const unsigned long long init[3] = {0ull, ~0ull, 0ull};
-    memcpy(hres.ptr, init, sizeof init);
-    VH_HIP(hipMemcpyAsync(d, hres.ptr, sizeof init, hipMemcpyHostToDevice, stream()));
-    const uint64_t n = end - begin;
-    if (n) {
-        const dim3 grd(std::max(1u, std::min(blocks_for(n, 256, 1), 256u))), blk(256);
-        switch (a->grid_isz) {
-        case 1: hipLaunchKernelGGL(k_occupancy<uint8_t>, grd, blk, 0, stream(), static_cast<const uint8_t *>(a->g.ptr), begin, end, d); break;
-        case 2: hipLaunchKernelGGL(k_occupancy<uint16_t>, grd, blk, 0, stream(), static_cast<const uint16_t *>(a->g.ptr), begin, end, d); break;
-        case 4: hipLaunchKernelGGL(k_occupancy<uint32_t>, grd, blk, 0, stream(), static_cast<const uint32_t *>(a->g.ptr), begin, end, d); break;
-        default: hipLaunchKernelGGL(k_occupancy<uint64_t>, grd, blk, 0, stream(), static_cast<const uint64_t *>(a->g.ptr), begin, end, d);
-        }
-        VH_HIP(hipGetLastError());
+    thread_local unsigned long long *hres_dev = nullptr;
+    constexpr uint32_t OCC_BLOCKS = 256;
+    dpart.ensure((size_t)OCC_BLOCKS * 3 * 8);
+    if (!hres.ptr) {
+        hres.ensure(64);
+        hipPointerAttribute_t at{};
+        VH_HIP(hipPointerGetAttributes(&at, hres.ptr));
+        if (!at.devicePointer) fail(VH_ERR_HIP, "page-locked result buffer without a device mapping");
+        hres_dev = static_cast<unsigned long long *>(at.devicePointer);
     }
-    VH_HIP(hipMemcpyAsync(hres.ptr, d, sizeof init, hipMemcpyDeviceToHost, stream()));
+    auto *part = dpart.as<unsigned long long>();
+    const uint64_t n = end - begin;
+    const uint32_t nb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(blocks_for(n, 256, 1), OCC_BLOCKS));
+    const dim3 grd(nb), blk(256);
+    switch (a->grid_isz) {
+    case 1: hipLaunchKernelGGL(k_occupancy<uint8_t>, grd, blk, 0, stream(), static_cast<const uint8_t *>(a->g.ptr), begin, end, part); break;
+    case 2: hipLaunchKernelGGL(k_occupancy<uint16_t>, grd, blk, 0, stream(), static_cast<const uint16_t *>(a->g.ptr), begin, end, part); break;
+    case 4: hipLaunchKernelGGL(k_occupancy<uint32_t>, grd, blk, 0, stream(), static_cast<const uint32_t *>(a->g.ptr), begin, end, part); break;
+    default: hipLaunchKernelGGL(k_occupancy<uint64_t>, grd, blk, 0, stream(), static_cast<const uint64_t *>(a->g.ptr), begin, end, part);
+    }
+    hipLaunchKernelGGL(k_occupancy_fin, dim3(1), dim3(256), 0, stream(), part, nb, hres_dev);
+    VH_HIP(hipGetLastError());
     VH_HIP(hipStreamSynchronize(stream()));
-    const auto *r = hres.as<unsigned long long>();
+    const auto *r = reinterpret_cast<const volatile unsigned long long *>(hres.ptr);
     out3[0] = (int64_t)r[0];
     out3[1] = r[0] ? (int64_t)r[1] : -1;
     out3[2] = r[0] ? (int64_t)r[2] - 1 : -1;
