@@ -50,6 +50,11 @@ namespace vh {
 constexpr int TF_THREADS = VH_TF_THREADS;
 constexpr int TF_RPT = 8;
 constexpr int TF_BATCH = TF_THREADS * TF_RPT;  // 4096 rows per batch
+#ifndef VH_TF_LG
+#define VH_TF_LG 2
+#endif
+constexpr int TF_LG = VH_TF_LG;  // rows per load group of the float64-binner pass A
+static_assert(TF_RPT % TF_LG == 0, "load groups tile the rows of a lane");
 constexpr int TFB_THREADS = 1024;
 constexpr uint32_t TF_S_LOG2 = 12;  // 4096 cells per tile: pass B LDS 8-B key + 4-B row = 48 KB
 constexpr uint32_t TF_MAX_TILES = 2048;
@@ -71,12 +76,15 @@ struct FirstParams {
     uint32_t *erow;   // spill-area entries only: the chunk row
     uint32_t *kbound; // [W][T][kh]: region position where the commit index reached 256 (j + 1)
     uint32_t kh;
+    uint32_t unmasked;  // float64 binners (ND > 0) without masks: the batch's loads go first
     unsigned long long *s_key, *s_row;  // the aggregator's per-cell scratch (AggDev)
     uint4 *list;                        // (cell, row, key lo, key hi)
     unsigned long long *list_fill;
     uint64_t list_cap;
     unsigned *flag;  // list overflow: the host redoes the chunk on the generic path
-    uint32_t debug;  // ablation build only (VH_FIRST_DEBUG): 1 = no stream reservation atomics
+    uint32_t debug;  // ablation build only (VH_FIRST_DEBUG, results wrong): 2 = no stream-out
+                     // stores, 4 = no staging / stream-out, 8 = value / order columns not loaded,
+                     // 16 = one LDS atomic per kept row for the rank, 32 = no rank, 64 = no scan
 };
 
 template <int ND> __device__ __forceinline__ uint64_t tf_cell(const BinPlan &p, uint64_t i) {
@@ -152,28 +160,75 @@ __global__ __launch_bounds__(TF_THREADS) void k_first_scatter(BinPlan p, AggDev 
         uint32_t key[TF_RPT];
         int32_t rank[TF_RPT];
         unsigned long long ok[TF_RPT];
+        // float64 binners without masks (UNMASKED): every column of the batch's rows is loaded
+        // before any is used -- one memory round trip per batch, not three per row (a load
+        // behind a binner's branches or a rank waits for the one before it)
+        // (in groups of TF_LG rows: fewer registers held, TF_RPT / TF_LG round trips)
+        double xr[ND > 0 ? ND : 1][TF_LG];
+        T vr[TF_LG], orr[TF_LG];
 #pragma unroll
         for (int r = 0; r < TF_RPT; r++) {
+            if constexpr (ND > 0) {
+                if (fp.unmasked && r % TF_LG == 0) {
+#pragma unroll
+                    for (int g = 0; g < TF_LG; g++) {
+                        const uint64_t i = b0 + (uint64_t)(r + g) * TF_THREADS + threadIdx.x;
+                        const uint64_t is = i < n ? i : n - 1;
+#pragma unroll
+                        for (int d = 0; d < ND; d++) xr[d][g] = static_cast<const double *>(p.b[d].data)[is];
+                        vr[g] = load_v<T>(a.data, is, a.flip);
+                        orr[g] = load_v<T>(a.data2, is, a.flip);
+                    }
+                }
+            }
             const uint64_t i = b0 + (uint64_t)r * TF_THREADS + threadIdx.x;
             const bool in = i < n;
             uint64_t c = 0;
             bool keep = false;
             ok[r] = 0;
-            if (in) {
+            bool done = false;
+            if constexpr (ND > 0) {
+                if (fp.unmasked) {
+                    done = true;
+                    if (in) {
+#pragma unroll
+                        for (int d = 0; d < ND; d++) c += scalar_cell<double>(p.b[d], xr[d][r % TF_LG], false) * p.b[d].stride;
+                        keep = !is_nan_v(vr[r % TF_LG]) && !is_nan_v(orr[r % TF_LG]);
+                        ok[r] = order_key(orr[r % TF_LG]);
+                    }
+                }
+            }
+            if (in && !done) {
                 c = tf_cell<ND>(p, i);
-                const T v = load_v<T>(a.data, i, a.flip), o = load_v<T>(a.data2, i, a.flip);
+                T v{}, o{};
+                if (DBG(fp.debug) & 8) {
+                    if constexpr (std::is_arithmetic<T>::value) {
+                        v = (T)1;
+                        o = (T)(i & 1023);
+                    }
+                } else {
+                    v = load_v<T>(a.data, i, a.flip);
+                    o = load_v<T>(a.data2, i, a.flip);
+                }
                 keep = !is_nan_v(v) && !is_nan_v(o);
                 ok[r] = order_key(o);
             }
             const uint32_t t = (uint32_t)(c >> fp.s_log2);
             key[r] = (t << 16) | ((uint32_t)c & smask);
-            rank[r] = wave_rank(hist, t, keep);
+            if (DBG(fp.debug) & 32) {
+                rank[r] = -1;
+                asm volatile("" ::"v"(t), "v"(keep));
+            } else if (DBG(fp.debug) & 16) {
+                rank[r] = keep ? (int32_t)atomicAdd(&hist[t], 1u) : -1;
+            } else {
+                rank[r] = wave_rank(hist, t, keep);
+            }
         }
         // B1: every rank taken -> wave 0 scans the histogram (clearing it for the next batch)
         // and advances this workgroup's regions; a run past a region's capacity reserves the
         // excess in the tile's spill area
         tf_lds_barrier();
-        if (threadIdx.x < 64) {
+        if (threadIdx.x < 64 && !(DBG(fp.debug) & 64)) {
             const uint32_t per = (NT + 63) / 64, t0 = lane * per;
             uint32_t s = 0;
             for (uint32_t t = t0; t < t0 + per && t < NT; t++) s += hist[t];
@@ -202,6 +257,7 @@ __global__ __launch_bounds__(TF_THREADS) void k_first_scatter(BinPlan p, AggDev 
         }
         // B2: rows stage at their sorted positions
         tf_lds_barrier();
+        if (DBG(fp.debug) & 4) continue;
 #pragma unroll
         for (int r = 0; r < TF_RPT; r++) {
             if (rank[r] < 0) continue;
@@ -234,6 +290,10 @@ __global__ __launch_bounds__(TF_THREADS) void k_first_scatter(BinPlan p, AggDev 
                 }
                 e = fp.spill_base + fp.spill_start[t] + si;
                 fp.erow[e] = row;  // spill entries carry their row (any workgroup, any commit)
+            }
+            if (DBG(fp.debug) & 2) {
+                asm volatile("" ::"v"(e), "v"(kk), "v"(off), "v"(sokey[k]));
+                continue;
             }
             fp.epack[e] = (kk & 0xfffu) | (off << 12) | packk;
             fp.eokey[e] = sokey[k];
@@ -592,6 +652,13 @@ bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t
     fp.erow = ws.erow.as<uint32_t>();
     fp.kbound = d_kbound;
     fp.kh = kh;
+    fp.unmasked = 0;
+    if (nd >= 1) {
+        fp.unmasked = 1;
+        for (int d = 0; d < nd; d++)
+            if (plan.b[d].mask) fp.unmasked = 0;
+    }
+    if (const char *e = getenv("VH_FIRST_LOADS_FIRST")) fp.unmasked = fp.unmasked && atoi(e) != 0;  // A/B
     fp.s_key = static_cast<unsigned long long *>(ad.s_key);
     fp.s_row = static_cast<unsigned long long *>(ad.s_row);
     fp.list = ws.list.as<uint4>();
