@@ -135,6 +135,33 @@ def test_first_row_layouts(layout):
     _check(got, exp, o.dtype)
 
 
+@pytest.mark.parametrize("layout", ["random", "y_sorted", "clustered"])
+def test_first_commit_index_boundaries(layout, monkeypatch):
+    """Pass A capped at 2 workgroups (VH_FIRST_MAX_WG): ~640 commits per workgroup, so region
+    entries carry the commit index mod 256 and pass B recovers its high bits from the positions
+    where it crossed 256 and 512 -- including regions that see fewer than 8 entries between two
+    crossings (sorted / clustered rows); order ties resolved by row; bit-exact."""
+    monkeypatch.setenv("VH_FIRST_MAX_WG", "2")
+    rng = np.random.default_rng(5)
+    n = (5 << 20) + 77
+    x = rng.normal(size=n)
+    if layout == "y_sorted":
+        y = np.sort(rng.normal(size=n))
+    elif layout == "clustered":
+        runs = rng.integers(1, 40000, n // 4000)
+        y = np.repeat(rng.normal(size=len(runs)), runs)[:n]
+        y = np.concatenate([y, rng.normal(size=n - len(y))])
+    else:
+        y = rng.normal(size=n)
+    w = rng.random(n)
+    o = rng.integers(0, 50, n).astype(np.float64)  # ties: the earliest row must win
+    specs = [("BinnerScalar_float64", x, -4.0, 4.0, 512), ("BinnerScalar_float64", y, -4.0, 4.0, 512)]
+    got = _run(specs, w, o)
+    exp = _oracle_first([oracle.Binner("scalar", x, vmin=-4, vmax=4, bins=512),
+                         oracle.Binner("scalar", y, vmin=-4, vmax=4, bins=512)], w, o)
+    _check(got, exp, o.dtype)
+
+
 def test_first_host_columns_several_chunks():
     """Host columns staged in 16 Mi-row chunks: chunks after the first carry their global row
     offset (ties between chunks go to the earlier chunk)."""

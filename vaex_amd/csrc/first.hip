@@ -385,10 +385,24 @@ __global__ __launch_bounds__(TFB_THREADS) void k_first_reduce(FirstParams fp, co
             // positions where the commit index crossed multiples of 256
             const uint32_t w = u.w0 + kk, q0 = (c - s_pre[kk]) * 8;
             const uint32_t *kb = fp.kbound + ((uint64_t)w * fp.T + t) * fp.kh;
+            // boundaries at or below the chunk's first position, and the first one above it
+            // (one pass of independent loads; a boundary inside the chunk -- a region with
+            // fewer than 8 entries in 256 commits -- takes the per-entry count)
+            uint32_t hi0 = 0, nb = ~0u;
+#pragma unroll 4
+            for (uint32_t h = 0; h < fp.kh; h++) {
+                const uint32_t b = kb[h];
+                hi0 += q0 >= b;
+                nb = b > q0 && b < nb ? b : nb;
+            }
+            const bool inside = nb <= q0 + 7;
 #pragma unroll
             for (int j = 0; j < 8; j++) {
-                uint32_t hi = 0;
-                for (uint32_t h = 0; h < fp.kh; h++) hi += q0 + j >= kb[h];
+                uint32_t hi = hi0;
+                if (inside) {
+                    hi = 0;
+                    for (uint32_t h = 0; h < fp.kh; h++) hi += q0 + j >= kb[h];
+                }
                 const uint32_t kcj = (hi << 8) | (pk[j] >> 24);
                 rows[j] = (kcj * fp.W + w) * (uint32_t)TF_BATCH + ((pk[j] >> 12) & 0xfffu);
             }
@@ -514,7 +528,10 @@ bool try_tiled_first(const BinPlan &plan, const AggDev &ad, uint64_t n, uint64_t
         }
         bpc = it->second;
     }
-    const uint32_t W = std::min<uint32_t>(1024, (uint32_t)cu_count() * (uint32_t)bpc);
+    uint32_t W = std::min<uint32_t>(1024, (uint32_t)cu_count() * (uint32_t)bpc);
+    // fewer pass-A workgroups (tests: hundreds of commits per workgroup, the commit-index
+    // boundaries, at a few million rows; same results)
+    if (const char *e = getenv("VH_FIRST_MAX_WG")) W = std::max<uint32_t>(1, std::min<uint32_t>(W, (uint32_t)atoi(e)));
     // meta: hist (2T u64) | cap | toff | spill_cap (T u32 each) | spill_start (T u64) | fills
     // (W T u32) | spill_fill (T u32) | list_fill | flag | units
     const uint64_t nb = (n + TF_BATCH - 1) / TF_BATCH;
