@@ -70,6 +70,47 @@ def _queries(df):
     return out
 
 
+def _check_vs_oracle(got):
+    """The query set's grids and groupbys against the oracle (not only against another run of
+    the product): 2-d count / sum, 1-d mean, max of an int16 column, first, and the dense /
+    hash / fused groupby sums and counts (map comparison for the unsorted fused result)."""
+    d = _data()
+    x, y, w, c = d["x"], d["y"], d["w"], d["c"]
+    sx = oracle.Binner("scalar", x, vmin=-3, vmax=3, bins=64)
+    sy = oracle.Binner("scalar", y, vmin=-3, vmax=3, bins=64)
+    np.testing.assert_array_equal(got["count"], oracle.extract_central_part(oracle.compute_grid([sx, sy], "count")))
+    np.testing.assert_allclose(got["sum"], oracle.extract_central_part(oracle.compute_grid([sx, sy], "sum", data=w)),
+                               rtol=1e-9, atol=1e-12)
+    s1 = oracle.Binner("scalar", x, vmin=-3, vmax=3, bins=100)
+    cs = oracle.extract_central_part(oracle.compute_grid([s1], "sum", data=w))
+    cc = oracle.extract_central_part(oracle.compute_grid([s1], "count", data=w))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        np.testing.assert_allclose(got["mean"], cs / cc, rtol=1e-9, atol=1e-12)
+    s40 = oracle.Binner("scalar", x, vmin=-3, vmax=3, bins=40)
+    np.testing.assert_array_equal(got["cmax"], oracle.extract_central_part(oracle.compute_grid([s40], "max", data=c)))
+    s20 = oracle.Binner("scalar", x, vmin=-3, vmax=3, bins=20)
+    np.testing.assert_array_equal(got["first"], oracle.extract_central_part(oracle.compute_grid([s20], "first", data=w, data2=y)))
+    uk, us, un = oracle.groupby_reference(d["key"], w)
+    for mode in ("dense", "hash"):
+        np.testing.assert_array_equal(got[f"gb_{mode}_key"], uk)
+        np.testing.assert_array_equal(got[f"gb_{mode}_n"], un)
+        np.testing.assert_allclose(got[f"gb_{mode}_sum"], us, rtol=1e-9, atol=1e-9)
+    fk, fs, fn = oracle.groupby_reference(d["skey"], w)
+    keys = got["gb_fused_skey"]
+    order = np.argsort(keys, kind="stable")
+    np.testing.assert_array_equal(keys[order], fk)
+    cols = [k for k in got if k.startswith("gb_fused_") and k != "gb_fused_skey"]
+    assert len(cols) == 3, cols
+    for k in cols:  # count(*) (named after the column, groupby.py's naming), sum, mean
+        v = got[k][order]
+        if v.dtype.kind in "iu":
+            np.testing.assert_array_equal(v, fn, err_msg=k)
+        elif "mean" in k:
+            np.testing.assert_allclose(v, fs / fn, rtol=1e-9, atol=1e-12, err_msg=k)
+        else:
+            np.testing.assert_allclose(v, fs, rtol=1e-9, atol=1e-9, err_msg=k)
+
+
 def _compare(got, ref):
     for k, v in ref.items():
         if k.endswith("sum") or k.endswith("mean") or k == "mean":
@@ -107,6 +148,7 @@ def test_two_rank_executor_matches_single_process():
         assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
         got = dict(np.load(path))
     _compare(got, _queries(vaex_amd.from_arrays(**_data())))
+    _check_vs_oracle(got)
 
 
 def _rccl_worker(path, port):

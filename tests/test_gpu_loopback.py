@@ -321,9 +321,12 @@ def _queries_rank(c):
 @pytest.mark.parametrize("world", [2, 3])
 def test_loopback_executor_queries_match_single_process(world):
     """The whole distributed query set (grids, limits, first, dense / hash / nunique / fused
-    groupby) with the device exchange, every rank's result against one process's."""
+    groupby) with the device exchange, every rank's result against one process's and against
+    the oracle."""
     import vaex_amd
-    from test_gpu_distributed import _compare, _data, _queries
+    from test_gpu_distributed import _check_vs_oracle, _compare, _data, _queries
     ref = _queries(vaex_amd.from_arrays(**_data()))
+    _check_vs_oracle(ref)
     for got in run_ranks(world, _queries_rank):
         _compare(got, ref)
+        _check_vs_oracle(got)
