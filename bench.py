@@ -48,6 +48,10 @@ def parse():
     p.add_argument("--groupby-rows", type=float, default=1e9)
     p.add_argument("--c4-rows", type=float, default=2e9,
                    help="rows of the C4 leg (2D mean streamed from a memory-mapped HDF5 file); 0 = skip")
+    p.add_argument("--h2o-rows", type=float, default=1e9,
+                   help="rows of the h2o G1 leg (benchmarks/groupbyh2o.py q1-q5, q7, q10); 0 = skip")
+    p.add_argument("--dist-groupby-rows", type=float, default=1e9, help="C3 rows per rank of the multi-GPU groupby legs")
+    p.add_argument("--dist-h2o-rows", type=float, default=2.5e8, help="h2o rows per rank of the multi-GPU leg; 0 = skip")
     p.add_argument("--check", action="store_true", help="verify size-independent properties")
     p.add_argument("--breakdown", action="store_true", help="print host-side timing of one step")
     p.add_argument("--no-aggs", action="store_true", help="skip the first / var legs on the C2 grid")
@@ -264,9 +268,23 @@ def main():
         extra["host_columns"] = bench_host_columns(x, y, w, int(min(args.host_rows, n)), bins)
     if rank == 0 and world == 1 and args.c4_rows > 0:
         extra["c4"] = bench_c4(int(args.c4_rows), bins)
+    if rank == 0 and world == 1 and args.h2o_rows > 0:
+        extra["h2o"] = bench_h2o(int(args.h2o_rows))
+    if dist is not None:
+        # the multi-GPU BASELINE configs through the RCCL path, every rank (C4: a streamed
+        # 2-d mean + grid all-reduce; C3 / C5: hash-partition exchange, dense all-reduce, h2o)
+        d = bench_dist(dist, rank, world, args)
+        if rank == 0:
+            extra["dist"] = d
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(x, y, w, n, bins, args.cpu_seconds)
+        cpu, oracle_grid = cpu_baseline(x, y, w, n, bins, args.cpu_seconds)
+        # driver-box parity: the oracle's grid of the baseline sample against the GPU's grid
+        # of the same rows, cell by cell (outside every timed region)
+        check["prefix_oracle"] = {"c2": prefix_parity_c2(x, y, w, bins, *oracle_grid)}
+        if not args.no_groupby:
+            cpu["groupby"], check["prefix_oracle"]["c3"] = cpu_baseline_groupby()
+        check["ok"] = bool(check["ok"] and all(v.get("ok") for v in check["prefix_oracle"].values()))
         extra["c1"] = bench_c1(args)
 
     if rank == 0:
@@ -768,6 +786,206 @@ def bench_groupby(n, args, layout="random"):
     return out
 
 
+H2O_BYTES = {"q1": 2, "q2": 2, "q3": 9, "q4": 6, "q5": 9, "q7": 5, "q10": 10}
+
+
+def h2o_frame(n, seed0=0, executor=None):
+    """benchmarks/fixtures.py:38-70's columns for G1_1e9_1e2 (i1_100 int8 in [5, 105), i4_1M
+    int32 in [5, 1e6 + 5), i1_10 int8 in [5, 15), x4 float32 normal), generated in HBM
+    (counter-based; seeds offset per rank), with benchmarks/groupbyh2o.py:26-36's aliases
+    (id1 / id2 / id4 / id5 = i1_100, id3 / id6 = i4_1M, v1 / v2 = i1_10, v3 = x4)."""
+    from vaex_amd.dataframe import DataFrame
+    from vaex_amd.device import DeviceArray
+    cols = {"i1_100": DeviceArray.random(n, "randint", seed=seed0 + 21, a=5, b=105, dtype="int8"),
+            "i4_1M": DeviceArray.random(n, "randint", seed=seed0 + 22, a=5, b=1_000_005, dtype="int32"),
+            "i1_10": DeviceArray.random(n, "randint", seed=seed0 + 23, a=5, b=15, dtype="int8"),
+            "x4": DeviceArray.random(n, "normal", seed=seed0 + 24, dtype="float32")}
+    df = DataFrame(cols, executor=executor)
+    for a, b in [("id1", "i1_100"), ("id2", "i1_100"), ("id3", "i4_1M"), ("id4", "i1_100"), ("id5", "i1_100"),
+                 ("id6", "i4_1M"), ("v1", "i1_10"), ("v2", "i1_10"), ("v3", "x4")]:
+        df.columns[a] = df.columns[b]
+    return df
+
+
+def h2o_queries(df):
+    """benchmarks/groupbyh2o.py:39-93 exactly as written there."""
+    return {
+        "q1": lambda: df.groupby(["id1"]).agg({"v1": "sum"}),
+        "q2": lambda: df.groupby(["id1", "id2"]).agg({"v1": "sum"}),
+        "q3": lambda: df.groupby(["id3"]).agg({"v1": "sum", "v3": "mean"}),
+        "q4": lambda: df.groupby(["id4"]).agg({"v1": "mean", "v2": "mean", "v3": "mean"}),
+        "q5": lambda: df.groupby(["id6"]).agg({"v1": "sum", "v2": "sum", "v3": "sum"}),
+        "q7": lambda: df.groupby(["id3"]).agg({"v1": "max", "v2": "min"}),
+        "q10": lambda: df.groupby(["id1", "id2", "id3", "id4", "id5", "id6"]).agg({"v3": "sum", "v1": "count"}),
+    }
+
+
+def h2o_check(q, r, n, sums):
+    """Size-independent properties of one h2o result: the group count the columns imply
+    (id1 = id2 = id4 = id5 and id3 = id6 alias one column each), a count total equal to the
+    rows (q10), the v1 sum total equal to an independent 0-d sum of i1_10 (q1, q3, q5)."""
+    groups = len(r)
+    exp = {"q1": 100, "q2": 100, "q4": 100}.get(q)
+    out = {"groups": groups}
+    ok = True
+    if exp is not None:
+        out["groups_expected"] = exp
+        ok = groups == exp
+    else:
+        ok = groups > 0
+    if q == "q10":
+        c = int(np.asarray(r["v1"].to_numpy()).sum())
+        out["count_total"] = c
+        ok = ok and c == n
+    if q in ("q1", "q3", "q5"):
+        s = int(np.asarray(r["v1"].to_numpy()).astype(np.int64).sum())
+        out["v1_sum_total"] = s
+        ok = ok and s == sums["v1"]
+    out["ok"] = bool(ok)
+    return out
+
+
+def bench_h2o(n, reps=3):
+    """C5's queries on one GPU (BASELINE configs[4] per rank): h2o groupby G1 at n rows,
+    q1-q5, q7, q10 of benchmarks/groupbyh2o.py on HBM columns, end to end (result DataFrame
+    on the host), best of `reps` after a warm-up (q10: one timed run); algorithmic bytes per
+    row = the distinct columns a query reads."""
+    from vaex_amd import _lib
+    df = h2o_frame(n)
+    sums = {"v1": int(df.sum("i1_10"))}
+    out = {"rows": n, "data": "fixtures.py schema generated in HBM (int8 / int32 / float32)"}
+    for q, f in h2o_queries(df).items():
+        f()
+        _lib.synchronize()
+        ts = []
+        for _ in range(1 if q == "q10" else reps):
+            t0 = time.perf_counter()
+            r = f()
+            _lib.synchronize()
+            ts.append(time.perf_counter() - t0)
+        t = min(ts)
+        out[q] = {"ms": round(t * 1e3, 3), "rows_per_s": n / t, "algorithmic_bytes_per_row": H2O_BYTES[q],
+                  "GBps": round(H2O_BYTES[q] * n / t / 1e9, 1), "check": h2o_check(q, r, n, sums)}
+    del df
+    return out
+
+
+def bench_dist(dist, rank, world, args, repeats=3):
+    """The multi-GPU BASELINE configs through the RCCL communicator (every rank runs this;
+    times are the max over ranks of the slowest rank, bracketed by barriers):
+      groupby_hash -- C3 / C5 shape: each rank its own 1e9-row shard (int32 key, 1e6 distinct,
+                      float64 value), the fused hash aggregation, then the hash-partition
+                      all-to-all of the groups (vh_hashagg_exchange: every group to owner
+                      splitmix64(key) % world, folded there), results left sharded by owner;
+      groupby_dense -- the same shards through DataFrame.groupby on ExecutorDistributed
+                      (dense key range: BinnerOrdinal grid per rank + RCCL grid all-reduce);
+      c4           -- mean(w, binby=[x, y], shape=1024) over one memory-mapped HDF5 file
+                      written by rank 0, rows sharded by range across the ranks, grid
+                      all-reduce (execution.py:214-289's fan-out at process granularity);
+      h2o          -- q1-q5, q7 on per-rank shards through ExecutorDistributed.
+    Checks: world-wide count totals and group counts against the rows generated."""
+    import shutil
+    import tempfile
+    import vaex_amd
+    from vaex_amd import _lib
+    from vaex_amd import distributed as vdist
+    from vaex_amd.dataframe import DataFrame
+    from vaex_amd.device import DeviceArray
+    from vaex_amd.hashagg import HashAgg
+    out = {"world": world, "rccl": bool(getattr(dist, "device", False))}
+
+    def timed(f):
+        ts = []
+        r = None
+        for _ in range(repeats):
+            vdist.barrier(dist)
+            _lib.synchronize()
+            t0 = time.perf_counter()
+            r = f()
+            _lib.synchronize()
+            vdist.barrier(dist)
+            ts.append(vdist.allreduce_scalar(time.perf_counter() - t0, "max", dist))
+        return r, min(ts)
+
+    ng = int(args.dist_groupby_rows)
+    keys = DeviceArray.random(ng, "randint", seed=5 + 1000 * rank, a=5, b=5 + 1_000_000, dtype="int32")
+    v = DeviceArray.random(ng, "normal", seed=6 + 1000 * rank)
+
+    def hash_exchange():
+        ha = HashAgg(keys.dtype, [v.dtype], [False])
+        ha.update(keys, [v])
+        return ha.finish(dist, gather=False)
+
+    hash_exchange()
+    (k, c, s, _), t = timed(hash_exchange)
+    groups = int(dist.allreduce(np.array([len(k)], np.int64))[0])
+    total = int(dist.allreduce(np.array([int(np.asarray(c).sum())], np.int64))[0])
+    out["groupby_hash"] = {"rows_per_rank": ng, "ms": round(t * 1e3, 3), "rows_per_s": ng * world / t,
+                           "groups": groups, "count_total": total,
+                           "ok": bool(total == ng * world and groups == 1_000_000)}
+    ddf = DataFrame({"key": keys, "v": v}, executor=vdist.ExecutorDistributed(dist, shard_rows=False))
+
+    def dense():
+        return ddf.groupby("key", agg={"v": ["sum", "count"]}, sort=True)
+    dense()
+    g, t = timed(dense)
+    total = int(np.asarray(g["v"].to_numpy()).sum())
+    out["groupby_dense"] = {"rows_per_rank": ng, "ms": round(t * 1e3, 3), "rows_per_s": ng * world / t,
+                            "groups": len(g), "count_total": total,
+                            "ok": bool(total == ng * world and len(g) == 1_000_000)}
+    del ddf, keys, v, g
+
+    if args.dist_h2o_rows > 0:
+        nh = int(args.dist_h2o_rows)
+        hdf = h2o_frame(nh, seed0=1000 * rank, executor=vdist.ExecutorDistributed(dist, shard_rows=False))
+        v1 = int(vdist.allreduce_scalar(float(vaex_amd.from_arrays(v=hdf.columns["i1_10"]).sum("v")), "sum", dist))
+        res = {"rows_per_rank": nh}
+        for q, f in h2o_queries(hdf).items():
+            if q == "q10":
+                continue  # the combined-key recursion is single-process (DESIGN §6)
+            f()
+            r, t = timed(f)
+            res[q] = {"ms": round(t * 1e3, 3), "rows_per_s": nh * world / t,
+                      "check": h2o_check(q, r, nh * world, {"v1": v1})}
+        out["h2o"] = res
+        del hdf
+
+    rows = int(args.c4_rows)
+    if rows > 0:
+        nbytes = 24 * rows
+        where = None
+        if rank == 0:
+            cands = [d for d in ("/dev/shm", tempfile.gettempdir()) if os.path.isdir(d)]
+            where = next((d for d in cands if shutil.disk_usage(d).free > 1.15 * nbytes), None)
+        where = dist.bcast(where) if hasattr(dist, "bcast") else where
+        if where is None:
+            out["c4"] = {"skipped": f"needs {1.15 * nbytes / 1e9:.0f} GB of file space"}
+            return out
+        path = os.path.join(where, f"vaex_amd_c4_dist_{os.environ.get('MASTER_PORT', 'x')}.hdf5")
+        try:
+            if rank == 0:
+                cols = {"x": DeviceArray.random(rows, "normal", seed=12), "y": DeviceArray.random(rows, "normal", seed=13),
+                        "w": DeviceArray.random(rows, "uniform", seed=14)}
+                vaex_amd.from_arrays(**cols).export_hdf5(path)
+                del cols
+            vdist.barrier(dist)
+            src = vaex_amd.open(path)
+            cdf = DataFrame(dict(src.columns), executor=vdist.ExecutorDistributed(dist, shard_rows=True))
+            lim = [[-4.0, 4.0], [-4.0, 4.0]]
+            cdf.mean("w", binby=["x", "y"], limits=lim, shape=args.bins)
+            m, t = timed(lambda: cdf.mean("w", binby=["x", "y"], limits=lim, shape=args.bins))
+            cnt = cdf.count(binby=["x", "y"], limits=lim, shape=args.bins, edges=True)
+            out["c4"] = {"rows": rows, "ms": round(t * 1e3, 3), "rows_per_s": rows / t,
+                         "host_GBps_total": round(nbytes / t / 1e9, 2), "finite_cells": int(np.isfinite(m).sum()),
+                         "count_total": int(np.asarray(cnt).sum()), "ok": bool(int(np.asarray(cnt).sum()) == rows)}
+            del cdf, src
+        finally:
+            vdist.barrier(dist)
+            if rank == 0 and os.path.exists(path):
+                os.remove(path)
+    return out
+
+
 def cpu_baseline(x, y, w, n, bins, target_seconds, repeats=5):
     """oracle/superagg_oracle.c or_bench_grid2d: reference threading model (1 Mi-row chunks,
     max(2, T//8) private grids for a >=1e7-byte part, serial reduce) on a bounded sample;
@@ -809,13 +1027,83 @@ def cpu_baseline(x, y, w, n, bins, target_seconds, repeats=5):
     # the same sample without the ideal_splits cap (one private grid per thread)
     unc = [run_parts(m, threads) for _ in range(repeats)]
     t_unc = float(np.median([r[0] for r in unc]))
+    grid = (m, cnt.copy(), sm.copy())  # the oracle's grid of the sample (parity check)
     return {"value": m / t, "unit": "rows/s", "cores": used, "kind": "port",
             "uncapped": {"value": m / t_unc, "cores": unc[0][1], "nparts": threads},
             "sample": f"first {m} rows of the same x,y,w columns, count+sum 1027x1027 grid, median of {repeats} "
                       f"runs ({t:.2f} s each)",
             "runs_s": [round(r[0], 4) for r in runs],
             "threads_available": threads, "nparts_rule": "max(2, T//8) (cpu.py:487-499)",
-            "cpu_model": cpu_model, "host": platform.node()}
+            "cpu_model": cpu_model, "host": platform.node()}, grid
+
+
+def prefix_parity_c2(x, y, w, bins, m, cnt, sm):
+    """The GPU's count + sum grid of the first m rows (the CPU baseline's sample) against the
+    oracle's grid of the same rows (or_bench_grid2d: superagg_binners.cpp:14-56 binning,
+    superagg.cpp:155-192,349-389 aggregation): counts exact, sums rtol 1e-6."""
+    from vaex_amd import superagg
+    bx = superagg.BinnerScalar_float64("x", -4.0, 4.0, bins)
+    by = superagg.BinnerScalar_float64("y", -4.0, 4.0, bins)
+    bx.set_data(x[:m])
+    by.set_data(y[:m])
+    grid = superagg.Grid([bx, by])
+    count = superagg.AggCount_int64(grid)
+    total = superagg.AggSum_float64(grid)
+    total.set_data(w[:m], 0)
+    grid.bin([count, total])
+    shape = (bins + 3, bins + 3)
+    gc, gs = np.asarray(count), np.asarray(total)
+    oc, osm = cnt.reshape(shape, order="F"), sm.reshape(shape, order="F")
+    diff = int(np.count_nonzero(gc != oc))
+    nz = osm != 0
+    rel = float(np.max(np.abs(gs[nz] - osm[nz]) / np.abs(osm[nz]))) if nz.any() else 0.0
+    zero_ok = bool(np.all(gs[~nz] == 0))
+    return {"rows": int(m), "cells": int(gc.size), "occupied_cells": int(np.count_nonzero(oc)),
+            "count_cells_differing": diff, "sum_max_rel_err": rel,
+            "ok": bool(diff == 0 and rel <= 1e-6 and zero_ok)}
+
+
+def cpu_baseline_groupby(m=1 << 25, repeats=3):
+    """C3 on a bounded sample: the first m rows of the bench's key / value columns (the
+    counter-based generator gives the same rows), groupby(key).agg({v: [sum, count]}) by the
+    oracle's NumPy restatement (oracle.groupby_reference: sort-based, sums in row order; one
+    core) -- timed as the C3 CPU baseline -- and through the GPU routes 'auto' (dense grid)
+    and assume_sparse=True (first-appearance order), compared group by group: keys and
+    counts exact, sums rtol 1e-6."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    from oracle import oracle
+    keys = DeviceArray.random(m, "randint", seed=5, a=5, b=5 + 1_000_000, dtype="int32")
+    v = DeviceArray.random(m, "normal", seed=6)
+    hk, hv = keys.to_numpy(), v.to_numpy()
+    ts = []
+    for _ in range(repeats):
+        t0 = time.perf_counter()
+        uk, us, uc = oracle.groupby_reference(hk, hv)
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    base = {"value": m / t, "unit": "rows/s", "cores": 1, "kind": "port",
+            "sample": f"first {m} rows of the C3 key / value columns, oracle.groupby_reference (NumPy), "
+                      f"median of {repeats} runs ({t:.2f} s each)"}
+    df = vaex_amd.from_arrays(key=keys, v=v)
+    parity = {"rows": m, "groups": int(len(uk))}
+    ok = True
+    for route, sparse in (("auto", "auto"), ("hash", True)):
+        g = df.groupby("key", agg={"v": ["sum", "count"]}, assume_sparse=sparse)
+        gk, gc, gs = g["key"].to_numpy(), g["v"].to_numpy(), g["v_sum"].to_numpy()
+        o = np.argsort(gk, kind="stable")
+        same = len(gk) == len(uk) and bool(np.array_equal(gk[o], uk)) and bool(np.array_equal(gc[o], uc))
+        big = np.abs(us) > 1e-6  # near-zero sums of normal values: the absolute bound below
+        rel = float(np.max(np.abs(gs[o][big] - us[big]) / np.abs(us[big]))) if same and big.any() else None
+        r_ok = same and bool(np.allclose(gs[o], us, rtol=1e-6, atol=1e-9))
+        if sparse is True and r_ok:  # first-appearance order: groups sorted by their first row
+            _, first = np.unique(hk, return_index=True)
+            r_ok = bool(np.array_equal(gk, uk[np.argsort(first, kind="stable")]))
+            parity[route + "_first_appearance_order"] = r_ok
+        parity[route] = {"keys_counts_equal": same, "sum_max_rel_err": rel, "ok": r_ok}
+        ok = ok and r_ok
+    parity["ok"] = ok
+    return base, parity
 
 
 def bench_c1(args, repeats=5, gpu_repeats=20):

@@ -95,8 +95,9 @@ int vh_memcpy_dtod(void *dst, const void *src, uint64_t bytes);
 int vh_memset(void *dptr, int value, uint64_t bytes);
 /* synthetic columns generated in HBM (bench/test data; counter-based
  * splitmix64, so any sub-range can be regenerated on the host):
- * dist 0 = uniform [a, b) f64, 1 = normal(mean a, sd b) f64,
- *      2 = uniform integer [a, b) stored as `dtype` (I32/I64),
+ * dist 0 = uniform [a, b), 1 = normal(mean a, sd b): F64, or F32 (the
+ *      float64 draw rounded),
+ *      2 = uniform integer [a, b) stored as `dtype` (I8/I32/I64),
  *      3 = sorted: a + b * normal quantile of (i + 0.5) / n (f64, ascending),
  *      4 = sorted integers [a, b) in equal consecutive runs (I32/I64). */
 int vh_fill_random(void *dptr, uint64_t n, int dtype, int dist, uint64_t seed, double a, double b);

@@ -401,3 +401,79 @@ def test_dense_first_order_device_finish(layout):
     np.testing.assert_array_equal(got["hi"].to_numpy(), hi[order])
     np.testing.assert_array_equal(got["n"].to_numpy(), np.bincount(inv, minlength=len(u))[order])
     np.testing.assert_allclose(got["s"].to_numpy(), s[order], rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("kdt,vdt", [("int8", "float32"), ("uint16", "int32"), ("int64", "datetime64[ns]"),
+                                     ("uint32", "timedelta64[us]"), ("int32", "int64")])
+def test_dense_device_finish_dtypes(kdt, vdt):
+    """The device-finish route (vh_dense_first_take) over narrow / wide / unsigned keys near the
+    top of their range and 4-byte, integer and datetime / timedelta value columns: the result
+    columns keep the descriptor's output dtype (min / max of a datetime column are datetimes,
+    an int32 sum is int64), values equal numpy per key in first-appearance order."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(5)
+    n = (1 << 21) + 17
+    kt = np.dtype(kdt)
+    info = np.iinfo(kt)
+    lo_k = 0 if kt.kind == "u" else int(info.min) + 7
+    span = min(int(info.max) - lo_k, 60_000)
+    base = int(info.max) - span  # keys up to the dtype's max (unsigned: near the top of the range)
+    keys = (base + rng.integers(0, span + 1, n)).astype(kt)
+    vt = np.dtype(vdt)
+    if vt.kind in "mM":
+        raw = rng.integers(-10 ** 12, 10 ** 12, n)
+        vals = raw.astype(np.int64).view(vt) if vt.kind == "M" else raw.astype(vt)
+        vcol = vals
+    else:
+        vals = (rng.normal(size=n) * 100).astype(vt) if vt.kind == "f" else rng.integers(-1000, 1000, n).astype(vt)
+        vcol = DeviceArray.from_numpy(vals)
+    df = vaex_amd.from_arrays(key=DeviceArray.from_numpy(keys), v=vcol)
+    aggs = {"lo": vaex_amd.agg.min("v"), "hi": vaex_amd.agg.max("v"), "n": vaex_amd.agg.count()}
+    if vt.kind not in "mM":
+        aggs["s"] = vaex_amd.agg.sum("v")
+    got = df.groupby("key", agg=aggs, assume_sparse=True)
+    u, first, inv = np.unique(keys, return_index=True, return_inverse=True)
+    order = np.argsort(first)
+    np.testing.assert_array_equal(got["key"].to_numpy(), u[order])
+    srt = np.argsort(inv, kind="stable")
+    bounds = np.r_[0, np.cumsum(np.bincount(inv, minlength=len(u)))]
+    lo = np.array([vals[srt[bounds[i]:bounds[i + 1]]].min() for i in range(len(u))], dtype=vals.dtype)
+    hi = np.array([vals[srt[bounds[i]:bounds[i + 1]]].max() for i in range(len(u))], dtype=vals.dtype)
+    glo, ghi = got["lo"].to_numpy(), got["hi"].to_numpy()
+    assert glo.dtype == vals.dtype and ghi.dtype == vals.dtype
+    np.testing.assert_array_equal(glo, lo[order])
+    np.testing.assert_array_equal(ghi, hi[order])
+    np.testing.assert_array_equal(got["n"].to_numpy(), np.bincount(inv, minlength=len(u))[order])
+    if "s" in aggs:
+        s = np.bincount(inv, weights=vals.astype(np.float64), minlength=len(u))
+        gs = got["s"].to_numpy()
+        if vt.kind in "iu":
+            assert gs.dtype == np.int64
+            np.testing.assert_array_equal(gs, s[order].astype(np.int64))
+        else:
+            np.testing.assert_allclose(gs, s[order], rtol=1e-5, atol=1e-3)
+
+
+def test_dense_device_finish_row_limit_and_reuse():
+    """row_limit on the device-finish route raises what the set build raises; a count
+    descriptor reused across queries carries no per-query state (occupancy) into the next."""
+    import vaex_amd
+    from vaex_amd.dataframe import RowLimitException
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(6)
+    keys = rng.integers(0, 5000, 1 << 20).astype(np.int32)
+    v = rng.normal(size=1 << 20)
+    df = vaex_amd.from_arrays(key=DeviceArray.from_numpy(keys), v=DeviceArray.from_numpy(v))
+    with pytest.raises(RowLimitException):
+        df.groupby("key", agg={"m": vaex_amd.agg.max("v")}, assume_sparse=True, row_limit=100)
+    cnt = vaex_amd.agg.count()
+    a = df.groupby("key", agg={"n": cnt, "m": vaex_amd.agg.max("v")}, assume_sparse=True)
+    assert not hasattr(cnt, "occupancy") and not getattr(cnt, "want_occupancy", False)
+    keys2 = keys[: 1 << 19] + 10_000
+    df2 = vaex_amd.from_arrays(key=DeviceArray.from_numpy(keys2), v=DeviceArray.from_numpy(v[: 1 << 19]))
+    b = df2.groupby("key", agg={"n": cnt, "m": vaex_amd.agg.max("v")}, assume_sparse=True)
+    for d, k in ((a, keys), (b, keys2)):
+        u, first, inv = np.unique(k, return_index=True, return_inverse=True)
+        np.testing.assert_array_equal(d["key"].to_numpy(), u[np.argsort(first)])
+        np.testing.assert_array_equal(d["n"].to_numpy(), np.bincount(inv)[np.argsort(first)])

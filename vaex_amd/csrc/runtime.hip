@@ -371,18 +371,24 @@ __global__ void k_fill_random(void *dst, uint64_t n, int dtype, int dist, uint64
             else reinterpret_cast<int64_t *>(dst)[i] = v;
             continue;
         }
-        if (dist == 0) {
-            reinterpret_cast<double *>(dst)[i] = a + (b - a) * u01(r1);
-        } else if (dist == 1) {
-            uint64_t r2 = splitmix64(s ^ (2 * i + 1));
-            double u1 = 1.0 - u01(r1);  // (0, 1]
-            double u2 = u01(r2);
-            double z = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
-            reinterpret_cast<double *>(dst)[i] = a + b * z;
+        if (dist == 0 || dist == 1) {
+            double d;
+            if (dist == 0) {
+                d = a + (b - a) * u01(r1);
+            } else {
+                uint64_t r2 = splitmix64(s ^ (2 * i + 1));
+                double u1 = 1.0 - u01(r1);  // (0, 1]
+                double u2 = u01(r2);
+                d = a + b * (sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+            }
+            // float32: the float64 draw rounded (the h2o fixture's x4 = x.astype('float32'))
+            if (dtype == VH_F32) reinterpret_cast<float *>(dst)[i] = (float)d;
+            else reinterpret_cast<double *>(dst)[i] = d;
         } else {
             uint64_t span = (uint64_t)(int64_t)(b - a);
             int64_t v = (int64_t)a + (int64_t)(span ? r1 % span : 0);
             if (dtype == VH_I32) reinterpret_cast<int32_t *>(dst)[i] = (int32_t)v;
+            else if (dtype == VH_I8) reinterpret_cast<int8_t *>(dst)[i] = (int8_t)v;
             else reinterpret_cast<int64_t *>(dst)[i] = v;
         }
     }
@@ -738,8 +744,10 @@ int vh_memset(void *dptr, int value, uint64_t bytes) {
 int vh_fill_random(void *dptr, uint64_t n, int dtype, int dist, uint64_t seed, double a, double b) {
     VH_API_BEGIN
     if (dist < 0 || dist > 4) fail(VH_ERR_ARG, "unknown distribution");
-    if ((dist < 2 || dist == 3) && dtype != VH_F64) fail(VH_ERR_ARG, "uniform/normal fill needs float64");
-    if ((dist == 2 || dist == 4) && dtype != VH_I32 && dtype != VH_I64) fail(VH_ERR_ARG, "integer fill needs int32/int64");
+    if (dist < 2 && dtype != VH_F64 && dtype != VH_F32) fail(VH_ERR_ARG, "uniform/normal fill needs float64/float32");
+    if (dist == 3 && dtype != VH_F64) fail(VH_ERR_ARG, "sorted normal fill needs float64");
+    if (dist == 2 && dtype != VH_I32 && dtype != VH_I64 && dtype != VH_I8) fail(VH_ERR_ARG, "integer fill needs int8/int32/int64");
+    if (dist == 4 && dtype != VH_I32 && dtype != VH_I64) fail(VH_ERR_ARG, "sorted integer fill needs int32/int64");
     if (n) {
         hipLaunchKernelGGL(k_fill_random, dim3(blocks_for(n, 256)), dim3(256), 0, stream(), dptr, n, dtype,
                            dist, seed, a, b);

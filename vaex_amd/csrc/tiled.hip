@@ -123,6 +123,16 @@ struct TileParams {
     // the slot's non-NaN values (mm_cnt_nn) or on every entry
     uint32_t mm_simple, mm_cnt_nn;
     int32_t mm_off[4];
+    // stream layout of the fast kernels (stream = 1): each pass-A workgroup appends every
+    // commit's padded, tile-sorted entries to ONE contiguous stream (w * wg_stride on), instead
+    // of T private per-tile regions, and records where each tile's run of the commit starts:
+    // tab[(w * (T + 1) + t) * ncw + c] = stream offset of tile t's run of commit c (row T: the
+    // commit's end; commits past a workgroup's last: its final offset, i.e. empty runs).  Pass B
+    // gathers a tile's (workgroup, commit) segments through the table.  256-512 write streams
+    // instead of T x W regions: the region pattern's cost and its dependence on where the
+    // scratch lands in HBM (r05: 6.2-7.4 ms for one C2 pass A) go away (scripts/bw_probe6.hip)
+    uint32_t stream, ncw;
+    uint32_t *tab;
 };
 
 // local cell of a padding entry (tiles hold at most 2^15 cells when runs are padded)
@@ -473,6 +483,16 @@ __global__ __launch_bounds__(TA_THREADS) void k_tile_sample(BinPlan p, uint64_t 
 #else
 #define TA_ATTR
 #endif
+// the count-only f64 pass A (NV = 0): VH_TA_WPE0 waves per SIMD at least (4 caps it at 128
+// VGPRs: two 512-thread workgroups per CU instead of one at 129)
+#ifndef VH_TA_WPE0
+#define VH_TA_WPE0 0
+#endif
+#if VH_TA_WAVES > 0
+#define TA_ATTR_F64(NV) TA_ATTR
+#else
+#define TA_ATTR_F64(NV) __attribute__((amdgpu_waves_per_eu(((NV) == 0 && VH_TA_WPE0 > 0) ? VH_TA_WPE0 : 1)))
+#endif
 
 __device__ inline void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -581,9 +601,25 @@ template <int NV> __device__ inline ScatterLds fast_lds(unsigned char *raw, uint
 __device__ inline void scatter_lds_init(const ScatterLds &l, const TileParams &tp, uint32_t T) {
     for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) {
         l.hist[t] = 0;
-        l.base[t] = (uint32_t)tp.toff[t];
-        l.lim[t] = (uint32_t)tp.toff[t] + tp.cap[t];
+        l.base[t] = tp.stream ? 0u : (uint32_t)tp.toff[t];
+        l.lim[t] = tp.stream ? ~0u : (uint32_t)tp.toff[t] + tp.cap[t];  // the stream is sized exactly
     }
+    if (threadIdx.x == 0) {  // stream layout: write cursor and commit index of this workgroup
+        l.wave_sums[1] = 0;
+        l.wave_sums[2] = 0;
+    }
+}
+
+// stream layout: the table rows of the commits a workgroup did not have (empty runs at its
+// final offset); after the pass-A loop, behind an LDS barrier
+__device__ inline void stream_tab_tail(const ScatterLds &l, const TileParams &tp, uint32_t T) {
+    if (!tp.stream) return;
+    const uint32_t cend = l.wave_sums[1], c0 = l.wave_sums[2], ncw = tp.ncw;
+    if (c0 >= ncw) return;
+    const uint64_t row0 = (uint64_t)blockIdx.x * (T + 1);
+    const uint32_t per = ncw - c0;
+    for (uint32_t i = threadIdx.x; i < (T + 1) * per; i += TA_THREADS)
+        tp.tab[(row0 + i / per) * ncw + c0 + i % per] = cend;
 }
 
 constexpr uint32_t DEST_OVERFLOW = 0x80000000u;  // | tile: region and spill full, global atomics
@@ -691,12 +727,19 @@ __device__ inline void batch_commit(const ScatterLds &l, const FusedAggs &fa, co
 // B1, which every wave reaches after its stream-out.
 // Wide stream-out (tp.wide): a tile's staged run is padded to hp = roundup8(h) entries with
 // DUMMY_CELL keys, so boff, the region bases and dbase stay multiples of 8.
+// Stream layout (tp.stream): every tile's dbase is the workgroup's stream cursor, so staged
+// entry k goes to cursor + k (the commit is written as one contiguous block), the tile's run
+// start is recorded in the table, and the cursor advances by the commit's padded total.
 __device__ inline void fast_scan(const ScatterLds &l, const TileParams &tp, uint32_t T) {
     if (threadIdx.x >= 64) return;
     const uint32_t lane = threadIdx.x;
     const uint32_t per = (T + 63) / 64;
     const uint32_t t0 = lane * per;
     const uint32_t pad = tp.wide ? 7u : 0u;
+    const bool stream = tp.stream != 0;
+    // (read by every lane before lane 63 advances them below: one wave, program order)
+    const uint32_t cur = stream ? l.wave_sums[1] : 0u, ci = stream ? l.wave_sums[2] : 0u;
+    uint32_t *tab = stream ? tp.tab + ((uint64_t)blockIdx.x * (T + 1)) * tp.ncw + ci : nullptr;
     uint32_t *sk = reinterpret_cast<uint32_t *>(l.sp);
     uint32_t s = 0;
     for (uint32_t t = t0; t < t0 + per && t < T; t++) s += (l.hist[t] + pad) & ~pad;
@@ -710,17 +753,25 @@ __device__ inline void fast_scan(const ScatterLds &l, const TileParams &tp, uint
     for (uint32_t t = t0; t < t0 + per && t < T; t++) {
         const uint32_t h0 = l.hist[t], h = (h0 + pad) & ~pad, b = l.base[t], lim = l.lim[t];
         l.boff[t] = acc;
-        l.dbase[t] = b - acc;
+        l.dbase[t] = stream ? cur : b - acc;
         l.base[t] = b + h;
         l.hist[t] = 0;
         for (uint32_t x = h0; x < h; x++) sk[acc + x] = (t << 16) | DUMMY_CELL;
+        if (stream) tab[(uint64_t)t * tp.ncw] = cur + acc;
         acc += h;
         if (b + h > lim) {  // rows past the region: reserve them in the tile's spill area
             const uint32_t first = max(b, lim);
             l.soff[t] = atomicAdd(&tp.spill_fill[t], b + h - first) - first;
         }
     }
-    if (lane == 63) l.wave_sums[0] = inc;
+    if (lane == 63) {
+        l.wave_sums[0] = inc;
+        if (stream) {
+            tab[(uint64_t)T * tp.ncw] = cur + inc;
+            l.wave_sums[1] = cur + inc;
+            l.wave_sums[2] = ci + 1;
+        }
+    }
 }
 
 // VT: the carried value type -- double (8-byte slots, or narrowed at the store when
@@ -1086,7 +1137,7 @@ __device__ inline uint32_t scalar_f64_index32(double v, double vmin, double scal
 // 16-byte pairs; the next batch loads into a second register buffer while the current
 // one is ranked, sorted and written.
 template <int ND, int NV, int SB>
-__global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
+__global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
     constexpr int NC = ND + NV;
     constexpr int PAIRS = TA_RPT / 2;
     extern __shared__ __align__(16) unsigned char lds_raw[];
@@ -1211,6 +1262,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_f64(BinPlan
     }
     lds_barrier();
     for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.base[t] - (uint32_t)tp.toff[t];
+    stream_tab_tail(l, tp, T);
 }
 
 // BinnerOrdinal<int32_t> index of a loaded key, native byte order, no mask
@@ -1395,6 +1447,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
     }
     lds_barrier();
     for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.base[t] - (uint32_t)tp.toff[t];
+    stream_tab_tail(l, tp, T);
 }
 
 template <int NV, bool MM>
@@ -1534,6 +1587,7 @@ __global__ __launch_bounds__(TBT) void k_tile_reduce(FusedAggs fa, TileParams tp
     extern __shared__ __align__(16) unsigned char lds_raw[];
     __shared__ uint32_t s_fill[1024 + 1];
     __shared__ uint32_t s_pre[1024 + 2];
+    __shared__ uint64_t s_base[1024 + 1];  // first entry of each region / segment of the round
     const WorkUnit u = units[blockIdx.x];
     const uint32_t t = u.tile;
     const uint32_t cap = tp.cap[t];
@@ -1545,32 +1599,100 @@ __global__ __launch_bounds__(TBT) void k_tile_reduce(FusedAggs fa, TileParams tp
     const uint32_t s0 = part == 0 ? 0u : min(F, (uint32_t)((uint64_t)F * part / parts) & ~7u);
     const uint32_t s1 = part + 1 >= parts ? F : min(F, (uint32_t)((uint64_t)F * (part + 1) / parts) & ~7u);
     const uint64_t spill0 = tp.spill_base + tp.spill_start[t] + s0;  // first entry of the slice
-    bool any = false;
-    for (uint32_t k = threadIdx.x; k < nw; k += TBT) {
-        const uint32_t f = k < nwr ? min(tp.fills[(uint64_t)t * tp.W + u.w_begin + k], cap) : (s1 > s0 ? s1 - s0 : 0u);
+    // Stream layout: the unit's segments are (workgroup, commit) pairs, w_begin <= w < w_end and
+    // c < ncw, taken in rounds of SEGS; segment g of the unit is w = w_begin + g / ncw,
+    // c = g % ncw, its run [tab[row], tab[row + ncw]) with row = (w (T + 1) + t) ncw + c
+    // (consecutive lanes read consecutive commits).  Regions: one round of nw regions.
+    // one segment per thread and round; the next round's table entries are fetched into
+    // registers while this round's chunks are processed
+    constexpr uint32_t SEGS = TBT;
+    static_assert(TBT <= 1024, "segments per round");
+    const bool stream = tp.stream != 0;
+    const uint32_t T = tp.ntiles, ncw = tp.ncw;
+    const uint32_t nseg = stream ? nwr * ncw : nw;
+    const uint32_t rounds = stream ? (nseg + SEGS - 1) / SEGS : 1u;
+    uint32_t pf_f = 0;
+    uint64_t pf_b = 0;
+    auto fetch = [&](uint32_t r) {
+        const uint32_t g = r * SEGS + threadIdx.x;
+        pf_f = 0;
+        if (g < nseg) {
+            const uint32_t w = u.w_begin + g / ncw, c = g % ncw;
+            const uint64_t row = ((uint64_t)w * (T + 1) + t) * ncw + c;
+            const uint32_t a = tp.tab[row], e = tp.tab[row + ncw];
+            pf_f = e - a;
+            pf_b = (uint64_t)w * tp.wg_stride + a;
+        }
+    };
+    // stream layout: the fetched segments into LDS and the block-wide exclusive scan of their
+    // chunk counts (wave shuffles + wave totals; one barrier inside); returns whether this
+    // thread's segment holds entries.  Threads past the unit's segments count 0 chunks, so
+    // s_pre[cnt] is the round's total for any cnt <= SEGS.
+    __shared__ uint32_t s_wsum[TBT / 64];
+    auto stream_round = [&](uint32_t r) -> bool {
+        const uint32_t k = threadIdx.x, lane = k & 63, wave = k >> 6;
+        const uint32_t f = r * SEGS + k < nseg ? pf_f : 0u, ch = (f + 7) >> 3;
         s_fill[k] = f;
-        any |= f != 0;
-    }
-    if (!__syncthreads_or(any)) return;
-    uint32_t *lw = reinterpret_cast<uint32_t *>(lds_raw);
-    for (uint32_t i = threadIdx.x; i < fa.lds_words; i += TBT) lw[i] = 0;
-    if (!tp.flags_mode && threadIdx.x < 64) {
-        // exclusive scan of the chunk counts by the first wave (per regions per lane)
-        const uint32_t lane = threadIdx.x, per = (nw + 63) / 64, k0 = lane * per;
+        s_base[k] = pf_b;
+        uint32_t inc = ch;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(inc, off, 64);
+            if ((int)lane >= off) inc += y;
+        }
+        if (lane == 63) s_wsum[wave] = inc;
+        __syncthreads();
+        uint32_t before = 0, tot = 0;
+#pragma unroll
+        for (uint32_t v = 0; v < TBT / 64; v++) {
+            const uint32_t x = s_wsum[v];
+            before += v < wave ? x : 0u;
+            tot += x;
+        }
+        s_pre[k] = before + inc - ch;
+        if (k == 0) s_pre[SEGS] = tot;
+        return f != 0;
+    };
+    auto load_round = [&]() -> bool {  // regions
+        bool any = false;
+        for (uint32_t k = threadIdx.x; k < nw; k += TBT) {
+            const uint32_t f = k < nwr ? min(tp.fills[(uint64_t)t * tp.W + u.w_begin + k], cap) : (s1 > s0 ? s1 - s0 : 0u);
+            s_fill[k] = f;
+            s_base[k] = k < nwr ? (uint64_t)(u.w_begin + k) * tp.wg_stride + tp.toff[t] : spill0;
+            any |= f != 0;
+        }
+        return any;
+    };
+    // exclusive scan of the round's chunk counts by the first wave (per segments per lane)
+    auto scan_round = [&]() {  // regions
+        if (threadIdx.x >= 64) return;
+        const uint32_t cnt = nw;
+        const uint32_t lane = threadIdx.x, per = (cnt + 63) / 64, k0 = lane * per;
         uint32_t sum = 0;
-        for (uint32_t k = k0; k < k0 + per && k < nw; k++) sum += (s_fill[k] + 7) >> 3;
+        for (uint32_t k = k0; k < k0 + per && k < cnt; k++) sum += (s_fill[k] + 7) >> 3;
         uint32_t inc = sum;
         for (int off = 1; off < 64; off <<= 1) {
             const uint32_t y = __shfl_up(inc, off, 64);
             if ((int)lane >= off) inc += y;
         }
         uint32_t acc = inc - sum;
-        for (uint32_t k = k0; k < k0 + per && k < nw; k++) {
+        for (uint32_t k = k0; k < k0 + per && k < cnt; k++) {
             s_pre[k] = acc;
             acc += (s_fill[k] + 7) >> 3;
         }
-        if (lane == 63) s_pre[nw] = inc;
+        if (lane == 63) s_pre[cnt] = inc;
+    };
+    bool any0;
+    if (stream) {
+        fetch(0);
+        any0 = stream_round(0);
+    } else {
+        any0 = load_round();
     }
+    if (!__syncthreads_or(any0 || (stream && rounds > 1))) return;
+    uint32_t *lw = reinterpret_cast<uint32_t *>(lds_raw);
+    for (uint32_t i = threadIdx.x; i < fa.lds_words; i += TBT) lw[i] = 0;
+    if (!tp.flags_mode && !stream) scan_round();
     __syncthreads();
     // MM: the plan has min / max aggregators (a separate instantiation: their code would
     // raise the count / sum kernel's registers past the 1024-thread budget)
@@ -1605,24 +1727,47 @@ __global__ __launch_bounds__(TBT) void k_tile_reduce(FusedAggs fa, TileParams tp
         // threads; a 512-thread form with two chunks and the entry loop unrolled kept 176 B per
         // lane in scratch memory and ran pass B at 10.6 against 5.5 ms)
         constexpr int VU = MM ? 1 : tb_vu<NV>();
-        const uint32_t C = s_pre[nw];
         const uint16_t *ent16 = reinterpret_cast<const uint16_t *>(tp.entries);
-        const uint64_t toff_t = tp.toff[t];
-        uint32_t kk = 0;  // region of this lane's current chunk
-        for (uint32_t c0 = 0; c0 < C; c0 += TBT * VU) {
+        for (uint32_t r = 0; r < rounds; r++) {
+        if (r > 0) {  // the next round's segments (every lane is done with this round's)
+            __syncthreads();
+            stream_round(r);
+            __syncthreads();
+        }
+        if (stream && r + 1 < rounds) fetch(r + 1);
+        const uint32_t cnt = stream ? min(SEGS, nseg - r * SEGS) : nw;
+        const uint32_t C = s_pre[cnt];
+        // wave-major chunks: wave v takes the contiguous chunk block [cb, ce), 64 consecutive
+        // chunks per load instruction, so a lane's chunks only grow and its segment cursor
+        // walks forward over the block's few segments (an interleaved assignment skipped
+        // TBT chunks, i.e. dozens of short segments, per step)
+        const uint32_t lane = threadIdx.x & 63, nwv = TBT / 64;
+        const uint32_t per_wave = ((C + nwv - 1) / nwv + 63) & ~63u;
+        const uint32_t cb = min(C, (threadIdx.x >> 6) * per_wave), ce = min(C, cb + per_wave);
+        uint32_t kk = 0;  // segment of this lane's current chunk: the last k with s_pre[k] <= cb
+        if (cb < ce) {
+            uint32_t lo = 0, hi = cnt;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_pre[mid] <= cb) lo = mid;
+                else hi = mid;
+            }
+            kk = lo;
+        }
+        for (uint32_t c0 = cb; c0 < ce; c0 += 64 * VU) {
             uint4 ev[VU];
             double2 vv[VU][NV > 0 ? NV : 1][4];
             uint32_t rem[VU];
 #pragma unroll
             for (int j = 0; j < VU; j++) {
-                const uint32_t c = c0 + j * TBT + threadIdx.x;
-                const uint32_t cc = c < C ? c : C - 1;
+                const uint32_t c = c0 + j * 64 + lane;
+                const uint32_t cc = c < ce ? c : ce - 1;
                 while (s_pre[kk + 1] <= cc) kk++;
                 const uint32_t q = (cc - s_pre[kk]) * 8;
-                // regions start at multiples of 8 entries and hold a multiple of 8, so the
-                // chunk never leaves its region (entries past the fill are ignored)
-                const uint64_t e = kk < nwr ? (uint64_t)(u.w_begin + kk) * tp.wg_stride + toff_t + q : spill0 + q;
-                rem[j] = c < C ? min(8u, s_fill[kk] - q) : 0u;
+                // regions / segments start at multiples of 8 entries and hold a multiple of 8,
+                // so the chunk never leaves its segment (entries past the fill are ignored)
+                const uint64_t e = s_base[kk] + q;
+                rem[j] = c < ce ? min(8u, s_fill[kk] - q) : 0u;
                 ev[j] = *reinterpret_cast<const uint4 *>(ent16 + e);
 #pragma unroll
                 for (int s = 0; s < NV; s++) {
@@ -1855,6 +2000,7 @@ __global__ __launch_bounds__(TBT) void k_tile_reduce(FusedAggs fa, TileParams tp
                 if constexpr (VU > 7) chunk(std::integral_constant<int, 7>{});
             }
         }
+        }  // rounds
     } else {
         for (uint32_t k = 0; k < nw; k++) {
             const uint32_t cnt = s_fill[k];
@@ -2099,7 +2245,7 @@ bool try_tiled(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t
 // by the library stream.
 struct TileScratch {
     std::mutex mu;
-    DevBuf entries, values, meta, mmtmp;
+    DevBuf entries, values, meta, mmtmp, tab;
 };
 
 static bool getenv_flag_off(const char *name) {  // NAME=0 turns a default-on path off (A/B runs)
@@ -2253,8 +2399,23 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     }
     bpc = std::max(1, std::min(bpc, TA_WG_PER_CU));
     const uint32_t W = std::min<uint32_t>(1024, (uint32_t)cu_count() * bpc);
-    // pass-B work units: sum over tiles of ceil(e_t / target) <= T + 4 cu (target = n / 4 cu)
-    const uint64_t max_units = (uint64_t)T + 4 * (uint64_t)cu_count() + 16;
+    const uint64_t nb = (n + TA_BATCH - 1) / TA_BATCH;
+    const uint64_t kbat = (nb + W - 1) / W;  // batches per workgroup (at most)
+    const uint64_t rows_per_wg = kbat * TA_BATCH;
+    const uint64_t ncw = (kbat + sb_k - 1) / sb_k;  // commits per workgroup (at most)
+    // stream layout (TileParams::stream): one exactly sized stream per workgroup, no sampled
+    // capacities, spill areas or overflow rows; VH_TILE_STREAM=0 keeps the per-tile regions
+    const bool stream_layout = wide && !getenv_flag_off("VH_TILE_STREAM") &&
+                               (uint64_t)W * (T + 1) * ncw < (1ull << 31);
+    // stream layout: a pass-B unit walks (workgroup, commit) segments in rounds of
+    // TB_THREADS; at most TB_ROUNDS rounds per unit (a cold tile's single unit would walk all
+    // W x ncw segments in one workgroup while the rest of the chip idles)
+    constexpr uint64_t TB_ROUNDS = 6;
+    const uint64_t wpu = std::max<uint64_t>(1, (uint64_t)TB_THREADS * TB_ROUNDS / std::max<uint64_t>(ncw, 1));
+    const uint64_t g_min = stream_layout ? (W + wpu - 1) / wpu : 1;
+    // pass-B work units: sum over tiles of max(g_min, ceil(e_t / target)) <= T g_min + 4 cu
+    // (target = n / 4 cu)
+    const uint64_t max_units = (uint64_t)T * g_min + 4 * (uint64_t)cu_count() + 16;
     DevBuf &meta = ws.meta;
     const uint64_t meta_bytes = 8 * (uint64_t)T /*hist*/ + 8 * (uint64_t)T /*hist2*/ + 8 * (uint64_t)T /*toff*/ +
                                 8 * (uint64_t)T /*spill_start*/ + 4 * (uint64_t)T /*spill_cap*/ + 4 * (uint64_t)T /*spill_fill*/ +
@@ -2272,7 +2433,6 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     uint32_t *d_fills = d_cap + ((T + 3) & ~3u);
     WorkUnit *d_units = reinterpret_cast<WorkUnit *>(d_fills + (uint64_t)T * W + 4 - ((uint64_t)T * W) % 4);
     uint32_t *d_brange = reinterpret_cast<uint32_t *>(d_units + max_units);
-    const uint64_t nb = (n + TA_BATCH - 1) / TA_BATCH;
     const uint64_t sblocks = std::min<uint64_t>(nb, SAMPLE_BLOCKS);
     const uint64_t bstride = std::max<uint64_t>(TA_BATCH, (n / sblocks));
     VH_HIP(hipMemsetAsync(d_hist, 0, 16 * (uint64_t)T, st));
@@ -2319,13 +2479,13 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     // workgroup's rows past its region go to the tile's spill area, sized from the spread the
     // sample measures per batch-sized block (clustered rows: each block all in or all out of
     // a tile) -- half the tile's expected rows when the rows are clustered.
-    const uint64_t kbat = (nb + W - 1) / W;  // batches per workgroup (at most)
-    const uint64_t rows_per_wg = kbat * TA_BATCH;
     // wide stream-out: up to 7 padding entries per (workgroup, tile) and commit
-    const uint64_t pad_wg = wide ? 7 * ((kbat + sb_k - 1) / sb_k) : 0;
+    const uint64_t pad_wg = wide ? 7 * ncw : 0;
     std::vector<uint32_t> cap(T), scap(T);
     std::vector<uint64_t> toff(T), sstart(T);
     uint64_t stride = 0, stotal = 0;
+    if (stream_layout) stride = (rows_per_wg + pad_wg * T + 8 + 7) & ~uint64_t(7);
+    for (uint32_t t = 0; t < T && stream_layout; t++) cap[t] = scap[t] = 0, toff[t] = sstart[t] = 0;
     const double blocks = (double)sblocks;  // every sample block is TA_BATCH rows, like a batch
     // clustered rows (block variance well above the Poisson value: each sample block all in
     // or all out of a tile) anywhere in the sample
@@ -2334,7 +2494,7 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         const double m = (double)hist[t] / blocks, var_b = std::max(0.0, (double)hist[T + t] / blocks - m * m);
         any_clustered = any_clustered || var_b > 4.0 * m + 1.0;
     }
-    for (uint32_t t = 0; t < T; t++) {
+    for (uint32_t t = 0; t < T && !stream_layout; t++) {
         const double p = (double)hist[t] / (double)sampled, e = (double)rows_per_wg * p;
         const double m = (double)hist[t] / blocks, var_b = std::max(0.0, (double)hist[T + t] / blocks - m * m);
         const bool clustered = var_b > 4.0 * m + 1.0;
@@ -2405,6 +2565,12 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     tp.spill_start = d_sstart;
     tp.spill_base = stride * W;
     tp.entries = ws.entries.ptr;
+    if (stream_layout) {
+        tp.stream = 1;
+        tp.ncw = (uint32_t)ncw;
+        ws.tab.ensure((uint64_t)W * (T + 1) * ncw * 4 + 256);
+        tp.tab = ws.tab.as<uint32_t>();
+    }
     for (int s = 0; s < nv; s++)
         tp.values[s] = vnarrow ? reinterpret_cast<double *>(ws.values.as<uint32_t>() + (uint64_t)s * total)
                                : ws.values.as<double>() + (uint64_t)s * total;
@@ -2424,11 +2590,23 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     // unit k of g of a tile also reads slice k of g of the tile's spill area
     std::vector<WorkUnit> units;
     const double target = std::max(1.0, (double)n / ((double)cu_count() * 4));
+    std::vector<double> unit_rows;
     for (uint32_t t = 0; t < T; t++) {
         const double e = (double)n * (double)hist[t] / (double)sampled;
-        uint32_t g = (uint32_t)std::min<double>(W, std::max(1.0, std::ceil(e / target)));
-        for (uint32_t k = 0; k < g; k++)
+        uint32_t g = (uint32_t)std::min<double>(W, std::max((double)g_min, std::ceil(e / target)));
+        for (uint32_t k = 0; k < g; k++) {
             units.push_back({t, (uint32_t)((uint64_t)W * k / g), (uint32_t)((uint64_t)W * (k + 1) / g), k | (g << 16)});
+            unit_rows.push_back(e / g);
+        }
+    }
+    if (stream_layout) {
+        // largest units first (they start before the small ones fill the chip's tail)
+        std::vector<uint32_t> ord(units.size());
+        for (uint32_t i = 0; i < ord.size(); i++) ord[i] = i;
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return unit_rows[a] > unit_rows[b]; });
+        std::vector<WorkUnit> sorted(units.size());
+        for (uint32_t i = 0; i < ord.size(); i++) sorted[i] = units[ord[i]];
+        units.swap(sorted);
     }
     if (units.size() > max_units) fail(VH_ERR_RUNTIME, "tiled binning: work-unit table overflow");
     if (!units.empty()) upload(d_units, units.data(), sizeof(WorkUnit) * units.size());

@@ -9,6 +9,8 @@ column materialised).  ``GrouperCategory`` (groupby.py:216-245) bins categorical
 directly.  ``GroupBy.agg`` (groupby.py:484-533) strips the edges; with >1 key the
 cartesian grid is filtered by count > 0.
 """
+import copy
+
 import numpy as np
 
 from . import agg as vagg
@@ -558,7 +560,12 @@ class GroupByBase:
             not np.ma.isMaskedArray(key_col) and np.dtype(key_col.dtype).kind in "iu" and all(
             type(a) is vagg.AggregatorDescriptorBasic and a.name in ("AggCount", "AggSum", "AggMin", "AggMax")
             and a.selection in (None, False) for _, a in parsed)
+        self.descs = {}
         for column_name, aggregate in parsed:
+            # per-query flags go on a copy: a user's descriptor object may be reused by later
+            # or concurrent queries (occupancy / keep_device are this query's state)
+            aggregate = copy.copy(aggregate)
+            self.descs[column_name] = aggregate
             aggregate.edges = True
             aggregate.keep_device = self.device_finish
             is_count = isinstance(aggregate, vagg.AggregatorDescriptorBasic) and aggregate.name == "AggCount" \
@@ -671,7 +678,12 @@ class GroupBy(GroupByBase):
         finally:
             labels = labels.result() if labels is not None else None
         if self.device_finish:
-            return self._agg_dense_device(arrays, counts)
+            from .taskparts import DeviceResult
+            if isinstance(counts.get(), DeviceResult) and all(isinstance(v.get(), DeviceResult) for v in arrays.values()):
+                return self._agg_dense_device(arrays, counts)
+            # a part handed a host result back (keep_device not honoured): key order on the
+            # host, and the caller applies the first-appearance order itself
+            self.device_finish = False
         arrays = {k: extract_central_part(np.asarray(v.get())) for k, v in arrays.items()}
         counts_edges = np.asarray(counts.get())
         central = extract_central_part(counts_edges)
@@ -729,7 +741,7 @@ class GroupBy(GroupByBase):
         if nnz == 0:
             columns = {g.label: np.empty(0, label_dt)}
             for k, a in aggs.items():
-                columns[k] = np.empty(0, a._grid_dtype)
+                columns[k] = np.empty(0, self.descs[k].dtype_out if k in self.descs else a._grid_dtype)
             return DataFrame(columns)
         names = list(aggs)
         outs = [_lib.pinned_empty(nnz, aggs[k]._grid_dtype) for k in names]
@@ -750,6 +762,12 @@ class GroupBy(GroupByBase):
                   (ctypes.c_void_p * max(k, 1))(*[o.ctypes.data for o in outs]), label_dt.itemsize, lab.ctypes.data)
         columns = {g.label: lab}
         for name, o in zip(names, outs):
+            # the grid's dtype is the binned one (datetime64 / timedelta64 bin as 64-bit
+            # integers): the result column takes the descriptor's output dtype, as
+            # TaskPartAggregation.get_result does (cpu.py:592-605)
+            dtype_out = np.dtype(self.descs[name].dtype_out) if name in self.descs else o.dtype
+            if dtype_out != o.dtype and dtype_out.itemsize == o.dtype.itemsize:
+                o = o.view(dtype_out.newbyteorder("=") if dtype_out.byteorder not in "<=|" else dtype_out)
             columns[name] = o
         return DataFrame(columns)
 
