@@ -55,7 +55,11 @@ constexpr int TF_BATCH = TF_THREADS * TF_RPT;  // 4096 rows per batch
 #endif
 constexpr int TF_LG = VH_TF_LG;  // rows per load group of the float64-binner pass A
 static_assert(TF_RPT % TF_LG == 0, "load groups tile the rows of a lane");
-constexpr int TFB_THREADS = 1024;
+#ifndef VH_TFB_THREADS
+#define VH_TFB_THREADS 1024
+#endif
+constexpr int TFB_THREADS = VH_TFB_THREADS;  // pass B threads (512: two workgroups per CU)
+static_assert((1 << 12) / TFB_THREADS <= 8, "merge: at most 8 cells of a 4096-cell tile per thread");
 constexpr uint32_t TF_S_LOG2 = 12;  // 4096 cells per tile: pass B LDS 8-B key + 4-B row = 48 KB
 constexpr uint32_t TF_MAX_TILES = 2048;
 constexpr int TF_SAMPLE_BLOCKS = 512;
@@ -354,43 +358,73 @@ __global__ __launch_bounds__(TFB_THREADS) void k_first_reduce(FirstParams fp, co
     const uint32_t C = s_pre[nw];
     const uint64_t toff_t = fp.toff[t];
     uint32_t kk = 0;  // region of this lane's current chunk (chunk indices of a lane only grow)
+    // One chunk of 8 entries per lane and step; the next step's chunk (its packed entries,
+    // order keys, and either its rows (spill area) or its region's commit-index boundaries)
+    // is loaded while this step's two LDS phases run (r05: every step waited for its own
+    // loads behind two barriers, 3.2 ms for 12 GB).
+    constexpr uint32_t KHM = 4;  // boundaries carried in registers (more: read per chunk)
+    struct Chunk {
+        uint32_t rem, w, q0;
+        bool spill;
+        uint4 p0, p1, r0, r1;
+        ulonglong2 k[4];
+        uint32_t kb[KHM];
+    };
+    auto load = [&](uint32_t c, Chunk &x) __attribute__((always_inline)) {
+        x.rem = 0;
+        x.spill = false;
+        x.p0 = x.p1 = x.r0 = x.r1 = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int h = 0; h < 4; h++) x.k[h] = ulonglong2{0, 0};
+#pragma unroll
+        for (uint32_t h = 0; h < KHM; h++) x.kb[h] = ~0u;
+        if (c >= C) return;
+        while (s_pre[kk + 1] <= c) kk++;
+        const uint32_t q = (c - s_pre[kk]) * 8;
+        const uint64_t e = kk < nwr ? (uint64_t)(u.w0 + kk) * fp.xstride + toff_t + q : eB + q;
+        x.rem = min(8u, s_fill[kk] - q);
+        x.spill = kk >= nwr;
+        x.w = u.w0 + kk;
+        x.q0 = q;
+        x.p0 = *reinterpret_cast<const uint4 *>(fp.epack + e);
+        x.p1 = *reinterpret_cast<const uint4 *>(fp.epack + e + 4);
+#pragma unroll
+        for (int h = 0; h < 4; h++) x.k[h] = *reinterpret_cast<const ulonglong2 *>(fp.eokey + e + 2 * h);
+        if (x.spill) {
+            x.r0 = *reinterpret_cast<const uint4 *>(fp.erow + e);
+            x.r1 = *reinterpret_cast<const uint4 *>(fp.erow + e + 4);
+        } else {
+            const uint32_t *kb = fp.kbound + ((uint64_t)x.w * fp.T + t) * fp.kh;
+#pragma unroll
+            for (uint32_t h = 0; h < KHM; h++)
+                if (h < fp.kh) x.kb[h] = kb[h];
+        }
+    };
+    Chunk cur, nxt;
+    load(threadIdx.x, nxt);
     __syncthreads();
     for (uint32_t c0 = 0; c0 < C; c0 += TFB_THREADS) {  // uniform trip count: barriers inside
-        const uint32_t c = c0 + threadIdx.x;
-        uint32_t rem = 0;
-        uint64_t e = 0;
-        if (c < C) {
-            while (s_pre[kk + 1] <= c) kk++;
-            const uint32_t q = (c - s_pre[kk]) * 8;
-            e = kk < nwr ? (uint64_t)(u.w0 + kk) * fp.xstride + toff_t + q : eB + q;
-            rem = min(8u, s_fill[kk] - q);
-        }
-        uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, r0 = p0, r1 = p0;
-        ulonglong2 k[4] = {};
-        const bool spill = kk >= nwr;
-        if (rem) {
-            p0 = *reinterpret_cast<const uint4 *>(fp.epack + e);
-            p1 = *reinterpret_cast<const uint4 *>(fp.epack + e + 4);
-#pragma unroll
-            for (int h = 0; h < 4; h++) k[h] = *reinterpret_cast<const ulonglong2 *>(fp.eokey + e + 2 * h);
-            if (spill) {
-                r0 = *reinterpret_cast<const uint4 *>(fp.erow + e);
-                r1 = *reinterpret_cast<const uint4 *>(fp.erow + e + 4);
-            }
-        }
-        const uint32_t pk[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-        uint32_t rows[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-        if (rem && !spill) {
+        cur = nxt;
+        load(c0 + TFB_THREADS + threadIdx.x, nxt);
+        const uint32_t rem = cur.rem;
+        const uint32_t pk[8] = {cur.p0.x, cur.p0.y, cur.p0.z, cur.p0.w, cur.p1.x, cur.p1.y, cur.p1.z, cur.p1.w};
+        uint32_t rows[8] = {cur.r0.x, cur.r0.y, cur.r0.z, cur.r0.w, cur.r1.x, cur.r1.y, cur.r1.z, cur.r1.w};
+        if (rem && !cur.spill) {
             // region entries: row = (k W + w) TF_BATCH + offset, k's high bits from the region
-            // positions where the commit index crossed multiples of 256
-            const uint32_t w = u.w0 + kk, q0 = (c - s_pre[kk]) * 8;
+            // positions where the commit index crossed multiples of 256: boundaries at or below
+            // the chunk's first position, and the first one above it (a boundary inside the
+            // chunk -- a region with fewer than 8 entries in 256 commits -- takes the per-entry
+            // count; more than KHM boundaries: read from memory)
+            const uint32_t q0 = cur.q0, w = cur.w;
             const uint32_t *kb = fp.kbound + ((uint64_t)w * fp.T + t) * fp.kh;
-            // boundaries at or below the chunk's first position, and the first one above it
-            // (one pass of independent loads; a boundary inside the chunk -- a region with
-            // fewer than 8 entries in 256 commits -- takes the per-entry count)
             uint32_t hi0 = 0, nb = ~0u;
-#pragma unroll 4
-            for (uint32_t h = 0; h < fp.kh; h++) {
+#pragma unroll
+            for (uint32_t h = 0; h < KHM; h++) {
+                const uint32_t b = cur.kb[h];
+                hi0 += q0 >= b;
+                nb = b > q0 && b < nb ? b : nb;
+            }
+            for (uint32_t h = KHM; h < fp.kh; h++) {
                 const uint32_t b = kb[h];
                 hi0 += q0 >= b;
                 nb = b > q0 && b < nb ? b : nb;
@@ -412,21 +446,22 @@ __global__ __launch_bounds__(TFB_THREADS) void k_first_reduce(FirstParams fp, co
         for (int j = 0; j < 8; j++) {
             if ((uint32_t)j >= rem) continue;
             const uint32_t cl = pk[j] & 0xfffu;
-            const unsigned long long kj = (j & 1) ? k[j >> 1].y : k[j >> 1].x;
+            const unsigned long long kj = (j & 1) ? cur.k[j >> 1].y : cur.k[j >> 1].x;
             const unsigned long long old = atomicMin(&lkey[cl], kj);
             if (kj < old) lrow[cl] = ~0u;
         }
-        __syncthreads();
+        tf_lds_barrier();
         // phase 2: the lowest row among the entries holding the cell's key
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             if ((uint32_t)j >= rem) continue;
             const uint32_t cl = pk[j] & 0xfffu;
-            const unsigned long long kj = (j & 1) ? k[j >> 1].y : k[j >> 1].x;
+            const unsigned long long kj = (j & 1) ? cur.k[j >> 1].y : cur.k[j >> 1].x;
             if (kj == lkey[cl]) atomicMin(&lrow[cl], rows[j]);
         }
-        __syncthreads();
+        tf_lds_barrier();
     }
+    __syncthreads();
     // merge: global minimum key per cell, and the candidates for its row into the list (one
     // list reservation per workgroup)
     const uint64_t cbase = (uint64_t)t << fp.s_log2;

@@ -486,7 +486,7 @@ __global__ __launch_bounds__(TA_THREADS) void k_tile_sample(BinPlan p, uint64_t 
 // the count-only f64 pass A (NV = 0): VH_TA_WPE0 waves per SIMD at least (4 caps it at 128
 // VGPRs: two 512-thread workgroups per CU instead of one at 129)
 #ifndef VH_TA_WPE0
-#define VH_TA_WPE0 0
+#define VH_TA_WPE0 4  // same-process A/B (C2 count-only, 1e9 rows): 3.77 -> 3.45 ms (profiles/r06_ab1.txt)
 #endif
 #if VH_TA_WAVES > 0
 #define TA_ATTR_F64(NV) TA_ATTR
@@ -2405,7 +2405,11 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     const uint64_t ncw = (kbat + sb_k - 1) / sb_k;  // commits per workgroup (at most)
     // stream layout (TileParams::stream): one exactly sized stream per workgroup, no sampled
     // capacities, spill areas or overflow rows; VH_TILE_STREAM=0 keeps the per-tile regions
-    const bool stream_layout = wide && !getenv_flag_off("VH_TILE_STREAM") &&
+    // count-only plans keep the per-tile regions: their 2-byte entries make a stream segment's
+    // partial lines a large share of pass B's reads (C2 count-only, same-process A/B: pass A
+    // unchanged, pass B 0.8 -> 1.2 ms), while value-carrying plans gain in pass A (C2 count+sum
+    // 7.56 -> 6.93 ms, C3 4.68 -> 4.14 ms; scripts/exp_stream.py, profiles/r06_stream.txt)
+    const bool stream_layout = wide && nv > 0 && !getenv_flag_off("VH_TILE_STREAM") &&
                                (uint64_t)W * (T + 1) * ncw < (1ull << 31);
     // stream layout: a pass-B unit walks (workgroup, commit) segments in rounds of
     // TB_THREADS; at most TB_ROUNDS rounds per unit (a cold tile's single unit would walk all
