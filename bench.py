@@ -851,6 +851,11 @@ def bench_h2o(n, reps=3):
     on the host), best of `reps` after a warm-up (q10: one timed run); algorithmic bytes per
     row = the distinct columns a query reads."""
     from vaex_amd import _lib
+    # the leg starts from empty block caches, as a fresh process would: the earlier legs'
+    # cached page-locked blocks (C4's bounce buffers, grids) would otherwise hold the cache's
+    # cap and q10's multi-GB result columns would be hipHostMalloc'd for every query
+    _lib.synchronize()
+    _lib.trim_caches()
     df = h2o_frame(n)
     sums = {"v1": int(df.sum("i1_10"))}
     out = {"rows": n, "data": "fixtures.py schema generated in HBM (int8 / int32 / float32)"}

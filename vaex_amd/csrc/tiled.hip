@@ -1585,9 +1585,16 @@ template <int NV, bool NARROW = false, bool MM = false, bool PK = false, bool MG
 __global__ __launch_bounds__(TBT) void k_tile_reduce(FusedAggs fa, TileParams tp, const WorkUnit *units) {
     static_assert(!PK || (NV == 2 && NARROW), "packed pairs of narrow slots");
     extern __shared__ __align__(16) unsigned char lds_raw[];
-    __shared__ uint32_t s_fill[1024 + 1];
-    __shared__ uint32_t s_pre[1024 + 2];
-    __shared__ uint64_t s_base[1024 + 1];  // first entry of each region / segment of the round
+    // per region (one round) / stream segment (rounds of SEGS): entries, chunk prefix, and the
+    // first entry -- regions: absolute (u64 s_rbase); segments: the offset in their pass-A
+    // workgroup's stream (u32 s_a; the workgroup follows from the segment index)
+    constexpr uint32_t SEGS = 2 * TBT;
+    __shared__ uint32_t s_fill[SEGS + 1];
+    __shared__ uint32_t s_pre[SEGS + 2];
+    __shared__ uint64_t s_b64[1024 + 1];  // s_rbase and s_a share it (one mode per launch)
+    uint64_t *s_rbase = s_b64;
+    uint32_t *s_a = reinterpret_cast<uint32_t *>(s_b64);
+    static_assert(2 * (1024 + 1) >= SEGS + 1, "s_a fits s_b64");
     const WorkUnit u = units[blockIdx.x];
     const uint32_t t = u.tile;
     const uint32_t cap = tp.cap[t];
@@ -1603,37 +1610,41 @@ __global__ __launch_bounds__(TBT) void k_tile_reduce(FusedAggs fa, TileParams tp
     // c < ncw, taken in rounds of SEGS; segment g of the unit is w = w_begin + g / ncw,
     // c = g % ncw, its run [tab[row], tab[row + ncw]) with row = (w (T + 1) + t) ncw + c
     // (consecutive lanes read consecutive commits).  Regions: one round of nw regions.
-    // one segment per thread and round; the next round's table entries are fetched into
-    // registers while this round's chunks are processed
-    constexpr uint32_t SEGS = TBT;
+    // two consecutive segments per thread and round; the next round's table entries are
+    // fetched into registers while this round's chunks are processed
     static_assert(TBT <= 1024, "segments per round");
     const bool stream = tp.stream != 0;
     const uint32_t T = tp.ntiles, ncw = tp.ncw;
     const uint32_t nseg = stream ? nwr * ncw : nw;
     const uint32_t rounds = stream ? (nseg + SEGS - 1) / SEGS : 1u;
-    uint32_t pf_f = 0;
-    uint64_t pf_b = 0;
+    uint32_t pf_f[2] = {0, 0}, pf_a[2] = {0, 0};
     auto fetch = [&](uint32_t r) {
-        const uint32_t g = r * SEGS + threadIdx.x;
-        pf_f = 0;
-        if (g < nseg) {
-            const uint32_t w = u.w_begin + g / ncw, c = g % ncw;
-            const uint64_t row = ((uint64_t)w * (T + 1) + t) * ncw + c;
-            const uint32_t a = tp.tab[row], e = tp.tab[row + ncw];
-            pf_f = e - a;
-            pf_b = (uint64_t)w * tp.wg_stride + a;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint32_t g = r * SEGS + 2 * threadIdx.x + h;
+            pf_f[h] = 0;
+            if (g < nseg) {
+                const uint32_t w = u.w_begin + g / ncw, c = g % ncw;
+                const uint64_t row = ((uint64_t)w * (T + 1) + t) * ncw + c;
+                const uint32_t a = tp.tab[row], e = tp.tab[row + ncw];
+                pf_f[h] = e - a;
+                pf_a[h] = a;
+            }
         }
     };
     // stream layout: the fetched segments into LDS and the block-wide exclusive scan of their
     // chunk counts (wave shuffles + wave totals; one barrier inside); returns whether this
-    // thread's segment holds entries.  Threads past the unit's segments count 0 chunks, so
-    // s_pre[cnt] is the round's total for any cnt <= SEGS.
+    // thread's segments hold entries.  Segments past the unit's count 0 chunks, so s_pre[cnt]
+    // is the round's total for any cnt <= SEGS.
     __shared__ uint32_t s_wsum[TBT / 64];
     auto stream_round = [&](uint32_t r) -> bool {
-        const uint32_t k = threadIdx.x, lane = k & 63, wave = k >> 6;
-        const uint32_t f = r * SEGS + k < nseg ? pf_f : 0u, ch = (f + 7) >> 3;
-        s_fill[k] = f;
-        s_base[k] = pf_b;
+        const uint32_t k = 2 * threadIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        const uint32_t f0 = r * SEGS + k < nseg ? pf_f[0] : 0u, f1 = r * SEGS + k + 1 < nseg ? pf_f[1] : 0u;
+        const uint32_t ch0 = (f0 + 7) >> 3, ch = ch0 + ((f1 + 7) >> 3);
+        s_fill[k] = f0;
+        s_fill[k + 1] = f1;
+        s_a[k] = pf_a[0];
+        s_a[k + 1] = pf_a[1];
         uint32_t inc = ch;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
@@ -1650,15 +1661,16 @@ __global__ __launch_bounds__(TBT) void k_tile_reduce(FusedAggs fa, TileParams tp
             tot += x;
         }
         s_pre[k] = before + inc - ch;
-        if (k == 0) s_pre[SEGS] = tot;
-        return f != 0;
+        s_pre[k + 1] = before + inc - ch + ch0;
+        if (threadIdx.x == 0) s_pre[SEGS] = tot;
+        return (f0 | f1) != 0;
     };
     auto load_round = [&]() -> bool {  // regions
         bool any = false;
         for (uint32_t k = threadIdx.x; k < nw; k += TBT) {
             const uint32_t f = k < nwr ? min(tp.fills[(uint64_t)t * tp.W + u.w_begin + k], cap) : (s1 > s0 ? s1 - s0 : 0u);
             s_fill[k] = f;
-            s_base[k] = k < nwr ? (uint64_t)(u.w_begin + k) * tp.wg_stride + tp.toff[t] : spill0;
+            s_rbase[k] = k < nwr ? (uint64_t)(u.w_begin + k) * tp.wg_stride + tp.toff[t] : spill0;
             any |= f != 0;
         }
         return any;
@@ -1766,7 +1778,7 @@ __global__ __launch_bounds__(TBT) void k_tile_reduce(FusedAggs fa, TileParams tp
                 const uint32_t q = (cc - s_pre[kk]) * 8;
                 // regions / segments start at multiples of 8 entries and hold a multiple of 8,
                 // so the chunk never leaves its segment (entries past the fill are ignored)
-                const uint64_t e = s_base[kk] + q;
+                const uint64_t e = (stream ? (uint64_t)(u.w_begin + (r * SEGS + kk) / ncw) * tp.wg_stride + s_a[kk] : s_rbase[kk]) + q;
                 rem[j] = c < ce ? min(8u, s_fill[kk] - q) : 0u;
                 ev[j] = *reinterpret_cast<const uint4 *>(ent16 + e);
 #pragma unroll
