@@ -2463,15 +2463,82 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         }
         VH_HIP(hipGetLastError());
     }
+    // scratch and parameters of the partition exchange (regions: after the sample sized them)
+    auto setup = [&](uint64_t stride, uint64_t stotal) {
+        const uint64_t total = stride * W + stotal + 16;  // regions | spill areas | padding
+        const int ebytes = flags_mode ? 4 : 2;
+        ws.entries.ensure(total * ebytes);
+        if (nv) ws.values.ensure(total * (vnarrow ? 4 : 8) * nv + 64);
+        tp.vnarrow = vnarrow ? 1u : 0u;
+        // the narrow ordinal pass A with two carried columns stores both in values[0], blocked
+        // by 8 entries (values[0] spans both slot arrays; values[1] is unused)
+        tp.vpacked = (fast_mode == 3 && nv == 2 && !flags_mode && !getenv_flag_off("VH_TILE_PACK")) ? 1u : 0u;
+        tp.vfloat = vfloat;
+        tp.vsigned = vsigned;
+        tp.s_log2 = s_log2;
+        tp.ntiles = T;
+        tp.flags_mode = flags_mode ? 1 : 0;
+        tp.nvals = nv;
+        tp.cells = cells;
+        tp.W = W;
+        tp.rows_per_wg = rows_per_wg;
+        tp.wg_stride = stride;
+        tp.cap = d_cap;
+        tp.toff = d_toff;
+        tp.fills = d_fills;
+        tp.spill_fill = d_sfill;
+        tp.spill_cap = d_scap;
+        tp.spill_start = d_sstart;
+        tp.spill_base = stride * W;
+        tp.entries = ws.entries.ptr;
+        if (stream_layout) {
+            tp.stream = 1;
+            tp.ncw = (uint32_t)ncw;
+            ws.tab.ensure((uint64_t)W * (T + 1) * ncw * 4 + 256);
+            tp.tab = ws.tab.as<uint32_t>();
+        }
+        for (int s = 0; s < nv; s++)
+            tp.values[s] = vnarrow ? reinterpret_cast<double *>(ws.values.as<uint32_t>() + (uint64_t)s * total)
+                                   : ws.values.as<double>() + (uint64_t)s * total;
+        VH_HIP(hipMemsetAsync(d_sfill, 0, 4 * (uint64_t)T, st));
+    };
+    bool a_launched = false;
+    auto launch_pass_a = [&]() {
+        TimedScope ts(fast ? "tile_scatter_f64" : ord ? (has_set ? "tile_scatter_set" : "tile_scatter_ord") : "tile_scatter");
+        const size_t lds = lds_a;
+        if (ord) {
+            const void *kf = ord_kernel(nv, fast_mode, has_set, tp.vdt[0], tp.vdt[1]);
+            void *args[] = {(void *)&plan, (void *)&fa, (void *)&tp, (void *)&n};
+            VH_HIP(hipLaunchKernel(kf, dim3(W), dim3(TA_THREADS), args, lds, st));
+        } else {
+            switch (nv) {
+            case 0: launch_scatter_nd<0>(nd_k, fast_mode, W, lds, plan, fa, tp, n); break;
+            case 1: launch_scatter_nd<1>(nd_k, fast_mode, W, lds, plan, fa, tp, n); break;
+            default: launch_scatter_nd<2>(nd_k, fast_mode, W, lds, plan, fa, tp, n);
+            }
+        }
+        VH_HIP(hipGetLastError());
+        a_launched = true;
+    };
     // the sample comes back and the plan goes out through a page-locked block (pageable
     // copies are staged by the runtime, each one a host wait): [download | upload]; reuse is
     // safe because every call waits on the stream for its download before writing the block
     thread_local PinnedBuf tstage;
+    thread_local hipEvent_t sample_ev = nullptr;
+    if (!sample_ev) VH_HIP(hipEventCreateWithFlags(&sample_ev, hipEventDisableTiming));
     const uint64_t dl_bytes = (16 * (uint64_t)T + 8 * sblocks + 255) & ~uint64_t(255);
     tstage.ensure(dl_bytes + 24 * (uint64_t)T + sizeof(WorkUnit) * max_units + 1024);
     VH_HIP(hipMemcpyAsync(tstage.ptr, d_hist, 16 * (uint64_t)T, hipMemcpyDeviceToHost, st));
     VH_HIP(hipMemcpyAsync(tstage.as<char>() + 16 * (uint64_t)T, d_brange, 8 * sblocks, hipMemcpyDeviceToHost, st));
-    VH_HIP(hipStreamSynchronize(st));
+    VH_HIP(hipEventRecord(sample_ev, st));
+    // stream layout: the streams are sized exactly without the sample (it only plans pass B),
+    // so pass A is queued right behind the sample's read-back and the host plans pass B while
+    // pass A runs (no host round trip between the two kernels)
+    if (stream_layout) {
+        setup((rows_per_wg + 7 * ncw * T + 8 + 7) & ~uint64_t(7), 0);
+        launch_pass_a();
+    }
+    VH_HIP(hipEventSynchronize(sample_ev));
     const uint64_t *hist = tstage.as<uint64_t>();
     const uint32_t *brange = reinterpret_cast<const uint32_t *>(tstage.as<char>() + 16 * (uint64_t)T);
     // sample blocks whose tile ranges follow each other (a column sorted, up or down, along
@@ -2500,7 +2567,6 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     std::vector<uint32_t> cap(T), scap(T);
     std::vector<uint64_t> toff(T), sstart(T);
     uint64_t stride = 0, stotal = 0;
-    if (stream_layout) stride = (rows_per_wg + pad_wg * T + 8 + 7) & ~uint64_t(7);
     for (uint32_t t = 0; t < T && stream_layout; t++) cap[t] = scap[t] = 0, toff[t] = sstart[t] = 0;
     const double blocks = (double)sblocks;  // every sample block is TA_BATCH rows, like a batch
     // clustered rows (block variance well above the Poisson value: each sample block all in
@@ -2555,41 +2621,7 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
             stotal += scap[t];
         }
     }
-    const uint64_t total = stride * W + stotal + 16;  // regions | spill areas | padding
-    const int ebytes = flags_mode ? 4 : 2;
-    ws.entries.ensure(total * ebytes);
-    if (nv) ws.values.ensure(total * (vnarrow ? 4 : 8) * nv + 64);
-    tp.vnarrow = vnarrow ? 1u : 0u;
-    // the narrow ordinal pass A with two carried columns stores both in values[0], blocked by 8
-    // entries (values[0] spans both slot arrays; values[1] is unused)
-    tp.vpacked = (fast_mode == 3 && nv == 2 && !flags_mode && !getenv_flag_off("VH_TILE_PACK")) ? 1u : 0u;
-    tp.vfloat = vfloat;
-    tp.vsigned = vsigned;
-    tp.s_log2 = s_log2;
-    tp.ntiles = T;
-    tp.flags_mode = flags_mode ? 1 : 0;
-    tp.nvals = nv;
-    tp.cells = cells;
-    tp.W = W;
-    tp.rows_per_wg = rows_per_wg;
-    tp.wg_stride = stride;
-    tp.cap = d_cap;
-    tp.toff = d_toff;
-    tp.fills = d_fills;
-    tp.spill_fill = d_sfill;
-    tp.spill_cap = d_scap;
-    tp.spill_start = d_sstart;
-    tp.spill_base = stride * W;
-    tp.entries = ws.entries.ptr;
-    if (stream_layout) {
-        tp.stream = 1;
-        tp.ncw = (uint32_t)ncw;
-        ws.tab.ensure((uint64_t)W * (T + 1) * ncw * 4 + 256);
-        tp.tab = ws.tab.as<uint32_t>();
-    }
-    for (int s = 0; s < nv; s++)
-        tp.values[s] = vnarrow ? reinterpret_cast<double *>(ws.values.as<uint32_t>() + (uint64_t)s * total)
-                               : ws.values.as<double>() + (uint64_t)s * total;
+    if (!stream_layout) setup(stride, stotal);
     char *upl = tstage.as<char>() + dl_bytes;  // upload region: cap | toff | sstart | scap | units
     auto upload = [&](void *dst, const void *src, uint64_t bytes) {
         memcpy(upl, src, bytes);
@@ -2600,7 +2632,6 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     upload(d_toff, toff.data(), 8 * (uint64_t)T);
     upload(d_sstart, sstart.data(), 8 * (uint64_t)T);
     upload(d_scap, scap.data(), 4 * (uint64_t)T);
-    VH_HIP(hipMemsetAsync(d_sfill, 0, 4 * (uint64_t)T, st));
 
     // ---- pass B work units: tiles split over ranges of pass-A workgroups by expected size;
     // unit k of g of a tile also reads slice k of g of the tile's spill area
@@ -2627,23 +2658,8 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     if (units.size() > max_units) fail(VH_ERR_RUNTIME, "tiled binning: work-unit table overflow");
     if (!units.empty()) upload(d_units, units.data(), sizeof(WorkUnit) * units.size());
 
-    // ---- pass A
-    {
-        TimedScope ts(fast ? "tile_scatter_f64" : ord ? (has_set ? "tile_scatter_set" : "tile_scatter_ord") : "tile_scatter");
-        const size_t lds = lds_a;
-        if (ord) {
-            const void *kf = ord_kernel(nv, fast_mode, has_set, tp.vdt[0], tp.vdt[1]);
-            void *args[] = {(void *)&plan, (void *)&fa, (void *)&tp, (void *)&n};
-            VH_HIP(hipLaunchKernel(kf, dim3(W), dim3(TA_THREADS), args, lds, st));
-        } else {
-            switch (nv) {
-            case 0: launch_scatter_nd<0>(nd_k, fast_mode, W, lds, plan, fa, tp, n); break;
-            case 1: launch_scatter_nd<1>(nd_k, fast_mode, W, lds, plan, fa, tp, n); break;
-            default: launch_scatter_nd<2>(nd_k, fast_mode, W, lds, plan, fa, tp, n);
-            }
-        }
-        VH_HIP(hipGetLastError());
-    }
+    // ---- pass A (launched before the sample comes back in the stream layout)
+    if (!a_launched) launch_pass_a();
     // ---- pass B
     {
         TimedScope ts("tile_reduce");
