@@ -53,7 +53,11 @@ constexpr int TA_THREADS = VH_TA_THREADS;
 #define VH_TA_NT 0
 #endif
 #ifndef VH_TA_DRAIN
-#define VH_TA_DRAIN 1  // fast pass A: the prefetched batch lands before the commit's stores
+// 1: the prefetched batch lands before the commit's stores; 0: it stays in flight across the
+// commit.  Round 6 found no difference outside the placement noise for the stream layout
+// (process A/B, profiles/r06_abp1.txt); a run-time choice cost the count-only kernel 48
+// spilled VGPRs
+#define VH_TA_DRAIN 1
 #endif
 #ifndef VH_TB_THREADS
 #define VH_TB_THREADS 1024
@@ -483,15 +487,15 @@ __global__ __launch_bounds__(TA_THREADS) void k_tile_sample(BinPlan p, uint64_t 
 #else
 #define TA_ATTR
 #endif
-// the count-only f64 pass A (NV = 0): VH_TA_WPE0 waves per SIMD at least (4 caps it at 128
-// VGPRs: two 512-thread workgroups per CU instead of one at 129)
+// the count-only f64 pass A (NV = 0, ND <= 2): VH_TA_WPE0 waves per SIMD at least (4 caps it at
+// 128 VGPRs: two 512-thread workgroups per CU instead of one at 129; the 3-d kernel would spill)
 #ifndef VH_TA_WPE0
 #define VH_TA_WPE0 4  // same-process A/B (C2 count-only, 1e9 rows): 3.77 -> 3.45 ms (profiles/r06_ab1.txt)
 #endif
 #if VH_TA_WAVES > 0
 #define TA_ATTR_F64(NV) TA_ATTR
 #else
-#define TA_ATTR_F64(NV) __attribute__((amdgpu_waves_per_eu(((NV) == 0 && VH_TA_WPE0 > 0) ? VH_TA_WPE0 : 1)))
+#define TA_ATTR_F64(NV) __attribute__((amdgpu_waves_per_eu(((NV) == 0 && ND <= 2 && VH_TA_WPE0 > 0) ? VH_TA_WPE0 : 1)))
 #endif
 
 __device__ inline void lds_barrier() {
@@ -1230,6 +1234,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
             }
         }
     };
+    constexpr bool drain = VH_TA_DRAIN != 0;
     double2 cur[PAIRS][NC], nxt[PAIRS][NC];
     load((uint64_t)w * TA_BATCH, cur);
     for (uint64_t b0 = (uint64_t)w * TA_BATCH; b0 < n; b0 += SB * bstep) {
@@ -1242,7 +1247,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
         for (int sb = 0; sb < SB; sb++) {
             load(b0 + (sb + 1) * bstep, nxt);
             rows(b0 + sb * bstep, cur, key + sb * TA_RPT, rank + sb * TA_RPT, vals + sb * TA_RPT);
-            if (sb + 1 < SB || VH_TA_DRAIN)
+            if (sb + 1 < SB || drain)
 #pragma unroll
                 for (int q = 0; q < PAIRS; q++)
 #pragma unroll
@@ -1254,7 +1259,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
         } else {
             batch_commit_fast<NV, SB * TA_RPT>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
         }
-        if (!VH_TA_DRAIN)
+        if (!drain)
 #pragma unroll
             for (int q = 0; q < PAIRS; q++)
 #pragma unroll
@@ -1425,6 +1430,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
             }
         }
     };
+    constexpr bool drain = VH_TA_DRAIN != 0;
     Regs cur, nxt;
     load((uint64_t)w * TA_BATCH, cur);
     for (uint64_t b0 = (uint64_t)w * TA_BATCH; b0 < n; b0 += SB * bstep) {
@@ -1435,7 +1441,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
         for (int sb = 0; sb < SB; sb++) {
             load(b0 + (sb + 1) * bstep, nxt);
             rows(b0 + sb * bstep, cur, key + sb * TA_RPT, rank + sb * TA_RPT, vals + sb * TA_RPT);
-            if (sb + 1 < SB || VH_TA_DRAIN) cur = nxt;
+            if (sb + 1 < SB || drain) cur = nxt;
         }
         if (DBG(tp.debug) & 32) {  // experiment: no commit (loads, cell math, ranking only)
 #pragma unroll
@@ -1443,7 +1449,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
         } else {
             batch_commit_fast<NV, SB * TA_RPT, VT>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
         }
-        if (!VH_TA_DRAIN) cur = nxt;
+        if (!drain) cur = nxt;
     }
     lds_barrier();
     for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.base[t] - (uint32_t)tp.toff[t];
@@ -2426,7 +2432,10 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     // stream layout: a pass-B unit walks (workgroup, commit) segments in rounds of
     // TB_THREADS; at most TB_ROUNDS rounds per unit (a cold tile's single unit would walk all
     // W x ncw segments in one workgroup while the rest of the chip idles)
-    constexpr uint64_t TB_ROUNDS = 6;
+#ifndef VH_TB_ROUNDS
+#define VH_TB_ROUNDS 6
+#endif
+    constexpr uint64_t TB_ROUNDS = VH_TB_ROUNDS;
     const uint64_t wpu = std::max<uint64_t>(1, (uint64_t)TB_THREADS * TB_ROUNDS / std::max<uint64_t>(ncw, 1));
     const uint64_t g_min = stream_layout ? (W + wpu - 1) / wpu : 1;
     // pass-B work units: sum over tiles of max(g_min, ceil(e_t / target)) <= T g_min + 4 cu
