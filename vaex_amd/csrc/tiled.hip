@@ -54,9 +54,8 @@ constexpr int TA_THREADS = VH_TA_THREADS;
 #endif
 #ifndef VH_TA_DRAIN
 // 1: the prefetched batch lands before the commit's stores; 0: it stays in flight across the
-// commit.  Round 6 found no difference outside the placement noise for the stream layout
-// (process A/B, profiles/r06_abp1.txt); a run-time choice cost the count-only kernel 48
-// spilled VGPRs
+// commit.  Round 6, both instantiations on one scratch: C2 count+sum pass A 6.126 vs 6.147 ms
+// (profiles/r06_drain_inproc.txt); a run-time choice cost the count-only kernel 48 spilled VGPRs
 #define VH_TA_DRAIN 1
 #endif
 #ifndef VH_TB_THREADS
@@ -2544,7 +2543,9 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     // so pass A is queued right behind the sample's read-back and the host plans pass B while
     // pass A runs (no host round trip between the two kernels)
     if (stream_layout) {
-        setup((rows_per_wg + 7 * ncw * T + 8 + 7) & ~uint64_t(7), 0);
+        uint64_t sstride = (rows_per_wg + 7 * ncw * T + 8 + 7) & ~uint64_t(7);
+        if (const char *e = getenv("VH_TILE_WGPAD")) sstride += ((uint64_t)strtoull(e, nullptr, 10) + 7) & ~uint64_t(7);
+        setup(sstride, 0);
         launch_pass_a();
     }
     VH_HIP(hipEventSynchronize(sample_ev));
