@@ -1,5 +1,5 @@
-"""Median HIP-event kernel times of the C2 (count+sum, count-only) and C3 (`auto`) tile-path
-passes in this process, as one JSON line -- for A/Bs run as separate processes, so every
+"""Median HIP-event kernel times of the C2 (count+sum, count-only), C3 (`auto`) and h2o q3
+tile-path passes in this process, as one JSON line -- for A/Bs run as separate processes, so every
 variant gets the same allocation sequence and hence the same scratch placement (two
 libraries in one process own scratch at different places: a +-7 % effect on pass A,
 DESIGN §5.10).  usage: [VAEX_AMD_LIB=...] [VH_...=...] python scripts/exp_kernels.py TAG [rows] [reps]"""
@@ -23,6 +23,10 @@ y = DeviceArray.random(n, "normal", seed=3)
 w = DeviceArray.random(n, "uniform", seed=4)
 keys = DeviceArray.random(n, "randint", seed=5, a=5, b=5 + 1_000_000, dtype="int32")
 df3 = vaex_amd.from_arrays(key=keys, v=x)
+# h2o q3's shape: int32 key, int8 sum + float32 mean (two narrow slots packed in one stream)
+v1 = DeviceArray.random(n, "randint", seed=6, a=5, b=15, dtype="int8")
+v3 = DeviceArray.random(n, "normal", seed=7, dtype="float32")
+dfq3 = vaex_amd.from_arrays(key=keys, v1=v1, v3=v3)
 
 
 def c2(with_sum):
@@ -42,7 +46,8 @@ def c2(with_sum):
 
 out = {"tag": tag}
 for name, f, ka in (("c2sum", lambda: c2(True), "tile_scatter_f64"), ("c2count", lambda: c2(False), "tile_scatter_f64"),
-                    ("c3", lambda: df3.groupby("key", agg={"v": ["sum", "count"]}), "tile_scatter_ord")):
+                    ("c3", lambda: df3.groupby("key", agg={"v": ["sum", "count"]}), "tile_scatter_ord"),
+                    ("q3", lambda: dfq3.groupby("key").agg({"v1": "sum", "v3": "mean"}), "tile_scatter_ord")):
     f()
     a, b = [], []
     for _ in range(reps):

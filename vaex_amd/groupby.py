@@ -631,7 +631,10 @@ class GroupBy(GroupByBase):
             desc = vagg.count(edges=True)
             if len(self.by) == 1 and isinstance(self.by[0], GrouperDense):
                 desc.want_occupancy = True
-                desc.keep_device = self.device_finish
+                # an internal count(*): only its occupancy is needed when every cell of the
+                # occupied range holds a group, so its grid stays in HBM (read back only for
+                # the compaction mask)
+                desc.keep_device = True
                 self.count_desc = desc
             counts = self.df._agg(desc, self.binners, delay=True)
         if len(self.by) == 1 and isinstance(self.by[0], GrouperDense):
@@ -684,15 +687,26 @@ class GroupBy(GroupByBase):
             # a part handed a host result back (keep_device not honoured): key order on the
             # host, and the caller applies the first-appearance order itself
             self.device_finish = False
+        from .taskparts import DeviceResult
         arrays = {k: extract_central_part(np.asarray(v.get())) for k, v in arrays.items()}
-        counts_edges = np.asarray(counts.get())
-        central = extract_central_part(counts_edges)
+        cres = counts.get()
         occ = getattr(self.count_desc, "occupancy", None)
-        nnz, first, last = occ if occ is not None else hostops.occupancy(central)
-        if g.speculative:
-            # keys outside the guessed range sit in the under / overflow cells
-            if counts_edges[1] or counts_edges[-1] or nnz == 0:
+        if isinstance(cres, DeviceResult) and occ is not None:
+            # the internal count(*) grid is still in HBM: the edge cells and the occupied range
+            # come from the device, the grid itself only when the range has empty cells
+            cagg, central = cres.agg, None
+            L = cagg.grid.length1d
+            nnz, first, last = occ
+            if g.speculative and (cagg.occupancy(1, 2)[0] or cagg.occupancy(L - 1, L)[0] or nnz == 0):
                 raise DenseRangeMiss(g.expression)
+        else:
+            counts_edges = np.asarray(cres)
+            central = extract_central_part(counts_edges)
+            nnz, first, last = occ if occ is not None else hostops.occupancy(central)
+            # keys outside the guessed range sit in the under / overflow cells
+            if g.speculative and (counts_edges[1] or counts_edges[-1] or nnz == 0):
+                raise DenseRangeMiss(g.expression)
+        if g.speculative:
             g.value_dtype = label_dtype(g.key_dtype, g.min_value + first, g.min_value + last)
         if self.row_limit is not None and nnz > self.row_limit:  # what Grouper's set build raises (groupby.py:125)
             raise RowLimitException(f"Resulting grouper has {nnz:,} unique combinations, which is "
@@ -708,6 +722,8 @@ class GroupBy(GroupByBase):
             for k, v in arrays.items():
                 columns[k] = v[sl]
             return DataFrame(columns)
+        if central is None:
+            central = extract_central_part(np.asarray(cres))
         mask = central[sl] > 0
         columns = {g.label: (np.flatnonzero(mask) + (g.min_value + first)).astype(g.value_dtype)}
         for k, v in arrays.items():
