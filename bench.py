@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
     p.add_argument("--no-groupby", action="store_true")
     p.add_argument("--no-count-only", action="store_true")
+    p.add_argument("--no-f32", action="store_true", help="skip the C2 leg on float32 copies of x, y, w")
     p.add_argument("--no-layouts", action="store_true", help="skip the sorted-layout legs")
     p.add_argument("--host-rows", type=float, default=2e8,
                    help="rows of the PCIe-inclusive measurement (host numpy columns); 0 = skip")
@@ -260,6 +261,8 @@ def main():
             extra["groupby_sorted_keys"] = bench_groupby(int(args.groupby_rows), args, layout="sorted")
     if rank == 0 and world == 1 and not args.no_count_only:
         extra["count_only"] = bench_count_only(x, y, n, bins, args)
+    if rank == 0 and world == 1 and not args.no_f32:
+        extra["c2_float32"] = bench_c2_float32(n, bins, args, check["sum_reference"])
     if rank == 0 and world == 1 and not args.no_aggs:
         extra["aggs"] = bench_other_aggs(x, y, w, n, bins, args, ms_per_step)
     if rank == 0 and world == 1 and not args.no_set:
@@ -383,6 +386,58 @@ def bench_count_only(x, y, n, bins, args):
             "kernel_frac": round(16 * n / (per[dom] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if dom else None,
             "pipeline_GBps": round(16 * n / (pipe * 1e-3) / 1e9, 1) if pipe else None,
             "pipeline_frac": round(16 * n / (pipe * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if pipe else None}
+
+
+def bench_c2_float32(n, bins, args, sum_reference):
+    """C2 on float32 copies of the x, y, w draws (vaex files often hold float32): count +
+    sum(w) on the 1027^2 grid through the fast float32 pass A (k_tile_scatter_f64<2, 1, 3,
+    float>), same timing method as the headline line; 12 B/row read.  Checks: every row
+    counted, and the grid's sum within 1e-6 of the float64 column's sum (float32 rounding of
+    U[0, 1) values is ~3e-8 relative)."""
+    from vaex_amd import _lib, superagg
+    from vaex_amd.device import DeviceArray
+    # the same counter-based draws as x, y, w (seeds 2, 3, 4), each rounded to float32
+    x4 = DeviceArray.random(n, "normal", seed=2, dtype="float32")
+    y4 = DeviceArray.random(n, "normal", seed=3, dtype="float32")
+    w4 = DeviceArray.random(n, "uniform", seed=4, dtype="float32")
+
+    def step():
+        bx = superagg.BinnerScalar_float32("x", -4.0, 4.0, bins)
+        by = superagg.BinnerScalar_float32("y", -4.0, 4.0, bins)
+        bx.set_data(x4)
+        by.set_data(y4)
+        grid = superagg.Grid([bx, by])
+        count = superagg.AggCount_int64(grid)
+        s = superagg.AggSum_float32(grid)
+        s.set_data(w4, 0)
+        grid.bin([count, s])
+        return count, s
+
+    for _ in range(max(1, args.warmup)):
+        res = step()
+    _lib.synchronize()
+    _lib.timing_reset()
+    _lib.timing_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    _lib.synchronize()
+    t = time.perf_counter() - t0
+    _lib.timing_enable(False)
+    per = {}
+    for k in TILE_KERNELS + ["tile_scatter_f32", "bin_fused_global", "bin_fused_lds"]:
+        c, ms = _lib.timing_read(k)
+        if c:
+            per[k] = ms / c
+    c_tot = int(np.asarray(res[0]).sum())
+    s_tot = float(np.asarray(res[1]).sum())
+    rel = abs(s_tot - sum_reference) / abs(sum_reference) if sum_reference else None
+    dom = max(per, key=per.get) if per else None
+    return {"rows": n, "ms_per_step": t / args.steps * 1e3, "rows_per_s": n * args.steps / t,
+            "algorithmic_bytes_per_row": 12, "per_kernel_ms": {k: round(v, 4) for k, v in per.items()},
+            "kernel": dom, "kernel_GBps": round(12 * n / (per[dom] * 1e-3) / 1e9, 1) if dom else None,
+            "check": {"count_total": c_tot, "count_equal": c_tot == n, "sum_total": s_tot, "sum_rel_err_vs_f64": rel,
+                      "ok": bool(c_tot == n and rel is not None and rel < 1e-6)}}
 
 
 def bench_other_aggs(x, y, w, n, bins, args, c2_ms):

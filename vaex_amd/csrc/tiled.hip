@@ -1139,21 +1139,28 @@ __device__ inline uint32_t scalar_f64_index32(double v, double vmin, double scal
 // masks, counts unconditional or keyed on a carried value (mean).  Rows are read as
 // 16-byte pairs; the next batch loads into a second register buffer while the current
 // one is ranked, sorted and written.
-template <int ND, int NV, int SB>
+// CT = float: the same over float32 columns (binners and sums): rows read as 8-byte pairs,
+// the binner value widened to double before the index math (BinnerScalar<float>::to_bins,
+// superagg_binners.cpp:14-56, scales the value as double), sums carried, staged and stored
+// as their 4-byte float32 bits (narrow slots, widened exactly in pass B)
+template <int ND, int NV, int SB, typename CT = double>
 __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
+    constexpr bool F32 = std::is_same_v<CT, float>;
+    using P2 = std::conditional_t<F32, float2, double2>;
+    using VS = std::conditional_t<F32, uint32_t, double>;  // carried / staged value slot
     constexpr int NC = ND + NV;
     constexpr int PAIRS = TA_RPT / 2;
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const uint32_t T = tp.ntiles;
-    const ScatterLds l = fast_lds<NV>(lds_raw, T, tp.lds_cap);
+    const ScatterLds l = fast_lds<NV>(lds_raw, T, tp.lds_cap, F32 ? 4 : 8);
     scatter_lds_init(l, tp, T);
     __syncthreads();
-    const double *col[NC];
+    const CT *col[NC];
     double vmin[ND > 0 ? ND : 1], scale[ND > 0 ? ND : 1], bins_d[ND > 0 ? ND : 1];
     uint32_t bins2[ND > 0 ? ND : 1], stride[ND > 0 ? ND : 1];
 #pragma unroll
     for (int d = 0; d < ND; d++) {
-        col[d] = reinterpret_cast<const double *>(p.b[d].data);
+        col[d] = reinterpret_cast<const CT *>(p.b[d].data);
         vmin[d] = p.b[d].vmin;
         scale[d] = p.b[d].scale;
         bins_d[d] = (double)p.b[d].bins;
@@ -1161,7 +1168,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
         stride[d] = (uint32_t)p.b[d].stride;
     }
 #pragma unroll
-    for (int s = 0; s < NV; s++) col[ND + s] = tp.vdata[s];
+    for (int s = 0; s < NV; s++) col[ND + s] = reinterpret_cast<const CT *>(tp.vdata[s]);
     // take flags: count(*) always; a sum, or a count keyed on a summed column, takes the
     // row when that value is not NaN (nan_keyed[s] = the aggregators keyed on slot s)
     uint32_t count_mask = 0, keyed_slot_of[MAX_FUSED_AGGS], nan_keyed[NV > 0 ? NV : 1] = {};
@@ -1186,7 +1193,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
     // inside [0, n) or wholly past it; past-the-end pairs load the clamped last pair and
     // are dropped by the i < n test.  With no load behind an exec branch the compiler
     // counts vmcnt instead of draining to 0, so the prefetched batch stays in flight.
-    auto load = [&](uint64_t b0, double2 (&dst)[PAIRS][NC]) {
+    auto load = [&](uint64_t b0, P2 (&dst)[PAIRS][NC]) {
 #pragma unroll
         for (int q = 0; q < PAIRS; q++) {
             const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + threadIdx.x);
@@ -1194,18 +1201,20 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
 #pragma unroll
             for (int c = 0; c < NC; c++) {
 #if VH_TA_NT  // experiment: non-temporal loads of the once-read columns
-                typedef double v2d __attribute__((ext_vector_type(2)));
-                const v2d t = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(col[c] + is));
-                dst[q][c] = make_double2(t.x, t.y);
-#else
-                dst[q][c] = *reinterpret_cast<const double2 *>(col[c] + is);
+                if constexpr (!F32) {
+                    typedef double v2d __attribute__((ext_vector_type(2)));
+                    const v2d t = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(col[c] + is));
+                    dst[q][c] = make_double2(t.x, t.y);
+                    continue;
+                }
 #endif
+                dst[q][c] = *reinterpret_cast<const P2 *>(col[c] + is);
             }
         }
     };
     // rank the rows of one batch: cell, take flags, (tile << 16 | cell) key, rank in tile
-    auto rows = [&](uint64_t b0, const double2 (&cur)[PAIRS][NC], uint32_t *key, int32_t *rank,
-                    double (*vals)[NV > 0 ? NV : 1]) {
+    auto rows = [&](uint64_t b0, const P2 (&cur)[PAIRS][NC], uint32_t *key, int32_t *rank,
+                    VS (*vals)[NV > 0 ? NV : 1]) {
 #pragma unroll
         for (int r = 0; r < TA_RPT; r++) {
             const int q = r >> 1, h = r & 1;
@@ -1213,14 +1222,16 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
             uint32_t c = 0;
 #pragma unroll
             for (int d = 0; d < ND; d++) {
-                const double v = h ? cur[q][d].y : cur[q][d].x;
+                const double v = (double)(h ? cur[q][d].y : cur[q][d].x);
                 c += scalar_f64_index32(v, vmin[d], scale[d], bins_d[d], bins2[d]) * stride[d];
             }
             uint32_t f = count_mask;
 #pragma unroll
             for (int s = 0; s < NV; s++) {
-                vals[r][s] = h ? cur[q][ND + s].y : cur[q][ND + s].x;
-                f |= vals[r][s] == vals[r][s] ? nan_keyed[s] : 0u;
+                const CT v = h ? cur[q][ND + s].y : cur[q][ND + s].x;
+                if constexpr (F32) vals[r][s] = __builtin_bit_cast(uint32_t, v);
+                else vals[r][s] = v;
+                f |= v == v ? nan_keyed[s] : 0u;
             }
             f = i < row_end ? f : 0u;
             const uint32_t t = c >> s_log2;
@@ -1234,12 +1245,12 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
         }
     };
     constexpr bool drain = VH_TA_DRAIN != 0;
-    double2 cur[PAIRS][NC], nxt[PAIRS][NC];
+    P2 cur[PAIRS][NC], nxt[PAIRS][NC];
     load((uint64_t)w * TA_BATCH, cur);
     for (uint64_t b0 = (uint64_t)w * TA_BATCH; b0 < n; b0 += SB * bstep) {
         uint32_t key[SB * TA_RPT];
         int32_t rank[SB * TA_RPT];
-        double vals[SB * TA_RPT][NV > 0 ? NV : 1];
+        VS vals[SB * TA_RPT][NV > 0 ? NV : 1];
         // the last prefetch stays in flight across the commit: it is moved into cur only
         // after the commit (a copy before it would wait for those loads)
 #pragma unroll
@@ -1256,7 +1267,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
 #pragma unroll
             for (int r = 0; r < SB * TA_RPT; r++) asm volatile("" ::"v"(key[r]), "v"(rank[r]));
         } else {
-            batch_commit_fast<NV, SB * TA_RPT>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
+            batch_commit_fast<NV, SB * TA_RPT, VS>(l, fa, tp, T, region0, key, rank, vals, count_mask, keyed_slot_of);
         }
         if (!drain)
 #pragma unroll
@@ -2102,6 +2113,10 @@ template <int ND, int NV>
 static void launch_scatter(int fast, unsigned grid, size_t lds, const BinPlan &plan, const FusedAggs &fa,
                            const TileParams &tp, uint64_t n) {
     if constexpr (ND > 0) {
+        if (fast == 5) {
+            hipLaunchKernelGGL((k_tile_scatter_f64<ND, NV, fast_sb_narrow(NV), float>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
+            return;
+        }
         if (fast == 2) {
             hipLaunchKernelGGL((k_tile_scatter_f64<ND, NV, fast_sb_nd(NV, ND)>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
             return;
@@ -2127,10 +2142,15 @@ static void launch_scatter_nd(int nd, int fast, unsigned grid, size_t lds, const
 }
 
 static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+static bool aligned8(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
 
 template <int ND, int NV> static int scatter_blocks_per_cu(int fast, size_t lds) {
     int nb = 0;
     if constexpr (ND > 0) {
+        if (fast == 5) {
+            VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter_f64<ND, NV, fast_sb_narrow(NV), float>, TA_THREADS, lds));
+            return nb;
+        }
         if (fast == 2) {
             VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter_f64<ND, NV, fast_sb_nd(NV, ND)>, TA_THREADS, lds));
             return nb;
@@ -2345,7 +2365,6 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     // generic pass A flavour: -1 = a set-ordinal binner (per-row form), 0 = hoisted dispatch
     bool has_set = false;
     for (int d = 0; d < plan.nb; d++) has_set = has_set || plan.b[d].kind == 2;
-    const int nd_k = nd_f64 > 0 ? nd_f64 : (has_set ? -1 : 0);
     for (int d = 0; d < plan.nb && fast; d++) fast = !plan.b[d].mask && aligned16(plan.b[d].data);
     for (int k = 0; k < fa.na; k++) {
         if (fa.a[k].mask) fast = false;
@@ -2355,6 +2374,28 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         }
         if (fa.a[k].kind == VH_AGG_COUNT && fa.a[k].data && fa.a[k].dtype != VH_F64) fast = false;
     }
+    // the fast float32 pass A (k_tile_scatter_f64<ND, NV, SB, float>): native float32 scalar
+    // binners without masks, float32 sums and counts (of every row, or keyed on a summed
+    // column), no aggregator masks, 8-byte aligned columns, n even (row pairs).  It replaces
+    // the generic pass A's per-dimension dtype dispatch, whose loads wait at every switch join
+    // (C2 on float32 columns: 11.3 ms generic pass A, profiles/r06_f32.txt)
+    int nd_f32 = 0;
+    if (!fast && nd_f64 == 0 && !flags_mode && n % 2 == 0 && plan.nb >= 1 && plan.nb <= 3 &&
+        !getenv_flag_off("VH_TILE_F32")) {
+        bool ok = true;
+        for (int d = 0; d < plan.nb; d++) {
+            const BinnerDev &b = plan.b[d];
+            ok = ok && b.kind == 0 && b.dtype == VH_F32 && !b.flip && !b.mask && aligned8(b.data);
+        }
+        for (int k = 0; k < fa.na; k++) {
+            const FusedAgg &a = fa.a[k];
+            ok = ok && !a.mask;
+            if (a.kind == VH_AGG_COUNT) ok = ok && (!a.data || a.dtype == VH_F32);
+            else ok = ok && a.kind == VH_AGG_SUM && a.data && a.dtype == VH_F32 && aligned8(a.data);
+        }
+        if (ok) nd_f32 = plan.nb;
+    }
+    const int nd_k = nd_f64 > 0 ? nd_f64 : nd_f32 > 0 ? nd_f32 : (has_set ? -1 : 0);
     const bool ord = !fast && n % 2 == 0 && ord_fast_ok(plan, fa);
     tp.vdt[0] = tp.vdt[1] = VH_F64;
     if (ord) for (int k = 0; k < fa.na; k++)
@@ -2373,18 +2414,22 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         if (dt == VH_I32 || dt == VH_I16 || dt == VH_I8) vsigned |= 1u << s;
     }
     // fast kernel: several batches per commit when that staging fits the LDS; the ordinal
-    // kernel with narrow slots stages 4-byte values (mode 3)
+    // kernel with narrow slots stages 4-byte values (mode 3); the float32 kernel too (mode 5:
+    // its sums are float32 bits in narrow slots)
     const bool narrow_ord = ord && vnarrow &&
                             fast_lds_bytes(nv, T, (uint32_t)(fast_sb_narrow(nv) * TA_BATCH), 4) <= LDS_MAX_BYTES;
-    const int fast_mode = !(fast || ord) ? 0
+    const bool f32_ok = nd_f32 > 0 && (nv == 0 || vnarrow) &&
+                        fast_lds_bytes(nv, T, (uint32_t)(fast_sb_narrow(nv) * TA_BATCH), 4) <= LDS_MAX_BYTES;
+    const int fast_mode = f32_ok ? 5
+                          : !(fast || ord) ? 0
                           : narrow_ord  ? 3
                           : fast_lds_bytes(nv, T, (uint32_t)(fast_sb_nd(nv, fast ? nd_f64 : 1) * TA_BATCH)) <= LDS_MAX_BYTES ? 2 : 1;
     // wide stream-out (batch_commit_fast): runs padded to 8 entries, 16-byte region stores;
     // needs 8 T more staged entries of LDS and tiles below 2^16 - 1 cells (DUMMY_CELL).
     // VH_TILE_WIDE: bit 0 wide, bit 1 non-temporal cell stores, bit 2 non-temporal value stores
-    const int sb_k = fast_mode == 3 ? fast_sb_narrow(nv) : fast_mode == 2 ? fast_sb_nd(nv, fast ? nd_f64 : 1) : 1;
+    const int sb_k = fast_mode == 3 || fast_mode == 5 ? fast_sb_narrow(nv) : fast_mode == 2 ? fast_sb_nd(nv, fast ? nd_f64 : 1) : 1;
     const uint32_t cap0 = (uint32_t)(sb_k * TA_BATCH);
-    const int vbytes = fast_mode == 3 ? 4 : 8;
+    const int vbytes = fast_mode == 3 || fast_mode == 5 ? 4 : 8;
     uint32_t wide_mode = 7;
     if (const char *e = getenv("VH_TILE_WIDE")) wide_mode = (uint32_t)atoi(e);
     const bool wide = (wide_mode & 1) && fast_mode != 0 && !flags_mode && S < DUMMY_CELL &&
@@ -2480,7 +2525,7 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         tp.vnarrow = vnarrow ? 1u : 0u;
         // the narrow ordinal pass A with two carried columns stores both in values[0], blocked
         // by 8 entries (values[0] spans both slot arrays; values[1] is unused)
-        tp.vpacked = (fast_mode == 3 && nv == 2 && !flags_mode && !getenv_flag_off("VH_TILE_PACK")) ? 1u : 0u;
+        tp.vpacked = ((fast_mode == 3 || fast_mode == 5) && nv == 2 && !flags_mode && !getenv_flag_off("VH_TILE_PACK")) ? 1u : 0u;
         tp.vfloat = vfloat;
         tp.vsigned = vsigned;
         tp.s_log2 = s_log2;
@@ -2512,7 +2557,7 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     };
     bool a_launched = false;
     auto launch_pass_a = [&]() {
-        TimedScope ts(fast ? "tile_scatter_f64" : ord ? (has_set ? "tile_scatter_set" : "tile_scatter_ord") : "tile_scatter");
+        TimedScope ts(fast ? "tile_scatter_f64" : fast_mode == 5 ? "tile_scatter_f32" : ord ? (has_set ? "tile_scatter_set" : "tile_scatter_ord") : "tile_scatter");
         const size_t lds = lds_a;
         if (ord) {
             const void *kf = ord_kernel(nv, fast_mode, has_set, tp.vdt[0], tp.vdt[1]);
