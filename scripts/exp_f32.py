@@ -1,6 +1,6 @@
 """Binning of float32 columns (vaex files often store float32): the C2 shape (2-D 1024^2
 count + sum) and small grids, kernel times per pass and the end-to-end step, against the
-float64 columns of the same values.  usage: python scripts/exp_f32.py [rows] [reps]"""
+float64 columns of the same values.  usage: [F32_CASES=small] python scripts/exp_f32.py [rows] [reps]"""
 import os
 import statistics
 import sys
@@ -35,7 +35,8 @@ def step(dt, bins, with_sum):
     return [np.asarray(a) for a in aggs]
 
 
-for bins, with_sum in ((1024, True), (1024, False), (256, True)):
+CASES = {"tile": ((1024, True), (1024, False), (256, True)), "small": ((64, True), (64, False), (128, False))}
+for bins, with_sum in CASES[os.environ.get("F32_CASES", "tile")]:
     ref = None
     for dt in ("float64", "float32"):
         step(dt, bins, with_sum)
@@ -50,7 +51,7 @@ for bins, with_sum in ((1024, True), (1024, False), (256, True)):
             ts.append(time.perf_counter() - t0)
             _lib.timing_enable(False)
             for k in ("tile_sample", "tile_scatter", "tile_scatter_f64", "tile_scatter_f32", "tile_reduce", "bin_small_f64",
-                      "bin_fused_lds", "bin_fused_global"):
+                      "bin_fused_lds", "bin_fused_global", "bin_cells", "bin_aggregate_lds", "bin_aggregate", "bin_indices", "bin_small_f32"):
                 v = _lib.timing_read(k)[1]
                 if v:
                     ks.setdefault(k, []).append(v)

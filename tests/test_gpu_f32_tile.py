@@ -1,4 +1,4 @@
-"""The fast float32 pass A (k_tile_scatter_f64<ND, NV, SB, float>, DESIGN §5.10): 1-, 2- and
+"""The fast float32 pass A (k_tile_scatter_f64<ND, NV, SB, float>, DESIGN §5.11): 1-, 2- and
 3-d grids too large for LDS over float32 columns, count(*) with 0, 1 or 2 float32 sums and
 the mean's keyed count, against the oracle's grids (counts exact, sums within 1e-6 relative,
 as north_star states for floating point) and against the generic pass A it replaces
@@ -86,3 +86,17 @@ def test_f32_tile_fallbacks_match_oracle(case):
     xs, ws = _cols(rng, n, 2, 1)
     out = _run(xs, ws, 1024, offset=1 if case == "unaligned" else 0)
     _check(xs, ws, 1024, out)
+
+
+@pytest.mark.parametrize("nd,bins,n,offset", [(1, 256, 3_000_001, 0), (2, 64, 3_000_000, 0), (3, 16, 2_000_000, 0),
+                                              (2, 64, 2_000_000, 1)])
+def test_f32_small_grid_count_matches_oracle(monkeypatch, nd, bins, n, offset):
+    """Small grids (LDS sub-grids, k_small_f64 with float32 row pairs): count(*) over float32
+    binner columns with NaNs, odd n (the last row alone) and a 4-byte-aligned view (k_fused
+    takes it), against the oracle and against k_fused (VH_SMALL_F32=0)."""
+    rng = np.random.default_rng(nd * 7 + offset)
+    xs, _ = _cols(rng, n, nd, 0)
+    out = _run(xs, [], bins, offset=offset)
+    _check(xs, [], bins, out)
+    monkeypatch.setenv("VH_SMALL_F32", "0")
+    np.testing.assert_array_equal(_run(xs, [], bins, offset=offset)[0], out[0])

@@ -754,8 +754,12 @@ __device__ inline void sg_row(const BinPlan &p, const SmallF64 &s, unsigned char
     }
 }
 
-template <int ND, int NC>
+// BT = float: float32 binner columns (8-byte row pairs), each value widened to double before
+// the scalar index math -- BinnerScalar<float>::to_bins scales the value as double
+// (superagg_binners.cpp:14-56); aggregator columns stay float64 (the fusable kinds)
+template <int ND, int NC, typename BT = double>
 __global__ __launch_bounds__(256) void k_small_f64(BinPlan p, SmallF64 s, uint64_t n, uint32_t *part) {
+    using B2 = std::conditional_t<std::is_same_v<BT, float>, float2, double2>;
     extern __shared__ __align__(16) unsigned char lds_raw[];
     uint32_t *w = reinterpret_cast<uint32_t *>(lds_raw);
     for (uint32_t i = threadIdx.x; i < s.lds_words; i += blockDim.x) w[i] = 0;
@@ -763,11 +767,12 @@ __global__ __launch_bounds__(256) void k_small_f64(BinPlan p, SmallF64 s, uint64
     const uint64_t nvec = n / 2, stride = (uint64_t)gridDim.x * blockDim.x;
     uint64_t v = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     for (; v + (SG_U - 1) * stride < nvec; v += SG_U * stride) {
-        double2 b[ND][SG_U], a[NC > 0 ? NC : 1][SG_U];
+        B2 b[ND][SG_U];
+        double2 a[NC > 0 ? NC : 1][SG_U];
 #pragma unroll
         for (int d = 0; d < ND; d++)
 #pragma unroll
-            for (int u = 0; u < SG_U; u++) b[d][u] = reinterpret_cast<const double2 *>(p.b[d].data)[v + u * stride];
+            for (int u = 0; u < SG_U; u++) b[d][u] = reinterpret_cast<const B2 *>(p.b[d].data)[v + u * stride];
 #pragma unroll
         for (int q = 0; q < NC; q++)
 #pragma unroll
@@ -776,12 +781,12 @@ __global__ __launch_bounds__(256) void k_small_f64(BinPlan p, SmallF64 s, uint64
         for (int u = 0; u < SG_U; u++) {
             double bx[ND], ax[NC > 0 ? NC : 1];
 #pragma unroll
-            for (int d = 0; d < ND; d++) bx[d] = b[d][u].x;
+            for (int d = 0; d < ND; d++) bx[d] = (double)b[d][u].x;
 #pragma unroll
             for (int q = 0; q < NC; q++) ax[q] = a[q][u].x;
             sg_row<ND, NC>(p, s, lds_raw, bx, ax);
 #pragma unroll
-            for (int d = 0; d < ND; d++) bx[d] = b[d][u].y;
+            for (int d = 0; d < ND; d++) bx[d] = (double)b[d][u].y;
 #pragma unroll
             for (int q = 0; q < NC; q++) ax[q] = a[q][u].y;
             sg_row<ND, NC>(p, s, lds_raw, bx, ax);
@@ -789,19 +794,20 @@ __global__ __launch_bounds__(256) void k_small_f64(BinPlan p, SmallF64 s, uint64
     }
     // the rest of the pairs one at a time, then the odd last row (block 0, lane 0)
     for (; v < nvec; v += stride) {
-        double2 b2[ND], a2[NC > 0 ? NC : 1];
+        B2 b2[ND];
+        double2 a2[NC > 0 ? NC : 1];
         double bx[ND], ax[NC > 0 ? NC : 1];
 #pragma unroll
-        for (int d = 0; d < ND; d++) b2[d] = reinterpret_cast<const double2 *>(p.b[d].data)[v];
+        for (int d = 0; d < ND; d++) b2[d] = reinterpret_cast<const B2 *>(p.b[d].data)[v];
 #pragma unroll
         for (int q = 0; q < NC; q++) a2[q] = s.col[q][v];
 #pragma unroll
-        for (int d = 0; d < ND; d++) bx[d] = b2[d].x;
+        for (int d = 0; d < ND; d++) bx[d] = (double)b2[d].x;
 #pragma unroll
         for (int q = 0; q < NC; q++) ax[q] = a2[q].x;
         sg_row<ND, NC>(p, s, lds_raw, bx, ax);
 #pragma unroll
-        for (int d = 0; d < ND; d++) bx[d] = b2[d].y;
+        for (int d = 0; d < ND; d++) bx[d] = (double)b2[d].y;
 #pragma unroll
         for (int q = 0; q < NC; q++) ax[q] = a2[q].y;
         sg_row<ND, NC>(p, s, lds_raw, bx, ax);
@@ -809,7 +815,7 @@ __global__ __launch_bounds__(256) void k_small_f64(BinPlan p, SmallF64 s, uint64
     if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
         double bx[ND], ax[NC > 0 ? NC : 1];
 #pragma unroll
-        for (int d = 0; d < ND; d++) bx[d] = reinterpret_cast<const double *>(p.b[d].data)[n - 1];
+        for (int d = 0; d < ND; d++) bx[d] = (double)reinterpret_cast<const BT *>(p.b[d].data)[n - 1];
 #pragma unroll
         for (int q = 0; q < NC; q++) ax[q] = reinterpret_cast<const double *>(s.col[q])[n - 1];
         sg_row<ND, NC>(p, s, lds_raw, bx, ax);
@@ -2207,13 +2213,28 @@ static bool launch_reduce0(const FusedAggs &fa, uint64_t n, Workspace &ws) {
     return true;
 }
 
+static bool getenv_off(const char *name) {  // NAME=0 turns a default-on path off (A/B runs)
+    const char *e = getenv(name);
+    return e && e[0] == '0' && e[1] == 0;
+}
+
 // small grids over float64 scalar binners (k_small_f64): false when a column is masked or
-// not 16-B aligned (k_fused takes it)
+// not 16-B aligned (k_fused takes it).  Native float32 scalar binners (8-B aligned) take the
+// same kernel with float32 row pairs (64^2 count(*) over 1e9 float32 rows: k_fused's per-row
+// dispatch 8.5 ms, profiles/r06_f32_small.txt)
 static bool launch_small_f64(const BinPlan &plan, const FusedAggs &fa, uint64_t n, uint64_t cells, int nd_f64,
                              Workspace &ws) {
-    if (nd_f64 < 1 || nd_f64 > 3 || n < 2) return false;
+    int nd32 = 0;
+    if (nd_f64 == 0 && plan.nb >= 1 && plan.nb <= 3 && !getenv_off("VH_SMALL_F32")) {
+        bool ok = true;
+        for (int d = 0; d < plan.nb; d++) ok = ok && plan.b[d].kind == 0 && plan.b[d].dtype == VH_F32 && !plan.b[d].flip;
+        if (ok) nd32 = plan.nb;
+    }
+    const int nd = nd_f64 ? nd_f64 : nd32;
+    if (nd < 1 || nd > 3 || n < 2) return false;
+    const uintptr_t amask = nd32 ? 7 : 15;
     for (int d = 0; d < plan.nb; d++)
-        if (plan.b[d].mask || (reinterpret_cast<uintptr_t>(plan.b[d].data) & 15)) return false;
+        if (plan.b[d].mask || (reinterpret_cast<uintptr_t>(plan.b[d].data) & amask)) return false;
     SmallF64 s{};
     s.na = fa.na;
     s.lds_words = fa.lds_words;
@@ -2239,16 +2260,18 @@ static bool launch_small_f64(const BinPlan &plan, const FusedAggs &fa, uint64_t 
     const unsigned nb = blocks_for((n / 2 + 2 * SG_U - 1) / (2 * SG_U), 256, per_cu);
     ws.idx.ensure((uint64_t)nb * lds_bytes);
     uint32_t *part = ws.idx.as<uint32_t>();
-    TimedScope ts("bin_small_f64");
+    TimedScope ts(nd32 ? "bin_small_f32" : "bin_small_f64");
     const dim3 grd(nb), blk(256);
-#define VH_SG(ND, NC) hipLaunchKernelGGL((k_small_f64<ND, NC>), grd, blk, lds_bytes, stream(), plan, s, n, part)
+#define VH_SG(ND, NC)                                                                                        \
+    if (nd32) hipLaunchKernelGGL((k_small_f64<ND, NC, float>), grd, blk, lds_bytes, stream(), plan, s, n, part); \
+    else hipLaunchKernelGGL((k_small_f64<ND, NC>), grd, blk, lds_bytes, stream(), plan, s, n, part)
 #define VH_SG_NC(ND) \
     switch (s.ncol) { \
     case 0: VH_SG(ND, 0); break; \
     case 1: VH_SG(ND, 1); break; \
     default: VH_SG(ND, 2); \
     }
-    switch (nd_f64) {
+    switch (nd) {
     case 1: VH_SG_NC(1); break;
     case 2: VH_SG_NC(2); break;
     default: VH_SG_NC(3);
