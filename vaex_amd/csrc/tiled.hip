@@ -136,6 +136,9 @@ struct TileParams {
     // scratch lands in HBM (r05: 6.2-7.4 ms for one C2 pass A) go away (scripts/bw_probe6.hip)
     uint32_t stream, ncw;
     uint32_t *tab;
+    // one keep mask shared by every aggregator (a selection or filter; 1 = keep) applied by the
+    // fast pass A per row: masked rows are dropped before the exchange (MK instantiations)
+    const uint8_t *rowmask;
 };
 
 // local cell of a padding entry (tiles hold at most 2^15 cells when runs are padded)
@@ -1143,7 +1146,10 @@ __device__ inline uint32_t scalar_f64_index32(double v, double vmin, double scal
 // the binner value widened to double before the index math (BinnerScalar<float>::to_bins,
 // superagg_binners.cpp:14-56, scales the value as double), sums carried, staged and stored
 // as their 4-byte float32 bits (narrow slots, widened exactly in pass B)
-template <int ND, int NV, int SB, typename CT = double>
+// MK: the plan's aggregators share one keep mask (tp.rowmask): two mask bytes per row pair
+// load with the pair, and a row whose byte is not 1 takes no aggregator (dropped from the
+// exchange, as the generic pass A drops a row no aggregator takes)
+template <int ND, int NV, int SB, typename CT = double, bool MK = false>
 __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
     constexpr bool F32 = std::is_same_v<CT, float>;
     using P2 = std::conditional_t<F32, float2, double2>;
@@ -1193,11 +1199,13 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
     // inside [0, n) or wholly past it; past-the-end pairs load the clamped last pair and
     // are dropped by the i < n test.  With no load behind an exec branch the compiler
     // counts vmcnt instead of draining to 0, so the prefetched batch stays in flight.
-    auto load = [&](uint64_t b0, P2 (&dst)[PAIRS][NC]) {
+    const uint8_t *rowmask = tp.rowmask;
+    auto load = [&](uint64_t b0, P2 (&dst)[PAIRS][NC], uint32_t (&mdst)[MK ? PAIRS : 1]) {
 #pragma unroll
         for (int q = 0; q < PAIRS; q++) {
             const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + threadIdx.x);
             const uint64_t is = i < n - 2 ? i : n - 2;
+            if constexpr (MK) mdst[q] = *reinterpret_cast<const uint16_t *>(rowmask + is);
 #pragma unroll
             for (int c = 0; c < NC; c++) {
 #if VH_TA_NT  // experiment: non-temporal loads of the once-read columns
@@ -1213,8 +1221,8 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
         }
     };
     // rank the rows of one batch: cell, take flags, (tile << 16 | cell) key, rank in tile
-    auto rows = [&](uint64_t b0, const P2 (&cur)[PAIRS][NC], uint32_t *key, int32_t *rank,
-                    VS (*vals)[NV > 0 ? NV : 1]) {
+    auto rows = [&](uint64_t b0, const P2 (&cur)[PAIRS][NC], const uint32_t (&mcur)[MK ? PAIRS : 1], uint32_t *key,
+                    int32_t *rank, VS (*vals)[NV > 0 ? NV : 1]) {
 #pragma unroll
         for (int r = 0; r < TA_RPT; r++) {
             const int q = r >> 1, h = r & 1;
@@ -1233,6 +1241,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
                 else vals[r][s] = v;
                 f |= v == v ? nan_keyed[s] : 0u;
             }
+            if constexpr (MK) f = ((h ? mcur[q] >> 8 : mcur[q]) & 0xffu) == 1u ? f : 0u;
             f = i < row_end ? f : 0u;
             const uint32_t t = c >> s_log2;
             key[r] = (t << 16) | (c & smask);
@@ -1246,7 +1255,8 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
     };
     constexpr bool drain = VH_TA_DRAIN != 0;
     P2 cur[PAIRS][NC], nxt[PAIRS][NC];
-    load((uint64_t)w * TA_BATCH, cur);
+    uint32_t mcur[MK ? PAIRS : 1] = {}, mnxt[MK ? PAIRS : 1] = {};
+    load((uint64_t)w * TA_BATCH, cur, mcur);
     for (uint64_t b0 = (uint64_t)w * TA_BATCH; b0 < n; b0 += SB * bstep) {
         uint32_t key[SB * TA_RPT];
         int32_t rank[SB * TA_RPT];
@@ -1255,13 +1265,15 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
         // after the commit (a copy before it would wait for those loads)
 #pragma unroll
         for (int sb = 0; sb < SB; sb++) {
-            load(b0 + (sb + 1) * bstep, nxt);
-            rows(b0 + sb * bstep, cur, key + sb * TA_RPT, rank + sb * TA_RPT, vals + sb * TA_RPT);
+            load(b0 + (sb + 1) * bstep, nxt, mnxt);
+            rows(b0 + sb * bstep, cur, mcur, key + sb * TA_RPT, rank + sb * TA_RPT, vals + sb * TA_RPT);
             if (sb + 1 < SB || drain)
 #pragma unroll
-                for (int q = 0; q < PAIRS; q++)
+                for (int q = 0; q < PAIRS; q++) {
 #pragma unroll
                     for (int c = 0; c < NC; c++) cur[q][c] = nxt[q][c];
+                    if constexpr (MK) mcur[q] = mnxt[q];
+                }
         }
         if (DBG(tp.debug) & 32) {  // experiment: no commit (loads, cell math, ranking only)
 #pragma unroll
@@ -1271,9 +1283,11 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
         }
         if (!drain)
 #pragma unroll
-            for (int q = 0; q < PAIRS; q++)
+            for (int q = 0; q < PAIRS; q++) {
 #pragma unroll
                 for (int c = 0; c < NC; c++) cur[q][c] = nxt[q][c];
+                if constexpr (MK) mcur[q] = mnxt[q];
+            }
     }
     lds_barrier();
     for (uint32_t t = threadIdx.x; t < T; t += TA_THREADS) tp.fills[(uint64_t)t * tp.W + w] = l.base[t] - (uint32_t)tp.toff[t];
@@ -2113,6 +2127,14 @@ template <int ND, int NV>
 static void launch_scatter(int fast, unsigned grid, size_t lds, const BinPlan &plan, const FusedAggs &fa,
                            const TileParams &tp, uint64_t n) {
     if constexpr (ND > 0) {
+        if (fast == 5 && tp.rowmask) {
+            hipLaunchKernelGGL((k_tile_scatter_f64<ND, NV, fast_sb_narrow(NV), float, true>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
+            return;
+        }
+        if (fast == 2 && tp.rowmask) {
+            hipLaunchKernelGGL((k_tile_scatter_f64<ND, NV, fast_sb_nd(NV, ND), double, true>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
+            return;
+        }
         if (fast == 5) {
             hipLaunchKernelGGL((k_tile_scatter_f64<ND, NV, fast_sb_narrow(NV), float>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
             return;
@@ -2144,9 +2166,17 @@ static void launch_scatter_nd(int nd, int fast, unsigned grid, size_t lds, const
 static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 static bool aligned8(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
 
-template <int ND, int NV> static int scatter_blocks_per_cu(int fast, size_t lds) {
+template <int ND, int NV> static int scatter_blocks_per_cu(int fast, size_t lds, bool mk) {
     int nb = 0;
     if constexpr (ND > 0) {
+        if (fast == 5 && mk) {
+            VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter_f64<ND, NV, fast_sb_narrow(NV), float, true>, TA_THREADS, lds));
+            return nb;
+        }
+        if (fast == 2 && mk) {
+            VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter_f64<ND, NV, fast_sb_nd(NV, ND), double, true>, TA_THREADS, lds));
+            return nb;
+        }
         if (fast == 5) {
             VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter_f64<ND, NV, fast_sb_narrow(NV), float>, TA_THREADS, lds));
             return nb;
@@ -2164,13 +2194,13 @@ template <int ND, int NV> static int scatter_blocks_per_cu(int fast, size_t lds)
     return nb;
 }
 
-template <int NV> static int scatter_blocks_per_cu_nd(int nd, int fast, size_t lds) {
+template <int NV> static int scatter_blocks_per_cu_nd(int nd, int fast, size_t lds, bool mk) {
     switch (nd) {
-    case 1: return scatter_blocks_per_cu<1, NV>(fast, lds);
-    case 2: return scatter_blocks_per_cu<2, NV>(fast, lds);
-    case 3: return scatter_blocks_per_cu<3, NV>(fast, lds);
-    case -1: return scatter_blocks_per_cu<-1, NV>(0, lds);
-    default: return scatter_blocks_per_cu<0, NV>(0, lds);
+    case 1: return scatter_blocks_per_cu<1, NV>(fast, lds, mk);
+    case 2: return scatter_blocks_per_cu<2, NV>(fast, lds, mk);
+    case 3: return scatter_blocks_per_cu<3, NV>(fast, lds, mk);
+    case -1: return scatter_blocks_per_cu<-1, NV>(0, lds, false);
+    default: return scatter_blocks_per_cu<0, NV>(0, lds, false);
     }
 }
 
@@ -2298,10 +2328,34 @@ static TileScratch &tile_scratch() {
     return *p;
 }
 
+static bool try_tiled_core(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64,
+                           const uint8_t *rowmask);
+
+// A plan whose aggregators all carry the same keep mask (a selection / filter) and whose
+// binners have none: the fast pass A applies the mask per row (MK kernels) and the rest of
+// the plan runs as unmasked -- counts of every kept row, no flag entries.  Only when a fast
+// kernel takes the plan; otherwise the masks go to the generic pass A as before.  (C2 with a
+// selection: generic pass A 12.0 ms, profiles/r06_mask.txt.)  VH_TILE_ROWMASK=0: off.
 static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64) {
+    const uint8_t *m = fa_in.na > 0 ? fa_in.a[0].mask : nullptr;
+    for (int k = 1; k < fa_in.na && m; k++)
+        if (fa_in.a[k].mask != m) m = nullptr;
+    for (int d = 0; d < plan.nb && m; d++)
+        if (plan.b[d].mask) m = nullptr;
+    if (m && !getenv_flag_off("VH_TILE_ROWMASK")) {
+        FusedAggs f2 = fa_in;
+        for (int k = 0; k < f2.na; k++) f2.a[k].mask = nullptr;
+        if (try_tiled_core(plan, f2, n, cells, nd_f64, m)) return true;
+    }
+    return try_tiled_core(plan, fa_in, n, cells, nd_f64, nullptr);
+}
+
+static bool try_tiled_core(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64,
+                           const uint8_t *rowmask) {
     TileScratch &ws = tile_scratch();
     std::lock_guard<std::mutex> ws_lock(ws.mu);
     TileParams tp{};
+    tp.rowmask = rowmask;
 #ifdef VH_ABLATION
     if (const char *dbg = getenv("VH_TILE_DEBUG")) tp.debug = (uint32_t)atoi(dbg);
 #endif
@@ -2424,6 +2478,8 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
                           : !(fast || ord) ? 0
                           : narrow_ord  ? 3
                           : fast_lds_bytes(nv, T, (uint32_t)(fast_sb_nd(nv, fast ? nd_f64 : 1) * TA_BATCH)) <= LDS_MAX_BYTES ? 2 : 1;
+    // a shared keep mask runs only on the fast f64 / f32 kernels' MK instantiations
+    if (rowmask && !((fast && fast_mode == 2) || fast_mode == 5)) return false;
     // wide stream-out (batch_commit_fast): runs padded to 8 entries, 16-byte region stores;
     // needs 8 T more staged entries of LDS and tiles below 2^16 - 1 cells (DUMMY_CELL).
     // VH_TILE_WIDE: bit 0 wide, bit 1 non-temporal cell stores, bit 2 non-temporal value stores
@@ -2443,7 +2499,8 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         static std::mutex mu;
         static std::map<std::tuple<int, int, int, int, size_t>, int> cache;
         std::lock_guard<std::mutex> lk(mu);
-        const auto key = std::make_tuple(current_device(), ord ? (has_set ? -3 : -2) - 4 * (tp.vdt[0] + 32 * tp.vdt[1]) : nd_k, nv, fast_mode, lds_a);
+        const auto key = std::make_tuple(current_device(), ord ? (has_set ? -3 : -2) - 4 * (tp.vdt[0] + 32 * tp.vdt[1]) : nd_k, nv,
+                                         fast_mode + (rowmask ? 16 : 0), lds_a);
         auto it = cache.find(key);
         if (it == cache.end()) {
             int v = 0;
@@ -2451,9 +2508,9 @@ static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
                 const void *kf = ord_kernel(nv, fast_mode, has_set, tp.vdt[0], tp.vdt[1]);
                 VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kf, TA_THREADS, lds_a));
             } else {
-                v = nv == 0 ? scatter_blocks_per_cu_nd<0>(nd_k, fast_mode, lds_a)
-                            : nv == 1 ? scatter_blocks_per_cu_nd<1>(nd_k, fast_mode, lds_a)
-                                      : scatter_blocks_per_cu_nd<2>(nd_k, fast_mode, lds_a);
+                v = nv == 0 ? scatter_blocks_per_cu_nd<0>(nd_k, fast_mode, lds_a, rowmask != nullptr)
+                            : nv == 1 ? scatter_blocks_per_cu_nd<1>(nd_k, fast_mode, lds_a, rowmask != nullptr)
+                                      : scatter_blocks_per_cu_nd<2>(nd_k, fast_mode, lds_a, rowmask != nullptr);
             }
             it = cache.emplace(key, v).first;
         }
