@@ -101,3 +101,50 @@ def test_selection_on_hbm_frame():
     np.testing.assert_array_equal(c, oracle.extract_central_part(oracle.compute_grid(ob, "count", mask=keep)))
     np.testing.assert_allclose(s, oracle.extract_central_part(oracle.compute_grid(ob, "sum", data=w, mask=keep)),
                                rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("vdt", ["float64", "int64"])
+def test_filtered_groupby_dense_route(vdt):
+    """groupby on a filtered HBM frame (df[df.w > 0.4]) takes the dense-grid route with the
+    filter as every aggregator's keep mask (float64 values: the ordinal kernel's MK
+    instantiation; int64 values: the generic pass A): groups, counts and sums equal
+    oracle.groupby_agg over the filtered rows, keys in sorted order (GrouperDense)."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(21)
+    n = 3_000_000
+    keys = rng.integers(5, 200_005, n).astype(np.int32)
+    w = rng.random(n)
+    v = rng.normal(size=n) if vdt == "float64" else rng.integers(-1000, 1000, n).astype(np.int64)
+    if vdt == "float64":
+        v[::89] = np.nan
+    df = vaex_amd.from_arrays(key=DeviceArray.from_numpy(keys), w=DeviceArray.from_numpy(w), v=DeviceArray.from_numpy(v))
+    g = df[df.w > 0.4].groupby("key", agg={"v": ["sum", "count"]})
+    keep = w > 0.4
+    # the string 'count' is count(*) under the column's name (parse_actions: vaex.agg.count())
+    want = oracle.groupby_agg({"key": keys[keep], "v": v[keep]}, ["key"], [("v_sum", "sum", "v"), ("v_count", "count", None)])
+    np.testing.assert_array_equal(g["key"].to_numpy(), want["key"])
+    np.testing.assert_array_equal(g["v"].to_numpy(), want["v_count"])
+    if vdt == "float64":
+        np.testing.assert_allclose(g["v_sum"].to_numpy(), want["v_sum"], rtol=1e-9, atol=1e-9)
+    else:
+        np.testing.assert_array_equal(g["v_sum"].to_numpy(), want["v_sum"])
+
+
+def test_filtered_groupby_empty_and_narrow_filters():
+    """A filter no row passes (no groups) and one that leaves a few keys (most dense cells
+    empty: compaction) give the oracle's groups."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(22)
+    n = 2_000_000
+    keys = rng.integers(0, 50_000, n).astype(np.int64)
+    v = rng.normal(size=n)
+    df = vaex_amd.from_arrays(key=DeviceArray.from_numpy(keys), v=DeviceArray.from_numpy(v))
+    g0 = df[df.v > 100].groupby("key", agg={"v": "sum"})
+    assert len(g0) == 0
+    sel = (keys >= 20_000) & (keys < 20_300) & (v > 0)
+    g1 = df[(df.key >= 20_000) & (df.key < 20_300) & (df.v > 0)].groupby("key", agg={"v": "sum"})
+    want = oracle.groupby_agg({"key": keys[sel], "v": v[sel]}, ["key"], [("v", "sum", "v")])
+    np.testing.assert_array_equal(g1["key"].to_numpy(), want["key"])
+    np.testing.assert_allclose(g1["v"].to_numpy(), want["v"], rtol=1e-9, atol=1e-12)

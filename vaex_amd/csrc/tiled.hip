@@ -1325,7 +1325,9 @@ __device__ inline uint32_t set_ord_cell(int64_t o, uint64_t count) {
 // VN: every carried column is <= 4 bytes (narrow slots): values are carried, staged and
 // stored as their 4-byte slot bits (half the LDS staging: two columns still commit three
 // batches at once)
-template <int NV, int SB, bool SET = false, int DT0 = VH_F64, int DT1 = VH_F64, bool VN = false>
+// MK: a keep mask shared by the aggregators (tp.rowmask; a filtered frame's groupby), applied
+// per row like the fast scalar kernels' MK instantiations
+template <int NV, int SB, bool SET = false, int DT0 = VH_F64, int DT1 = VH_F64, bool VN = false, bool MK = false>
 __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
     constexpr int PAIRS = TA_RPT / 2;
     using VT = std::conditional_t<VN, uint32_t, double>;
@@ -1362,7 +1364,9 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
     struct Regs {
         int2 k[PAIRS];
         double2 v[PAIRS][NV > 0 ? NV : 1];
+        uint32_t m[MK ? PAIRS : 1];
     };
+    const uint8_t *rowmask = tp.rowmask;
     int vsz[NV > 0 ? NV : 1];
 #pragma unroll
     for (int s = 0; s < NV; s++) {
@@ -1377,6 +1381,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
             const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + threadIdx.x);
             const uint64_t is = i < n - 2 ? i : n - 2;
             R.k[q] = *reinterpret_cast<const int2 *>(keys + is);
+            if constexpr (MK) R.m[q] = *reinterpret_cast<const uint16_t *>(rowmask + is);
 #pragma unroll
             for (int s = 0; s < NV; s++) {
                 const char *cb = reinterpret_cast<const char *>(col[s]);
@@ -1443,6 +1448,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR void k_tile_scatter_ord(BinPlan
                     f |= vals[r][s] == vals[r][s] ? nan_keyed[s] : 0u;
                 }
             }
+            if constexpr (MK) f = ((h ? cur.m[q] >> 8 : cur.m[q]) & 0xffu) == 1u ? f : 0u;
             f = i < row_end ? f : 0u;
             const uint32_t t = c >> s_log2;
             key[r] = (t << 16) | (c & smask);
@@ -2232,9 +2238,18 @@ template <int NV, int SB, bool SET, typename F> static void ord_by_dts(int dt0, 
 #undef VH_ORD_DT
     f(k_tile_scatter_ord<NV, SB, SET, -1, -1>);
 }
-template <bool SET> static const void *ord_kernel_t(int nv, int fast_mode, int dt0, int dt1) {
+template <bool SET> static const void *ord_kernel_t(int nv, int fast_mode, int dt0, int dt1, bool mk) {
     const void *k = nullptr;
     auto take = [&](auto kern) { k = reinterpret_cast<const void *>(kern); };
+    if (mk) {  // shared keep mask: int32 key, float64 values (or none), batched commits
+        if constexpr (!SET) {
+            if (nv == 0) return reinterpret_cast<const void *>(k_tile_scatter_ord<0, 1, false, VH_F64, VH_F64, false, true>);
+            if (fast_mode != 2 || dt0 != VH_F64 || (nv > 1 && dt1 != VH_F64)) return nullptr;
+            return nv == 1 ? reinterpret_cast<const void *>(k_tile_scatter_ord<1, fast_sb(1), false, VH_F64, VH_F64, false, true>)
+                           : reinterpret_cast<const void *>(k_tile_scatter_ord<2, fast_sb(2), false, VH_F64, VH_F64, false, true>);
+        }
+        return nullptr;
+    }
     if constexpr (!SET) {
         if (fast_mode == 3) {  // narrow slots, fast_sb_narrow(nv) batches per commit
             if (nv == 1) ord_by_dts_narrow<1, fast_sb_narrow(1)>(dt0, dt1, take);
@@ -2252,8 +2267,8 @@ template <bool SET> static const void *ord_kernel_t(int nv, int fast_mode, int d
     }
     return k;
 }
-static const void *ord_kernel(int nv, int fast_mode, bool set, int dt0, int dt1) {
-    return set ? ord_kernel_t<true>(nv, fast_mode, dt0, dt1) : ord_kernel_t<false>(nv, fast_mode, dt0, dt1);
+static const void *ord_kernel(int nv, int fast_mode, bool set, int dt0, int dt1, bool mk = false) {
+    return set ? ord_kernel_t<true>(nv, fast_mode, dt0, dt1, mk) : ord_kernel_t<false>(nv, fast_mode, dt0, dt1, mk);
 }
 
 static bool try_tiled_impl(const BinPlan &plan, const FusedAggs &fa_in, uint64_t n, uint64_t cells, int nd_f64);
@@ -2479,7 +2494,9 @@ static bool try_tiled_core(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
                           : narrow_ord  ? 3
                           : fast_lds_bytes(nv, T, (uint32_t)(fast_sb_nd(nv, fast ? nd_f64 : 1) * TA_BATCH)) <= LDS_MAX_BYTES ? 2 : 1;
     // a shared keep mask runs only on the fast f64 / f32 kernels' MK instantiations
-    if (rowmask && !((fast && fast_mode == 2) || fast_mode == 5)) return false;
+    if (rowmask && !((fast && fast_mode == 2) || fast_mode == 5 ||
+                     (ord && ord_kernel(nv, fast_mode, has_set, tp.vdt[0], tp.vdt[1], true) != nullptr)))
+        return false;
     // wide stream-out (batch_commit_fast): runs padded to 8 entries, 16-byte region stores;
     // needs 8 T more staged entries of LDS and tiles below 2^16 - 1 cells (DUMMY_CELL).
     // VH_TILE_WIDE: bit 0 wide, bit 1 non-temporal cell stores, bit 2 non-temporal value stores
@@ -2505,7 +2522,7 @@ static bool try_tiled_core(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         if (it == cache.end()) {
             int v = 0;
             if (ord) {
-                const void *kf = ord_kernel(nv, fast_mode, has_set, tp.vdt[0], tp.vdt[1]);
+                const void *kf = ord_kernel(nv, fast_mode, has_set, tp.vdt[0], tp.vdt[1], rowmask != nullptr);
                 VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kf, TA_THREADS, lds_a));
             } else {
                 v = nv == 0 ? scatter_blocks_per_cu_nd<0>(nd_k, fast_mode, lds_a, rowmask != nullptr)
@@ -2617,7 +2634,7 @@ static bool try_tiled_core(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         TimedScope ts(fast ? "tile_scatter_f64" : fast_mode == 5 ? "tile_scatter_f32" : ord ? (has_set ? "tile_scatter_set" : "tile_scatter_ord") : "tile_scatter");
         const size_t lds = lds_a;
         if (ord) {
-            const void *kf = ord_kernel(nv, fast_mode, has_set, tp.vdt[0], tp.vdt[1]);
+            const void *kf = ord_kernel(nv, fast_mode, has_set, tp.vdt[0], tp.vdt[1], rowmask != nullptr);
             void *args[] = {(void *)&plan, (void *)&fa, (void *)&tp, (void *)&n};
             VH_HIP(hipLaunchKernel(kf, dim3(W), dim3(TA_THREADS), args, lds, st));
         } else {

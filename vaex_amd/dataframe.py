@@ -612,12 +612,14 @@ class DataFrame:
             # pass + BinnerOrdinal grid, GrouperDense); otherwise count/sum/mean run as one
             # hash-partitioned pass (hashagg.py).
             from .hashagg import eligible_key, try_groupby
-            key = eligible_key(self, by)
+            # a filtered frame takes the dense route too (its groups: the occupied cells of the
+            # filtered counts); the fused hash pass has no filter
+            key = eligible_key(self, by, allow_filtered=True)
             if key is not None:
                 rng = _dense_range(self, key, speculative=_speculate)
                 if rng is not None:
                     dense_ranges[key] = rng
-                else:
+                elif not self.filtered:
                     res = try_groupby(self, by, agg, lambda a, g: parse_actions(self, a, g), sort=sort,
                                       row_limit=row_limit)
                     if res is not None:

@@ -171,8 +171,10 @@ def _dense_range(df, expression, speculative=False):
     if col is None or np.ma.isMaskedArray(col):
         return None
     dtype = np.dtype(col.dtype)
-    if dtype.kind not in "iu" or df.filtered:
+    if dtype.kind not in "iu":
         return None
+    # a filtered frame: the sampled range is the unfiltered column's (a superset; the empty
+    # cells of the filtered counts are dropped), the exact range the filtered min / max
     n = df.length_unfiltered()
     if n == 0:
         return None
@@ -181,6 +183,8 @@ def _dense_range(df, expression, speculative=False):
         if span <= DENSE_KEY_MAX and span <= 4 * n + 1024 and abs(rng[0]) < 2 ** 53 and abs(rng[1]) < 2 ** 53:
             return rng[0], rng[1], True
     vmin, vmax = df.minmax(expression)
+    if not (np.isfinite(vmin) and np.isfinite(vmax)):  # no rows (an empty filter)
+        return None
     if not (abs(int(vmin)) < 2 ** 53 and abs(int(vmax)) < 2 ** 53):
         return None
     span = int(vmax) - int(vmin) + 1

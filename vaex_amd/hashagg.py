@@ -119,9 +119,10 @@ class HashAgg:
         return keys, counts, sums, nonnull
 
 
-def eligible_key(df, by):
+def eligible_key(df, by, allow_filtered=False):
     """The key column name when ``by`` is one plain, unmasked, native integer column on an
-    unfiltered frame (the fused path's key), else None."""
+    unfiltered frame (the fused path's key), else None.  allow_filtered: filtered frames too
+    (the dense-grid route, whose aggregators take the filter as their keep mask)."""
     if isinstance(by, (list, tuple)):
         if len(by) != 1:
             return None
@@ -129,7 +130,7 @@ def eligible_key(df, by):
     if not isinstance(by, str) and type(by).__name__ != "Expression":
         return None
     by = str(by)
-    if df.filtered or by not in df.columns or df.is_category(by):
+    if (df.filtered and not allow_filtered) or by not in df.columns or df.is_category(by):
         return None
     key = df.columns[by]
     if np.ma.isMaskedArray(key) or np.dtype(key.dtype).name not in KEY_DTYPES:

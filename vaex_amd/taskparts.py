@@ -134,15 +134,24 @@ class TaskPartAggregation:
                 binner.clear_data_mask()
             references.append(block)
         all_aggregators = []
+        # one mask per selection and chunk: every aggregator of a selection shares it (one
+        # evaluation; the tile path runs a mask shared by all aggregators as a row mask)
+        sel_masks = {}
         for desc, selections, aggs, _ in self.aggregations:
             for selection_index, selection in enumerate(selections):
                 agg = aggs[selection_index]
                 all_aggregators.append(agg)
                 selection_mask = None
                 if not (selection is None or selection is False):
-                    selection_mask = self.df.evaluate_selection_mask(selection, i1=i1, i2=i2, filter_mask=filter_mask)
-                    if not isinstance(selection_mask, DeviceArray):
-                        selection_mask = np.asarray(selection_mask)
+                    skey = selection if isinstance(selection, (str, bool)) else None
+                    if skey is not None and skey in sel_masks:
+                        selection_mask = sel_masks[skey]
+                    else:
+                        selection_mask = self.df.evaluate_selection_mask(selection, i1=i1, i2=i2, filter_mask=filter_mask)
+                        if not isinstance(selection_mask, DeviceArray):
+                            selection_mask = np.asarray(selection_mask)
+                        if skey is not None:
+                            sel_masks[skey] = selection_mask
                 elif device_filter:
                     selection_mask = filter_mask
                 if selection_mask is not None and hasattr(agg, "set_selection_mask"):
