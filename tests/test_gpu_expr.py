@@ -117,3 +117,33 @@ def test_groupby_on_filtered_device_frame():
     order = np.argsort(res["key"].to_numpy())
     np.testing.assert_array_equal(res["key"].to_numpy()[order], keys)
     np.testing.assert_array_equal(res["n"].to_numpy()[order], counts)
+
+
+TERMS = ["x > 0.4", "(x > 0.3) & (f < 2)", "(i >= -20) & (i < 30) & (w > 0.1)", "(x > 0.3) | (i32 == 3)",
+         "~(y <= 2)", "u8 > 200", "i8 < -3", "(f > 0.5) & (i32 >= 0)", "x != x", "(i > 3) & (x > 0) & (y > 1) & (w < 0.9)",
+         "i32 > 2.5", "f >= 0.1"]
+
+
+@pytest.mark.parametrize("e", TERMS)
+@pytest.mark.parametrize("offset", [0, 3])
+def test_comparison_terms_kernel(monkeypatch, e, offset):
+    """Conjunctions / disjunctions of column-vs-constant comparisons run the 8-rows-per-lane
+    kernel (k_expr_terms); it must equal numpy and the interpreter (VH_EXPR_TERMS=0) byte for
+    byte, on whole frames and on views starting mid-block (tail rows, unaligned columns),
+    with NaNs in the float columns."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    h = _host()
+    h["x"][::37] = np.nan
+    h["f"][::41] = np.nan
+    hv = {k: v[offset:] for k, v in h.items()}
+    full = {k: DeviceArray.from_numpy(v) for k, v in h.items()}
+    df = vaex_amd.from_arrays(**{k: d[offset:] for k, d in full.items()})
+    got = df.evaluate(e).to_numpy()
+    monkeypatch.setenv("VH_EXPR_TERMS", "0")
+    interp = df.evaluate(e).to_numpy()
+    ns = dict(hv)
+    with np.errstate(all="ignore"):
+        expected = np.asarray(eval(e, {"__builtins__": {}}, ns))  # noqa: S307
+    np.testing.assert_array_equal(got, expected)
+    np.testing.assert_array_equal(got, interp)

@@ -311,9 +311,144 @@ __global__ __launch_bounds__(EX_THREADS) void k_expr(ExprProg prog, uint64_t n, 
     }
 }
 
+// ---- conjunctions / disjunctions of column-vs-constant comparisons -----------------------
+// The common filter and selection shape, (a > c1) & (b <= c2) & ...: the interpreter above
+// issues each column's loads inside its program step and shifts the register stack per push
+// (`w > 0.4` over 1e9 float64 rows: 7.4 ms, 1.2 TB/s, profiles/r06_filter_tl.txt).  Here each
+// lane takes 8 consecutive rows: a term's column is read with 16-byte loads (8 rows of its
+// dtype), compared with the term's constant by the interpreter's own `binary` / `unary`
+// (identical results by construction), folded into the 8 keep bytes, stored as one 8-byte
+// word.  vh_expr_eval recognises the program shape; anything else runs the interpreter.
+constexpr int EX_MAX_TERMS = 8;
+constexpr int EXT_RPT = 8;
+struct ExprTerms {
+    const void *col[EX_MAX_TERMS];
+    uint64_t c[EX_MAX_TERMS];
+    int32_t dt[EX_MAX_TERMS];
+    uint32_t ucol[EX_MAX_TERMS], ucon[EX_MAX_TERMS], cmp[EX_MAX_TERMS];  // ucol / ucon: 0 or op | arg << 8
+    int32_t nt, conj, neg;
+};
+
+// 8 consecutive rows' 64-bit slots (load_slot's widening) from 16-byte loads when the column
+// block is aligned and whole, else element by element
+__device__ inline void load_slots8(const void *p, int dt, uint64_t base, uint32_t cnt, uint64_t (&v)[EXT_RPT]) {
+    const int isz = dt == VH_F64 || dt == VH_I64 || dt == VH_U64 ? 8 : dt == VH_F32 || dt == VH_I32 || dt == VH_U32 ? 4
+                  : dt == VH_I16 || dt == VH_U16 ? 2 : 1;
+    const char *b = static_cast<const char *>(p) + base * isz;
+    if (cnt == EXT_RPT && (reinterpret_cast<uintptr_t>(b) & 15) == 0 && isz >= 2) {
+        uint32_t w[16];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (q * 16 < EXT_RPT * isz) {
+                const uint4 u = reinterpret_cast<const uint4 *>(b)[q];
+                w[4 * q] = u.x;
+                w[4 * q + 1] = u.y;
+                w[4 * q + 2] = u.z;
+                w[4 * q + 3] = u.w;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < EXT_RPT; r++) {
+            uint64_t raw;
+            if (isz == 8) raw = (uint64_t)w[2 * r] | ((uint64_t)w[2 * r + 1] << 32);
+            else if (isz == 4) raw = w[r];
+            else raw = (w[r >> 1] >> (16 * (r & 1))) & 0xffffu;
+            switch (dt) {
+            case VH_F32: v[r] = fb((double)__builtin_bit_cast(float, (uint32_t)raw)); break;
+            case VH_I32: v[r] = (uint64_t)(int64_t)(int32_t)(uint32_t)raw; break;
+            case VH_I16: v[r] = (uint64_t)(int64_t)(int16_t)(uint16_t)raw; break;
+            default: v[r] = raw;  // float64 bits, int64, uint64 / 32 / 16
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int r = 0; r < EXT_RPT; r++) v[r] = (uint32_t)r < cnt ? load_slot(p, dt, base + r) : 0;
+}
+
+__global__ __launch_bounds__(EX_THREADS) void k_expr_terms(ExprTerms t, uint64_t n, uint8_t *out) {
+    const uint64_t stride = (uint64_t)gridDim.x * EX_THREADS * EXT_RPT;
+    for (uint64_t base = ((uint64_t)blockIdx.x * EX_THREADS + threadIdx.x) * EXT_RPT; base < n; base += stride) {
+        const uint32_t cnt = (uint32_t)min<uint64_t>(EXT_RPT, n - base);
+        uint32_t acc[EXT_RPT];
+#pragma unroll
+        for (int r = 0; r < EXT_RPT; r++) acc[r] = t.conj ? 1u : 0u;
+        for (int k = 0; k < t.nt; k++) {
+            uint64_t v[EXT_RPT];
+            load_slots8(t.col[k], t.dt[k], base, cnt, v);
+            const uint32_t uc = t.ucol[k], cop = t.cmp[k];
+            const uint64_t c = t.ucon[k] ? unary<false>(t.ucon[k] & 0xff, t.ucon[k] >> 8, t.c[k]) : t.c[k];
+#pragma unroll
+            for (int r = 0; r < EXT_RPT; r++) {
+                const uint64_t x = uc ? unary<false>(uc & 0xff, uc >> 8, v[r]) : v[r];
+                const uint32_t bit = (uint32_t)binary<false>(cop, x, c);
+                acc[r] = t.conj ? (acc[r] & bit) : (acc[r] | bit);
+            }
+        }
+        uint64_t word = 0;
+#pragma unroll
+        for (int r = 0; r < EXT_RPT; r++) word |= (uint64_t)((acc[r] ^ (uint32_t)t.neg) & 1u) << (8 * r);
+        if (cnt == EXT_RPT && (reinterpret_cast<uintptr_t>(out + base) & 7) == 0) {
+            *reinterpret_cast<uint64_t *>(out + base) = word;
+        } else {
+            for (uint32_t r = 0; r < cnt; r++) out[base + r] = (uint8_t)(word >> (8 * r));
+        }
+    }
+}
+
+// the program as T (T COMB)* [NOT_B] with T = COL [cvt] CONST [cvt] CMP, one COMB kind
+// (AND_I or OR_I) and a 1-byte output; false: another shape
+static bool match_terms(const uint32_t *code, int ncode, const uint64_t *consts, const void *const *cols,
+                        const int *col_dtypes, int out_dtype, ExprTerms &t) {
+    if (dtype_itemsize(out_dtype) != 1) return false;
+    auto cvt = [](uint32_t op) { return op == OP_I2F || op == OP_U2F || op == OP_ROUND_F32 || op == OP_WRAP; };
+    auto cmp = [](uint32_t op) { return op >= OP_LT_F && op <= OP_GE_U; };
+    t = ExprTerms{};
+    t.conj = -1;
+    int i = 0;
+    while (i < ncode) {
+        if (t.nt == EX_MAX_TERMS) return false;
+        uint32_t op = code[i] & 0xff;
+        if (op != OP_COL) break;
+        const int k = t.nt;
+        t.col[k] = cols[code[i] >> 8];
+        t.dt[k] = col_dtypes[code[i] >> 8];
+        i++;
+        if (i < ncode && cvt(code[i] & 0xff)) t.ucol[k] = code[i++];
+        if (i >= ncode || (code[i] & 0xff) != OP_CONST) return false;
+        t.c[k] = consts[code[i] >> 8];
+        i++;
+        if (i < ncode && cvt(code[i] & 0xff)) t.ucon[k] = code[i++];
+        if (i >= ncode || !cmp(code[i] & 0xff)) return false;
+        t.cmp[k] = code[i] & 0xff;
+        i++;
+        t.nt++;
+        if (k > 0) {  // a combiner follows every term after the first
+            if (i >= ncode) return false;
+            op = code[i] & 0xff;
+            const int cj = op == OP_AND_I ? 1 : op == OP_OR_I ? 0 : -1;
+            if (cj < 0 || (t.conj >= 0 && cj != t.conj)) return false;
+            t.conj = cj;
+            i++;
+        }
+    }
+    if (t.nt == 0) return false;
+    if (t.conj < 0) t.conj = 1;
+    if (i < ncode && (code[i] & 0xff) == OP_NOT_B) {
+        t.neg = 1;
+        i++;
+    }
+    return i == ncode;
+}
+
 }  // namespace vh
 
 using namespace vh;
+
+static bool getenv_off_expr(const char *name) {  // NAME=0: the interpreter for every program (A/Bs)
+    const char *e = getenv(name);
+    return e && e[0] == '0' && e[1] == 0;
+}
 
 extern "C" int vh_expr_eval(const uint32_t *code, int ncode, const uint64_t *consts, int nconsts,
                             const void *const *cols, const int *col_dtypes, int ncols, uint64_t n, int out_dtype,
@@ -355,7 +490,15 @@ extern "C" int vh_expr_eval(const uint32_t *code, int ncode, const uint64_t *con
     dtype_itemsize(out_dtype);
     p.ncode = ncode;
     p.out_dtype = out_dtype;
-    if (n) {
+    ExprTerms terms;
+    if (n && !getenv_off_expr("VH_EXPR_TERMS") &&
+        match_terms(code, ncode, consts, cols, col_dtypes, out_dtype, terms)) {
+        TimedScope ts("expr");
+        const uint64_t per_block = (uint64_t)EX_THREADS * EXT_RPT;
+        const unsigned grid = (unsigned)std::min<uint64_t>((n + per_block - 1) / per_block, (uint64_t)cu_count() * 8);
+        hipLaunchKernelGGL(k_expr_terms, dim3(grid), dim3(EX_THREADS), 0, stream(), terms, n, static_cast<uint8_t *>(out));
+        VH_HIP(hipGetLastError());
+    } else if (n) {
         TimedScope ts("expr");
         const uint64_t per_block = (uint64_t)EX_THREADS * (math ? 1 : 4);
         const uint64_t want = (n + per_block - 1) / per_block;
