@@ -43,6 +43,7 @@ def parse():
     p.add_argument("--no-groupby", action="store_true")
     p.add_argument("--no-count-only", action="store_true")
     p.add_argument("--no-f32", action="store_true", help="skip the C2 leg on float32 copies of x, y, w")
+    p.add_argument("--no-filtered", action="store_true", help="skip the selection / filtered-groupby legs")
     p.add_argument("--no-layouts", action="store_true", help="skip the sorted-layout legs")
     p.add_argument("--host-rows", type=float, default=2e8,
                    help="rows of the PCIe-inclusive measurement (host numpy columns); 0 = skip")
@@ -263,6 +264,8 @@ def main():
         extra["count_only"] = bench_count_only(x, y, n, bins, args)
     if rank == 0 and world == 1 and not args.no_f32:
         extra["c2_float32"] = bench_c2_float32(n, bins, args, check["sum_reference"])
+    if rank == 0 and world == 1 and not args.no_filtered:
+        extra["filtered"] = bench_filtered(x, y, w, n, bins, args)
     if rank == 0 and world == 1 and not args.no_aggs:
         extra["aggs"] = bench_other_aggs(x, y, w, n, bins, args, ms_per_step)
     if rank == 0 and world == 1 and not args.no_set:
@@ -438,6 +441,75 @@ def bench_c2_float32(n, bins, args, sum_reference):
             "kernel": dom, "kernel_GBps": round(12 * n / (per[dom] * 1e-3) / 1e9, 1) if dom else None,
             "check": {"count_total": c_tot, "count_equal": c_tot == n, "sum_total": s_tot, "sum_rel_err_vs_f64": rel,
                       "ok": bool(c_tot == n and rel is not None and rel < 1e-6)}}
+
+
+def bench_filtered(x, y, w, n, bins, args):
+    """Selections and filters (one keep mask per chunk, shared by the aggregators; DESIGN
+    §5.11).  c2_selection: C2's count + sum(w) with the selection w > 0.5 -- the mask
+    evaluated by the expression kernel inside every step, then the row-masked fast pass A.
+    groupby_filtered: C3's groupby(key).agg(sum) on df[df.v > 0] through the DataFrame API
+    (filter evaluation, dense route, row-masked ordinal pass A).  Checks: the masked grid's
+    count total equals the number of kept rows; the groups' count total equals the filtered
+    frame's length."""
+    import vaex_amd
+    from vaex_amd import _lib, superagg
+    from vaex_amd.device import DeviceArray
+    out = {}
+    dfc = vaex_amd.from_arrays(x=x, y=y, w=w)
+
+    def c2_step():
+        keep = dfc.evaluate("w > 0.5")
+        bx = superagg.BinnerScalar_float64("x", -4.0, 4.0, bins)
+        by = superagg.BinnerScalar_float64("y", -4.0, 4.0, bins)
+        bx.set_data(x)
+        by.set_data(y)
+        grid = superagg.Grid([bx, by])
+        count = superagg.AggCount_int64(grid)
+        s = superagg.AggSum_float64(grid)
+        s.set_data(w, 0)
+        count.set_data_mask(keep)
+        s.set_data_mask(keep)
+        grid.bin([count, s])
+        return count, keep
+
+    def timed(fn, names):
+        for _ in range(max(1, args.warmup)):
+            res = fn()
+        _lib.synchronize()
+        _lib.timing_reset()
+        _lib.timing_enable(True)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            res = fn()
+        _lib.synchronize()
+        t = time.perf_counter() - t0
+        _lib.timing_enable(False)
+        per = {}
+        for k in names:
+            c, ms = _lib.timing_read(k)
+            if c:
+                per[k] = round(ms / c, 4)
+        return res, t / args.steps, per
+
+    (count, keep), t, per = timed(c2_step, ["expr", "tile_sample", "tile_scatter_f64", "tile_scatter", "tile_reduce"])
+    kept = int(np.count_nonzero(keep.to_numpy()))
+    c_tot = int(np.asarray(count).sum())
+    out["c2_selection"] = {"rows": n, "selection": "w > 0.5", "ms_per_step": t * 1e3, "rows_per_s": n / t,
+                           "per_kernel_ms": per, "check": {"count_total": c_tot, "kept_rows": kept, "ok": c_tot == kept}}
+    del count, keep
+    m = int(args.groupby_rows)
+    keys = DeviceArray.random(m, "randint", seed=5, a=5, b=5 + 1_000_000, dtype="int32")
+    v = DeviceArray.random(m, "normal", seed=6)
+    dff = vaex_amd.from_arrays(key=keys, v=v)
+    dff = dff[dff.v > 0]
+    res, t, per = timed(lambda: dff.groupby("key", agg={"v": ["sum", "count"]}),
+                        ["expr", "tile_sample", "tile_scatter_ord", "tile_scatter", "tile_reduce"])
+    g_tot = int(np.asarray(res["v"].to_numpy()).sum())
+    flen = len(dff)
+    out["groupby_filtered"] = {"rows": m, "filter": "v > 0", "ms": t * 1e3, "rows_per_s": m / t, "groups": len(res),
+                               "per_kernel_ms": per, "check": {"count_total": g_tot, "filtered_rows": flen,
+                                                                "ok": g_tot == flen and len(res) > 0}}
+    return out
 
 
 def bench_other_aggs(x, y, w, n, bins, args, c2_ms):

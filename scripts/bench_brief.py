@@ -10,6 +10,9 @@ print("C2", round(d["value"] / 1e9, 2), "G rows/s", round(d["ms_per_step"], 3), 
 c = d.get("count_only")
 if c:
     print("count_only", round(c["ms_per_step"], 3), "ms", c["per_kernel_ms"], "frac", c["kernel_frac"])
+c = d.get("filtered")
+if c:
+    print("filtered", {k: (round(v.get("ms_per_step", v.get("ms", 0)), 3), v["per_kernel_ms"], v["check"]["ok"]) for k, v in c.items()})
 c = d.get("c2_float32")
 if c:
     print("c2_float32", round(c["ms_per_step"], 3), "ms", c["per_kernel_ms"], "ok", c["check"]["ok"])
