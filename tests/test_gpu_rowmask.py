@@ -148,3 +148,26 @@ def test_filtered_groupby_empty_and_narrow_filters():
     want = oracle.groupby_agg({"key": keys[sel], "v": v[sel]}, ["key"], [("v", "sum", "v")])
     np.testing.assert_array_equal(g1["key"].to_numpy(), want["key"])
     np.testing.assert_allclose(g1["v"].to_numpy(), want["v"], rtol=1e-9, atol=1e-12)
+
+
+def test_filter_mask_cache_follows_columns():
+    """A filtered HBM frame keeps its filter mask between queries (the reference's per-block
+    filter-mask cache) and evaluates it again when a column is replaced."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(23)
+    n = 2_000_000
+    keys = rng.integers(0, 10_000, n).astype(np.int32)
+    v = rng.normal(size=n)
+    base = vaex_amd.from_arrays(key=DeviceArray.from_numpy(keys), v=DeviceArray.from_numpy(v))
+    dff = base[base.v > 0]
+    for _ in range(2):  # the second query reuses the mask
+        g = dff.groupby("key", agg={"v": "sum"})
+        want = oracle.groupby_agg({"key": keys[v > 0], "v": v[v > 0]}, ["key"], [("v", "sum", "v")])
+        np.testing.assert_allclose(g["v"].to_numpy(), want["v"], rtol=1e-9, atol=1e-12)
+    v2 = rng.normal(size=n)
+    dff.columns["v"] = DeviceArray.from_numpy(v2)
+    g = dff.groupby("key", agg={"v": "sum"})
+    want = oracle.groupby_agg({"key": keys[v2 > 0], "v": v2[v2 > 0]}, ["key"], [("v", "sum", "v")])
+    np.testing.assert_array_equal(g["key"].to_numpy(), want["key"])
+    np.testing.assert_allclose(g["v"].to_numpy(), want["v"], rtol=1e-9, atol=1e-12)

@@ -197,6 +197,9 @@ class DataFrame:
         df._categories = dict(self._categories)
         df.selection_expressions = dict(self.selection_expressions)
         df._filter = self._filter
+        # copies share the filter-mask cache (its keys hold the filter and the columns, so a
+        # copy that changes either misses; groupby works on a copy)
+        df._filter_mask_cache = self.__dict__.setdefault("_filter_mask_cache", {})
         return df
 
     def add_column(self, name, data):
@@ -332,7 +335,20 @@ class DataFrame:
 
     def evaluate_filter_mask(self, i1, i2):
         if self.is_device_resident():
-            return self._eval_device(self._filter, i1, i2)
+            # the device mask of the filter, per (i1, i2) block, kept while the frame's columns,
+            # virtual columns and variables stay the same objects (the reference keeps filter
+            # masks per block too: _selection_mask_caches[FILTER_SELECTION_NAME],
+            # dataframe.py:4161,5967, dropped by _invalidate_selection_cache)
+            key = (self._filter, i1, i2,
+                   tuple((k, getattr(c, "ptr", id(c)), len(c)) for k, c in self.columns.items()),
+                   tuple(sorted(self.virtual_columns.items())), tuple((k, id(v)) for k, v in self.variables.items()))
+            cache = self.__dict__.setdefault("_filter_mask_cache", {})
+            m = cache.get(key)
+            if m is None:
+                if len(cache) >= 8:
+                    cache.clear()
+                m = cache[key] = self._eval_device(self._filter, i1, i2)
+            return m
         return np.asarray(self._eval_host(self._filter, i1, i2), dtype=bool)
 
     def data_type(self, expression):
