@@ -171,3 +171,25 @@ def test_filter_mask_cache_follows_columns():
     want = oracle.groupby_agg({"key": keys[v2 > 0], "v": v2[v2 > 0]}, ["key"], [("v", "sum", "v")])
     np.testing.assert_array_equal(g["key"].to_numpy(), want["key"])
     np.testing.assert_allclose(g["v"].to_numpy(), want["v"], rtol=1e-9, atol=1e-12)
+
+
+def test_selection_mask_cache_follows_select():
+    """Selection masks of an HBM frame are kept per block (cpu.py:548 asks for cached masks);
+    a new df.select() expression or a replaced column evaluates again."""
+    import vaex_amd
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(24)
+    n = 2_000_000
+    x, w = rng.normal(size=n), rng.random(n)
+    df = vaex_amd.from_arrays(x=DeviceArray.from_numpy(x), w=DeviceArray.from_numpy(w))
+    spec = oracle.Binner("scalar", x, vmin=-4, vmax=4, bins=64)
+    for thr in (0.3, 0.3, 0.7):
+        df.select(f"w > {thr}")
+        got = np.asarray(df.count(binby="x", limits=[-4, 4], shape=64, selection=True))
+        want = oracle.extract_central_part(oracle.compute_grid([spec], "count", mask=(w > thr).astype(np.uint8)))
+        np.testing.assert_array_equal(got, want)
+    w2 = rng.random(n)
+    df.columns["w"] = DeviceArray.from_numpy(w2)
+    got = np.asarray(df.count(binby="x", limits=[-4, 4], shape=64, selection=True))
+    want = oracle.extract_central_part(oracle.compute_grid([spec], "count", mask=(w2 > 0.7).astype(np.uint8)))
+    np.testing.assert_array_equal(got, want)

@@ -339,17 +339,20 @@ class DataFrame:
             # virtual columns and variables stay the same objects (the reference keeps filter
             # masks per block too: _selection_mask_caches[FILTER_SELECTION_NAME],
             # dataframe.py:4161,5967, dropped by _invalidate_selection_cache)
-            key = (self._filter, i1, i2,
-                   tuple((k, getattr(c, "ptr", id(c)), len(c)) for k, c in self.columns.items()),
-                   tuple(sorted(self.virtual_columns.items())), tuple((k, id(v)) for k, v in self.variables.items()))
-            cache = self.__dict__.setdefault("_filter_mask_cache", {})
-            m = cache.get(key)
-            if m is None:
-                if len(cache) >= 8:
-                    cache.clear()
-                m = cache[key] = self._eval_device(self._filter, i1, i2)
-            return m
+            return self._cached_device_mask(self._filter, i1, i2)
         return np.asarray(self._eval_host(self._filter, i1, i2), dtype=bool)
+
+    def _cached_device_mask(self, expr, i1, i2):
+        key = (expr, i1, i2,
+               tuple((k, getattr(c, "ptr", id(c)), len(c)) for k, c in self.columns.items()),
+               tuple(sorted(self.virtual_columns.items())), tuple((k, id(v)) for k, v in self.variables.items()))
+        cache = self.__dict__.setdefault("_filter_mask_cache", {})
+        m = cache.get(key)
+        if m is None:
+            if len(cache) >= 8:
+                cache.clear()
+            m = cache[key] = self._eval_device(expr, i1, i2)
+        return m
 
     def data_type(self, expression):
         expression = str(expression)
@@ -371,9 +374,11 @@ class DataFrame:
             selection = self.selection_expressions[selection]
         return str(selection)
 
-    def device_keep_mask(self, i1, i2, selection=None, invert=False):
+    def device_keep_mask(self, i1, i2, selection=None, invert=False, cache=False):
         """HBM frame: one device mask of the rows a part takes (filter & selection), or its
-        complement (invert: the skip mask of the min/max kernel); None = every row."""
+        complement (invert: the skip mask of the min/max kernel); None = every row.  cache:
+        kept per block like the filter mask (the reference's aggregation parts ask for cached
+        selection masks, cpu.py:548)."""
         parts = []
         if self._filter is not None:
             parts.append(f"({self._filter})")
@@ -382,7 +387,8 @@ class DataFrame:
         if not parts:
             return None
         expr = " & ".join(parts)
-        return self._eval_device(f"~({expr})" if invert else expr, i1, i2)
+        expr = f"~({expr})" if invert else expr
+        return self._cached_device_mask(expr, i1, i2) if cache else self._eval_device(expr, i1, i2)
 
     # ---- selections --------------------------------------------------------------
     def select(self, expression, name="default"):
@@ -398,7 +404,7 @@ class DataFrame:
         i2 = self._length if i2 is None else i2
         if isinstance(filter_mask, DeviceArray) or (filter_mask is None and self.is_device_resident()):
             # HBM frame: the device mask of (filter &) selection over the whole chunk
-            return self.device_keep_mask(i1, i2, selection)
+            return self.device_keep_mask(i1, i2, selection, cache=cache)
         selection = self._selection_expression(selection)
         mask = self._eval_host(str(selection), i1, i2, filter_mask)
         if np.ma.isMaskedArray(mask):

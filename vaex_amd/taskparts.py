@@ -147,7 +147,8 @@ class TaskPartAggregation:
                     if skey is not None and skey in sel_masks:
                         selection_mask = sel_masks[skey]
                     else:
-                        selection_mask = self.df.evaluate_selection_mask(selection, i1=i1, i2=i2, filter_mask=filter_mask)
+                        selection_mask = self.df.evaluate_selection_mask(selection, i1=i1, i2=i2, filter_mask=filter_mask,
+                                                                         cache=True)  # cpu.py:548
                         if not isinstance(selection_mask, DeviceArray):
                             selection_mask = np.asarray(selection_mask)
                         if skey is not None:
