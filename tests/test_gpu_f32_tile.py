@@ -100,3 +100,54 @@ def test_f32_small_grid_count_matches_oracle(monkeypatch, nd, bins, n, offset):
     _check(xs, [], bins, out)
     monkeypatch.setenv("VH_SMALL_F32", "0")
     np.testing.assert_array_equal(_run(xs, [], bins, offset=offset)[0], out[0])
+
+
+@pytest.mark.parametrize("bdt,vdt,nv", [("float64", "float32", 1), ("float64", "float32", 2), ("float32", "float64", 1),
+                                        ("float32", "float64", 2)])
+def test_mixed_column_types_match_oracle(monkeypatch, bdt, vdt, nv):
+    """Mixed plans on the fast pass A (float64 binners with float32 sums, float32 binners with
+    float64 sums: the value columns in a second register array of their own pair type),
+    against the oracle and the generic pass A (VH_TILE_F32=0)."""
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(31 + nv)
+    n = 3_000_000
+    xs = [rng.normal(size=n).astype(bdt) for _ in range(2)]
+    for x in xs:
+        x[::997] = np.nan
+    ws = [rng.random(n).astype(vdt) for _ in range(nv)]
+    for w in ws:
+        w[::101] = np.nan
+
+    def run():
+        bs = []
+        for i, x in enumerate(xs):
+            b = getattr(sa(), "BinnerScalar_" + bdt)(f"x{i}", -4, 4, 1024)
+            b.set_data(DeviceArray.from_numpy(x))
+            bs.append(b)
+        grid = sa().Grid(bs)
+        aggs = [sa().AggCount_int64(grid)]
+        for w in ws:
+            s = getattr(sa(), "AggSum_" + vdt)(grid)
+            s.set_data(DeviceArray.from_numpy(w), 0)
+            aggs.append(s)
+        grid.bin(aggs)
+        return [np.asarray(a).copy() for a in aggs]
+
+    out = run()
+    _check(xs, ws, 1024, out)
+    monkeypatch.setenv("VH_TILE_F32", "0")
+    gen = run()
+    np.testing.assert_array_equal(out[0], gen[0])
+    for a, b in zip(out[1:], gen[1:]):
+        np.testing.assert_allclose(a, b, rtol=1e-9, atol=1e-9)
+
+
+def test_f32_plan_past_the_fast_kernels_lds():
+    """A float32 plan whose tiles do not fit the fast kernel's LDS (2^25 bins: 4096 tiles)
+    runs the generic pass A with its per-dtype loads (not an ND > 0 kernel that reads float64
+    columns), against the oracle."""
+    rng = np.random.default_rng(41)
+    n = 2_000_000
+    xs, ws = _cols(rng, n, 1, 1)
+    out = _run(xs, ws, 1 << 25)
+    _check(xs, ws, 1 << 25, out)

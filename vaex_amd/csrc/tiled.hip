@@ -1149,19 +1149,26 @@ __device__ inline uint32_t scalar_f64_index32(double v, double vmin, double scal
 // MK: the plan's aggregators share one keep mask (tp.rowmask): two mask bytes per row pair
 // load with the pair, and a row whose byte is not 1 takes no aggregator (dropped from the
 // exchange, as the generic pass A drops a row no aggregator takes)
-template <int ND, int NV, int SB, typename CT = double, bool MK = false>
+// VT != CT (mixed plans: float64 binners with float32 sums, float32 binners with float64
+// sums): the value columns load into a second register array of their own pair type
+template <int ND, int NV, int SB, typename CT = double, bool MK = false, typename VT = CT>
 __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
     constexpr bool F32 = std::is_same_v<CT, float>;
+    constexpr bool MIX = !std::is_same_v<CT, VT>;
+    constexpr bool VF32 = std::is_same_v<VT, float>;
     using P2 = std::conditional_t<F32, float2, double2>;
-    using VS = std::conditional_t<F32, uint32_t, double>;  // carried / staged value slot
-    constexpr int NC = ND + NV;
+    using VP2 = std::conditional_t<VF32, float2, double2>;
+    using VS = std::conditional_t<VF32, uint32_t, double>;  // carried / staged value slot
+    constexpr int NC = ND + (MIX ? 0 : NV);  // columns in the CT pair array
+    constexpr int NVX = MIX ? NV : 0;        // value columns in the VT pair array
     constexpr int PAIRS = TA_RPT / 2;
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const uint32_t T = tp.ntiles;
-    const ScatterLds l = fast_lds<NV>(lds_raw, T, tp.lds_cap, F32 ? 4 : 8);
+    const ScatterLds l = fast_lds<NV>(lds_raw, T, tp.lds_cap, VF32 ? 4 : 8);
     scatter_lds_init(l, tp, T);
     __syncthreads();
-    const CT *col[NC];
+    const CT *col[NC > 0 ? NC : 1];
+    const VT *vcol[NVX > 0 ? NVX : 1];
     double vmin[ND > 0 ? ND : 1], scale[ND > 0 ? ND : 1], bins_d[ND > 0 ? ND : 1];
     uint32_t bins2[ND > 0 ? ND : 1], stride[ND > 0 ? ND : 1];
 #pragma unroll
@@ -1174,7 +1181,10 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
         stride[d] = (uint32_t)p.b[d].stride;
     }
 #pragma unroll
-    for (int s = 0; s < NV; s++) col[ND + s] = reinterpret_cast<const CT *>(tp.vdata[s]);
+    for (int s = 0; s < NV; s++) {
+        if constexpr (MIX) vcol[s] = reinterpret_cast<const VT *>(tp.vdata[s]);
+        else col[ND + s] = reinterpret_cast<const CT *>(tp.vdata[s]);
+    }
     // take flags: count(*) always; a sum, or a count keyed on a summed column, takes the
     // row when that value is not NaN (nan_keyed[s] = the aggregators keyed on slot s)
     uint32_t count_mask = 0, keyed_slot_of[MAX_FUSED_AGGS], nan_keyed[NV > 0 ? NV : 1] = {};
@@ -1200,12 +1210,15 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
     // are dropped by the i < n test.  With no load behind an exec branch the compiler
     // counts vmcnt instead of draining to 0, so the prefetched batch stays in flight.
     const uint8_t *rowmask = tp.rowmask;
-    auto load = [&](uint64_t b0, P2 (&dst)[PAIRS][NC], uint32_t (&mdst)[MK ? PAIRS : 1]) {
+    auto load = [&](uint64_t b0, P2 (&dst)[PAIRS][NC > 0 ? NC : 1], VP2 (&vdst)[PAIRS][NVX > 0 ? NVX : 1],
+                    uint32_t (&mdst)[MK ? PAIRS : 1]) {
 #pragma unroll
         for (int q = 0; q < PAIRS; q++) {
             const uint64_t i = b0 + 2 * ((uint64_t)q * TA_THREADS + threadIdx.x);
             const uint64_t is = i < n - 2 ? i : n - 2;
             if constexpr (MK) mdst[q] = *reinterpret_cast<const uint16_t *>(rowmask + is);
+#pragma unroll
+            for (int s = 0; s < NVX; s++) vdst[q][s] = *reinterpret_cast<const VP2 *>(vcol[s] + is);
 #pragma unroll
             for (int c = 0; c < NC; c++) {
 #if VH_TA_NT  // experiment: non-temporal loads of the once-read columns
@@ -1221,8 +1234,8 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
         }
     };
     // rank the rows of one batch: cell, take flags, (tile << 16 | cell) key, rank in tile
-    auto rows = [&](uint64_t b0, const P2 (&cur)[PAIRS][NC], const uint32_t (&mcur)[MK ? PAIRS : 1], uint32_t *key,
-                    int32_t *rank, VS (*vals)[NV > 0 ? NV : 1]) {
+    auto rows = [&](uint64_t b0, const P2 (&cur)[PAIRS][NC > 0 ? NC : 1], const VP2 (&vcur)[PAIRS][NVX > 0 ? NVX : 1],
+                    const uint32_t (&mcur)[MK ? PAIRS : 1], uint32_t *key, int32_t *rank, VS (*vals)[NV > 0 ? NV : 1]) {
 #pragma unroll
         for (int r = 0; r < TA_RPT; r++) {
             const int q = r >> 1, h = r & 1;
@@ -1236,8 +1249,10 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
             uint32_t f = count_mask;
 #pragma unroll
             for (int s = 0; s < NV; s++) {
-                const CT v = h ? cur[q][ND + s].y : cur[q][ND + s].x;
-                if constexpr (F32) vals[r][s] = __builtin_bit_cast(uint32_t, v);
+                VT v;
+                if constexpr (MIX) v = h ? vcur[q][s].y : vcur[q][s].x;
+                else v = h ? cur[q][ND + s].y : cur[q][ND + s].x;
+                if constexpr (VF32) vals[r][s] = __builtin_bit_cast(uint32_t, v);
                 else vals[r][s] = v;
                 f |= v == v ? nan_keyed[s] : 0u;
             }
@@ -1254,9 +1269,10 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
         }
     };
     constexpr bool drain = VH_TA_DRAIN != 0;
-    P2 cur[PAIRS][NC], nxt[PAIRS][NC];
+    P2 cur[PAIRS][NC > 0 ? NC : 1], nxt[PAIRS][NC > 0 ? NC : 1];
+    VP2 vcur[PAIRS][NVX > 0 ? NVX : 1], vnxt[PAIRS][NVX > 0 ? NVX : 1];
     uint32_t mcur[MK ? PAIRS : 1] = {}, mnxt[MK ? PAIRS : 1] = {};
-    load((uint64_t)w * TA_BATCH, cur, mcur);
+    load((uint64_t)w * TA_BATCH, cur, vcur, mcur);
     for (uint64_t b0 = (uint64_t)w * TA_BATCH; b0 < n; b0 += SB * bstep) {
         uint32_t key[SB * TA_RPT];
         int32_t rank[SB * TA_RPT];
@@ -1265,13 +1281,15 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
         // after the commit (a copy before it would wait for those loads)
 #pragma unroll
         for (int sb = 0; sb < SB; sb++) {
-            load(b0 + (sb + 1) * bstep, nxt, mnxt);
-            rows(b0 + sb * bstep, cur, mcur, key + sb * TA_RPT, rank + sb * TA_RPT, vals + sb * TA_RPT);
+            load(b0 + (sb + 1) * bstep, nxt, vnxt, mnxt);
+            rows(b0 + sb * bstep, cur, vcur, mcur, key + sb * TA_RPT, rank + sb * TA_RPT, vals + sb * TA_RPT);
             if (sb + 1 < SB || drain)
 #pragma unroll
                 for (int q = 0; q < PAIRS; q++) {
 #pragma unroll
                     for (int c = 0; c < NC; c++) cur[q][c] = nxt[q][c];
+#pragma unroll
+                    for (int c = 0; c < NVX; c++) vcur[q][c] = vnxt[q][c];
                     if constexpr (MK) mcur[q] = mnxt[q];
                 }
         }
@@ -1286,6 +1304,8 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
             for (int q = 0; q < PAIRS; q++) {
 #pragma unroll
                 for (int c = 0; c < NC; c++) cur[q][c] = nxt[q][c];
+#pragma unroll
+                for (int c = 0; c < NVX; c++) vcur[q][c] = vnxt[q][c];
                 if constexpr (MK) mcur[q] = mnxt[q];
             }
     }
@@ -2145,6 +2165,16 @@ static void launch_scatter(int fast, unsigned grid, size_t lds, const BinPlan &p
             hipLaunchKernelGGL((k_tile_scatter_f64<ND, NV, fast_sb_narrow(NV), float>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
             return;
         }
+        if constexpr (NV > 0) {
+            if (fast == 6) {
+                hipLaunchKernelGGL((k_tile_scatter_f64<ND, NV, fast_sb_nd(NV, ND), float, false, double>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
+                return;
+            }
+            if (fast == 7) {
+                hipLaunchKernelGGL((k_tile_scatter_f64<ND, NV, fast_sb_narrow(NV), double, false, float>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
+                return;
+            }
+        }
         if (fast == 2) {
             hipLaunchKernelGGL((k_tile_scatter_f64<ND, NV, fast_sb_nd(NV, ND)>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
             return;
@@ -2186,6 +2216,16 @@ template <int ND, int NV> static int scatter_blocks_per_cu(int fast, size_t lds,
         if (fast == 5) {
             VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter_f64<ND, NV, fast_sb_narrow(NV), float>, TA_THREADS, lds));
             return nb;
+        }
+        if constexpr (NV > 0) {
+            if (fast == 6) {
+                VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter_f64<ND, NV, fast_sb_nd(NV, ND), float, false, double>, TA_THREADS, lds));
+                return nb;
+            }
+            if (fast == 7) {
+                VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter_f64<ND, NV, fast_sb_narrow(NV), double, false, float>, TA_THREADS, lds));
+                return nb;
+            }
         }
         if (fast == 2) {
             VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter_f64<ND, NV, fast_sb_nd(NV, ND)>, TA_THREADS, lds));
@@ -2448,23 +2488,34 @@ static bool try_tiled_core(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     // column), no aggregator masks, 8-byte aligned columns, n even (row pairs).  It replaces
     // the generic pass A's per-dimension dtype dispatch, whose loads wait at every switch join
     // (C2 on float32 columns: 11.3 ms generic pass A, profiles/r06_f32.txt)
-    int nd_f32 = 0;
-    if (!fast && nd_f64 == 0 && !flags_mode && n % 2 == 0 && plan.nb >= 1 && plan.nb <= 3 &&
-        !getenv_flag_off("VH_TILE_F32")) {
+    // Mixed plans take the same kernel with a second value-pair array (modes 6 / 7 below).
+    int nd_f32 = 0, mix_mode = 0;  // 5: float32 / float32, 6: float32 binners + float64 values, 7: the reverse
+    if (!fast && !flags_mode && n % 2 == 0 && plan.nb >= 1 && plan.nb <= 3 && !getenv_flag_off("VH_TILE_F32")) {
         bool ok = true;
+        int bt = -1, vt = -1;
         for (int d = 0; d < plan.nb; d++) {
             const BinnerDev &b = plan.b[d];
-            ok = ok && b.kind == 0 && b.dtype == VH_F32 && !b.flip && !b.mask && aligned8(b.data);
+            const int dt = b.dtype;
+            ok = ok && b.kind == 0 && (dt == VH_F32 || dt == VH_F64) && (bt < 0 || dt == bt) && !b.flip && !b.mask &&
+                 (dt == VH_F64 ? aligned16(b.data) : aligned8(b.data));
+            bt = dt;
         }
         for (int k = 0; k < fa.na; k++) {
             const FusedAgg &a = fa.a[k];
             ok = ok && !a.mask;
-            if (a.kind == VH_AGG_COUNT) ok = ok && (!a.data || a.dtype == VH_F32);
-            else ok = ok && a.kind == VH_AGG_SUM && a.data && a.dtype == VH_F32 && aligned8(a.data);
+            if (a.kind == VH_AGG_COUNT) continue;
+            ok = ok && a.kind == VH_AGG_SUM && a.data && (a.dtype == VH_F32 || a.dtype == VH_F64) && (vt < 0 || a.dtype == vt) &&
+                 (a.dtype == VH_F64 ? aligned16(a.data) : aligned8(a.data));
+            vt = a.dtype;
         }
-        if (ok) nd_f32 = plan.nb;
+        if (vt < 0) vt = bt;
+        for (int k = 0; k < fa.na; k++)  // counts of a column: the summed one (flags_mode otherwise)
+            if (fa.a[k].kind == VH_AGG_COUNT && fa.a[k].data) ok = ok && fa.a[k].dtype == vt;
+        if (ok) {
+            mix_mode = bt == VH_F32 ? (vt == VH_F32 ? 5 : 6) : (vt == VH_F32 ? 7 : 0);
+            if (mix_mode) nd_f32 = plan.nb;
+        }
     }
-    const int nd_k = nd_f64 > 0 ? nd_f64 : nd_f32 > 0 ? nd_f32 : (has_set ? -1 : 0);
     const bool ord = !fast && n % 2 == 0 && ord_fast_ok(plan, fa);
     tp.vdt[0] = tp.vdt[1] = VH_F64;
     if (ord) for (int k = 0; k < fa.na; k++)
@@ -2487,12 +2538,19 @@ static bool try_tiled_core(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     // its sums are float32 bits in narrow slots)
     const bool narrow_ord = ord && vnarrow &&
                             fast_lds_bytes(nv, T, (uint32_t)(fast_sb_narrow(nv) * TA_BATCH), 4) <= LDS_MAX_BYTES;
-    const bool f32_ok = nd_f32 > 0 && (nv == 0 || vnarrow) &&
-                        fast_lds_bytes(nv, T, (uint32_t)(fast_sb_narrow(nv) * TA_BATCH), 4) <= LDS_MAX_BYTES;
-    const int fast_mode = f32_ok ? 5
+    const bool vf32 = mix_mode == 5 || mix_mode == 7;
+    const int sb_mix = vf32 ? fast_sb_narrow(nv) : fast_sb_nd(nv, plan.nb);
+    const bool f32_ok = mix_mode != 0 && (nv == 0 || vnarrow == vf32) &&
+                        fast_lds_bytes(nv, T, (uint32_t)(sb_mix * TA_BATCH), vf32 ? 4 : 8) <= LDS_MAX_BYTES;
+    const int fast_mode = f32_ok ? mix_mode
                           : !(fast || ord) ? 0
                           : narrow_ord  ? 3
                           : fast_lds_bytes(nv, T, (uint32_t)(fast_sb_nd(nv, fast ? nd_f64 : 1) * TA_BATCH)) <= LDS_MAX_BYTES ? 2 : 1;
+    // the scatter kernels' ND: float64 binner dimensions (fast or generic kernels read them as
+    // float64), the float32 / mixed kernels' dimensions only when one of them runs, else the
+    // generic dispatch (0) or the set-ordinal form (-1) -- a float32 plan the fast kernels do
+    // not take must not reach an ND > 0 generic kernel, which would read its columns as float64
+    const int nd_k = nd_f64 > 0 ? nd_f64 : fast_mode >= 5 ? nd_f32 : (has_set ? -1 : 0);
     // a shared keep mask runs only on the fast f64 / f32 kernels' MK instantiations
     if (rowmask && !((fast && fast_mode == 2) || fast_mode == 5 ||
                      (ord && ord_kernel(nv, fast_mode, has_set, tp.vdt[0], tp.vdt[1], true) != nullptr)))
@@ -2500,9 +2558,9 @@ static bool try_tiled_core(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     // wide stream-out (batch_commit_fast): runs padded to 8 entries, 16-byte region stores;
     // needs 8 T more staged entries of LDS and tiles below 2^16 - 1 cells (DUMMY_CELL).
     // VH_TILE_WIDE: bit 0 wide, bit 1 non-temporal cell stores, bit 2 non-temporal value stores
-    const int sb_k = fast_mode == 3 || fast_mode == 5 ? fast_sb_narrow(nv) : fast_mode == 2 ? fast_sb_nd(nv, fast ? nd_f64 : 1) : 1;
+    const int sb_k = fast_mode >= 5 ? sb_mix : fast_mode == 3 ? fast_sb_narrow(nv) : fast_mode == 2 ? fast_sb_nd(nv, fast ? nd_f64 : 1) : 1;
     const uint32_t cap0 = (uint32_t)(sb_k * TA_BATCH);
-    const int vbytes = fast_mode == 3 || fast_mode == 5 ? 4 : 8;
+    const int vbytes = fast_mode == 3 || fast_mode == 5 || fast_mode == 7 ? 4 : 8;
     uint32_t wide_mode = 7;
     if (const char *e = getenv("VH_TILE_WIDE")) wide_mode = (uint32_t)atoi(e);
     const bool wide = (wide_mode & 1) && fast_mode != 0 && !flags_mode && S < DUMMY_CELL &&
@@ -2599,7 +2657,7 @@ static bool try_tiled_core(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         tp.vnarrow = vnarrow ? 1u : 0u;
         // the narrow ordinal pass A with two carried columns stores both in values[0], blocked
         // by 8 entries (values[0] spans both slot arrays; values[1] is unused)
-        tp.vpacked = ((fast_mode == 3 || fast_mode == 5) && nv == 2 && !flags_mode && !getenv_flag_off("VH_TILE_PACK")) ? 1u : 0u;
+        tp.vpacked = ((fast_mode == 3 || fast_mode == 5 || fast_mode == 7) && nv == 2 && !flags_mode && !getenv_flag_off("VH_TILE_PACK")) ? 1u : 0u;
         tp.vfloat = vfloat;
         tp.vsigned = vsigned;
         tp.s_log2 = s_log2;
@@ -2631,7 +2689,7 @@ static bool try_tiled_core(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     };
     bool a_launched = false;
     auto launch_pass_a = [&]() {
-        TimedScope ts(fast ? "tile_scatter_f64" : fast_mode == 5 ? "tile_scatter_f32" : ord ? (has_set ? "tile_scatter_set" : "tile_scatter_ord") : "tile_scatter");
+        TimedScope ts(fast ? "tile_scatter_f64" : fast_mode == 5 ? "tile_scatter_f32" : fast_mode >= 6 ? "tile_scatter_mixed" : ord ? (has_set ? "tile_scatter_set" : "tile_scatter_ord") : "tile_scatter");
         const size_t lds = lds_a;
         if (ord) {
             const void *kf = ord_kernel(nv, fast_mode, has_set, tp.vdt[0], tp.vdt[1], rowmask != nullptr);
