@@ -1003,10 +1003,16 @@ def bench_h2o(n, reps=3):
             # the previous result is dropped first, as a query loop that discards its results
             # does (its page-locked result columns go back to the block cache)
             r = None
+            if os.environ.get("BENCH_H2O_TRACE"):
+                _lib.trace_report()
             t0 = time.perf_counter()
             r = f()
             _lib.synchronize()
             ts.append(time.perf_counter() - t0)
+            if os.environ.get("BENCH_H2O_TRACE"):  # per-call C-ABI times (VAEX_AMD_TRACE_CALLS=1)
+                top = sorted(_lib.trace_report().items(), key=lambda kv: -kv[1][1])[:5]
+                print(f"# h2o {q}: {ts[-1] * 1e3:.1f} ms " + " ".join(f"{k} {1e3 * v[1]:.1f}" for k, v in top),
+                      file=sys.stderr, flush=True)
         t = min(ts)
         out[q] = {"ms": round(t * 1e3, 3), "rows_per_s": n / t, "algorithmic_bytes_per_row": H2O_BYTES[q],
                   "GBps": round(H2O_BYTES[q] * n / t / 1e9, 1), "check": h2o_check(q, r, n, sums)}

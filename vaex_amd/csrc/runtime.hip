@@ -58,15 +58,17 @@ DeviceScope::~DeviceScope() {
 
 // ---- device block cache (common.hpp) ---------------------------------------------------
 namespace {
-// Freed device blocks are kept for reuse (exact sizes, 1 MiB granularity): at most 1/8 of
+// Freed device blocks are kept for reuse (exact sizes, 1 MiB granularity): at most 1/4 of
 // the device's memory (VAEX_AMD_DEVICE_CACHE_MB overrides it per process, 0 disables the
 // cache), blocks of up to 1/16 of it.  Large blocks matter: a 1e9-row query
 // allocates multi-GB temporaries (h2o q10's 8 GB combined key column), and a fresh hipMalloc
-// of 8 GB stalled for 5.7 s every few queries on a device holding ~60 GB.  A failed
+// of 8 GB stalled for 5.7 s every few queries on a device holding ~60 GB.  A freed block
+// past the cap evicts the longest-cached blocks first (a full cache of an earlier query's
+// block sizes made every q10 hipMalloc its temporaries: 1.1 s of 1.7 s, round 6).  A failed
 // allocation drops the cache and retries.
 struct BlockCache {
-    std::multimap<uint64_t, void *> free;
-    uint64_t cached = 0;
+    std::multimap<uint64_t, std::pair<void *, uint64_t>> free;  // size -> (block, free sequence)
+    uint64_t cached = 0, seq = 0;
     uint64_t max_bytes = 0, max_block = 0;
     bool limits_set = false;
 };
@@ -77,7 +79,7 @@ void cache_limits(BlockCache &c) {
         (void)hipGetLastError();
         total = 32ull << 30;
     }
-    c.max_bytes = total / 8;
+    c.max_bytes = total / 4;
     c.max_block = total / 16;
     if (const char *e = getenv("VAEX_AMD_DEVICE_CACHE_MB")) {
         c.max_bytes = (uint64_t)strtoull(e, nullptr, 10) << 20;
@@ -99,7 +101,7 @@ void *dev_alloc(uint64_t &bytes) {
         BlockCache &c = g_cache[d];
         auto it = c.free.find(bytes);
         if (it != c.free.end()) {
-            void *p = it->second;
+            void *p = it->second.first;
             c.free.erase(it);
             c.cached -= bytes;
             return p;
@@ -112,7 +114,7 @@ void *dev_alloc(uint64_t &bytes) {
         {  // drop the cache and retry once
             std::lock_guard<std::mutex> lk(g_cache_mu);
             BlockCache &c = g_cache[d];
-            for (auto &kv : c.free) (void)hipFree(kv.second);
+            for (auto &kv : c.free) (void)hipFree(kv.second.first);
             c.free.clear();
             c.cached = 0;
         }
@@ -131,8 +133,16 @@ void dev_free(void *ptr, uint64_t bytes) {
         std::lock_guard<std::mutex> lk(g_cache_mu);
         BlockCache &c = g_cache[current_device()];
         cache_limits(c);
-        if (bytes <= c.max_block && c.cached + bytes <= c.max_bytes) {
-            c.free.emplace(bytes, ptr);
+        if (bytes <= c.max_block && bytes <= c.max_bytes) {
+            while (c.cached + bytes > c.max_bytes && !c.free.empty()) {  // evict the oldest
+                auto old = c.free.begin();
+                for (auto it = c.free.begin(); it != c.free.end(); ++it)
+                    if (it->second.second < old->second.second) old = it;
+                (void)hipFree(old->second.first);
+                c.cached -= old->first;
+                c.free.erase(old);
+            }
+            c.free.emplace(bytes, std::make_pair(ptr, ++c.seq));
             c.cached += bytes;
             return;
         }
@@ -638,7 +648,7 @@ int vh_device_cache_trim(void) {
         if (c.free.empty()) continue;
         DeviceScope ds(dc.first);
         VH_HIP(hipStreamSynchronize(stream()));
-        for (auto &kv : c.free) (void)hipFree(kv.second);
+        for (auto &kv : c.free) (void)hipFree(kv.second.first);
         c.free.clear();
         c.cached = 0;
     }
