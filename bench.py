@@ -326,7 +326,7 @@ def main():
 
 
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_c2.json")
-PMC_KERNEL = {"tile_scatter_f64": "k_tile_scatter_f64<2, 1, 3, double, false>", "tile_scatter": "k_tile_scatter<2, 1>",
+PMC_KERNEL = {"tile_scatter_f64": "k_tile_scatter_f64<2, 1, 3, double, false, double>", "tile_scatter": "k_tile_scatter<2, 1>",
               "tile_reduce": "k_tile_reduce<1>"}
 
 
