@@ -151,3 +151,48 @@ def test_f32_plan_past_the_fast_kernels_lds():
     xs, ws = _cols(rng, n, 1, 1)
     out = _run(xs, ws, 1 << 25)
     _check(xs, ws, 1 << 25, out)
+
+
+@pytest.mark.parametrize("bdt", ["int32", "int64"])
+@pytest.mark.parametrize("vdt,nv", [(None, 0), ("float64", 1), ("float32", 1), ("float64", 2)])
+def test_integer_binners_match_oracle(monkeypatch, bdt, vdt, nv):
+    """Integer binby columns on the fast pass A (BinnerScalar<int>: the value widened to
+    double before the index math), 1- and 2-d, with float64 / float32 sums or count only,
+    against the oracle and the generic pass A (VH_TILE_F32=0)."""
+    from vaex_amd.device import DeviceArray
+    rng = np.random.default_rng(51 + nv)
+    n = 3_000_000
+    for nd, bins in ((2, 1000), (1, 1 << 20)):
+        hi = 1200 if nd == 2 else 1_100_000
+        xs = [rng.integers(-100, hi, n).astype(bdt) for _ in range(nd)]
+        ws = [rng.random(n).astype(vdt) for _ in range(nv)]
+        for w in ws:
+            w[::101] = np.nan
+        lim = (0, 1000) if nd == 2 else (0, 1 << 20)
+
+        def run():
+            bs = []
+            for i, x in enumerate(xs):
+                b = getattr(sa(), "BinnerScalar_" + bdt)(f"x{i}", lim[0], lim[1], bins)
+                b.set_data(DeviceArray.from_numpy(x))
+                bs.append(b)
+            grid = sa().Grid(bs)
+            aggs = [sa().AggCount_int64(grid)]
+            for w in ws:
+                s = getattr(sa(), "AggSum_" + vdt)(grid)
+                s.set_data(DeviceArray.from_numpy(w), 0)
+                aggs.append(s)
+            grid.bin(aggs)
+            return [np.asarray(a).copy() for a in aggs]
+
+        out = run()
+        ob = [oracle.Binner("scalar", x, vmin=lim[0], vmax=lim[1], bins=bins) for x in xs]
+        np.testing.assert_array_equal(out[0], oracle.compute_grid(ob, "count"))
+        for k, w in enumerate(ws):
+            np.testing.assert_allclose(out[1 + k], oracle.compute_grid(ob, "sum", data=w), rtol=1e-6, atol=1e-9)
+        monkeypatch.setenv("VH_TILE_F32", "0")
+        gen = run()
+        monkeypatch.delenv("VH_TILE_F32")
+        np.testing.assert_array_equal(out[0], gen[0])
+        for a, b in zip(out[1:], gen[1:]):
+            np.testing.assert_allclose(a, b, rtol=1e-9, atol=1e-9)

@@ -1150,13 +1150,20 @@ __device__ inline uint32_t scalar_f64_index32(double v, double vmin, double scal
 // load with the pair, and a row whose byte is not 1 takes no aggregator (dropped from the
 // exchange, as the generic pass A drops a row no aggregator takes)
 // VT != CT (mixed plans: float64 binners with float32 sums, float32 binners with float64
-// sums): the value columns load into a second register array of their own pair type
+// sums): the value columns load into a second register array of their own pair type.
+// CT = int32_t / int64_t: integer binner columns (BinnerScalar<int>: the value widened to
+// double before the same index math, superagg_binners.cpp:14-56)
+template <typename T> struct PairOf;
+template <> struct PairOf<double> { using type = double2; };
+template <> struct PairOf<float> { using type = float2; };
+template <> struct PairOf<int32_t> { using type = int2; };
+template <> struct PairOf<int64_t> { using type = longlong2; };
 template <int ND, int NV, int SB, typename CT = double, bool MK = false, typename VT = CT>
 __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64(BinPlan p, FusedAggs fa, TileParams tp, uint64_t n) {
     constexpr bool F32 = std::is_same_v<CT, float>;
     constexpr bool MIX = !std::is_same_v<CT, VT>;
     constexpr bool VF32 = std::is_same_v<VT, float>;
-    using P2 = std::conditional_t<F32, float2, double2>;
+    using P2 = typename PairOf<CT>::type;
     using VP2 = std::conditional_t<VF32, float2, double2>;
     using VS = std::conditional_t<VF32, uint32_t, double>;  // carried / staged value slot
     constexpr int NC = ND + (MIX ? 0 : NV);  // columns in the CT pair array
@@ -1222,7 +1229,7 @@ __global__ __launch_bounds__(TA_THREADS) TA_ATTR_F64(NV) void k_tile_scatter_f64
 #pragma unroll
             for (int c = 0; c < NC; c++) {
 #if VH_TA_NT  // experiment: non-temporal loads of the once-read columns
-                if constexpr (!F32) {
+                if constexpr (std::is_same_v<CT, double>) {
                     typedef double v2d __attribute__((ext_vector_type(2)));
                     const v2d t = __builtin_nontemporal_load(reinterpret_cast<const v2d *>(col[c] + is));
                     dst[q][c] = make_double2(t.x, t.y);
@@ -2147,6 +2154,40 @@ __global__ __launch_bounds__(TBT) void k_tile_reduce(FusedAggs fa, TileParams tp
     }
 }
 
+// integer binner kernels (fast modes 8-11): int32 / int64 binners, float64 (or no) / float32 values
+template <int ND, int NV, typename F> static void int_kernel(int fast, F &&f) {
+    if constexpr (NV == 0) {
+        if (fast == 8) f(k_tile_scatter_f64<ND, 0, fast_sb_nd(0, ND), int32_t, false, double>);
+        else f(k_tile_scatter_f64<ND, 0, fast_sb_nd(0, ND), int64_t, false, double>);
+    } else {
+        switch (fast) {
+        case 8: f(k_tile_scatter_f64<ND, NV, fast_sb_nd(NV, ND), int32_t, false, double>); break;
+        case 9: f(k_tile_scatter_f64<ND, NV, fast_sb_narrow(NV), int32_t, false, float>); break;
+        case 10: f(k_tile_scatter_f64<ND, NV, fast_sb_nd(NV, ND), int64_t, false, double>); break;
+        default: f(k_tile_scatter_f64<ND, NV, fast_sb_narrow(NV), int64_t, false, float>);
+        }
+    }
+}
+template <int ND, int NV>
+static void launch_scatter_int(int fast, unsigned grid, size_t lds, const BinPlan &plan, const FusedAggs &fa,
+                               const TileParams &tp, uint64_t n) {
+    int_kernel<ND, NV>(fast, [&](auto kern) {
+        BinPlan p = plan;
+        FusedAggs f = fa;
+        TileParams t = tp;
+        uint64_t nn = n;
+        void *args[] = {(void *)&p, (void *)&f, (void *)&t, (void *)&nn};
+        VH_HIP(hipLaunchKernel(reinterpret_cast<const void *>(kern), dim3(grid), dim3(TA_THREADS), args, lds, stream()));
+    });
+}
+template <int ND, int NV> static int scatter_int_blocks(int fast, size_t lds) {
+    int nb = 0;
+    int_kernel<ND, NV>(fast, [&](auto kern) {
+        VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(kern), TA_THREADS, lds));
+    });
+    return nb;
+}
+
 // fast: 0 = generic kernel, 1 = fast kernel one batch per commit, 2 = fast kernel with
 // fast_sb(NV) batches per commit (when its LDS fits)
 template <int ND, int NV>
@@ -2164,6 +2205,12 @@ static void launch_scatter(int fast, unsigned grid, size_t lds, const BinPlan &p
         if (fast == 5) {
             hipLaunchKernelGGL((k_tile_scatter_f64<ND, NV, fast_sb_narrow(NV), float>), dim3(grid), dim3(TA_THREADS), lds, stream(), plan, fa, tp, n);
             return;
+        }
+        if constexpr (ND <= 2) {
+            if (fast >= 8 && fast <= 11) {
+                launch_scatter_int<ND, NV>(fast, grid, lds, plan, fa, tp, n);
+                return;
+            }
         }
         if constexpr (NV > 0) {
             if (fast == 6) {
@@ -2216,6 +2263,9 @@ template <int ND, int NV> static int scatter_blocks_per_cu(int fast, size_t lds,
         if (fast == 5) {
             VH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_scatter_f64<ND, NV, fast_sb_narrow(NV), float>, TA_THREADS, lds));
             return nb;
+        }
+        if constexpr (ND <= 2) {
+            if (fast >= 8 && fast <= 11) return scatter_int_blocks<ND, NV>(fast, lds);
         }
         if constexpr (NV > 0) {
             if (fast == 6) {
@@ -2496,8 +2546,8 @@ static bool try_tiled_core(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         for (int d = 0; d < plan.nb; d++) {
             const BinnerDev &b = plan.b[d];
             const int dt = b.dtype;
-            ok = ok && b.kind == 0 && (dt == VH_F32 || dt == VH_F64) && (bt < 0 || dt == bt) && !b.flip && !b.mask &&
-                 (dt == VH_F64 ? aligned16(b.data) : aligned8(b.data));
+            ok = ok && b.kind == 0 && (dt == VH_F32 || dt == VH_F64 || dt == VH_I32 || dt == VH_I64) && (bt < 0 || dt == bt) &&
+                 !b.flip && !b.mask && (dt == VH_F64 || dt == VH_I64 ? aligned16(b.data) : aligned8(b.data));
             bt = dt;
         }
         for (int k = 0; k < fa.na; k++) {
@@ -2511,8 +2561,12 @@ static bool try_tiled_core(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         if (vt < 0) vt = bt;
         for (int k = 0; k < fa.na; k++)  // counts of a column: the summed one (flags_mode otherwise)
             if (fa.a[k].kind == VH_AGG_COUNT && fa.a[k].data) ok = ok && fa.a[k].dtype == vt;
+        if (vt == VH_I32 || vt == VH_I64) vt = VH_F64;  // integer binners, no values: the float64 form
         if (ok) {
-            mix_mode = bt == VH_F32 ? (vt == VH_F32 ? 5 : 6) : (vt == VH_F32 ? 7 : 0);
+            if (bt == VH_I32 || bt == VH_I64)  // integer binners (1- and 2-d): 8 / 9 int32, 10 / 11 int64
+                mix_mode = plan.nb > 2 ? 0 : (bt == VH_I32 ? 8 : 10) + (vt == VH_F32 ? 1 : 0);
+            else
+                mix_mode = bt == VH_F32 ? (vt == VH_F32 ? 5 : 6) : (vt == VH_F32 ? 7 : 0);
             if (mix_mode) nd_f32 = plan.nb;
         }
     }
@@ -2538,7 +2592,7 @@ static bool try_tiled_core(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     // its sums are float32 bits in narrow slots)
     const bool narrow_ord = ord && vnarrow &&
                             fast_lds_bytes(nv, T, (uint32_t)(fast_sb_narrow(nv) * TA_BATCH), 4) <= LDS_MAX_BYTES;
-    const bool vf32 = mix_mode == 5 || mix_mode == 7;
+    const bool vf32 = mix_mode == 5 || mix_mode == 7 || mix_mode == 9 || mix_mode == 11;
     const int sb_mix = vf32 ? fast_sb_narrow(nv) : fast_sb_nd(nv, plan.nb);
     const bool f32_ok = mix_mode != 0 && (nv == 0 || vnarrow == vf32) &&
                         fast_lds_bytes(nv, T, (uint32_t)(sb_mix * TA_BATCH), vf32 ? 4 : 8) <= LDS_MAX_BYTES;
@@ -2560,7 +2614,7 @@ static bool try_tiled_core(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     // VH_TILE_WIDE: bit 0 wide, bit 1 non-temporal cell stores, bit 2 non-temporal value stores
     const int sb_k = fast_mode >= 5 ? sb_mix : fast_mode == 3 ? fast_sb_narrow(nv) : fast_mode == 2 ? fast_sb_nd(nv, fast ? nd_f64 : 1) : 1;
     const uint32_t cap0 = (uint32_t)(sb_k * TA_BATCH);
-    const int vbytes = fast_mode == 3 || fast_mode == 5 || fast_mode == 7 ? 4 : 8;
+    const int vbytes = fast_mode == 3 || (fast_mode >= 5 && vf32) ? 4 : 8;
     uint32_t wide_mode = 7;
     if (const char *e = getenv("VH_TILE_WIDE")) wide_mode = (uint32_t)atoi(e);
     const bool wide = (wide_mode & 1) && fast_mode != 0 && !flags_mode && S < DUMMY_CELL &&
@@ -2657,7 +2711,7 @@ static bool try_tiled_core(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
         tp.vnarrow = vnarrow ? 1u : 0u;
         // the narrow ordinal pass A with two carried columns stores both in values[0], blocked
         // by 8 entries (values[0] spans both slot arrays; values[1] is unused)
-        tp.vpacked = ((fast_mode == 3 || fast_mode == 5 || fast_mode == 7) && nv == 2 && !flags_mode && !getenv_flag_off("VH_TILE_PACK")) ? 1u : 0u;
+        tp.vpacked = ((fast_mode == 3 || (fast_mode >= 5 && vf32)) && nv == 2 && !flags_mode && !getenv_flag_off("VH_TILE_PACK")) ? 1u : 0u;
         tp.vfloat = vfloat;
         tp.vsigned = vsigned;
         tp.s_log2 = s_log2;
@@ -2689,7 +2743,7 @@ static bool try_tiled_core(const BinPlan &plan, const FusedAggs &fa_in, uint64_t
     };
     bool a_launched = false;
     auto launch_pass_a = [&]() {
-        TimedScope ts(fast ? "tile_scatter_f64" : fast_mode == 5 ? "tile_scatter_f32" : fast_mode >= 6 ? "tile_scatter_mixed" : ord ? (has_set ? "tile_scatter_set" : "tile_scatter_ord") : "tile_scatter");
+        TimedScope ts(fast ? "tile_scatter_f64" : fast_mode == 5 ? "tile_scatter_f32" : fast_mode >= 8 ? "tile_scatter_int" : fast_mode >= 6 ? "tile_scatter_mixed" : ord ? (has_set ? "tile_scatter_set" : "tile_scatter_ord") : "tile_scatter");
         const size_t lds = lds_a;
         if (ord) {
             const void *kf = ord_kernel(nv, fast_mode, has_set, tp.vdt[0], tp.vdt[1], rowmask != nullptr);
